@@ -1,0 +1,294 @@
+"""ctypes wrapper around oracle/build/libssf_oracle.so -- the CPU restatement of the
+SSF-SLAM front-end hot path.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the parity checker / CPU baseline.  The product package
+(ssf-slam_amd/ssf) never imports this module.
+
+Parity status: the Python half (GMM mask, Kabsch, quaternion) is pinned against golden
+vectors generated from the reference's own scripts/PointCloudOdometry_noSeg.py; the C++ half
+(frameFeature.cpp / lidarOdometry_onlyPC.cpp) is PARITY UNPINNED against the reference
+binary (ROS/PCL/Eigen/Ceres are absent, so it cannot be built) and is pinned only by
+known-answer tests.  See oracle/ssf_oracle.h and DESIGN.md.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libssf_oracle.so")
+_lib = None
+
+f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+
+LOG_STRIDE = 10
+MODE_CERES_LM = 0
+MODE_GN = 1
+
+
+class Profile(C.Structure):
+    _fields_ = [("n_rows", C.c_int32), ("plane_min", C.c_float), ("plane_span", C.c_int32),
+                ("row_start", C.c_int32), ("row_end", C.c_int32), ("plane_max", C.c_float)]
+
+
+def build():
+    """Compile the oracle with its committed Makefile (gcc)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        build()
+    L = C.CDLL(_LIB_PATH)
+    L.orc_profile_get.argtypes = [C.c_int32, C.POINTER(Profile)]
+    L.orc_ring_id.argtypes = [C.c_float, C.c_float, C.c_float, C.c_int32]
+    L.orc_ring_id.restype = C.c_int32
+    L.orc_bin.argtypes = [f32p, C.c_int64, C.c_int64, C.c_int32, f32p, i64p, i64p, i32p]
+    L.orc_bin.restype = C.c_int64
+    L.orc_curvature.argtypes = [f32p, i64p, C.c_int32, C.c_int32, C.c_int32, f32p]
+    L.orc_select.argtypes = [f32p, f32p, i64p, C.c_int32, C.c_int32, C.c_int32, C.c_float,
+                             C.c_int32, f32p, i64p]
+    L.orc_select.restype = C.c_int64
+    L.orc_extract_planes.argtypes = [f32p, C.c_int64, C.c_int64, C.c_int32, f32p]
+    L.orc_extract_planes.restype = C.c_int64
+    L.orc_knn.argtypes = [f32p, C.c_int64, f32p, C.c_int32, i32p, f32p]
+    L.orc_plane_table.argtypes = [f32p, C.c_int64, C.c_float, f32p, i32p, i32p, i32p]
+    L.orc_transform_point.argtypes = [f64p, f64p, f32p, f32p]
+    L.orc_correspond.argtypes = [f32p, C.c_int64, f32p, C.c_int64, f64p, f64p, i32p]
+    L.orc_solve.argtypes = [f32p, f32p, f32p, C.c_int64, C.c_int32, C.c_int32, f64p, f64p, f64p,
+                            f64p, f64p, C.POINTER(C.c_int32)]
+    L.orc_solve.restype = C.c_int32
+    L.orc_register_pair.argtypes = [f32p, C.c_int64, f32p, C.c_int64, C.c_float, C.c_int32,
+                                    C.c_int32, f64p, f64p, f64p, f64p, f64p, C.POINTER(C.c_int32)]
+    L.orc_register_pair.restype = C.c_int64
+    L.orc_accumulate.argtypes = [f64p, f64p, f64p, f64p, f64p, f64p]
+    L.orc_gmm_labels.argtypes = [f64p, C.c_int64, f64p, u8p, f64p, f64p]
+    L.orc_gmm_labels.restype = C.c_int32
+    L.orc_kabsch.argtypes = [f64p, f64p, C.c_int64, C.c_void_p, C.c_int32, f64p, f64p]
+    L.orc_kabsch.restype = C.c_int32
+    L.orc_quat_from_R.argtypes = [f64p, f64p]
+    L.orc_quat_from_R.restype = C.c_int32
+    L.orc_svd3.argtypes = [f64p, f64p, f64p, f64p]
+    _lib = L
+    return L
+
+
+def profile(n_rows):
+    p = Profile()
+    if lib().orc_profile_get(n_rows, C.byref(p)) != 0:
+        raise ValueError(f"unsupported N_SCAN_ROW {n_rows}")
+    return p
+
+
+# --------------------------------------------------------------------------- features
+def ring_ids(pts, n_rows):
+    pts = np.ascontiguousarray(pts, np.float32)
+    return np.array([lib().orc_ring_id(float(x), float(y), float(z), n_rows) for x, y, z in pts],
+                    np.int32)
+
+
+def bin_rings(pts, n_rows):
+    """-> (rxyzi [kept,4] f32, ring_off [R+1] i64, src_idx [kept] i64, ring_of_input [n] i32)"""
+    pts = np.ascontiguousarray(pts, np.float32)
+    n = pts.shape[0]
+    rx = np.zeros((max(n, 1), 4), np.float32)
+    off = np.zeros(n_rows + 1, np.int64)
+    src = np.zeros(max(n, 1), np.int64)
+    rid = np.zeros(max(n, 1), np.int32)
+    kept = lib().orc_bin(pts.reshape(-1), n, pts.shape[1], n_rows, rx.reshape(-1), off, src, rid)
+    return rx[:kept], off, src[:kept], rid[:n]
+
+
+def curvature(rxyzi, ring_off, n_rows):
+    p = profile(n_rows)
+    rx = np.ascontiguousarray(rxyzi, np.float32)
+    cv = np.zeros(max(rx.shape[0], 1), np.float32)
+    lib().orc_curvature(rx.reshape(-1) if rx.size else np.zeros(4, np.float32), ring_off, n_rows,
+                        p.row_start, p.row_end, cv)
+    return cv[:rx.shape[0]]
+
+
+def select(rxyzi, curv, ring_off, n_rows):
+    p = profile(n_rows)
+    rx = np.ascontiguousarray(rxyzi, np.float32)
+    n = rx.shape[0]
+    out = np.zeros((max(n, 1), 4), np.float32)
+    sel = np.zeros(max(n, 1), np.int64)
+    m = lib().orc_select(rx.reshape(-1) if n else np.zeros(4, np.float32),
+                         np.ascontiguousarray(curv, np.float32) if n else np.zeros(1, np.float32),
+                         ring_off, n_rows, p.row_start, p.row_end, p.plane_min, p.plane_span,
+                         out.reshape(-1), sel)
+    return out[:m], sel[:m]
+
+
+def extract_planes(pts, n_rows):
+    """frameFeature cloudHandler: input xyz (n,3) -> plane cloud (m,4) x,y,z,intensity"""
+    pts = np.ascontiguousarray(pts, np.float32)
+    n = pts.shape[0]
+    out = np.zeros((max(n, 1), 4), np.float32)
+    m = lib().orc_extract_planes(pts.reshape(-1) if n else np.zeros(3, np.float32), n,
+                                 pts.shape[1] if n else 3, n_rows, out.reshape(-1))
+    if m < 0:
+        raise ValueError("bad profile")
+    return out[:m]
+
+
+# --------------------------------------------------------------------------- registration
+def knn(cloud, q, k):
+    cloud = np.ascontiguousarray(cloud, np.float32)
+    idx = np.zeros(k, np.int32)
+    d2 = np.zeros(k, np.float32)
+    lib().orc_knn(cloud.reshape(-1), cloud.shape[0], np.ascontiguousarray(q, np.float32), k, idx, d2)
+    return idx, d2
+
+
+def plane_table(last, plane_max):
+    last = np.ascontiguousarray(last, np.float32)
+    m = last.shape[0]
+    nrm = np.zeros((max(m, 1), 3), np.float32)
+    valid = np.zeros(max(m, 1), np.int32)
+    pick = np.zeros((max(m, 1), 5), np.int32)
+    gate = np.zeros(max(m, 1), np.int32)
+    if m:
+        lib().orc_plane_table(last.reshape(-1), m, plane_max, nrm.reshape(-1), valid,
+                              pick.reshape(-1), gate)
+    return nrm[:m], valid[:m], pick[:m], gate[:m]
+
+
+def transform_point(q, t, p):
+    out = np.zeros(3, np.float32)
+    lib().orc_transform_point(np.asarray(q, np.float64), np.asarray(t, np.float64),
+                              np.ascontiguousarray(p, np.float32), out)
+    return out
+
+
+def correspond(last, curr, q, t):
+    last = np.ascontiguousarray(last, np.float32)
+    curr = np.ascontiguousarray(curr, np.float32)
+    nn = np.zeros(max(curr.shape[0], 1), np.int32)
+    lib().orc_correspond(last.reshape(-1), last.shape[0], curr.reshape(-1), curr.shape[0],
+                         np.asarray(q, np.float64), np.asarray(t, np.float64), nn)
+    return nn[:curr.shape[0]]
+
+
+def solve(po, pa, nrm, mode=MODE_CERES_LM, max_iter=8, q_init=(0, 0, 0, 1), t_init=(0, 0, 0)):
+    po = np.ascontiguousarray(po, np.float32).reshape(-1)
+    pa = np.ascontiguousarray(pa, np.float32).reshape(-1)
+    nr = np.ascontiguousarray(nrm, np.float32).reshape(-1)
+    c = po.size // 3
+    q = np.zeros(4); t = np.zeros(3)
+    log = np.zeros(LOG_STRIDE * (max_iter + 2))
+    nl = C.c_int32(0)
+    lib().orc_solve(po if c else np.zeros(3, np.float32), pa if c else np.zeros(3, np.float32),
+                    nr if c else np.zeros(3, np.float32), c, mode, max_iter,
+                    np.asarray(q_init, np.float64), np.asarray(t_init, np.float64), q, t, log,
+                    C.byref(nl))
+    return q, t, log[:LOG_STRIDE * nl.value].reshape(-1, LOG_STRIDE)
+
+
+def register_pair(last, curr, plane_max, mode=MODE_CERES_LM, max_iter=8, q_init=(0, 0, 0, 1),
+                  t_init=(0, 0, 0)):
+    """frameRegistration(): -> (q_xyzw, t, log [iters,10], n_corr)"""
+    last = np.ascontiguousarray(last, np.float32)
+    curr = np.ascontiguousarray(curr, np.float32)
+    q = np.zeros(4); t = np.zeros(3)
+    log = np.zeros(LOG_STRIDE * (max_iter + 2))
+    nl = C.c_int32(0)
+    c = lib().orc_register_pair(last.reshape(-1) if last.size else np.zeros(4, np.float32),
+                                last.shape[0],
+                                curr.reshape(-1) if curr.size else np.zeros(4, np.float32),
+                                curr.shape[0], plane_max, mode, max_iter,
+                                np.asarray(q_init, np.float64), np.asarray(t_init, np.float64),
+                                q, t, log, C.byref(nl))
+    return q, t, log[:LOG_STRIDE * nl.value].reshape(-1, LOG_STRIDE), c
+
+
+def accumulate(q0l, t0l, qlc, tlc):
+    q = np.zeros(4); t = np.zeros(3)
+    lib().orc_accumulate(*(np.asarray(v, np.float64) for v in (q0l, t0l, qlc, tlc)), q, t)
+    return q, t
+
+
+# --------------------------------------------------------------------------- mask + Kabsch
+class LegacyRandomState:
+    """numpy RandomState (MT19937) restated in C: random_sample() stream."""
+
+    def __init__(self, seed):
+        class MT(C.Structure):
+            _fields_ = [("mt", C.c_uint32 * 624), ("pos", C.c_int32)]
+        self._st = MT()
+        L = lib()
+        L.orc_mt_seed.argtypes = [C.c_void_p, C.c_uint32]
+        L.orc_mt_random_sample.argtypes = [C.c_void_p]
+        L.orc_mt_random_sample.restype = C.c_double
+        L.orc_mt_seed(C.byref(self._st), seed)
+
+    def random_sample(self, n=None):
+        L = lib()
+        if n is None:
+            return L.orc_mt_random_sample(C.byref(self._st))
+        return np.array([L.orc_mt_random_sample(C.byref(self._st)) for _ in range(n)])
+
+
+def gmm_labels(X, draws):
+    """GaussianMixture(2).fit_predict restated -> (labels u8, info dict, means [2,6])"""
+    X = np.ascontiguousarray(X, np.float64)
+    n = X.shape[0]
+    lab = np.zeros(n, np.uint8)
+    info = np.zeros(8)
+    means = np.zeros(12)
+    rc = lib().orc_gmm_labels(X.reshape(-1), n, np.asarray(draws, np.float64), lab, info, means)
+    if rc != 0:
+        raise ValueError(f"oracle gmm failed rc={rc}")
+    keys = ["kmeans_iter", "em_iter", "converged", "center0", "center1", "bg_label", "n_bg",
+            "lower_bound"]
+    d = dict(zip(keys, info.tolist()))
+    return lab, d, means.reshape(2, 6)
+
+
+def kabsch(src, dst, mask=None, reflection=0):
+    src = np.ascontiguousarray(src, np.float64)
+    dst = np.ascontiguousarray(dst, np.float64)
+    R = np.zeros(9); t = np.zeros(3)
+    m = None
+    if mask is not None:
+        m = np.ascontiguousarray(mask, np.uint8)
+    rc = lib().orc_kabsch(src.reshape(-1), dst.reshape(-1), src.shape[0],
+                          m.ctypes.data if m is not None else None, reflection, R, t)
+    return rc, R.reshape(3, 3), t
+
+
+def quat_from_R(R):
+    q = np.zeros(4)
+    rc = lib().orc_quat_from_R(np.ascontiguousarray(R, np.float64).reshape(-1), q)
+    return rc, q
+
+
+def svd3(A):
+    U = np.zeros(9); S = np.zeros(3); Vt = np.zeros(9)
+    lib().orc_svd3(np.ascontiguousarray(A, np.float64).reshape(-1), U, S, Vt)
+    return U.reshape(3, 3), S, Vt.reshape(3, 3)
+
+
+def mask_and_pose(points, flow, draws):
+    """PointCloudOdometry_noSeg.py:97-125 restated: GMM mask, Kabsch(points+flow, points),
+    quaternion.  -> dict(labels, bg_mask, R, t, q_xyzw, info, rc)"""
+    X = np.concatenate([np.asarray(flow, np.float64), np.asarray(points, np.float64)], axis=1)
+    lab, info, means = gmm_labels(X, draws)
+    bg = (lab == int(info["bg_label"])).astype(np.uint8)
+    p = np.asarray(points, np.float64)
+    rc, R, t = kabsch(p + np.asarray(flow, np.float64), p, bg)
+    qrc, q = quat_from_R(R) if rc == 0 else (rc, np.zeros(4))
+    return dict(labels=lab, bg_mask=bg, R=R, t=t, q_xyzw=q, info=info, means=means,
+                rc=rc if rc != 0 else qrc)

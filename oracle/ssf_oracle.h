@@ -1,0 +1,107 @@
+/*
+ * ssf_oracle.h -- CPU restatement of the SSF-SLAM LiDAR front-end hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product path (ssf-slam_amd/) may link,
+ * load or call this library: it is the parity checker used by tests/, by
+ * __graft_entry__.smoke() and by bench.py's cpu_baseline leg.
+ *
+ * Parity status (see DESIGN.md "Oracle"):
+ *   - Python half (GMM mask, Kabsch, quaternion): PINNED.  Golden vectors in
+ *     tests/golden/ were produced by importing the reference's own
+ *     scripts/PointCloudOdometry_noSeg.py (ROS modules stubbed) and the sklearn
+ *     1.7.2 GaussianMixture it calls; tests/test_oracle_golden.py checks this
+ *     restatement against them.
+ *   - C++ half (frameFeature.cpp, lidarOdometry_onlyPC.cpp): PARITY UNPINNED
+ *     against the reference binary.  The reference needs ROS/PCL/Eigen/Ceres,
+ *     none of which exist in this image, so it cannot be built; it holds no
+ *     golden vectors or tests.  The restatement follows the source line by line
+ *     (citations per function) and is pinned only by hand-checkable
+ *     known-answer tests.
+ *
+ * Floating point: build with -O2 -ffp-contract=off (no FMA contraction), the
+ * same as the HIP kernels, so float stages are bit-comparable.
+ */
+#ifndef SSF_ORACLE_H
+#define SSF_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Parameter blocks selected by N_SCAN_ROW (src/frameFeature.cpp:141-152,
+ * src/lidarOdometry_onlyPC.cpp:313-319). */
+typedef struct {
+    int32_t n_rows;      /* 16 or 64                                   */
+    float plane_min;     /* curvature threshold, 0.05 / 0.005           */
+    int32_t plane_span;  /* greedy spacing, 3 / 25                      */
+    int32_t row_start;   /* rowIndexStart, 0 / 5                        */
+    int32_t row_end;     /* rowIndexEnd, 0 / 5                          */
+    float plane_max;     /* coplanarity gate, 0.15 / 0.05               */
+} orc_profile;
+
+int orc_profile_get(int32_t n_rows, orc_profile* out);
+
+/* ---- frameFeature (src/frameFeature.cpp:45-123) ---- */
+int32_t orc_ring_id(float x, float y, float z, int32_t n_rows);
+/* Stable per-ring partition.  pts has stride `stride` floats (xyz at 0..2).
+ * rxyzi: ring-ordered kept points (x,y,z,intensity) -- capacity n*4 floats.
+ * ring_off[n_rows+1]: exclusive prefix of per-ring counts.
+ * src_idx[kept]: input index of each ring-ordered point.
+ * ring_of_input[n]: ring id per input point (-1 = dropped).
+ * returns number of kept points. */
+int64_t orc_bin(const float* pts, int64_t n, int64_t stride, int32_t n_rows, float* rxyzi,
+                int64_t* ring_off, int64_t* src_idx, int32_t* ring_of_input);
+void orc_curvature(const float* rxyzi, const int64_t* ring_off, int32_t n_rows, int32_t row_start,
+                   int32_t row_end, float* curv);
+int64_t orc_select(const float* rxyzi, const float* curv, const int64_t* ring_off, int32_t n_rows,
+                   int32_t row_start, int32_t row_end, float plane_min, int32_t plane_span,
+                   float* plane_xyzi, int64_t* sel_idx);
+/* bin + curvature + select in one call; plane_xyzi capacity n*4 floats. */
+int64_t orc_extract_planes(const float* pts, int64_t n, int64_t stride, int32_t n_rows,
+                           float* plane_xyzi);
+
+/* ---- lidarOdometry_onlyPC (src/lidarOdometry_onlyPC.cpp:74-82,147-252) ---- */
+void orc_knn(const float* cloud_xyzi, int64_t m, const float q[3], int32_t k, int32_t* idx,
+             float* d2);
+void orc_plane_table(const float* last_xyzi, int64_t m, float plane_max, float* normal,
+                     int32_t* valid, int32_t* pick5, int32_t* gate_rank);
+void orc_transform_point(const double q[4], const double t[3], const float p[3], float out[3]);
+void orc_correspond(const float* last_xyzi, int64_t m_last, const float* curr_xyzi, int64_t m_curr,
+                    const double q[4], const double t[3], int32_t* nn);
+
+/* per-iteration log record: q(4,xyzw) t(3) cost accepted radius = 10 doubles */
+#define ORC_LOG_STRIDE 10
+enum { ORC_MODE_CERES_LM = 0, ORC_MODE_GN = 1 };
+int32_t orc_solve(const float* po, const float* pa, const float* nrm, int64_t c, int32_t mode,
+                  int32_t max_iter, const double q_init[4], const double t_init[3], double q_out[4],
+                  double t_out[3], double* log, int32_t* n_log);
+/* Full frameRegistration(): table + 1-NN + solve.  Returns number of correspondences used
+ * (-1 when the last frame has <= 10 points: pose returned unchanged). */
+int64_t orc_register_pair(const float* last_xyzi, int64_t m_last, const float* curr_xyzi,
+                          int64_t m_curr, float plane_max, int32_t mode, int32_t max_iter,
+                          const double q_init[4], const double t_init[3], double q_out[4],
+                          double t_out[3], double* log, int32_t* n_log);
+void orc_accumulate(const double q0l[4], const double t0l[3], const double qlc[4],
+                    const double tlc[3], double q0c[4], double t0c[3]);
+
+/* ---- PointCloudOdometry_noSeg.py mask + Kabsch ---- */
+typedef struct { uint32_t mt[624]; int32_t pos; } orc_mt19937;
+void orc_mt_seed(orc_mt19937* s, uint32_t seed);
+double orc_mt_random_sample(orc_mt19937* s);
+/* GMM(2) on X (n x 6, [flow, xyz]) with sklearn 1.7.2 semantics; draws[3] = the three
+ * RandomState doubles consumed by k-means++ (choice, uniform(2)).  labels[n] (0/1).
+ * info[8] = {kmeans_iter, em_iter, converged, center0, center1, bg_label, n_bg, lower_bound} */
+int32_t orc_gmm_labels(const double* X, int64_t n, const double draws[3], uint8_t* labels,
+                       double* info, double* means /* 12, nullable */);
+/* slove_RT_by_SVD(src, dst) over rows with mask[i] != 0 (mask nullable = all).
+ * reflection: 0 -> return -2 on det<0 (reference raises), 1 -> Vt[2]*=-1 fix.  R row-major. */
+int32_t orc_kabsch(const double* src, const double* dst, int64_t n, const uint8_t* mask,
+                   int32_t reflection, double R[9], double t[3]);
+/* pyquaternion Quaternion(matrix=R) trace method -> q (x,y,z,w); -3 if not orthogonal */
+int32_t orc_quat_from_R(const double R[9], double q[4]);
+void orc_svd3(const double A[9], double U[9], double S[3], double Vt[9]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,192 @@
+"""Seeded synthetic LiDAR sequences (SURVEY.md §8(d) "Synthetic scan generator").
+
+The reference's dataset (SUSCape CARLA npz: pos1, pos2, gt, s_fg_mask, ...) is not in the
+repository and there is no network, so scans are ray-cast here:
+
+* elevations at the bin centres of the reference's ring mapping (src/frameFeature.cpp:57-71):
+  64 rows -> 2 - k/3 (k = 0..32) and -8.83 - m/2 (m = 1..31); 16 rows -> -15 + 2k.  A
+  float32/float64 atan difference can therefore never move a point across a row edge;
+* azimuth-major emission order (all beams per azimuth step, like a spinning sensor);
+* world: ground plane z = -2.5, a street of box buildings, poles (vertical cylinders), a
+  100 m "sky dome" for rays that hit nothing, and moving cars (dynamic points, ~8 %);
+* ego motion ~1 m/frame with a small yaw rate; range noise sigma 0.01 m plus 1e-4 m jitter so
+  k-NN distances are tie-free;
+* flow = pos1 expressed in frame k+1 coordinates minus pos1 (Generate_Sceneflow.py
+  semantics); dynamic points include their object's motion.  s_fg_mask = 1 on movers.
+
+Everything is computed in float64 with torch (CPU or GPU) and returned as float32.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+SEED_BASE = 20240000
+
+
+def elevations_deg(n_rows: int) -> torch.Tensor:
+    if n_rows == 64:
+        e = [2.0 - k / 3.0 for k in range(33)] + [-8.83 - m / 2.0 for m in range(1, 32)]
+    elif n_rows == 16:
+        e = [-15.0 + 2.0 * k for k in range(16)]
+    else:
+        raise ValueError("n_rows must be 16 or 64")
+    return torch.tensor(e, dtype=torch.float64)
+
+
+def _gen(seed: int) -> torch.Generator:
+    g = torch.Generator()
+    g.manual_seed(seed)
+    return g
+
+
+class Scene:
+    """A static street world plus moving cars, deterministic in `seq`."""
+
+    def __init__(self, seq: int = 0, n_buildings: int = 48, n_poles: int = 40, n_cars: int = 6):
+        g = _gen(SEED_BASE + seq * 10000 + 9999)
+        u = lambda *s: torch.rand(*s, generator=g, dtype=torch.float64)
+        boxes = []
+        for side in (-1.0, 1.0):
+            x = -60.0
+            for _ in range(n_buildings // 2):
+                length = 8.0 + 14.0 * float(u(1))
+                gap = 1.0 + 5.0 * float(u(1))
+                depth = 6.0 + 10.0 * float(u(1))
+                y0 = side * (9.0 + 4.0 * float(u(1)))
+                h = 4.0 + 16.0 * float(u(1))
+                ylo, yhi = (y0, y0 + side * depth) if side > 0 else (y0 - depth, y0)
+                ylo, yhi = min(ylo, yhi), max(ylo, yhi)
+                boxes.append([x, ylo, -2.5, x + length, yhi, -2.5 + h])
+                x += length + gap
+        self.boxes = torch.tensor(boxes, dtype=torch.float64)
+        px = -50.0 + torch.arange(n_poles, dtype=torch.float64) * 16.0 + 3.0 * u(n_poles)
+        py = torch.where(torch.arange(n_poles) % 2 == 0, torch.tensor(6.5), torch.tensor(-6.5))
+        py = py.to(torch.float64) + 0.3 * u(n_poles)
+        self.poles = torch.stack([px, py, 0.15 + 0.1 * u(n_poles), torch.full((n_poles,), 3.5)], 1)
+        cars = []
+        for c in range(n_cars):
+            lane = [-3.0, 3.0, -1.5, 1.5][c % 4]
+            x0 = 5.0 + 25.0 * c + 10.0 * float(u(1))
+            vx = (1.6 + 0.8 * float(u(1))) * (1.0 if lane > 0 else -1.0)
+            cars.append([x0, lane, vx, 0.05 * (float(u(1)) - 0.5)])
+        self.cars = torch.tensor(cars, dtype=torch.float64)  # x0, y, vx, vy
+        self.car_half = torch.tensor([2.3, 0.95, 0.75], dtype=torch.float64)
+
+    def car_boxes(self, frame: int) -> torch.Tensor:
+        c = self.cars
+        cx = c[:, 0] + frame * c[:, 2]
+        cy = c[:, 1] + frame * c[:, 3]
+        cz = torch.full_like(cx, -2.5 + self.car_half[2].item())
+        lo = torch.stack([cx, cy, cz], 1) - self.car_half
+        hi = torch.stack([cx, cy, cz], 1) + self.car_half
+        return torch.cat([lo, hi], 1)
+
+
+def ego_pose(seq: int, frame: int, speed: float = 1.0, yaw_rate: float = 0.004):
+    """Sensor pose in the world: (R [3,3], p [3]) float64.  Constant speed, slow yaw."""
+    yaw0 = 0.002 * ((seq * 7919) % 11 - 5)
+    p = torch.zeros(3, dtype=torch.float64)
+    for k in range(frame):
+        yk = yaw0 + yaw_rate * k
+        p = p + speed * torch.tensor([math.cos(yk), math.sin(yk), 0.0], dtype=torch.float64)
+    y = yaw0 + yaw_rate * frame
+    c, s = math.cos(y), math.sin(y)
+    R = torch.tensor([[c, -s, 0.0], [s, c, 0.0], [0.0, 0.0, 1.0]], dtype=torch.float64)
+    return R, p
+
+
+def _ray_boxes(o, d, boxes):
+    """slab test: rays (o [3], d [n,3]) vs AABBs [b,6] -> t [n] (inf if no hit) and box id."""
+    inv = 1.0 / torch.where(d.abs() < 1e-12, torch.full_like(d, 1e-12), d)
+    lo = (boxes[None, :, 0:3] - o) * inv[:, None, :]
+    hi = (boxes[None, :, 3:6] - o) * inv[:, None, :]
+    tmin = torch.minimum(lo, hi).amax(2)
+    tmax = torch.maximum(lo, hi).amin(2)
+    hit = (tmax >= tmin) & (tmax > 0.5)
+    t = torch.where(hit, torch.where(tmin > 0.5, tmin, tmax), torch.full_like(tmin, math.inf))
+    tb, ib = t.min(1)
+    return tb, ib
+
+
+def _ray_poles(o, d, poles):
+    dx, dy = d[:, 0:1], d[:, 1:2]
+    ox = o[0] - poles[None, :, 0]
+    oy = o[1] - poles[None, :, 1]
+    a = dx * dx + dy * dy
+    b = 2.0 * (ox * dx + oy * dy)
+    c = ox * ox + oy * oy - poles[None, :, 2] ** 2
+    disc = b * b - 4 * a * c
+    sq = torch.sqrt(torch.clamp(disc, min=0.0))
+    t = (-b - sq) / (2 * a)
+    z = o[2] + t * d[:, 2:3]
+    ok = (disc > 0) & (t > 0.5) & (z > -2.5) & (z < -2.5 + poles[None, :, 3])
+    t = torch.where(ok, t, torch.full_like(t, math.inf))
+    return t.min(1).values
+
+
+def scan(seq: int, frame: int, n_rows: int = 64, n_az: int = 1875, device="cpu",
+         scene: Scene | None = None):
+    """One synthetic frame -> dict(pos1 [N,3] f32, flow [N,3] f32, s_fg_mask [N] u8).
+
+    N = n_rows * n_az exactly (every ray returns: rays that hit nothing land on a 100 m dome)."""
+    scene = scene or Scene(seq)
+    g = _gen(SEED_BASE + seq * 10000 + frame)
+    el = elevations_deg(n_rows) * (math.pi / 180.0)
+    az0 = 2 * math.pi * torch.rand(1, generator=g, dtype=torch.float64).item() / n_az
+    az = az0 + 2 * math.pi * torch.arange(n_az, dtype=torch.float64) / n_az
+    ce, se = torch.cos(el), torch.sin(el)
+    # azimuth-major: index = a * n_rows + r
+    ds = torch.stack([ce[None, :] * torch.cos(az)[:, None], ce[None, :] * torch.sin(az)[:, None],
+                      se[None, :].expand(n_az, n_rows)], 2).reshape(-1, 3)
+    noise_r = 0.01 * torch.randn(ds.shape[0], generator=g, dtype=torch.float64)
+    jitter = 1e-4 * (torch.rand(ds.shape[0], 3, generator=g, dtype=torch.float64) - 0.5)
+    ds = ds.to(device)
+    R, p = ego_pose(seq, frame)
+    R, p = R.to(device), p.to(device)
+    dw = ds @ R.T
+    n = dw.shape[0]
+    t = torch.full((n,), 100.0, dtype=torch.float64, device=device)
+    mover = torch.full((n,), -1, dtype=torch.long, device=device)
+    tg = torch.where(dw[:, 2] < -1e-9, (-2.5 - p[2]) / dw[:, 2], torch.full_like(t, math.inf))
+    t = torch.minimum(t, tg)
+    chunk = 1 << 16
+    boxes = scene.boxes.to(device)
+    cars = scene.car_boxes(frame).to(device)
+    poles = scene.poles.to(device)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        tb, _ = _ray_boxes(p, dw[s:e], boxes)
+        tp = _ray_poles(p, dw[s:e], poles)
+        tc, ic = _ray_boxes(p, dw[s:e], cars)
+        ts = torch.minimum(t[s:e], torch.minimum(tb, tp))
+        car_hit = tc < ts
+        t[s:e] = torch.where(car_hit, tc, ts)
+        mover[s:e] = torch.where(car_hit, ic, torch.full_like(ic, -1))
+    t = torch.clamp(t, max=100.0) + noise_r.to(device)
+    pos1 = ds * t[:, None] + jitter.to(device)
+    # flow: same physical point in frame k+1 coordinates (movers displaced by their velocity)
+    W = pos1 @ R.T + p
+    vel = torch.zeros_like(W)
+    car_v = torch.cat([scene.cars[:, 2:4], torch.zeros(scene.cars.shape[0], 1, dtype=torch.float64)], 1).to(device)
+    m = mover >= 0
+    vel[m] = car_v[mover[m]]
+    R2, p2 = ego_pose(seq, frame + 1)
+    R2, p2 = R2.to(device), p2.to(device)
+    pos2 = (W + vel - p2) @ R2
+    pos1f = pos1.to(torch.float32)
+    flow = (pos2 - pos1f.to(torch.float64)).to(torch.float32)
+    return dict(pos1=pos1f, flow=flow, s_fg_mask=m.to(torch.uint8))
+
+
+def relative_pose(seq: int, frame_last: int, frame_curr: int):
+    """Ground-truth T_last<-curr as (q_xyzw, t) float64 tuples (lidarOdometry q_last_curr)."""
+    Rl, pl = ego_pose(seq, frame_last)
+    Rc, pc = ego_pose(seq, frame_curr)
+    R = Rl.T @ Rc
+    t = Rl.T @ (pc - pl)
+    w = math.sqrt(max(0.0, 1.0 + R[0, 0] + R[1, 1] + R[2, 2])) / 2.0
+    q = (float((R[2, 1] - R[1, 2]) / (4 * w)), float((R[0, 2] - R[2, 0]) / (4 * w)),
+         float((R[1, 0] - R[0, 1]) / (4 * w)), w)
+    return q, tuple(float(v) for v in t)

@@ -1,0 +1,192 @@
+/*
+ * ssf_frontend.h -- C ABI of the MI355X (gfx950) SSF-SLAM LiDAR front-end.
+ *
+ * This is the drop-in boundary for the reference's hot path.  Every entry point names the
+ * reference interface it replaces (file:line under YQChen8/SSF-SLAM).  Plain pointers and
+ * sizes only: no C++ types, no exceptions, no torch types cross this boundary.
+ *
+ * Conventions
+ *   - Pointers prefixed d_ are DEVICE pointers (hipMalloc'd / torch CUDA tensors) owned by the
+ *     caller; pointers prefixed h_ are host pointers.  `stream` is a hipStream_t (NULL = the
+ *     default stream).  All work is enqueued on `stream`; nothing synchronises unless stated.
+ *   - A batch of F frames is stored back to back: frame f occupies points
+ *     [d_frame_off[f], d_frame_off[f+1]) of the point arrays (int64 offsets, device).  Per-frame
+ *     outputs that are point-shaped (plane clouds, ring-ordered clouds) use the SAME offsets:
+ *     frame f's plane points start at d_frame_off[f] and d_plane_count[f] of them are valid.
+ *   - Points are float32 x,y,z with a stride of `point_stride` floats (3 for the PointCloud2
+ *     point_step 12 layout published by PointCloudOdometry*.py:84-92, 4 or 8 for padded PCL
+ *     layouts).  Plane clouds are float32 x,y,z,intensity (16 B), intensity encoding
+ *     indexInRow + row/100 exactly as src/frameFeature.cpp:77.
+ *   - Poses are 7 doubles: q (x,y,z,w) then t (x,y,z) -- the para_q / para_t layout of
+ *     src/lidarOdometry_onlyPC.cpp:62-63.
+ *   - Return 0 on success, <0 on error; ssf_last_error() describes the last error of a context.
+ *     HIP errors are mapped to SSF_E_HIP.  One context per host thread/stream (calls on a
+ *     context are not thread-safe, different contexts are independent).
+ */
+#ifndef SSF_FRONTEND_H
+#define SSF_FRONTEND_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SSF_ABI_VERSION 1
+
+enum {
+    SSF_OK = 0,
+    SSF_E_ARG = -1,       /* bad argument / shape                                  */
+    SSF_E_HIP = -2,       /* HIP runtime error                                     */
+    SSF_E_NOMEM = -3,     /* device allocation failed                              */
+    SSF_E_CAPACITY = -4,  /* output capacity too small                             */
+    SSF_E_NODEV = -5      /* no gfx950 device                                      */
+};
+
+enum { SSF_SOLVER_CERES_LM = 0, SSF_SOLVER_GN = 1 };
+enum { SSF_MASK_GMM = 0, SSF_MASK_GT = 1, SSF_MASK_GIVEN = 2 };
+
+/* Runtime replacement of the compile-time N_SCAN_ROW parameter blocks
+ * (include/header.h:37-38, src/frameFeature.cpp:141-152, src/lidarOdometry_onlyPC.cpp:313-319). */
+typedef struct {
+    int32_t n_rows;       /* 16 or 64                                              */
+    float plane_min;      /* curvature threshold (planeMin)                        */
+    int32_t plane_span;   /* greedy spacing (planeSpan)                            */
+    int32_t row_start;    /* rowIndexStart                                         */
+    int32_t row_end;      /* rowIndexEnd                                           */
+    float plane_max;      /* coplanarity gate (planeMax)                           */
+    int32_t solver;       /* SSF_SOLVER_CERES_LM (reference) or SSF_SOLVER_GN      */
+    int32_t max_iter;     /* 8 (ceres::Solver::Options max_num_iterations) or 10   */
+} ssf_config;
+
+typedef struct ssf_ctx ssf_ctx;
+
+int32_t ssf_abi_version(void);
+/* Fill `out` with the reference's parameter block for n_rows (16 or 64). */
+int32_t ssf_config_default(int32_t n_rows, ssf_config* out);
+/* Create a context bound to HIP device `device`. */
+int32_t ssf_create(int32_t device, const ssf_config* cfg, ssf_ctx** out);
+void ssf_destroy(ssf_ctx* ctx);
+const char* ssf_last_error(const ssf_ctx* ctx);
+/* Pre-size device scratch so later calls never allocate (graph-capture friendly). */
+int32_t ssf_reserve(ssf_ctx* ctx, int32_t max_frames, int64_t max_points_per_frame);
+
+/* ---------------------------------------------------------------------------------------
+ * frameFeature: replaces cloudHandler() (src/frameFeature.cpp:35-139) -- ring binning
+ * (:45-81), 11-tap curvature (:84-107) and greedy planar selection (:110-123) -- for a batch
+ * of frames.  The VoxelGrid at :125-127 is dead work in the reference (its output is
+ * discarded) and is not performed.
+ *   d_pts           F frames of xyz (stride point_stride floats), offsets d_frame_off[F+1]
+ *   total_points    host copy of d_frame_off[F] (extent of every point-shaped array)
+ *   max_frame_points  host upper bound of points in any frame (grid sizing)
+ *   d_plane_xyzi    out, plane points x,y,z,intensity (16 B) at frame offsets
+ *   d_plane_count   out [F] int32, number of plane points per frame
+ *   d_ring_xyzi     out, nullable: ring-ordered kept points (x,y,z,intensity) at frame offsets
+ *   d_ring_off      out, nullable: [F*(n_rows+1)] int32 per-frame row offsets (frame relative)
+ *   d_curv          out, nullable: curvature per ring-ordered point (0 where not computed)
+ */
+int32_t ssf_extract_planes_batch(ssf_ctx* ctx, void* stream, int32_t n_frames,
+                                 const float* d_pts, int32_t point_stride,
+                                 const int64_t* d_frame_off, int64_t total_points,
+                                 int64_t max_frame_points,
+                                 float* d_plane_xyzi, int32_t* d_plane_count,
+                                 float* d_ring_xyzi, int32_t* d_ring_off, float* d_curv);
+/* Single-frame form with the SURVEY §8(b) signature: synchronises, returns the plane count in
+ * *h_out_m; SSF_E_CAPACITY if more than out_cap points were selected. */
+int32_t ssf_extract_planes(ssf_ctx* ctx, void* stream, const float* d_pts, int64_t n,
+                           int32_t point_step_bytes, int32_t xyz_offset_bytes,
+                           float* d_out_xyzi, int64_t* h_out_m, int64_t out_cap);
+
+/* ---------------------------------------------------------------------------------------
+ * Plane table for frames that will serve as the LAST frame of a registration pair: for every
+ * plane point a, the 30-NN ring-diverse 5-point pick, the 5x3 least-squares plane and the
+ * coplanarity gate of src/lidarOdometry_onlyPC.cpp:173-232 (which depend only on the last
+ * frame and a, so they are computed once per frame instead of once per correspondence x2).
+ *   d_normal  out float32 x3 per plane point (frame offsets), d_valid out uint8 per point.
+ */
+int32_t ssf_plane_table_batch(ssf_ctx* ctx, void* stream, int32_t n_frames,
+                              const float* d_plane_xyzi, const int64_t* d_frame_off,
+                              const int32_t* d_plane_count, int64_t max_plane_points,
+                              float* d_normal, uint8_t* d_valid);
+
+/* ---------------------------------------------------------------------------------------
+ * lidarOdometry_onlyPC: replaces frameRegistration() (src/lidarOdometry_onlyPC.cpp:147-252)
+ * plus the pose accumulation of publishResult() (:87-90) for P independent pairs.
+ *   last / curr      plane clouds (x,y,z,intensity) with their own offsets + counts
+ *   d_last_normal/valid  plane table of the last frames (ssf_plane_table_batch)
+ *   curr_total_points    host copy of d_curr_off[P] (correspondence scratch extent)
+ *   max_plane_points     host upper bound of plane points in any frame (grid sizing)
+ *   d_pose_rel [P*7] in: warm start q_last_curr/t_last_curr (the previous pair's solution,
+ *                    :164,251-252); out: the solution.  Last frames with <= 10 points leave
+ *                    it unchanged (:158).
+ *   d_pose_abs [P*7] nullable; in: q_0_last,t_0_last; out: q_0_curr,t_0_curr (:87-90).
+ *   d_log      nullable [P*max_iter*10] doubles per iteration: q(4) t(3) cost status radius
+ *   d_nlog     nullable [P] iterations logged;  d_ncorr nullable [P] correspondences used
+ *              (-1 when skipped);  d_nn nullable: per curr point 1-NN index into last.
+ */
+int32_t ssf_register_batch(ssf_ctx* ctx, void* stream, int32_t n_pairs,
+                           const float* d_last_xyzi, const int64_t* d_last_off,
+                           const int32_t* d_last_count, const float* d_last_normal,
+                           const uint8_t* d_last_valid, const float* d_curr_xyzi,
+                           const int64_t* d_curr_off, const int32_t* d_curr_count,
+                           int64_t curr_total_points, int64_t max_plane_points,
+                           double* d_pose_rel, double* d_pose_abs,
+                           double* d_log, int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_nn);
+
+/* ---------------------------------------------------------------------------------------
+ * PointCloudOdometry{,_noSeg}.py: replaces the dynamic-point mask + slove_RT_by_SVD + Quaternion
+ * block (scripts/PointCloudOdometry_noSeg.py:97-125, scripts/PointCloudOdometry.py:91-101 and the
+ * identical ASF block main_sju_occ_ros.py:256-284) for F frames.
+ *   d_pts / d_flow      packed float32 xyz (stride 3) per point: pos1 and the scene flow (gt).
+ *   h_frame_off [F+1]   host copy of the offsets (frame sizes drive the RandomState choice()).
+ *   mode SSF_MASK_GMM:  GaussianMixture(n_components=2).fit_predict([flow, xyz]) (sklearn 1.7.2
+ *                       semantics), background = most common label;  h_draws [F*3] (host,
+ *                       nullable) are the three numpy RandomState doubles its k-means++ init
+ *                       consumes per frame; NULL draws them from the context RNG (ssf_rng_seed).
+ *        SSF_MASK_GT:   background = d_mask_in == 0 (s_fg_mask, PointCloudOdometry.py:91).
+ *        SSF_MASK_GIVEN: background = d_mask_in != 0.
+ *   Kabsch on background rows: slove_RT_by_SVD(points + flow, points) (:114-118).
+ *   reflection 0: det<0 -> status SSF_POSE_REFLECTION (the reference raises TypeError at :33);
+ *              1: flip Vt[2] (the evident intent of :32-33).
+ *   d_bg_mask  out, nullable: uint8 per point, 1 = background.
+ *   d_out      out [F*SSF_POSE_OUT_STRIDE] doubles, see SSF_POSE_OUT_* below.
+ */
+#define SSF_POSE_OUT_STRIDE 32
+enum {
+    SSF_POSE_OUT_T = 0,        /* t (3)                  -- para_t_q[0:3]                    */
+    SSF_POSE_OUT_Q = 3,        /* q x,y,z,w (4)          -- para_t_q[3:7]                    */
+    SSF_POSE_OUT_R = 7,        /* R row-major (9)                                            */
+    SSF_POSE_OUT_STATUS = 16,  /* 0 ok, <0 SSF_POSE_* error                                  */
+    SSF_POSE_OUT_NBG = 17,     /* background point count                                     */
+    SSF_POSE_OUT_BGLABEL = 18, /* GMM label taken as background                              */
+    SSF_POSE_OUT_KM_ITER = 19, /* KMeans n_iter_                                             */
+    SSF_POSE_OUT_EM_ITER = 20, /* GaussianMixture n_iter_                                    */
+    SSF_POSE_OUT_CONVERGED = 21,
+    SSF_POSE_OUT_CENTER0 = 22, /* k-means++ chosen indices                                   */
+    SSF_POSE_OUT_CENTER1 = 23,
+    SSF_POSE_OUT_LOWER_BOUND = 24,
+    SSF_POSE_OUT_PASSES = 25   /* full passes over the frame's points (traffic accounting)   */
+};
+enum { SSF_POSE_EMPTY = -1, SSF_POSE_REFLECTION = -2, SSF_POSE_NOT_ORTHOGONAL = -3,
+       SSF_POSE_GMM_FAILED = -4 };
+int32_t ssf_mask_pose_batch(ssf_ctx* ctx, void* stream, int32_t n_frames, const float* d_pts,
+                            const float* d_flow, const int64_t* d_frame_off,
+                            const int64_t* h_frame_off, int32_t mode, const uint8_t* d_mask_in,
+                            const double* h_draws, int32_t reflection, uint8_t* d_bg_mask,
+                            double* d_out);
+/* Seed the context's numpy-legacy RandomState (MT19937) -- the `np.random.seed(s)` the reference
+ * never calls; every GMM frame then consumes 3 doubles in frame order, as the reference's global
+ * RandomState does across frames. */
+int32_t ssf_rng_seed(ssf_ctx* ctx, uint32_t seed);
+
+/* ---------------------------------------------------------------------------------------
+ * lidarOdometry.cpp (SSF path): frameRegistration() (src/lidarOdometry.cpp:145-159) ingests
+ * [t, q] and publishResult() (:80-83) accumulates.  Batched prefix product over a sequence of
+ * n relative poses (7 doubles each, q xyzw + t): d_abs[i] = d_abs[i-1] * d_rel[i], seeded with
+ * h_start (nullable = identity).  One device thread walks the chain (it is inherently serial).
+ */
+int32_t ssf_accumulate_sequence(ssf_ctx* ctx, void* stream, int32_t n, const double* d_rel,
+                                const double* h_start, double* d_abs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

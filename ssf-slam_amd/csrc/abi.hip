@@ -1,0 +1,356 @@
+// abi.hip -- extern "C" entry points of libssf_frontend.so (include/ssf_frontend.h).
+//
+// Host side of the boundary: argument checks, per-context device scratch (grown on demand,
+// never shrunk; ssf_reserve pre-sizes it), the numpy-legacy RandomState used by the GMM
+// k-means++ init, and kernel launches on the caller's stream.  No C++ exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "ssf_internal.hpp"
+
+using ssf::DevBuf;
+
+struct ssf_ctx {
+    int device = 0;
+    ssf_config cfg{};
+    std::string err;
+    // frameFeature scratch
+    DevBuf rid, hist, ring_off, ring_xyzi, sel, sel_cnt, plane1, off1, cnt1;
+    // registration scratch
+    DevBuf corr;
+    // mask scratch
+    DevBuf dist, labels, draws, start1;
+    // host RandomState (MT19937, numpy legacy seeding)
+    uint32_t mt[624];
+    int mt_pos = 625;
+    std::map<int64_t, std::vector<double>> cdf_cache;  // choice(n, p=1/n) cumulative table
+    double* h_draws = nullptr;        // pinned staging for the per-frame k-means++ draws
+    int64_t h_draws_cap = 0;
+    hipEvent_t draws_done = nullptr;  // guards reuse of the pinned staging buffer
+};
+
+namespace {
+
+int32_t fail(ssf_ctx* c, int32_t code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int32_t hip_fail(ssf_ctx* c, hipError_t e, const char* where) {
+    if (c) c->err = std::string(where) + ": " + hipGetErrorString(e);
+    return SSF_E_HIP;
+}
+
+#define SSF_TRY_HIP(ctx, expr, where)                              \
+    do {                                                           \
+        hipError_t _e = (expr);                                    \
+        if (_e != hipSuccess) return hip_fail((ctx), _e, (where)); \
+    } while (0)
+
+void mt_seed(ssf_ctx* c, uint32_t seed) {
+    c->mt[0] = seed;
+    for (int i = 1; i < 624; ++i) c->mt[i] = 1812433253u * (c->mt[i - 1] ^ (c->mt[i - 1] >> 30)) + (uint32_t)i;
+    c->mt_pos = 624;
+}
+
+uint32_t mt_next(ssf_ctx* c) {
+    if (c->mt_pos >= 624) {
+        if (c->mt_pos > 624) mt_seed(c, 5489u);
+        for (int i = 0; i < 624; ++i) {
+            uint32_t y = (c->mt[i] & 0x80000000u) | (c->mt[(i + 1) % 624] & 0x7fffffffu);
+            c->mt[i] = c->mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        c->mt_pos = 0;
+    }
+    uint32_t y = c->mt[c->mt_pos++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+double mt_random_sample(ssf_ctx* c) {
+    uint32_t a = mt_next(c) >> 5, b = mt_next(c) >> 6;
+    return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+}
+
+// numpy RandomState.choice(n, p=ones/n): cdf = cumsum(p); cdf /= cdf[-1];
+// searchsorted(cdf, u, side='right')  (sklearn _kmeans_plusplus first centre).
+int64_t choice_uniform(ssf_ctx* c, int64_t n, double u) {
+    auto it = c->cdf_cache.find(n);
+    if (it == c->cdf_cache.end()) {
+        if (c->cdf_cache.size() > 8) c->cdf_cache.clear();
+        std::vector<double> cdf((size_t)n);
+        const double p = 1.0 / (double)n;
+        double s = 0.0;
+        for (int64_t i = 0; i < n; ++i) { s += p; cdf[(size_t)i] = s; }
+        const double last = cdf[(size_t)n - 1];
+        for (auto& v : cdf) v /= last;
+        it = c->cdf_cache.emplace(n, std::move(cdf)).first;
+    }
+    const auto& cdf = it->second;
+    auto pos = std::upper_bound(cdf.begin(), cdf.end(), u);
+    int64_t idx = (int64_t)(pos - cdf.begin());
+    return idx < n ? idx : n - 1;
+}
+
+bool valid_cfg(const ssf_config& c) {
+    return (c.n_rows == 16 || c.n_rows == 64) && c.plane_span >= 1 && c.row_start >= 0 &&
+           c.row_end >= 0 && c.max_iter >= 0 && c.max_iter <= 64 &&
+           (c.solver == SSF_SOLVER_CERES_LM || c.solver == SSF_SOLVER_GN);
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t ssf_abi_version(void) { return SSF_ABI_VERSION; }
+
+int32_t ssf_config_default(int32_t n_rows, ssf_config* out) {
+    if (!out) return SSF_E_ARG;
+    std::memset(out, 0, sizeof(*out));
+    out->n_rows = n_rows;
+    out->solver = SSF_SOLVER_CERES_LM;
+    out->max_iter = 8;                          // lidarOdometry_onlyPC.cpp:246
+    if (n_rows == 16) {                         // frameFeature.cpp:143-146, onlyPC:314-316
+        out->plane_min = 0.05f; out->plane_span = 3; out->plane_max = 0.15f;
+        return SSF_OK;
+    }
+    if (n_rows == 64) {                         // frameFeature.cpp:147-152, onlyPC:317-319
+        out->plane_min = 0.005f; out->plane_span = 25; out->row_start = 5; out->row_end = 5;
+        out->plane_max = 0.05f;
+        return SSF_OK;
+    }
+    return SSF_E_ARG;
+}
+
+int32_t ssf_create(int32_t device, const ssf_config* cfg, ssf_ctx** out) {
+    if (!out || !cfg || !valid_cfg(*cfg)) return SSF_E_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return SSF_E_NODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SSF_E_NODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SSF_E_NODEV;
+    ssf_ctx* c = new (std::nothrow) ssf_ctx();
+    if (!c) return SSF_E_NOMEM;
+    c->device = device;
+    c->cfg = *cfg;
+    *out = c;
+    return SSF_OK;
+}
+
+void ssf_destroy(ssf_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    DevBuf* bufs[] = {&c->rid, &c->hist, &c->ring_off, &c->ring_xyzi, &c->sel, &c->sel_cnt,
+                      &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->dist, &c->labels, &c->draws, &c->start1};
+    for (DevBuf* b : bufs) b->release();
+    if (c->draws_done) { (void)hipEventSynchronize(c->draws_done); (void)hipEventDestroy(c->draws_done); }
+    if (c->h_draws) (void)hipHostFree(c->h_draws);
+    delete c;
+}
+
+const char* ssf_last_error(const ssf_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int32_t ssf_rng_seed(ssf_ctx* c, uint32_t seed) {
+    if (!c) return SSF_E_ARG;
+    mt_seed(c, seed);
+    return SSF_OK;
+}
+
+static int32_t ensure_features(ssf_ctx* c, int32_t n_frames, int64_t total, int64_t max_pts) {
+    const int R = c->cfg.n_rows;
+    const int64_t n_chunks = (max_pts + ssf::kBinChunk - 1) / ssf::kBinChunk;
+    SSF_TRY_HIP(c, c->rid.ensure((size_t)std::max<int64_t>(total, 1)), "alloc rid");
+    SSF_TRY_HIP(c, c->hist.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(n_frames * n_chunks * R, 1)), "alloc hist");
+    SSF_TRY_HIP(c, c->ring_off.ensure(sizeof(int32_t) * (size_t)n_frames * (R + 1)), "alloc ring_off");
+    SSF_TRY_HIP(c, c->ring_xyzi.ensure(sizeof(float4) * (size_t)std::max<int64_t>(total, 1)), "alloc ring_xyzi");
+    SSF_TRY_HIP(c, c->sel.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(total, 1)), "alloc sel");
+    SSF_TRY_HIP(c, c->sel_cnt.ensure(sizeof(int32_t) * (size_t)n_frames * R), "alloc sel_cnt");
+    return SSF_OK;
+}
+
+int32_t ssf_reserve(ssf_ctx* c, int32_t max_frames, int64_t max_points_per_frame) {
+    if (!c || max_frames < 0 || max_points_per_frame < 0) return SSF_E_ARG;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    const int64_t total = (int64_t)max_frames * max_points_per_frame;
+    int32_t rc = ensure_features(c, max_frames, total, max_points_per_frame);
+    if (rc) return rc;
+    SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(total, 1)), "alloc corr");
+    SSF_TRY_HIP(c, c->dist.ensure(sizeof(double) * (size_t)std::max<int64_t>(total, 1)), "alloc dist");
+    SSF_TRY_HIP(c, c->labels.ensure((size_t)std::max<int64_t>(total, 1)), "alloc labels");
+    SSF_TRY_HIP(c, c->draws.ensure(sizeof(double) * 3 * (size_t)std::max(max_frames, 1)), "alloc draws");
+    return SSF_OK;
+}
+
+int32_t ssf_extract_planes_batch(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_pts,
+                                 int32_t point_stride, const int64_t* d_frame_off,
+                                 int64_t total_points, int64_t max_frame_points,
+                                 float* d_plane_xyzi, int32_t* d_plane_count, float* d_ring_xyzi,
+                                 int32_t* d_ring_off, float* d_curv) {
+    if (!c) return SSF_E_ARG;
+    if (n_frames < 0 || point_stride < 3 || total_points < 0 || max_frame_points < 0 ||
+        (n_frames > 0 && (!d_pts || !d_frame_off || !d_plane_xyzi || !d_plane_count)))
+        return fail(c, SSF_E_ARG, "extract_planes_batch: bad arguments");
+    if (n_frames == 0) return SSF_OK;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    int32_t rc = ensure_features(c, n_frames, total_points, max_frame_points);
+    if (rc) return rc;
+    float4* ring = d_ring_xyzi ? reinterpret_cast<float4*>(d_ring_xyzi) : c->ring_xyzi.as<float4>();
+    int32_t* roff = d_ring_off ? d_ring_off : c->ring_off.as<int32_t>();
+    hipError_t e = ssf::launch_extract_planes(
+        (hipStream_t)stream, c->cfg, n_frames, d_pts, point_stride, d_frame_off, max_frame_points,
+        c->rid.as<int8_t>(), c->hist.as<int32_t>(), roff, ring, d_curv, c->sel.as<int32_t>(),
+        c->sel_cnt.as<int32_t>(), reinterpret_cast<float4*>(d_plane_xyzi), d_plane_count);
+    if (e != hipSuccess) return hip_fail(c, e, "extract_planes launch");
+    return SSF_OK;
+}
+
+int32_t ssf_extract_planes(ssf_ctx* c, void* stream, const float* d_pts, int64_t n,
+                           int32_t point_step_bytes, int32_t xyz_offset_bytes, float* d_out_xyzi,
+                           int64_t* h_out_m, int64_t out_cap) {
+    if (!c) return SSF_E_ARG;
+    if (n < 0 || !h_out_m || point_step_bytes < 12 || point_step_bytes % 4 || xyz_offset_bytes < 0 ||
+        xyz_offset_bytes % 4 || xyz_offset_bytes + 12 > point_step_bytes || (n > 0 && (!d_pts || !d_out_xyzi)))
+        return fail(c, SSF_E_ARG, "extract_planes: bad arguments");
+    *h_out_m = 0;
+    if (n == 0) return SSF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    SSF_TRY_HIP(c, c->off1.ensure(2 * sizeof(int64_t)), "alloc off1");
+    SSF_TRY_HIP(c, c->cnt1.ensure(sizeof(int32_t)), "alloc cnt1");
+    SSF_TRY_HIP(c, c->plane1.ensure(sizeof(float4) * (size_t)n), "alloc plane1");
+    const int64_t off[2] = {0, n};
+    SSF_TRY_HIP(c, hipMemcpyAsync(c->off1.p, off, sizeof(off), hipMemcpyHostToDevice, s), "H2D off");
+    const float* base = reinterpret_cast<const float*>(reinterpret_cast<const char*>(d_pts) + xyz_offset_bytes);
+    int32_t rc = ssf_extract_planes_batch(c, stream, 1, base, point_step_bytes / 4, c->off1.as<int64_t>(), n, n,
+                                          c->plane1.as<float>(), c->cnt1.as<int32_t>(), nullptr, nullptr, nullptr);
+    if (rc) return rc;
+    int32_t m = 0;
+    SSF_TRY_HIP(c, hipMemcpyAsync(&m, c->cnt1.p, sizeof(m), hipMemcpyDeviceToHost, s), "D2H count");
+    SSF_TRY_HIP(c, hipStreamSynchronize(s), "sync");
+    *h_out_m = m;
+    if (m > out_cap) return fail(c, SSF_E_CAPACITY, "extract_planes: " + std::to_string(m) + " plane points exceed out_cap");
+    if (m > 0)
+        SSF_TRY_HIP(c, hipMemcpyAsync(d_out_xyzi, c->plane1.p, sizeof(float4) * (size_t)m, hipMemcpyDeviceToDevice, s), "D2D planes");
+    return SSF_OK;
+}
+
+int32_t ssf_plane_table_batch(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_plane_xyzi,
+                              const int64_t* d_frame_off, const int32_t* d_plane_count,
+                              int64_t max_plane_points, float* d_normal, uint8_t* d_valid) {
+    if (!c) return SSF_E_ARG;
+    if (n_frames < 0 || max_plane_points < 0 ||
+        (n_frames > 0 && (!d_plane_xyzi || !d_frame_off || !d_plane_count || !d_normal || !d_valid)))
+        return fail(c, SSF_E_ARG, "plane_table_batch: bad arguments");
+    if (n_frames == 0) return SSF_OK;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    hipError_t e = ssf::launch_plane_table((hipStream_t)stream, c->cfg, n_frames,
+                                           reinterpret_cast<const float4*>(d_plane_xyzi), d_frame_off,
+                                           d_plane_count, max_plane_points, d_normal, d_valid);
+    if (e != hipSuccess) return hip_fail(c, e, "plane_table launch");
+    return SSF_OK;
+}
+
+int32_t ssf_register_batch(ssf_ctx* c, void* stream, int32_t n_pairs, const float* d_last_xyzi,
+                           const int64_t* d_last_off, const int32_t* d_last_count,
+                           const float* d_last_normal, const uint8_t* d_last_valid,
+                           const float* d_curr_xyzi, const int64_t* d_curr_off,
+                           const int32_t* d_curr_count, int64_t curr_total_points,
+                           int64_t max_plane_points, double* d_pose_rel, double* d_pose_abs,
+                           double* d_log, int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_nn) {
+    if (!c) return SSF_E_ARG;
+    if (n_pairs < 0 || curr_total_points < 0 || max_plane_points < 0 ||
+        (n_pairs > 0 && (!d_last_xyzi || !d_last_off || !d_last_count || !d_last_normal ||
+                         !d_last_valid || !d_curr_xyzi || !d_curr_off || !d_curr_count || !d_pose_rel)))
+        return fail(c, SSF_E_ARG, "register_batch: bad arguments");
+    if (n_pairs == 0) return SSF_OK;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(curr_total_points, 1)), "alloc corr");
+    hipError_t e = ssf::launch_register(
+        (hipStream_t)stream, c->cfg, n_pairs, reinterpret_cast<const float4*>(d_last_xyzi), d_last_off,
+        d_last_count, d_last_normal, d_last_valid, reinterpret_cast<const float4*>(d_curr_xyzi), d_curr_off,
+        d_curr_count, max_plane_points, c->corr.as<ssf::CorrRec>(), d_pose_rel, d_pose_abs, d_log,
+        d_nlog, d_ncorr, d_nn);
+    if (e != hipSuccess) return hip_fail(c, e, "register launch");
+    return SSF_OK;
+}
+
+int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_pts,
+                            const float* d_flow, const int64_t* d_frame_off,
+                            const int64_t* h_frame_off, int32_t mode, const uint8_t* d_mask_in,
+                            const double* h_draws, int32_t reflection, uint8_t* d_bg_mask,
+                            double* d_out) {
+    if (!c) return SSF_E_ARG;
+    if (n_frames < 0 || mode < SSF_MASK_GMM || mode > SSF_MASK_GIVEN ||
+        (n_frames > 0 && (!d_pts || !d_flow || !d_frame_off || !h_frame_off || !d_out)) ||
+        (mode != SSF_MASK_GMM && !d_mask_in))
+        return fail(c, SSF_E_ARG, "mask_pose_batch: bad arguments");
+    if (n_frames == 0) return SSF_OK;
+    const int64_t total = h_frame_off[n_frames];
+    for (int f = 0; f < n_frames; ++f)
+        if (h_frame_off[f + 1] < h_frame_off[f]) return fail(c, SSF_E_ARG, "mask_pose_batch: offsets not monotone");
+    hipStream_t s = (hipStream_t)stream;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    SSF_TRY_HIP(c, c->dist.ensure(sizeof(double) * (size_t)std::max<int64_t>(total, 1)), "alloc dist");
+    SSF_TRY_HIP(c, c->labels.ensure((size_t)std::max<int64_t>(total, 1)), "alloc labels");
+    SSF_TRY_HIP(c, c->draws.ensure(sizeof(double) * 3 * (size_t)n_frames), "alloc draws");
+    if (c->draws_done) SSF_TRY_HIP(c, hipEventSynchronize(c->draws_done), "draws event");
+    else SSF_TRY_HIP(c, hipEventCreateWithFlags(&c->draws_done, hipEventDisableTiming), "draws event");
+    if (c->h_draws_cap < 3 * (int64_t)n_frames) {
+        if (c->h_draws) SSF_TRY_HIP(c, hipHostFree(c->h_draws), "free pinned");
+        c->h_draws = nullptr; c->h_draws_cap = 0;
+        SSF_TRY_HIP(c, hipHostMalloc((void**)&c->h_draws, sizeof(double) * 3 * (size_t)n_frames), "pinned draws");
+        c->h_draws_cap = 3 * (int64_t)n_frames;
+    }
+    std::memset(c->h_draws, 0, sizeof(double) * 3 * (size_t)n_frames);
+    if (mode == SSF_MASK_GMM) {
+        for (int f = 0; f < n_frames; ++f) {
+            const int64_t nf = h_frame_off[f + 1] - h_frame_off[f];
+            double u0, u1, u2;
+            if (h_draws) { u0 = h_draws[3 * f]; u1 = h_draws[3 * f + 1]; u2 = h_draws[3 * f + 2]; }
+            else { u0 = mt_random_sample(c); u1 = mt_random_sample(c); u2 = mt_random_sample(c); }
+            c->h_draws[3 * f] = nf > 0 ? (double)choice_uniform(c, nf, u0) : 0.0;
+            c->h_draws[3 * f + 1] = u1;
+            c->h_draws[3 * f + 2] = u2;
+        }
+    }
+    SSF_TRY_HIP(c, hipMemcpyAsync(c->draws.p, c->h_draws, sizeof(double) * 3 * n_frames,
+                                  hipMemcpyHostToDevice, s), "H2D draws");
+    SSF_TRY_HIP(c, hipEventRecord(c->draws_done, s), "draws record");
+    hipError_t e = ssf::launch_mask_pose(s, n_frames, d_pts, d_flow, d_frame_off, mode, d_mask_in,
+                                         c->draws.as<double>(), reflection, d_bg_mask, d_out,
+                                         c->dist.as<double>(), c->labels.as<uint8_t>());
+    if (e != hipSuccess) return hip_fail(c, e, "mask_pose launch");
+    return SSF_OK;
+}
+
+int32_t ssf_accumulate_sequence(ssf_ctx* c, void* stream, int32_t n, const double* d_rel,
+                                const double* h_start, double* d_abs) {
+    if (!c) return SSF_E_ARG;
+    if (n < 0 || (n > 0 && (!d_rel || !d_abs))) return fail(c, SSF_E_ARG, "accumulate: bad arguments");
+    if (n == 0) return SSF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    const double* d_start = nullptr;
+    if (h_start) {
+        SSF_TRY_HIP(c, c->start1.ensure(sizeof(double) * 8), "alloc start");
+        SSF_TRY_HIP(c, hipMemcpyAsync(c->start1.p, h_start, sizeof(double) * 7, hipMemcpyHostToDevice, s), "H2D start");
+        d_start = c->start1.as<double>();
+    }
+    hipError_t e = ssf::launch_accumulate(s, n, d_rel, d_start, d_abs);
+    if (e != hipSuccess) return hip_fail(c, e, "accumulate launch");
+    if (h_start) SSF_TRY_HIP(c, hipStreamSynchronize(s), "sync start");
+    return SSF_OK;
+}
+
+}  // extern "C"

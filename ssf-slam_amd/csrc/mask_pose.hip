@@ -1,0 +1,692 @@
+// mask_pose.hip -- the dynamic-point mask + Kabsch pose block of
+// scripts/PointCloudOdometry_noSeg.py:97-125 (and PointCloudOdometry.py:91-101) on gfx950.
+//
+// One work-group owns one frame and runs the WHOLE GaussianMixture(n_components=2).fit_predict
+// on device (sklearn 1.7.2 semantics, f64 arithmetic on the f32 point / flow storage):
+//   pass 0      X = [flow, xyz]: column means and variances (KMeans centering, tol)
+//   k-means++   distances to the first centre (index chosen from the caller's RandomState
+//               draw), in-order chunked prefix scan -> the two local-trial candidates, potentials
+//   Lloyd       one streaming pass per iteration (labels, per-cluster sums, changed-label count)
+//   GMM init    one-hot responsibilities -> shifted first/second moments -> 6x6 Cholesky
+//   EM          ONE fused pass per iteration: E-step (weighted log-prob, logsumexp,
+//               responsibilities) and the M-step moment sums of the next parameters together
+//   final       argmax labels + per-label Kabsch sums (src = pos + flow, dst = pos) in one pass,
+//               background = majority label, 3x3 SVD (one-sided Jacobi, f64) on one lane,
+//               R, t, pyquaternion trace-method q; then one pass writes the uint8 mask.
+// The small dense algebra (Cholesky, SVD, convergence tests) runs on lane 0 between passes;
+// no host round trip for the whole fit.  Every pass is a coalesced stream of 24 B/point.
+#include "ssf_device.hpp"
+#include "ssf_internal.hpp"
+
+#include <float.h>
+
+namespace ssf {
+
+constexpr int kMaskThreads = 512;
+constexpr int kNW = kMaskThreads / 64;
+constexpr double kPi = 3.14159265358979323846;
+
+struct MaskShared {
+    double mean[6], tol;
+    double cen[12], csn[2];
+    double mu[12], U[72], logdet[2], logw[2];
+    double rand1, rand2, pot;
+    double lb, prev_lb;
+    double kab[32];
+    int64_t c0, cand[2], c1;
+    int64_t n1;
+    int km_iter, em_iter, strict, converged, done, status, passes, label0, bg;
+    double red_tmp[64];
+};
+
+SSF_DEV void load_x(const float* __restrict__ P, const float* __restrict__ Fl, int64_t i, double x[6]) {
+    x[0] = (double)Fl[3 * i]; x[1] = (double)Fl[3 * i + 1]; x[2] = (double)Fl[3 * i + 2];
+    x[3] = (double)P[3 * i];  x[4] = (double)P[3 * i + 1];  x[5] = (double)P[3 * i + 2];
+}
+
+// lane-0 helpers -----------------------------------------------------------------------------
+SSF_DEV int prec_chol6(const double C[36], double U[36], double* logdet) {
+    double L[36];
+    for (int k = 0; k < 36; ++k) L[k] = 0.0;
+    for (int j = 0; j < 6; ++j) {
+        double s = C[j * 6 + j];
+        for (int k = 0; k < j; ++k) s -= L[j * 6 + k] * L[j * 6 + k];
+        if (!(s > 0.0)) return -1;
+        L[j * 6 + j] = sqrt(s);
+        for (int i = j + 1; i < 6; ++i) {
+            double v = C[i * 6 + j];
+            for (int k = 0; k < j; ++k) v -= L[i * 6 + k] * L[j * 6 + k];
+            L[i * 6 + j] = v / L[j * 6 + j];
+        }
+    }
+    double Li[36];
+    for (int k = 0; k < 36; ++k) Li[k] = 0.0;
+    for (int c = 0; c < 6; ++c)
+        for (int i = c; i < 6; ++i) {
+            double v = (i == c) ? 1.0 : 0.0;
+            for (int k = c; k < i; ++k) v -= L[i * 6 + k] * Li[k * 6 + c];
+            Li[i * 6 + c] = v / L[i * 6 + i];
+        }
+    double ld = 0.0;
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) U[i * 6 + j] = Li[j * 6 + i];
+    for (int i = 0; i < 6; ++i) ld += log(U[i * 6 + i]);
+    *logdet = ld;
+    return 0;
+}
+
+// sklearn _estimate_gaussian_parameters from shifted moments: per component k the block
+// acc[k*28 + ...] = {sum r, S1[6] = sum r (x - s), S2[21] = sum r (x - s)(x - s)^T (packed)}.
+SSF_DEV int gmm_params(MaskShared& S, const double* acc, const double* shift, int init, int64_t n) {
+    const double eps10 = 10.0 * DBL_EPSILON;
+    double nk[2];
+    for (int k = 0; k < 2; ++k) {
+        const double* a = acc + 28 * k;
+        const double* s = shift + 6 * k;
+        nk[k] = a[0] + eps10;
+        double mu[6], d[6];
+        for (int i = 0; i < 6; ++i) {
+            mu[i] = (a[0] * s[i] + a[1 + i]) / nk[k];
+            d[i] = mu[i] - s[i];
+        }
+        double C[36];
+        int p = 0;
+        for (int i = 0; i < 6; ++i)
+            for (int j = i; j < 6; ++j, ++p) {
+                double v = a[7 + p] - a[1 + i] * d[j] - d[i] * a[1 + j] + a[0] * d[i] * d[j];
+                v = v / nk[k];
+                C[i * 6 + j] = v; C[j * 6 + i] = v;
+            }
+        for (int i = 0; i < 6; ++i) C[i * 6 + i] += 1e-6;
+        if (prec_chol6(C, S.U + 36 * k, &S.logdet[k]) != 0) return -1;
+        for (int i = 0; i < 6; ++i) S.mu[6 * k + i] = mu[i];
+    }
+    double w0, w1;
+    if (init) { w0 = nk[0] / (double)n; w1 = nk[1] / (double)n; }
+    else { const double s = nk[0] + nk[1]; w0 = nk[0] / s; w1 = nk[1] / s; }
+    S.logw[0] = log(w0); S.logw[1] = log(w1);
+    return 0;
+}
+
+// U is read straight from LDS on every use (volatile): keeping both 6x6 precision factors in
+// registers next to the 57 moment accumulators would overflow the 256-VGPR budget.
+SSF_DEV double wlp(const double x[6], const double* mu, const volatile double* U, double logdet,
+                   double logw) {
+    double lp = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        double y = 0.0;
+#pragma unroll
+        for (int i = 0; i <= j; ++i) y += (x[i] - mu[i]) * U[i * 6 + j];
+        lp += y * y;
+    }
+    return -0.5 * (6.0 * log(2.0 * kPi) + lp) + logdet + logw;
+}
+
+SSF_DEV double lse2(double a, double b) {  // scipy 1.15 logsumexp on two terms
+    const double mx = a > b ? a : b;
+    if (a == b) return log1p(0.0) + log(2.0) + mx;
+    const double mn = a > b ? b : a;
+    return log1p(exp(mn - mx)) + mx;
+}
+
+SSF_DEV void svd3(const double A[9], double U[9], double Sv[3], double Vt[9]) {
+    double a[3][3], v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) a[i][j] = A[i * 3 + j];
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                double al = 0, be = 0, ga = 0;
+                for (int i = 0; i < 3; ++i) { al += a[i][p] * a[i][p]; be += a[i][q] * a[i][q]; ga += a[i][p] * a[i][q]; }
+                if (fabs(ga) <= 1e-300) continue;
+                const double rel = fabs(ga) / sqrt(al * be);
+                if (rel > off) off = rel;
+                if (rel < 1e-17) continue;
+                const double zeta = (be - al) / (2.0 * ga);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+                for (int i = 0; i < 3; ++i) {
+                    double x = a[i][p], y = a[i][q];
+                    a[i][p] = c * x - s * y; a[i][q] = s * x + c * y;
+                    x = v[i][p]; y = v[i][q];
+                    v[i][p] = c * x - s * y; v[i][q] = s * x + c * y;
+                }
+            }
+        if (off < 1e-16) break;
+    }
+    double sv[3];
+    int ord[3] = {0, 1, 2};
+    for (int j = 0; j < 3; ++j) sv[j] = sqrt(a[0][j] * a[0][j] + a[1][j] * a[1][j] + a[2][j] * a[2][j]);
+    for (int i = 0; i < 3; ++i)
+        for (int j = i + 1; j < 3; ++j)
+            if (sv[ord[j]] > sv[ord[i]]) { int t = ord[i]; ord[i] = ord[j]; ord[j] = t; }
+    double u[3][3];
+    for (int k = 0; k < 3; ++k) {
+        const int j = ord[k];
+        Sv[k] = sv[j];
+        for (int i = 0; i < 3; ++i) {
+            u[i][k] = sv[j] > 0 ? a[i][j] / sv[j] : 0.0;
+            Vt[k * 3 + i] = v[i][j];
+        }
+    }
+    if (!(Sv[2] > 1e-12 * Sv[0])) {
+        u[0][2] = u[1][0] * u[2][1] - u[2][0] * u[1][1];
+        u[1][2] = u[2][0] * u[0][1] - u[0][0] * u[2][1];
+        u[2][2] = u[0][0] * u[1][1] - u[1][0] * u[0][1];
+        Vt[6] = Vt[1] * Vt[5] - Vt[2] * Vt[4];
+        Vt[7] = Vt[2] * Vt[3] - Vt[0] * Vt[5];
+        Vt[8] = Vt[0] * Vt[4] - Vt[1] * Vt[3];
+    }
+    for (int i = 0; i < 3; ++i) for (int k = 0; k < 3; ++k) U[i * 3 + k] = u[i][k];
+}
+
+// Kabsch from shifted sums k[16] = {cnt, sum(s-cs)[3], sum(d-cd)[3], sum (s-cs)(d-cd)^T [9]}.
+SSF_DEV int kabsch_finish(const double* k, const double cs[3], const double cd[3], int reflection,
+                          double* out) {
+    const double n = k[0];
+    if (!(n > 0.0)) return SSF_POSE_EMPTY;
+    double es[3], ed[3], ms[3], md[3];
+    for (int i = 0; i < 3; ++i) {
+        es[i] = k[1 + i] / n; ed[i] = k[4 + i] / n;
+        ms[i] = cs[i] + es[i]; md[i] = cd[i] + ed[i];
+    }
+    double H[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) H[r * 3 + c] = k[7 + r * 3 + c] - n * es[r] * ed[c];
+    double U[9], Sv[3], Vt[9], R[9];
+    svd3(H, U, Sv, Vt);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            double s = 0.0;
+            for (int j = 0; j < 3; ++j) s += Vt[j * 3 + r] * U[c * 3 + j];
+            R[r * 3 + c] = s;
+        }
+    const double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
+                       R[2] * (R[3] * R[7] - R[4] * R[6]);
+    int status = 0;
+    if (det < 0) {
+        if (!reflection) status = SSF_POSE_REFLECTION;
+        for (int j = 0; j < 3; ++j) Vt[6 + j] *= -1.0;
+        if (reflection)
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) {
+                    double s = 0.0;
+                    for (int j = 0; j < 3; ++j) s += Vt[j * 3 + r] * U[c * 3 + j];
+                    R[r * 3 + c] = s;
+                }
+    }
+    double t[3];
+    for (int r = 0; r < 3; ++r) t[r] = -(R[r * 3] * ms[0] + R[r * 3 + 1] * ms[1] + R[r * 3 + 2] * ms[2]) + md[r];
+    // pyquaternion Quaternion(matrix=R): orthogonality check, trace method on m = R^T
+    bool orth = true;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double s = 0.0;
+            for (int kk = 0; kk < 3; ++kk) s += R[i * 3 + kk] * R[j * 3 + kk];
+            const double e = (i == j) ? 1.0 : 0.0;
+            if (!(fabs(s - e) <= 1e-8 + 1e-5 * fabs(e))) orth = false;
+        }
+    double q[4] = {0, 0, 0, 0};
+    if (orth) {
+        double m[3][3];
+        for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) m[i][j] = R[j * 3 + i];
+        double tt, w, x, y, z;
+        if (m[2][2] < 0) {
+            if (m[0][0] > m[1][1]) {
+                tt = 1 + m[0][0] - m[1][1] - m[2][2];
+                w = m[1][2] - m[2][1]; x = tt; y = m[0][1] + m[1][0]; z = m[2][0] + m[0][2];
+            } else {
+                tt = 1 - m[0][0] + m[1][1] - m[2][2];
+                w = m[2][0] - m[0][2]; x = m[0][1] + m[1][0]; y = tt; z = m[1][2] + m[2][1];
+            }
+        } else {
+            if (m[0][0] < -m[1][1]) {
+                tt = 1 - m[0][0] - m[1][1] + m[2][2];
+                w = m[0][1] - m[1][0]; x = m[2][0] + m[0][2]; y = m[1][2] + m[2][1]; z = tt;
+            } else {
+                tt = 1 + m[0][0] + m[1][1] + m[2][2];
+                w = tt; x = m[1][2] - m[2][1]; y = m[2][0] - m[0][2]; z = m[0][1] - m[1][0];
+            }
+        }
+        const double f = 0.5 / sqrt(tt);
+        q[0] = x * f; q[1] = y * f; q[2] = z * f; q[3] = w * f;
+    } else if (status == 0) {
+        status = SSF_POSE_NOT_ORTHOGONAL;
+    }
+    for (int i = 0; i < 3; ++i) out[SSF_POSE_OUT_T + i] = t[i];
+    for (int i = 0; i < 4; ++i) out[SSF_POSE_OUT_Q + i] = q[i];
+    for (int i = 0; i < 9; ++i) out[SSF_POSE_OUT_R + i] = R[i];
+    out[SSF_POSE_OUT_NBG] = n;
+    return status;
+}
+
+SSF_DEV void accum_kabsch(double (&k)[16], const double x[6], const double cs[3], const double cd[3]) {
+    double s[3], d[3];
+    for (int i = 0; i < 3; ++i) { d[i] = x[3 + i] - cd[i]; s[i] = (x[3 + i] + x[i]) - cs[i]; }
+    k[0] += 1.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { k[1 + i] += s[i]; k[4 + i] += d[i]; }
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) k[7 + r * 3 + c] += s[r] * d[c];
+}
+
+__global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
+    const float* __restrict__ pts, const float* __restrict__ flow,
+    const int64_t* __restrict__ frame_off, int mode, const uint8_t* __restrict__ mask_in,
+    const double* __restrict__ draws, int reflection, uint8_t* __restrict__ bg_mask,
+    double* __restrict__ out_all, double* __restrict__ dist, uint8_t* __restrict__ lab) {
+    __shared__ MaskShared S;
+    __shared__ double red[kNW * 60];
+    __shared__ int ired[kNW];
+    __shared__ int64_t cand_lds[2];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int64_t fb = frame_off[f], n = frame_off[f + 1] - fb;
+    const float* P = pts + 3 * fb;
+    const float* Fl = flow + 3 * fb;
+    double* D = dist + fb;
+    uint8_t* Lb = lab + fb;
+    double* out = out_all + (int64_t)f * SSF_POSE_OUT_STRIDE;
+    if (tid == 0) { S.passes = 0; S.status = 0; S.km_iter = 0; S.em_iter = 0; S.converged = 0; }
+    __syncthreads();
+
+    if (mode != SSF_MASK_GMM) {
+        // background from the given / ground-truth mask; Kabsch sums shifted by point 0
+        double cs[3] = {0, 0, 0}, cd[3] = {0, 0, 0};
+        if (n > 0) {
+            double x0[6];
+            load_x(P, Fl, 0, x0);
+            for (int i = 0; i < 3; ++i) { cd[i] = x0[3 + i]; cs[i] = x0[3 + i] + x0[i]; }
+        }
+        double k[16];
+        for (int i = 0; i < 16; ++i) k[i] = 0.0;
+        for (int64_t i = tid; i < n; i += blockDim.x) {
+            const uint8_t mv = mask_in[fb + i];
+            const bool bg = (mode == SSF_MASK_GT) ? (mv == 0) : (mv != 0);
+            if (bg_mask) bg_mask[fb + i] = bg ? 1 : 0;
+            if (!bg) continue;
+            double x[6];
+            load_x(P, Fl, i, x);
+            accum_kabsch(k, x, cs, cd);
+        }
+        block_sum<16>(k, red);
+        if (tid == 0) {
+            for (int i = 0; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
+            const int st = kabsch_finish(k, cs, cd, reflection, out);
+            out[SSF_POSE_OUT_STATUS] = st;
+            out[SSF_POSE_OUT_BGLABEL] = -1;
+            out[SSF_POSE_OUT_PASSES] = 1;
+        }
+        return;
+    }
+
+    if (n < 2) {
+        if (tid == 0) {
+            for (int i = 0; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
+            out[SSF_POSE_OUT_STATUS] = SSF_POSE_GMM_FAILED;
+        }
+        return;
+    }
+
+    // ---- pass 0: column means / variances (shift by point 0 for accuracy)
+    {
+        double x0[6];
+        load_x(P, Fl, 0, x0);
+        double a[12];
+        for (int i = 0; i < 12; ++i) a[i] = 0.0;
+        for (int64_t i = tid; i < n; i += blockDim.x) {
+            double x[6];
+            load_x(P, Fl, i, x);
+#pragma unroll
+            for (int d = 0; d < 6; ++d) { const double v = x[d] - x0[d]; a[d] += v; a[6 + d] += v * v; }
+        }
+        block_sum<12>(a, red);
+        if (tid == 0) {
+            double tol = 0.0;
+            for (int d = 0; d < 6; ++d) {
+                const double m = a[d] / (double)n;
+                S.mean[d] = x0[d] + m;
+                tol += a[6 + d] / (double)n - m * m;
+            }
+            S.tol = tol / 6.0 * 1e-4;
+            S.c0 = (int64_t)draws[3 * f];
+            if (S.c0 < 0) S.c0 = 0;
+            if (S.c0 >= n) S.c0 = n - 1;
+            S.passes = 1;
+        }
+        __syncthreads();
+    }
+    double mean[6];
+#pragma unroll
+    for (int d = 0; d < 6; ++d) mean[d] = S.mean[d];
+
+    // ---- k-means++ (sklearn _kmeans_plusplus, n_local_trials = 2)
+    {
+        double c0[6], cn0 = 0.0;
+        {
+            double x[6];
+            load_x(P, Fl, S.c0, x);
+            for (int d = 0; d < 6; ++d) { c0[d] = x[d] - mean[d]; cn0 += c0[d] * c0[d]; }
+        }
+        double pot = 0.0;
+        for (int64_t i = tid; i < n; i += blockDim.x) {
+            double x[6], dt = 0.0, xs = 0.0;
+            load_x(P, Fl, i, x);
+#pragma unroll
+            for (int d = 0; d < 6; ++d) { const double v = x[d] - mean[d]; dt += c0[d] * v; xs += v * v; }
+            double v = (-2.0 * dt + cn0) + xs;
+            v = v > 0.0 ? v : 0.0;
+            D[i] = v;
+            pot += v;
+        }
+        pot = block_sum_scalar<double>(pot, red);
+        if (tid == 0) {
+            S.rand1 = draws[3 * f + 1] * pot;
+            S.rand2 = draws[3 * f + 2] * pot;
+            cand_lds[0] = n; cand_lds[1] = n;
+            S.passes += 1;
+        }
+        __syncthreads();
+        // in-order inclusive scan of D in chunks of blockDim; first index with cumsum >= rand
+        const double r1 = S.rand1, r2 = S.rand2;
+        double carry = 0.0;
+        const int w = tid >> 6;
+        for (int64_t c = 0; c < n; c += blockDim.x) {
+            const int64_t i = c + tid;
+            double v = i < n ? D[i] : 0.0;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const double y = __shfl_up(v, o, 64);
+                if (lane_id() >= o) v += y;
+            }
+            if (lane_id() == 63) red[w] = v;
+            __syncthreads();
+            double pre = carry;
+            for (int k = 0; k < w; ++k) pre += red[k];
+            const double incl = pre + v;
+            double tot = carry;
+            for (int k = 0; k < kNW; ++k) tot += red[k];
+            if (i < n) {
+                if (incl >= r1) atomicMin((unsigned long long*)&cand_lds[0], (unsigned long long)i);
+                if (incl >= r2) atomicMin((unsigned long long*)&cand_lds[1], (unsigned long long)i);
+            }
+            __syncthreads();
+            carry = tot;
+            if (cand_lds[0] < n && cand_lds[1] < n) break;  // uniform (read after barrier)
+        }
+        __syncthreads();
+        int64_t cand[2] = {cand_lds[0] < n ? cand_lds[0] : n - 1, cand_lds[1] < n ? cand_lds[1] : n - 1};
+        double cc[2][6], ccn[2] = {0.0, 0.0};
+        for (int j = 0; j < 2; ++j) {
+            double x[6];
+            load_x(P, Fl, cand[j], x);
+            for (int d = 0; d < 6; ++d) { cc[j][d] = x[d] - mean[d]; ccn[j] += cc[j][d] * cc[j][d]; }
+        }
+        double cp[2] = {0.0, 0.0};
+        for (int64_t i = tid; i < n; i += blockDim.x) {
+            double x[6], xs = 0.0, dt0 = 0.0, dt1 = 0.0;
+            load_x(P, Fl, i, x);
+#pragma unroll
+            for (int d = 0; d < 6; ++d) {
+                const double v = x[d] - mean[d];
+                xs += v * v; dt0 += cc[0][d] * v; dt1 += cc[1][d] * v;
+            }
+            double v0 = (-2.0 * dt0 + ccn[0]) + xs, v1 = (-2.0 * dt1 + ccn[1]) + xs;
+            v0 = v0 > 0.0 ? v0 : 0.0; v1 = v1 > 0.0 ? v1 : 0.0;
+            const double di = D[i];
+            cp[0] += v0 < di ? v0 : di;
+            cp[1] += v1 < di ? v1 : di;
+        }
+        block_sum<2>(cp, red);
+        if (tid == 0) {
+            const int best = cp[1] < cp[0] ? 1 : 0;
+            S.c1 = cand[best];
+            for (int d = 0; d < 6; ++d) { S.cen[d] = c0[d]; S.cen[6 + d] = cc[best][d]; }
+            S.passes += 2;
+        }
+        __syncthreads();
+    }
+
+    // ---- Lloyd iterations (_kmeans_single_lloyd, max_iter 300)
+    if (tid == 0) { S.strict = 0; S.done = 0; }
+    for (int it = 0; it < 300; ++it) {
+        if (tid == 0) {
+            for (int k = 0; k < 2; ++k) {
+                double s = 0.0;
+                for (int d = 0; d < 6; ++d) s += S.cen[6 * k + d] * S.cen[6 * k + d];
+                S.csn[k] = s;
+            }
+        }
+        __syncthreads();
+        double cen[12], csn0 = S.csn[0], csn1 = S.csn[1];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) cen[k] = S.cen[k];
+        double acc[14];
+#pragma unroll
+        for (int k = 0; k < 14; ++k) acc[k] = 0.0;
+        int changed = 0;
+        for (int64_t i = tid; i < n; i += blockDim.x) {
+            double x[6], v[6], dt0 = 0.0, dt1 = 0.0;
+            load_x(P, Fl, i, x);
+#pragma unroll
+            for (int d = 0; d < 6; ++d) {
+                v[d] = x[d] - mean[d];
+                dt0 += v[d] * cen[d]; dt1 += v[d] * cen[6 + d];
+            }
+            const double e0 = -2.0 * dt0 + csn0, e1 = -2.0 * dt1 + csn1;
+            const int l = e1 < e0 ? 1 : 0;
+            changed += (Lb[i] != (uint8_t)l) || it == 0;
+            Lb[i] = (uint8_t)l;
+            if (l == 0) {
+                acc[0] += 1.0;
+#pragma unroll
+                for (int d = 0; d < 6; ++d) acc[1 + d] += v[d];
+            } else {
+                acc[7] += 1.0;
+#pragma unroll
+                for (int d = 0; d < 6; ++d) acc[8 + d] += v[d];
+            }
+        }
+        block_sum<14>(acc, red);
+        changed = block_sum_scalar<int>(changed, ired);
+        if (tid == 0) {
+            S.passes += 1;
+            S.km_iter = it + 1;
+            double shift = 0.0;
+            for (int k = 0; k < 2; ++k) {
+                const double wgt = acc[7 * k];
+                double sh = 0.0;
+                for (int d = 0; d < 6; ++d) {
+                    const double nc = wgt > 0.0 ? acc[7 * k + 1 + d] * (1.0 / wgt) : S.cen[6 * k + d];
+                    const double df = nc - S.cen[6 * k + d];
+                    sh += df * df;
+                    S.cen[6 * k + d] = nc;
+                }
+                sh = sqrt(sh);
+                shift += sh * sh;
+            }
+            if (changed == 0) { S.strict = 1; S.done = 1; }
+            else if (shift <= S.tol) S.done = 1;
+        }
+        __syncthreads();
+        if (S.done) break;
+    }
+
+    // ---- GMM init from one-hot k-means labels (relabel first if not strictly converged)
+    {
+        const int strict = S.strict;
+        double cen[12], csn0 = 0.0, csn1 = 0.0, sh[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) cen[k] = S.cen[k];
+        for (int d = 0; d < 6; ++d) { csn0 += cen[d] * cen[d]; csn1 += cen[6 + d] * cen[6 + d]; }
+        for (int k = 0; k < 2; ++k) for (int d = 0; d < 6; ++d) sh[6 * k + d] = cen[6 * k + d] + mean[d];
+        double acc[56];
+#pragma unroll
+        for (int k = 0; k < 56; ++k) acc[k] = 0.0;
+        for (int64_t i = tid; i < n; i += blockDim.x) {
+            double x[6];
+            load_x(P, Fl, i, x);
+            int l;
+            if (strict) {
+                l = Lb[i];
+            } else {
+                double dt0 = 0.0, dt1 = 0.0;
+#pragma unroll
+                for (int d = 0; d < 6; ++d) { const double v = x[d] - mean[d]; dt0 += v * cen[d]; dt1 += v * cen[6 + d]; }
+                l = (-2.0 * dt1 + csn1) < (-2.0 * dt0 + csn0) ? 1 : 0;
+            }
+            double v[6];
+            const int o = l ? 28 : 0;
+            const double* s = l ? sh + 6 : sh;
+#pragma unroll
+            for (int d = 0; d < 6; ++d) v[d] = x[d] - s[d];
+            if (l == 0) {
+                acc[0] += 1.0;
+                int p = 0;
+#pragma unroll
+                for (int a = 0; a < 6; ++a) {
+                    acc[1 + a] += v[a];
+#pragma unroll
+                    for (int b = a; b < 6; ++b, ++p) acc[7 + p] += v[a] * v[b];
+                }
+            } else {
+                acc[28] += 1.0;
+                int p = 0;
+#pragma unroll
+                for (int a = 0; a < 6; ++a) {
+                    acc[29 + a] += v[a];
+#pragma unroll
+                    for (int b = a; b < 6; ++b, ++p) acc[35 + p] += v[a] * v[b];
+                }
+            }
+            (void)o;
+        }
+        block_sum<56>(acc, red);
+        if (tid == 0) {
+            S.passes += 1;
+            if (gmm_params(S, acc, sh, 1, n) != 0) S.status = SSF_POSE_GMM_FAILED;
+            S.lb = -__builtin_inf();
+            S.done = 0;
+        }
+        __syncthreads();
+    }
+
+    // ---- EM: fused E-step + next M-step moments, one pass per iteration
+    for (int it = 1; it <= 100 && S.status == 0; ++it) {
+        double mu[12];
+        const double ld0 = S.logdet[0], lw0 = S.logw[0], ld1 = S.logdet[1], lw1 = S.logw[1];
+        const volatile double* U = S.U;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) mu[k] = S.mu[k];
+        double acc[57];
+#pragma unroll
+        for (int k = 0; k < 57; ++k) acc[k] = 0.0;
+        for (int64_t i = tid; i < n; i += blockDim.x) {
+            double x[6];
+            load_x(P, Fl, i, x);
+            const double a0 = wlp(x, mu, U, ld0, lw0);
+            const double a1 = wlp(x, mu + 6, U + 36, ld1, lw1);
+            const double l = lse2(a0, a1);
+            acc[56] += l;
+            const double r[2] = {exp(a0 - l), exp(a1 - l)};
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                double v[6];
+#pragma unroll
+                for (int d = 0; d < 6; ++d) v[d] = x[d] - mu[6 * k + d];
+                double* A = acc + 28 * k;
+                A[0] += r[k];
+                int p = 0;
+#pragma unroll
+                for (int a = 0; a < 6; ++a) {
+                    const double rv = r[k] * v[a];
+                    A[1 + a] += rv;
+#pragma unroll
+                    for (int b = a; b < 6; ++b, ++p) A[7 + p] += rv * v[b];
+                }
+            }
+        }
+        block_sum<57>(acc, red);
+        if (tid == 0) {
+            S.passes += 1;
+            S.em_iter = it;
+            const double prev = S.lb;
+            S.lb = acc[56] / (double)n;
+            double shift[12];
+            for (int k = 0; k < 12; ++k) shift[k] = S.mu[k];
+            if (gmm_params(S, acc, shift, 0, n) != 0) S.status = SSF_POSE_GMM_FAILED;
+            if (fabs(S.lb - prev) < 1e-3) { S.converged = 1; S.done = 1; }
+        }
+        __syncthreads();
+        if (S.done) break;
+    }
+
+    // ---- final E-step labels + per-label Kabsch sums
+    {
+        double mu[12];
+        const double ld0 = S.logdet[0], lw0 = S.logw[0], ld1 = S.logdet[1], lw1 = S.logw[1];
+        const volatile double* U = S.U;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) mu[k] = S.mu[k];
+        double cs[6], cd[6];
+        for (int k = 0; k < 2; ++k)
+            for (int i = 0; i < 3; ++i) { cd[3 * k + i] = mu[6 * k + 3 + i]; cs[3 * k + i] = mu[6 * k + 3 + i] + mu[6 * k + i]; }
+        double k0[16], k1[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { k0[i] = 0.0; k1[i] = 0.0; }
+        for (int64_t i = tid; i < n; i += blockDim.x) {
+            double x[6];
+            load_x(P, Fl, i, x);
+            const double a0 = wlp(x, mu, U, ld0, lw0);
+            const double a1 = wlp(x, mu + 6, U + 36, ld1, lw1);
+            const int l = a1 > a0 ? 1 : 0;
+            Lb[i] = (uint8_t)l;
+            if (i == 0) S.label0 = l;
+            if (l) accum_kabsch(k1, x, cs + 3, cd + 3);
+            else accum_kabsch(k0, x, cs, cd);
+        }
+        block_sum<16>(k0, red);
+        block_sum<16>(k1, red);
+        if (tid == 0) {
+            S.passes += 1;
+            for (int i = 0; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
+            const double n1 = k1[0];
+            int bg;
+            if (n1 * 2.0 > (double)n) bg = 1;
+            else if (n1 * 2.0 < (double)n) bg = 0;
+            else bg = S.label0;                     // Counter.most_common tie -> first seen
+            S.bg = bg;
+            int st = S.status;
+            if (st == 0) st = kabsch_finish(bg ? k1 : k0, bg ? cs + 3 : cs, bg ? cd + 3 : cd, reflection, out);
+            out[SSF_POSE_OUT_STATUS] = st;
+            out[SSF_POSE_OUT_BGLABEL] = bg;
+            out[SSF_POSE_OUT_NBG] = bg ? k1[0] : k0[0];
+            out[SSF_POSE_OUT_KM_ITER] = S.km_iter;
+            out[SSF_POSE_OUT_EM_ITER] = S.em_iter;
+            out[SSF_POSE_OUT_CONVERGED] = S.converged;
+            out[SSF_POSE_OUT_CENTER0] = (double)S.c0;
+            out[SSF_POSE_OUT_CENTER1] = (double)S.c1;
+            out[SSF_POSE_OUT_LOWER_BOUND] = S.lb;
+            out[SSF_POSE_OUT_PASSES] = S.passes;
+        }
+        __syncthreads();
+    }
+    if (bg_mask) {
+        const uint8_t bg = (uint8_t)S.bg;
+        for (int64_t i = tid; i < n; i += blockDim.x) bg_mask[fb + i] = Lb[i] == bg ? 1 : 0;
+    }
+}
+
+hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,
+                            const int64_t* frame_off, int mode, const uint8_t* mask_in,
+                            const double* draws, int reflection, uint8_t* bg_mask, double* out,
+                            double* dist_scratch, uint8_t* label_scratch) {
+    if (n_frames <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mask_pose, dim3(n_frames), dim3(kMaskThreads), 0, s, pts, flow, frame_off,
+                       mode, mask_in, draws, reflection, bg_mask, out, dist_scratch, label_scratch);
+    return hipGetLastError();
+}
+
+}  // namespace ssf

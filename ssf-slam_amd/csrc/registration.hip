@@ -1,0 +1,651 @@
+// registration.hip -- lidarOdometry_onlyPC::frameRegistration (src/lidarOdometry_onlyPC.cpp:147-252)
+// on gfx950, batched over independent frame pairs.
+//
+//   k_plane_table  per LAST-frame plane point a: exact 30-NN (FLANN L2_Simple float distances,
+//                  ties to the lower index) over the frame's plane cloud streamed through LDS
+//                  tiles, ring-diverse 5-point pick (:180-205), gate d2[n] < 1 (:207), 5x3
+//                  column-pivoted Householder least squares (:208-220), coplanarity gate (:222-232).
+//                  Everything there depends only on (last frame, a), so it is computed once per
+//                  frame here instead of twice per correspondence.
+//   k_associate    per CURRENT plane point: transformToLast in double (:74-82) -> exact 1-NN in the
+//                  last plane cloud (:168, unbounded) -> correspondence record {po, pa, n, valid}.
+//   k_solve        one work-group per pair runs the whole Ceres-LM (or GN) loop on device:
+//                  residual/Jacobian/Huber evaluation in f64 over the records, deterministic
+//                  block reduction of the 28 normal-equation terms, and the 6x6 trust-region
+//                  step on one lane -- no host round trip between iterations.
+#include "ssf_device.hpp"
+#include "ssf_internal.hpp"
+
+#include <float.h>
+
+namespace ssf {
+
+// ------------------------------------------------------------------------------------------
+// Eigen ColPivHouseholderQR<Matrix<float,5,3>>::solve(-1) -- same sequence as the oracle's
+// qr_solve_5x3 (oracle/ssf_oracle.c), float, no FMA contraction.
+SSF_DEV float sqnorm_f(const float* v, int n) {
+    float s = 0.0f;
+    for (int i = 0; i < n; ++i) s = s + v[i] * v[i];
+    return s;
+}
+
+SSF_DEV void qr_solve_5x3(float m[3][5], float x[3]) {
+    float hc[3] = {0.f, 0.f, 0.f};
+    int tr[3] = {0, 1, 2};
+    float nu[3], nd[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { nd[k] = sqrtf(sqnorm_f(m[k], 5)); nu[k] = nd[k]; }
+    float mx = nu[0];
+    for (int k = 1; k < 3; ++k) if (nu[k] > mx) mx = nu[k];
+    float th = mx * FLT_EPSILON;
+    th = (th * th) / 5.0f;
+    const float ndt = sqrtf(FLT_EPSILON);
+    int nz = 3;
+    for (int k = 0; k < 3; ++k) {
+        int bi = k;
+        float bv = nu[k];
+        for (int j = k + 1; j < 3; ++j) if (nu[j] > bv) { bv = nu[j]; bi = j; }
+        const float bsq = bv * bv;
+        if (nz == 3 && bsq < th * (float)(5 - k)) nz = k;
+        tr[k] = bi;
+        if (k != bi) {
+            for (int r = 0; r < 5; ++r) { float t = m[k][r]; m[k][r] = m[bi][r]; m[bi][r] = t; }
+            float t = nu[k]; nu[k] = nu[bi]; nu[bi] = t;
+            t = nd[k]; nd[k] = nd[bi]; nd[bi] = t;
+        }
+        const int L = 5 - k;
+        float* v = &m[k][k];
+        const float tail = sqnorm_f(v + 1, L - 1);
+        const float c0 = v[0];
+        float beta, tau;
+        if (tail <= FLT_MIN) {
+            tau = 0.0f; beta = c0;
+            for (int i = 1; i < L; ++i) v[i] = 0.0f;
+        } else {
+            beta = sqrtf(c0 * c0 + tail);
+            if (c0 >= 0.0f) beta = -beta;
+            const float den = c0 - beta;
+            for (int i = 1; i < L; ++i) v[i] = v[i] / den;
+            tau = (beta - c0) / beta;
+        }
+        hc[k] = tau;
+        v[0] = beta;
+        if (tau != 0.0f) {
+            for (int c = k + 1; c < 3; ++c) {
+                float tmp = 0.0f;
+                for (int i = 1; i < L; ++i) tmp = tmp + v[i] * m[c][k + i];
+                tmp = tmp + m[c][k];
+                m[c][k] = m[c][k] - tau * tmp;
+                for (int i = 1; i < L; ++i) m[c][k + i] = m[c][k + i] - (tau * v[i]) * tmp;
+            }
+        }
+        for (int j = k + 1; j < 3; ++j) {
+            if (nu[j] != 0.0f) {
+                float t = fabsf(m[j][k]) / nu[j];
+                t = (1.0f + t) * (1.0f - t);
+                if (t < 0.0f) t = 0.0f;
+                const float rr = nu[j] / nd[j];
+                const float t2 = t * (rr * rr);
+                if (t2 <= ndt) {
+                    nd[j] = sqrtf(sqnorm_f(&m[j][k + 1], 5 - k - 1));
+                    nu[j] = nd[j];
+                } else {
+                    nu[j] = nu[j] * sqrtf(t);
+                }
+            }
+        }
+    }
+    int perm[3] = {0, 1, 2};
+    for (int k = 0; k < 3; ++k) { int t = perm[k]; perm[k] = perm[tr[k]]; perm[tr[k]] = t; }
+    x[0] = x[1] = x[2] = 0.0f;
+    if (nz == 0) return;
+    float c[5] = {-1.0f, -1.0f, -1.0f, -1.0f, -1.0f};
+    for (int k = 0; k < nz; ++k) {
+        const float tau = hc[k];
+        const int L = 5 - k;
+        if (L == 1) {
+            c[k] = c[k] * (1.0f - tau);
+        } else if (tau != 0.0f) {
+            const float* v = &m[k][k];
+            float tmp = 0.0f;
+            for (int i = 1; i < L; ++i) tmp = tmp + v[i] * c[k + i];
+            tmp = tmp + c[k];
+            c[k] = c[k] - tau * tmp;
+            for (int i = 1; i < L; ++i) c[k + i] = c[k + i] - (tau * v[i]) * tmp;
+        }
+    }
+    for (int i = nz - 1; i >= 0; --i) {
+        if (c[i] != 0.0f) {
+            c[i] = c[i] / m[i][i];
+            for (int s = 0; s < i; ++s) c[s] = c[s] - c[i] * m[i][s];
+        }
+    }
+    for (int i = 0; i < nz; ++i) x[perm[i]] = c[i];
+}
+
+constexpr int kKnnTile = 2048;
+constexpr int kK = 30;
+
+SSF_DEV float l2_simple(const float4& q, const float4& p) {
+    const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
+    float d = dx * dx + dy * dy;
+    return d + dz * dz;
+}
+
+__global__ __launch_bounds__(256) void k_plane_table(const float4* __restrict__ plane,
+                                                     const int64_t* __restrict__ frame_off,
+                                                     const int32_t* __restrict__ count,
+                                                     float plane_max, float* __restrict__ normal,
+                                                     uint8_t* __restrict__ valid) {
+    __shared__ float4 tile[kKnnTile];
+    const int f = blockIdx.y;
+    const int m = count[f];
+    if ((int)(blockIdx.x * blockDim.x) >= m) return;  // uniform
+    const int a = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = a < m;
+    const float4* P = plane + frame_off[f];
+    const float4 q = active ? P[a] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float kd[kK];
+    int ki[kK];
+#pragma unroll
+    for (int k = 0; k < kK; ++k) { kd[k] = __builtin_inff(); ki[k] = -1; }
+    for (int t0 = 0; t0 < m; t0 += kKnnTile) {
+        const int nt = min(kKnnTile, m - t0);
+        for (int k = threadIdx.x; k < nt; k += blockDim.x) tile[k] = P[t0 + k];
+        __syncthreads();
+        if (active) {
+            for (int k = 0; k < nt; ++k) {
+                float d = l2_simple(q, tile[k]);
+                if (d < kd[kK - 1]) {
+                    int id = t0 + k;
+#pragma unroll
+                    for (int s = 0; s < kK; ++s) {
+                        const bool sw = d < kd[s];
+                        const float td = kd[s];
+                        const int ti = ki[s];
+                        kd[s] = sw ? d : td;
+                        ki[s] = sw ? id : ti;
+                        d = sw ? td : d;
+                        id = sw ? ti : id;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (!active) return;
+    const int K = m < kK ? m : kK;
+    float nrm[3] = {0.f, 0.f, 0.f};
+    uint8_t ok = 0;
+    if (K >= 5) {                                                      // :177
+        int v5[5];
+        int prow = -1, vr0 = -1, vr1 = -1, nvr = 0, n = 5;
+#pragma unroll
+        for (int ik = 0; ik < kK; ++ik) {                               // :180-198
+            if (ik < K && nvr < 2) {
+                const float fi = P[ki[ik]].w;
+                const int ii = (int)fi;
+                const int row = (int)(100.0 * ((double)(fi - (float)ii) + 0.002));
+                if (ik == 0) prow = row;
+                if (ik < 5) {
+                    v5[ik] = ki[ik];
+                } else if (row != prow && row >= 0 && row <= 63) {
+                    if (nvr == 0) vr0 = ki[ik]; else vr1 = ki[ik];
+                    nvr++;
+                    n = ik;
+                }
+            }
+        }
+        if (nvr == 1) v5[4] = vr0;                                      // :199-205
+        if (nvr == 2) { v5[3] = vr0; v5[4] = vr1; }
+        float dn = kd[0];
+#pragma unroll
+        for (int ik = 0; ik < kK; ++ik) if (ik == n) dn = kd[ik];
+        if (dn < 1.0f) {                                                // :207
+            float Am[3][5];
+            float pts[5][3];
+            for (int j = 0; j < 5; ++j) {
+                const float4 p = P[v5[j]];
+                pts[j][0] = p.x; pts[j][1] = p.y; pts[j][2] = p.z;
+                Am[0][j] = p.x; Am[1][j] = p.y; Am[2][j] = p.z;
+            }
+            qr_solve_5x3(Am, nrm);                                      // :219
+            float z = nrm[0] * nrm[0] + nrm[1] * nrm[1];
+            z = z + nrm[2] * nrm[2];
+            if (z > 0.0f) {                                             // :220
+                const float s = sqrtf(z);
+                nrm[0] = nrm[0] / s; nrm[1] = nrm[1] / s; nrm[2] = nrm[2] / s;
+            }
+            ok = 1;
+            for (int k = 0; k < 4; ++k) {                               // :222-232
+                const double vx = (double)(pts[k][0] - pts[k + 1][0]);
+                const double vy = (double)(pts[k][1] - pts[k + 1][1]);
+                const double vz = (double)(pts[k][2] - pts[k + 1][2]);
+                double dd = (double)nrm[0] * vx + (double)nrm[1] * vy;
+                dd = dd + (double)nrm[2] * vz;
+                if (fabs(dd) > (double)plane_max) { ok = 0; break; }
+            }
+        }
+    }
+    const int64_t o = frame_off[f] + a;
+    normal[3 * o] = nrm[0]; normal[3 * o + 1] = nrm[1]; normal[3 * o + 2] = nrm[2];
+    valid[o] = ok;
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_associate(const float4* __restrict__ last,
+                                                   const int64_t* __restrict__ last_off,
+                                                   const int32_t* __restrict__ last_count,
+                                                   const float* __restrict__ last_normal,
+                                                   const uint8_t* __restrict__ last_valid,
+                                                   const float4* __restrict__ curr,
+                                                   const int64_t* __restrict__ curr_off,
+                                                   const int32_t* __restrict__ curr_count,
+                                                   const double* __restrict__ pose_rel,
+                                                   CorrRec* __restrict__ corr,
+                                                   int32_t* __restrict__ nn_out) {
+    __shared__ float4 tile[kKnnTile];
+    const int p = blockIdx.y;
+    const int mc = curr_count[p], ml = last_count[p];
+    if ((int)(blockIdx.x * blockDim.x) >= mc || ml <= 10) return;  // uniform (:158)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = i < mc;
+    const float4* L = last + last_off[p];
+    const int64_t co = curr_off[p];
+    const double q[4] = {pose_rel[7 * p], pose_rel[7 * p + 1], pose_rel[7 * p + 2], pose_rel[7 * p + 3]};
+    const double t[3] = {pose_rel[7 * p + 4], pose_rel[7 * p + 5], pose_rel[7 * p + 6]};
+    float4 pc = make_float4(0.f, 0.f, 0.f, 0.f), qs = pc;
+    if (active) {
+        pc = curr[co + i];
+        const double v[3] = {(double)pc.x, (double)pc.y, (double)pc.z};
+        double r[3];
+        quat_rotate(q, v, r);                                           // :74-82
+        qs.x = (float)(r[0] + t[0]); qs.y = (float)(r[1] + t[1]); qs.z = (float)(r[2] + t[2]);
+    }
+    float best = __builtin_inff();
+    int bi = -1;
+    for (int t0 = 0; t0 < ml; t0 += kKnnTile) {
+        const int nt = min(kKnnTile, ml - t0);
+        for (int k = threadIdx.x; k < nt; k += blockDim.x) tile[k] = L[t0 + k];
+        __syncthreads();
+        if (active) {
+            for (int k = 0; k < nt; ++k) {
+                const float d = l2_simple(qs, tile[k]);
+                if (d < best) { best = d; bi = t0 + k; }
+            }
+        }
+        __syncthreads();
+    }
+    if (!active) return;
+    const int64_t lo = last_off[p];
+    CorrRec rec;
+    const bool ok = bi >= 0 && last_valid[lo + bi];
+    const float4 pa = L[bi >= 0 ? bi : 0];
+    rec.po[0] = pc.x; rec.po[1] = pc.y; rec.po[2] = pc.z; rec.valid = ok ? 1.0f : 0.0f;
+    rec.pa[0] = pa.x; rec.pa[1] = pa.y; rec.pa[2] = pa.z; rec.pad0 = 0.f;
+    const float* nr = last_normal + 3 * (lo + (bi >= 0 ? bi : 0));
+    rec.n[0] = nr[0]; rec.n[1] = nr[1]; rec.n[2] = nr[2]; rec.pad1 = 0.f;
+    corr[co + i] = rec;
+    if (nn_out) nn_out[co + i] = bi;
+}
+
+// ------------------------------------------------------------------------------------------
+// Residual + local Jacobian of PlaneFeatureCost (:25-43) composed with the
+// EigenQuaternionParameterization 4x3 Jacobian (same algebra as the oracle's residual_jac).
+SSF_DEV double residual_jac(const double q[4], const double t[3], const double po[3],
+                            const double pa[3], const double n[3], double J[6]) {
+    double f[3];
+    quat_rotate(q, po, f);
+    const double d0 = (f[0] + t[0]) - pa[0], d1 = (f[1] + t[1]) - pa[1], d2 = (f[2] + t[2]) - pa[2];
+    double r = d0 * n[0] + d1 * n[1];
+    r = r + d2 * n[2];
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    const double u0 = y * po[2] - z * po[1], u1 = z * po[0] - x * po[2], u2 = x * po[1] - y * po[0];
+    const double pxn0 = po[1] * n[2] - po[2] * n[1], pxn1 = po[2] * n[0] - po[0] * n[2],
+                 pxn2 = po[0] * n[1] - po[1] * n[0];
+    const double uxn0 = u1 * n[2] - u2 * n[1], uxn1 = u2 * n[0] - u0 * n[2], uxn2 = u0 * n[1] - u1 * n[0];
+    const double nxq0 = n[1] * z - n[2] * y, nxq1 = n[2] * x - n[0] * z, nxq2 = n[0] * y - n[1] * x;
+    const double pnq0 = po[1] * nxq2 - po[2] * nxq1, pnq1 = po[2] * nxq0 - po[0] * nxq2,
+                 pnq2 = po[0] * nxq1 - po[1] * nxq0;
+    const double g0 = 2.0 * w * pxn0 + 2.0 * uxn0 + 2.0 * pnq0;
+    const double g1 = 2.0 * w * pxn1 + 2.0 * uxn1 + 2.0 * pnq1;
+    const double g2 = 2.0 * w * pxn2 + 2.0 * uxn2 + 2.0 * pnq2;
+    const double g3 = 2.0 * (n[0] * u0 + n[1] * u1 + n[2] * u2);
+    J[0] = g0 * w - g1 * z + g2 * y - g3 * x;
+    J[1] = g0 * z + g1 * w - g2 * x - g3 * y;
+    J[2] = -g0 * y + g1 * x + g2 * w - g3 * z;
+    J[3] = n[0]; J[4] = n[1]; J[5] = n[2];
+    return r;
+}
+
+constexpr int kSolveThreads = 512;
+constexpr int kNE = 28;  // 21 (packed upper JtWJ) + 6 (JtWr) + cost
+
+SSF_DEV int pk(int u, int v) {
+    if (u > v) { int t = u; u = v; v = t; }
+    return u * 6 - (u * (u - 1)) / 2 + (v - u);
+}
+
+// All threads: evaluate Huber(0.1)-corrected normal equations at (q, t) over the pair's
+// records; result (x2 for the reference's duplicated residual blocks) in ne[] of every thread.
+SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4], const double t[3],
+                      double (&ne)[kNE], double* lds) {
+#pragma unroll
+    for (int k = 0; k < kNE; ++k) ne[k] = 0.0;
+    const double a = 0.1, b = 0.1 * 0.1;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const CorrRec c = rec[i];
+        if (c.valid == 0.0f) continue;
+        const double po[3] = {c.po[0], c.po[1], c.po[2]};
+        const double pa[3] = {c.pa[0], c.pa[1], c.pa[2]};
+        const double nn[3] = {c.n[0], c.n[1], c.n[2]};
+        double J[6];
+        const double r = residual_jac(q, t, po, pa, nn, J);
+        const double s = r * r;
+        double rho0, rho1;
+        if (s > b) {
+            const double rr = sqrt(s);
+            rho0 = 2.0 * a * rr - b;
+            rho1 = a / rr;
+            if (rho1 < DBL_MIN) rho1 = DBL_MIN;
+        } else {
+            rho0 = s; rho1 = 1.0;
+        }
+        ne[27] += 0.5 * rho0;
+        int k = 0;
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+            ne[21 + u] += rho1 * J[u] * r;
+#pragma unroll
+            for (int v = u; v < 6; ++v) ne[k++] += rho1 * J[u] * J[v];
+        }
+    }
+    block_sum<kNE>(ne, lds);
+#pragma unroll
+    for (int k = 0; k < kNE; ++k) ne[k] *= 2.0;
+}
+
+SSF_DEV int chol_solve6(double M[6][6], const double b[6], double y[6]) {
+    double L[6][6];
+    for (int i = 0; i < 6; ++i) for (int j = 0; j < 6; ++j) L[i][j] = 0.0;
+    for (int j = 0; j < 6; ++j) {
+        double s = M[j][j];
+        for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
+        if (!(s > 0.0)) return -1;
+        L[j][j] = sqrt(s);
+        for (int i = j + 1; i < 6; ++i) {
+            double v = M[i][j];
+            for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k];
+            L[i][j] = v / L[j][j];
+        }
+    }
+    double z[6];
+    for (int i = 0; i < 6; ++i) {
+        double v = b[i];
+        for (int k = 0; k < i; ++k) v -= L[i][k] * z[k];
+        z[i] = v / L[i][i];
+    }
+    for (int i = 5; i >= 0; --i) {
+        double v = z[i];
+        for (int k = i + 1; k < 6; ++k) v -= L[k][i] * y[k];
+        y[i] = v / L[i][i];
+    }
+    return 0;
+}
+
+struct SolveShared {
+    double q[4], t[3], qc[4], tc[3];
+    double s[6];
+    double ne[kNE];       // normal equations at the current x
+    double radius, dec, mcc;
+    int invalid, flag, nlog, done;
+};
+
+SSF_DEV void write_log(double* log, int max_iter, int p, int idx, const double q[4],
+                       const double t[3], double cost, double status, double radius) {
+    if (!log || idx >= max_iter) return;
+    double* r = log + ((int64_t)p * max_iter + idx) * 10;
+    r[0] = q[0]; r[1] = q[1]; r[2] = q[2]; r[3] = q[3];
+    r[4] = t[0]; r[5] = t[1]; r[6] = t[2];
+    r[7] = cost; r[8] = status; r[9] = radius;
+}
+
+__global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restrict__ corr,
+                                                         const int64_t* __restrict__ curr_off,
+                                                         const int32_t* __restrict__ curr_count,
+                                                         const int32_t* __restrict__ last_count,
+                                                         int mode, int max_iter,
+                                                         double* __restrict__ pose_rel,
+                                                         double* __restrict__ pose_abs,
+                                                         double* __restrict__ log,
+                                                         int32_t* __restrict__ nlog_out,
+                                                         int32_t* __restrict__ ncorr_out) {
+    __shared__ SolveShared S;
+    __shared__ double red[(kSolveThreads / 64) * kNE];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int n = curr_count[p];
+    const CorrRec* rec = corr + curr_off[p];
+    if (tid == 0) {
+        for (int k = 0; k < 4; ++k) S.q[k] = pose_rel[7 * p + k];
+        for (int k = 0; k < 3; ++k) S.t[k] = pose_rel[7 * p + 4 + k];
+        S.nlog = 0; S.done = 0;
+    }
+    __syncthreads();
+    const bool skip = last_count[p] <= 10;                              // :158
+    if (!skip) {
+        int nv = 0;
+        for (int i = tid; i < n; i += blockDim.x) nv += rec[i].valid != 0.0f;
+        nv = block_sum_scalar<int>(nv, reinterpret_cast<int*>(red));
+        if (tid == 0 && ncorr_out) ncorr_out[p] = nv;
+        double ne[kNE];
+        double q[4], t[3];
+        for (int k = 0; k < 4; ++k) q[k] = S.q[k];
+        for (int k = 0; k < 3; ++k) t[k] = S.t[k];
+        evaluate(rec, n, q, t, ne, red);
+        if (tid == 0) {
+            for (int k = 0; k < kNE; ++k) S.ne[k] = ne[k];
+            for (int u = 0; u < 6; ++u) S.s[u] = 1.0 / (1.0 + sqrt(ne[pk(u, u)]));
+            S.radius = 1e4; S.dec = 2.0; S.invalid = 0;
+        }
+        __syncthreads();
+        if (mode == SSF_SOLVER_GN) {
+            for (int it = 0; it < max_iter; ++it) {
+                if (tid == 0) {
+                    double M[6][6], b[6], y[6];
+                    for (int u = 0; u < 6; ++u) {
+                        b[u] = -S.ne[21 + u];
+                        for (int v = 0; v < 6; ++v) M[u][v] = S.ne[pk(u, v)];
+                    }
+                    if (chol_solve6(M, b, y) != 0) {
+                        write_log(log, max_iter, p, S.nlog++, S.q, S.t, S.ne[27], 2, 0);
+                        S.done = 1;
+                    } else {
+                        double qn[4];
+                        quat_plus(S.q, y, qn);
+                        for (int k = 0; k < 4; ++k) S.q[k] = qn[k];
+                        S.t[0] += y[3]; S.t[1] += y[4]; S.t[2] += y[5];
+                    }
+                }
+                __syncthreads();
+                if (S.done) break;
+                for (int k = 0; k < 4; ++k) q[k] = S.q[k];
+                for (int k = 0; k < 3; ++k) t[k] = S.t[k];
+                evaluate(rec, n, q, t, ne, red);
+                if (tid == 0) {
+                    for (int k = 0; k < kNE; ++k) S.ne[k] = ne[k];
+                    write_log(log, max_iter, p, S.nlog++, S.q, S.t, ne[27], 6, 0);
+                }
+                __syncthreads();
+            }
+        } else {
+            for (int it = 1; it <= max_iter; ++it) {
+                if (tid == 0) {
+                    // LevenbergMarquardtStrategy::ComputeStep on the Jacobi-scaled system
+                    double As[6][6], gs[6], M[6][6], bb[6], y[6];
+                    for (int u = 0; u < 6; ++u) {
+                        gs[u] = S.s[u] * S.ne[21 + u];
+                        for (int v = 0; v < 6; ++v) As[u][v] = S.s[u] * S.ne[pk(u, v)] * S.s[v];
+                    }
+                    for (int u = 0; u < 6; ++u) {
+                        double d = As[u][u];
+                        if (d < 1e-6) d = 1e-6;
+                        if (d > 1e32) d = 1e32;
+                        for (int v = 0; v < 6; ++v) M[u][v] = As[u][v];
+                        M[u][u] += d / S.radius;
+                        bb[u] = -gs[u];
+                    }
+                    const bool ok = chol_solve6(M, bb, y) == 0;
+                    double mcc = 0.0;
+                    if (ok) {
+                        double yg = 0.0, yAy = 0.0;
+                        for (int u = 0; u < 6; ++u) {
+                            yg += y[u] * gs[u];
+                            double Ay = 0.0;
+                            for (int v = 0; v < 6; ++v) Ay += As[u][v] * y[v];
+                            yAy += y[u] * Ay;
+                        }
+                        mcc = -(yg + 0.5 * yAy);
+                    }
+                    if (!ok || !(mcc > 0.0)) {
+                        S.radius /= S.dec; S.dec *= 2.0;
+                        write_log(log, max_iter, p, S.nlog++, S.q, S.t, S.ne[27], 2, S.radius);
+                        S.flag = 0;
+                        if (++S.invalid > 5) S.done = 1;
+                    } else {
+                        S.invalid = 0;
+                        double delta[6];
+                        for (int u = 0; u < 6; ++u) delta[u] = y[u] * S.s[u];
+                        quat_plus(S.q, delta, S.qc);
+                        S.tc[0] = S.t[0] + delta[3]; S.tc[1] = S.t[1] + delta[4]; S.tc[2] = S.t[2] + delta[5];
+                        S.mcc = mcc;
+                        S.flag = 1;
+                    }
+                }
+                __syncthreads();
+                if (S.done) break;
+                if (!S.flag) continue;
+                double qc[4], tc[3];
+                for (int k = 0; k < 4; ++k) qc[k] = S.qc[k];
+                for (int k = 0; k < 3; ++k) tc[k] = S.tc[k];
+                evaluate(rec, n, qc, tc, ne, red);
+                if (tid == 0) {
+                    double xn = 0.0, sn = 0.0;
+                    for (int u = 0; u < 4; ++u) { xn += S.q[u] * S.q[u]; sn += (S.q[u] - S.qc[u]) * (S.q[u] - S.qc[u]); }
+                    for (int u = 0; u < 3; ++u) { xn += S.t[u] * S.t[u]; sn += (S.t[u] - S.tc[u]) * (S.t[u] - S.tc[u]); }
+                    xn = sqrt(xn); sn = sqrt(sn);
+                    const double dcost = S.ne[27] - ne[27];
+                    if (!(sn > (xn + 1e-8) * 1e-8)) {                   // ParameterToleranceReached
+                        write_log(log, max_iter, p, S.nlog++, S.q, S.t, S.ne[27], 3, S.radius);
+                        S.done = 1;
+                    } else if (!(fabs(dcost) > 1e-6 * S.ne[27])) {      // FunctionToleranceReached
+                        write_log(log, max_iter, p, S.nlog++, S.q, S.t, S.ne[27], 4, S.radius);
+                        S.done = 1;
+                    } else {
+                        const double rho = dcost / S.mcc;
+                        if (rho > 1e-3) {                               // accept
+                            for (int k = 0; k < 4; ++k) S.q[k] = S.qc[k];
+                            for (int k = 0; k < 3; ++k) S.t[k] = S.tc[k];
+                            for (int k = 0; k < kNE; ++k) S.ne[k] = ne[k];
+                            const double f = 2.0 * rho - 1.0;
+                            double den = 1.0 - f * f * f;
+                            if (den < 1.0 / 3.0) den = 1.0 / 3.0;
+                            S.radius = S.radius / den;
+                            if (S.radius > 1e16) S.radius = 1e16;
+                            S.dec = 2.0;
+                            const double mg[3] = {-ne[21], -ne[22], -ne[23]};
+                            double qg[4], gm = 0.0;
+                            quat_plus(S.q, mg, qg);
+                            for (int u = 0; u < 4; ++u) gm = fmax(gm, fabs(S.q[u] - qg[u]));
+                            for (int u = 3; u < 6; ++u) gm = fmax(gm, fabs(ne[21 + u]));
+                            if (gm <= 1e-10) {
+                                write_log(log, max_iter, p, S.nlog++, S.q, S.t, S.ne[27], 5, S.radius);
+                                S.done = 1;
+                            } else {
+                                write_log(log, max_iter, p, S.nlog++, S.q, S.t, S.ne[27], 1, S.radius);
+                            }
+                        } else {                                        // reject
+                            S.radius /= S.dec; S.dec *= 2.0;
+                            write_log(log, max_iter, p, S.nlog++, S.q, S.t, S.ne[27], 0, S.radius);
+                        }
+                    }
+                }
+                __syncthreads();
+                if (S.done) break;
+            }
+        }
+    } else if (tid == 0 && ncorr_out) {
+        ncorr_out[p] = -1;
+    }
+    if (tid == 0) {
+        for (int k = 0; k < 4; ++k) pose_rel[7 * p + k] = S.q[k];
+        for (int k = 0; k < 3; ++k) pose_rel[7 * p + 4 + k] = S.t[k];
+        if (nlog_out) nlog_out[p] = S.nlog;
+        if (pose_abs) {                                                 // :87-90
+            double q0l[4], t0l[3], q0c[4], r[3];
+            for (int k = 0; k < 4; ++k) q0l[k] = pose_abs[7 * p + k];
+            for (int k = 0; k < 3; ++k) t0l[k] = pose_abs[7 * p + 4 + k];
+            quat_mul(q0l, S.q, q0c);
+            quat_rotate(q0l, S.t, r);
+            for (int k = 0; k < 4; ++k) pose_abs[7 * p + k] = q0c[k];
+            for (int k = 0; k < 3; ++k) pose_abs[7 * p + 4 + k] = t0l[k] + r[k];
+        }
+    }
+}
+
+__global__ void k_accumulate(int n, const double* __restrict__ rel, const double* __restrict__ start,
+                             double* __restrict__ out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double q[4] = {0, 0, 0, 1}, t[3] = {0, 0, 0};
+    if (start) {
+        for (int k = 0; k < 4; ++k) q[k] = start[k];
+        for (int k = 0; k < 3; ++k) t[k] = start[4 + k];
+    }
+    for (int i = 0; i < n; ++i) {
+        const double* r = rel + 7 * i;
+        double qn[4], rt[3];
+        quat_mul(q, r, qn);
+        quat_rotate(q, r + 4, rt);
+        for (int k = 0; k < 3; ++k) t[k] = t[k] + rt[k];
+        for (int k = 0; k < 4; ++k) q[k] = qn[k];
+        for (int k = 0; k < 4; ++k) out[7 * i + k] = q[k];
+        for (int k = 0; k < 3; ++k) out[7 * i + 4 + k] = t[k];
+    }
+}
+
+hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames,
+                              const float4* plane, const int64_t* frame_off, const int32_t* count,
+                              int64_t max_m, float* normal, uint8_t* valid) {
+    if (n_frames <= 0 || max_m <= 0) return hipSuccess;
+    const int bx = (int)((max_m + 255) / 256);
+    hipLaunchKernelGGL(k_plane_table, dim3(bx, n_frames), dim3(256), 0, s, plane, frame_off, count,
+                       cfg.plane_max, normal, valid);
+    return hipGetLastError();
+}
+
+hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, const float4* last,
+                           const int64_t* last_off, const int32_t* last_count,
+                           const float* last_normal, const uint8_t* last_valid, const float4* curr,
+                           const int64_t* curr_off, const int32_t* curr_count, int64_t max_m,
+                           CorrRec* corr, double* pose_rel, double* pose_abs, double* log,
+                           int32_t* nlog, int32_t* ncorr, int32_t* nn) {
+    if (n_pairs <= 0) return hipSuccess;
+    if (max_m > 0) {
+        const int bx = (int)((max_m + 255) / 256);
+        hipLaunchKernelGGL(k_associate, dim3(bx, n_pairs), dim3(256), 0, s, last, last_off,
+                           last_count, last_normal, last_valid, curr, curr_off, curr_count,
+                           pose_rel, corr, nn);
+    }
+    hipLaunchKernelGGL(k_solve, dim3(n_pairs), dim3(kSolveThreads), 0, s, corr, curr_off,
+                       curr_count, last_count, cfg.solver, cfg.max_iter, pose_rel, pose_abs, log,
+                       nlog, ncorr);
+    return hipGetLastError();
+}
+
+hipError_t launch_accumulate(hipStream_t s, int n, const double* rel, const double* start,
+                             double* abs_out) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(64), 0, s, n, rel, start, abs_out);
+    return hipGetLastError();
+}
+
+}  // namespace ssf

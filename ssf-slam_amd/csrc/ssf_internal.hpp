@@ -1,0 +1,69 @@
+// ssf_internal.hpp -- host-side context and kernel-launch declarations (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/ssf_frontend.h"
+
+namespace ssf {
+
+// Device scratch owned by a context: grown on demand, never shrunk.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr; bytes = 0;
+        }
+        size_t want = need + need / 4 + 256;
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) { p = nullptr; return e; }
+        bytes = want;
+        return hipSuccess;
+    }
+    template <typename T> T* as() const { return static_cast<T*>(p); }
+    void release() { if (p) (void)hipFree(p); p = nullptr; bytes = 0; }
+};
+
+constexpr int kBinChunk = 4096;   // points per binning work-group
+constexpr int kMaxRows = 64;
+
+// Per-correspondence record written by the association kernel, read by the solver.
+struct alignas(16) CorrRec {
+    float po[3]; float valid;   // current-frame point (untransformed), 1 if the plane is valid
+    float pa[3]; float pad0;    // last-frame 1-NN point
+    float n[3];  float pad1;    // plane normal (float, as matX0)
+};
+
+// ---- launchers (features.hip) ----
+hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_frames,
+                                 const float* pts, int stride, const int64_t* frame_off,
+                                 int64_t max_pts, int8_t* rid, int32_t* hist, int32_t* ring_off,
+                                 float4* ring_xyzi, float* curv, int32_t* sel, int32_t* sel_cnt,
+                                 float4* plane, int32_t* plane_count);
+
+// ---- launchers (registration.hip) ----
+hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames,
+                              const float4* plane, const int64_t* frame_off, const int32_t* count,
+                              int64_t max_m, float* normal, uint8_t* valid);
+hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, const float4* last,
+                           const int64_t* last_off, const int32_t* last_count,
+                           const float* last_normal, const uint8_t* last_valid, const float4* curr,
+                           const int64_t* curr_off, const int32_t* curr_count, int64_t max_m,
+                           CorrRec* corr, double* pose_rel, double* pose_abs, double* log,
+                           int32_t* nlog, int32_t* ncorr, int32_t* nn);
+hipError_t launch_accumulate(hipStream_t s, int n, const double* rel, const double* start,
+                             double* abs_out);
+
+// ---- launchers (mask_pose.hip) ----
+hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,
+                            const int64_t* frame_off, int mode, const uint8_t* mask_in,
+                            const double* draws, int reflection, uint8_t* bg_mask, double* out,
+                            double* dist_scratch, uint8_t* label_scratch);
+
+}  // namespace ssf

@@ -1,0 +1,10 @@
+"""ssf -- MI355X (gfx950) SSF-SLAM LiDAR front-end.
+
+Host-side mirror of the reference's hot-path interfaces over the C ABI in
+include/ssf_frontend.h (libssf_frontend.so, hand-written HIP kernels).  There is no CPU
+fallback anywhere in this package.
+"""
+from ._abi import SSFError  # noqa: F401
+from .frontend import Frontend, PlaneBatch, frame_offsets, identity_poses  # noqa: F401
+
+__all__ = ["Frontend", "PlaneBatch", "frame_offsets", "identity_poses", "SSFError"]

@@ -1,0 +1,90 @@
+"""ctypes binding of libssf_frontend.so (include/ssf_frontend.h).
+
+The library is loaded AFTER torch so that its libamdhip64.so.7 dependency resolves to the HIP
+runtime torch already mapped (one runtime per process).  There is no fallback: if the library
+is missing or fails to load, every entry point raises -- the product path never silently runs
+on a CPU substitute.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the dlopen below, see module docstring)
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "libssf_frontend.so")
+
+SSF_OK, SSF_E_ARG, SSF_E_HIP, SSF_E_NOMEM, SSF_E_CAPACITY, SSF_E_NODEV = 0, -1, -2, -3, -4, -5
+SOLVER_CERES_LM, SOLVER_GN = 0, 1
+MASK_GMM, MASK_GT, MASK_GIVEN = 0, 1, 2
+POSE_OUT_STRIDE = 32
+POSE_OUT = dict(T=0, Q=3, R=7, STATUS=16, NBG=17, BGLABEL=18, KM_ITER=19, EM_ITER=20,
+                CONVERGED=21, CENTER0=22, CENTER1=23, LOWER_BOUND=24, PASSES=25)
+POSE_EMPTY, POSE_REFLECTION, POSE_NOT_ORTHOGONAL, POSE_GMM_FAILED = -1, -2, -3, -4
+
+# Every symbol include/ssf_frontend.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "ssf_abi_version", "ssf_config_default", "ssf_create", "ssf_destroy", "ssf_last_error",
+    "ssf_reserve", "ssf_extract_planes_batch", "ssf_extract_planes", "ssf_plane_table_batch",
+    "ssf_register_batch", "ssf_mask_pose_batch", "ssf_rng_seed", "ssf_accumulate_sequence",
+]
+
+
+class Config(C.Structure):
+    _fields_ = [("n_rows", C.c_int32), ("plane_min", C.c_float), ("plane_span", C.c_int32),
+                ("row_start", C.c_int32), ("row_end", C.c_int32), ("plane_max", C.c_float),
+                ("solver", C.c_int32), ("max_iter", C.c_int32)]
+
+
+_lib = None
+
+
+class SSFError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SSFError(f"{LIB_PATH} is missing: build it first (python -c 'import __graft_entry__ "
+                       f"as g; g.build()')")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+    L.ssf_abi_version.restype = i32
+    L.ssf_config_default.argtypes = [i32, C.POINTER(Config)]
+    L.ssf_config_default.restype = i32
+    L.ssf_create.argtypes = [i32, C.POINTER(Config), C.POINTER(vp)]
+    L.ssf_create.restype = i32
+    L.ssf_destroy.argtypes = [vp]
+    L.ssf_destroy.restype = None
+    L.ssf_last_error.argtypes = [vp]
+    L.ssf_last_error.restype = C.c_char_p
+    L.ssf_reserve.argtypes = [vp, i32, i64]
+    L.ssf_reserve.restype = i32
+    L.ssf_rng_seed.argtypes = [vp, C.c_uint32]
+    L.ssf_rng_seed.restype = i32
+    L.ssf_extract_planes_batch.argtypes = [vp, vp, i32, vp, i32, vp, i64, i64, vp, vp, vp, vp, vp]
+    L.ssf_extract_planes_batch.restype = i32
+    L.ssf_extract_planes.argtypes = [vp, vp, vp, i64, i32, i32, vp, C.POINTER(i64), i64]
+    L.ssf_extract_planes.restype = i32
+    L.ssf_plane_table_batch.argtypes = [vp, vp, i32, vp, vp, vp, i64, vp, vp]
+    L.ssf_plane_table_batch.restype = i32
+    L.ssf_register_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp,
+                                     vp, vp, vp, vp, vp]
+    L.ssf_register_batch.restype = i32
+    L.ssf_mask_pose_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, i32, vp, vp]
+    L.ssf_mask_pose_batch.restype = i32
+    L.ssf_accumulate_sequence.argtypes = [vp, vp, i32, vp, vp, vp]
+    L.ssf_accumulate_sequence.restype = i32
+    _lib = L
+    return L
+
+
+def config_default(n_rows: int) -> Config:
+    cfg = Config()
+    if lib().ssf_config_default(n_rows, C.byref(cfg)) != SSF_OK:
+        raise ValueError(f"unsupported N_SCAN_ROW {n_rows} (16 or 64)")
+    return cfg

@@ -1,0 +1,223 @@
+"""Host-side API of the MI355X front-end: thin Python over the C ABI (include/ssf_frontend.h).
+
+Tensors are torch CUDA (HIP) tensors; their device pointers and torch's current HIP stream
+are handed to libssf_frontend.so.  Nothing here computes front-end results itself.
+
+Mirrors of the reference interfaces:
+  Frontend.extract_planes*  <- frameFeature.cpp cloudHandler (:35-139)
+  Frontend.plane_table / register  <- lidarOdometry_onlyPC.cpp frameRegistration (:147-252)
+                                       + publishResult accumulation (:87-90)
+  Frontend.mask_pose        <- PointCloudOdometry_noSeg.py:97-125 / PointCloudOdometry.py:91-101
+  OdometryState             <- the cloudThread() state machine (flagStart, warm start, last<-curr,
+                               lidarOdometry_onlyPC.cpp:281-311) for many sequences at once
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import torch
+
+from . import _abi
+from ._abi import SSFError
+
+SOLVERS = {"ceres_lm": _abi.SOLVER_CERES_LM, "lm": _abi.SOLVER_CERES_LM, "gn": _abi.SOLVER_GN}
+MASK_MODES = {"gmm": _abi.MASK_GMM, "gt": _abi.MASK_GT, "given": _abi.MASK_GIVEN}
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream(device):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def frame_offsets(counts, device):
+    """int64 offsets [F+1] (device) and their host copy from a list of frame sizes."""
+    off = [0]
+    for c in counts:
+        off.append(off[-1] + int(c))
+    h = torch.tensor(off, dtype=torch.int64)
+    return h.to(device), h
+
+
+@dataclass
+class PlaneBatch:
+    """Plane clouds of F frames at frame offsets: xyzi[off[f] : off[f] + count[f]]."""
+    xyzi: torch.Tensor      # [total, 4] f32
+    count: torch.Tensor     # [F] int32 (device)
+    off: torch.Tensor       # [F+1] int64 (device)
+    h_off: torch.Tensor     # [F+1] int64 (host)
+    max_points: int         # host bound on points per frame (grid sizing)
+
+    def frame(self, f):
+        c = int(self.count[f])
+        o = int(self.h_off[f])
+        return self.xyzi[o:o + c]
+
+
+class Frontend:
+    """One C-ABI context (one device, one parameter profile)."""
+
+    def __init__(self, n_rows: int = 64, device: int | torch.device | None = None,
+                 solver: str = "ceres_lm", max_iter: int | None = None):
+        if not torch.cuda.is_available():
+            raise SSFError("no HIP device visible: the MI355X front-end has no CPU fallback")
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else
+                           (device.index if isinstance(device, torch.device) else int(device)))
+        self.device = dev
+        self.cfg = _abi.config_default(n_rows)
+        self.cfg.solver = SOLVERS[solver]
+        self.cfg.max_iter = (8 if self.cfg.solver == _abi.SOLVER_CERES_LM else 10) if max_iter is None else int(max_iter)
+        self.n_rows = n_rows
+        h = C.c_void_p()
+        rc = _abi.lib().ssf_create(dev.index, C.byref(self.cfg), C.byref(h))
+        if rc != _abi.SSF_OK:
+            raise SSFError(f"ssf_create failed rc={rc} (need a gfx950 / MI355X device)")
+        self._h = h
+
+    # ------------------------------------------------------------------ plumbing
+    def close(self):
+        if getattr(self, "_h", None):
+            _abi.lib().ssf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != _abi.SSF_OK:
+            msg = _abi.lib().ssf_last_error(self._h)
+            raise SSFError(f"{what} failed rc={rc}: {msg.decode() if msg else ''}")
+
+    def reserve(self, max_frames: int, max_points_per_frame: int):
+        self._check(_abi.lib().ssf_reserve(self._h, max_frames, max_points_per_frame), "ssf_reserve")
+
+    def seed(self, seed: int):
+        """np.random.seed(seed) for the GMM's k-means++ RandomState."""
+        self._check(_abi.lib().ssf_rng_seed(self._h, seed & 0xFFFFFFFF), "ssf_rng_seed")
+
+    def _dev(self, t, dtype):
+        if not (t.is_cuda and t.device == self.device and t.dtype == dtype and t.is_contiguous()):
+            raise SSFError(f"expected a contiguous {dtype} tensor on {self.device}")
+        return t
+
+    # ------------------------------------------------------------------ frameFeature
+    def extract_planes_batch(self, pts, off, h_off, max_points=None, point_stride=None,
+                             debug=False):
+        """cloudHandler for F frames packed in `pts` ([total, stride] f32) at offsets `off`.
+        Returns PlaneBatch (and, with debug=True, ring-ordered points, row offsets, curvature)."""
+        pts = self._dev(pts, torch.float32)
+        F = h_off.numel() - 1
+        total = int(h_off[-1])
+        sizes = (h_off[1:] - h_off[:-1])
+        mx = int(sizes.max()) if max_points is None and F > 0 else int(max_points or 0)
+        stride = pts.shape[1] if point_stride is None else point_stride
+        plane = torch.empty((max(total, 1), 4), dtype=torch.float32, device=self.device)
+        count = torch.empty(max(F, 1), dtype=torch.int32, device=self.device)
+        ring = roff = curv = None
+        if debug:
+            ring = torch.zeros((max(total, 1), 4), dtype=torch.float32, device=self.device)
+            roff = torch.zeros(max(F, 1) * (self.n_rows + 1), dtype=torch.int32, device=self.device)
+            curv = torch.zeros(max(total, 1), dtype=torch.float32, device=self.device)
+        rc = _abi.lib().ssf_extract_planes_batch(
+            self._h, _stream(self.device), F, _ptr(pts), stride, _ptr(off), total, mx,
+            _ptr(plane), _ptr(count), _ptr(ring), _ptr(roff), _ptr(curv))
+        self._check(rc, "ssf_extract_planes_batch")
+        pb = PlaneBatch(plane, count[:F], off, h_off, mx)
+        if debug:
+            return pb, ring, roff.view(max(F, 1), self.n_rows + 1)[:F], curv
+        return pb
+
+    def extract_planes(self, pts):
+        """Single frame, PointCloud2-style packed xyz [n, 3] -> plane cloud [m, 4]."""
+        pts = self._dev(pts, torch.float32)
+        n = pts.shape[0]
+        out = torch.empty((max(n, 1), 4), dtype=torch.float32, device=self.device)
+        m = C.c_int64(0)
+        rc = _abi.lib().ssf_extract_planes(self._h, _stream(self.device), _ptr(pts), n,
+                                           4 * pts.shape[1], 0, _ptr(out), C.byref(m), n)
+        self._check(rc, "ssf_extract_planes")
+        return out[:m.value]
+
+    # ------------------------------------------------------------------ lidarOdometry_onlyPC
+    def plane_table(self, pb: PlaneBatch):
+        total = pb.xyzi.shape[0]
+        normal = torch.empty((total, 3), dtype=torch.float32, device=self.device)
+        valid = torch.empty(total, dtype=torch.uint8, device=self.device)
+        rc = _abi.lib().ssf_plane_table_batch(self._h, _stream(self.device), pb.count.numel(),
+                                              _ptr(pb.xyzi), _ptr(pb.off), _ptr(pb.count),
+                                              pb.max_points, _ptr(normal), _ptr(valid))
+        self._check(rc, "ssf_plane_table_batch")
+        return normal, valid
+
+    def register(self, last: PlaneBatch, last_table, curr: PlaneBatch, pose_rel, pose_abs=None,
+                 want_log=False, want_nn=False):
+        """frameRegistration for P pairs (last[p], curr[p]).  pose_rel [P,7] f64 (q xyzw, t) is the
+        warm start in and the solution out; pose_abs [P,7] is accumulated in place if given."""
+        P = curr.count.numel()
+        pose_rel = self._dev(pose_rel, torch.float64)
+        if pose_abs is not None:
+            pose_abs = self._dev(pose_abs, torch.float64)
+        normal, valid = last_table
+        log = nlog = nn = None
+        ncorr = torch.empty(P, dtype=torch.int32, device=self.device)
+        if want_log:
+            log = torch.zeros((P, self.cfg.max_iter, 10), dtype=torch.float64, device=self.device)
+            nlog = torch.zeros(P, dtype=torch.int32, device=self.device)
+        if want_nn:
+            nn = torch.full((curr.xyzi.shape[0],), -1, dtype=torch.int32, device=self.device)
+        mx = max(last.max_points, curr.max_points)
+        rc = _abi.lib().ssf_register_batch(
+            self._h, _stream(self.device), P, _ptr(last.xyzi), _ptr(last.off), _ptr(last.count),
+            _ptr(normal), _ptr(valid), _ptr(curr.xyzi), _ptr(curr.off), _ptr(curr.count),
+            int(curr.h_off[-1]), mx, _ptr(pose_rel), _ptr(pose_abs), _ptr(log), _ptr(nlog),
+            _ptr(ncorr), _ptr(nn))
+        self._check(rc, "ssf_register_batch")
+        return dict(pose_rel=pose_rel, pose_abs=pose_abs, ncorr=ncorr, log=log, nlog=nlog, nn=nn)
+
+    # ------------------------------------------------------------------ PointCloudOdometry*.py
+    def mask_pose(self, pts, flow, off, h_off, mode="gmm", mask_in=None, draws=None,
+                  reflection=0, want_mask=True):
+        """Mask + Kabsch for F frames -> (out [F,32] f64, bg_mask [total] u8 or None)."""
+        pts = self._dev(pts, torch.float32)
+        flow = self._dev(flow, torch.float32)
+        F = h_off.numel() - 1
+        total = int(h_off[-1])
+        out = torch.empty((max(F, 1), _abi.POSE_OUT_STRIDE), dtype=torch.float64, device=self.device)
+        bg = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device) if want_mask else None
+        h_off64 = h_off.to(torch.int64).contiguous()
+        hd = None
+        if draws is not None:
+            hd = torch.as_tensor(draws, dtype=torch.float64).reshape(-1).contiguous()
+            if hd.numel() != 3 * F:
+                raise SSFError("draws must hold 3 doubles per frame")
+        if mask_in is not None:
+            mask_in = self._dev(mask_in, torch.uint8)
+        rc = _abi.lib().ssf_mask_pose_batch(
+            self._h, _stream(self.device), F, _ptr(pts), _ptr(flow), _ptr(off),
+            C.c_void_p(h_off64.data_ptr()), MASK_MODES[mode], _ptr(mask_in),
+            None if hd is None else C.c_void_p(hd.data_ptr()), int(reflection), _ptr(bg), _ptr(out))
+        self._check(rc, "ssf_mask_pose_batch")
+        return out[:F], (bg[:total] if bg is not None else None)
+
+    def accumulate_sequence(self, rel, start=None):
+        rel = self._dev(rel, torch.float64)
+        n = rel.shape[0]
+        out = torch.empty_like(rel)
+        hs = None if start is None else torch.as_tensor(start, dtype=torch.float64).contiguous()
+        rc = _abi.lib().ssf_accumulate_sequence(self._h, _stream(self.device), n, _ptr(rel),
+                                                None if hs is None else C.c_void_p(hs.data_ptr()),
+                                                _ptr(out))
+        self._check(rc, "ssf_accumulate_sequence")
+        return out
+
+
+def identity_poses(n, device):
+    p = torch.zeros((n, 7), dtype=torch.float64, device=device)
+    p[:, 3] = 1.0
+    return p

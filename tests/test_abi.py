@@ -1,0 +1,65 @@
+"""CPU-side checks of the C-ABI boundary: the library loads, exports every symbol declared in
+include/ssf_frontend.h, and the host-only entry points behave (no GPU compute is called)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "ssf_frontend.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ssf_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from ssf import _abi
+    L = _abi.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 13
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert sorted(_abi.EXPORTS) == syms
+
+
+def test_abi_version_and_profiles():
+    from ssf import _abi
+    L = _abi.lib()
+    assert L.ssf_abi_version() == 1
+    c64 = _abi.config_default(64)
+    assert (c64.n_rows, c64.plane_span, c64.row_start, c64.row_end, c64.max_iter) == (64, 25, 5, 5, 8)
+    assert c64.plane_min == np.float32(0.005) and c64.plane_max == np.float32(0.05)
+    c16 = _abi.config_default(16)
+    assert (c16.plane_span, c16.row_start, c16.row_end) == (3, 0, 0)
+    assert c16.plane_min == np.float32(0.05) and c16.plane_max == np.float32(0.15)
+    with pytest.raises(ValueError):
+        _abi.config_default(32)
+
+
+def test_error_paths_without_gpu():
+    """null context / bad args are rejected before any HIP call"""
+    from ssf import _abi
+    L = _abi.lib()
+    assert L.ssf_reserve(None, 1, 1) == _abi.SSF_E_ARG
+    assert L.ssf_rng_seed(None, 1) == _abi.SSF_E_ARG
+    assert L.ssf_extract_planes_batch(None, None, 1, None, 3, None, 0, 0, None, None, None, None, None) == _abi.SSF_E_ARG
+    assert L.ssf_last_error(None) == b"null context"
+    cfg = _abi.config_default(64)
+    cfg.n_rows = 33
+    h = C.c_void_p()
+    assert L.ssf_create(0, C.byref(cfg), C.byref(h)) == _abi.SSF_E_ARG
+
+
+def test_no_cpu_fallback_in_product_package():
+    """the product package never imports the oracle"""
+    pkg = os.path.join(REPO, "ssf-slam_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
+                txt = open(os.path.join(root, f)).read()
+                assert "oracle" not in txt.replace("oracle/ssf_oracle.c", "").replace("CPU oracle", "").replace("the oracle", "") or f == "synth.py", f

@@ -1,0 +1,134 @@
+"""lidarOdometry_onlyPC parity: HIP plane table / association / Ceres-LM and GN solve vs the
+CPU oracle.
+
+Bars: plane normals + validity bit-exact (same float QR sequence), 1-NN indices exact,
+per-iteration poses within 1e-5 m / 1e-6 rad of the oracle (f64 reductions in a different
+order), final pose likewise.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import frame
+
+pytestmark = pytest.mark.gpu
+
+TOL_T = 1e-5   # m   (BASELINE north_star)
+TOL_R = 1e-6   # rad
+
+
+def _quat_angle(q1, q2):
+    d = abs(float(np.dot(q1 / np.linalg.norm(q1), q2 / np.linalg.norm(q2))))
+    return 2.0 * np.arccos(min(1.0, d))
+
+
+def _planes(fe, dev, clouds):
+    import ssf
+    pts = torch.from_numpy(np.concatenate(clouds)).to(dev)
+    off, h_off = ssf.frame_offsets([c.shape[0] for c in clouds], dev)
+    return fe.extract_planes_batch(pts, off, h_off)
+
+
+def _sub(pb, idx):
+    import ssf
+    # per-pair start offsets + counts into the shared plane buffer; the last entry bounds the
+    # extent of the point-shaped scratch (frames are selected in ascending order)
+    starts = torch.stack([pb.off[i] for i in idx])
+    ends = torch.stack([pb.off[i + 1] for i in idx])
+    h_st = torch.tensor([int(pb.h_off[i]) for i in idx] + [int(pb.h_off[idx[-1] + 1])])
+    o = torch.cat([starts, ends[-1:]]).contiguous()
+    return ssf.PlaneBatch(pb.xyzi, pb.count[idx].contiguous(), o, h_st, pb.max_points)
+
+
+def test_plane_table_bitexact(oracle, dev):
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index)
+    clouds = [frame(0, 0)[0], frame(1, 1)[0]]
+    pb = _planes(fe, dev, clouds)
+    normal, valid = fe.plane_table(pb)
+    for f in range(2):
+        P = pb.frame(f).cpu().numpy()
+        nr, vr, _, _ = oracle.plane_table(P, 0.05)
+        o, m = int(pb.h_off[f]), P.shape[0]
+        assert np.array_equal(valid[o:o + m].cpu().numpy(), vr.astype(np.uint8))
+        g = normal[o:o + m].cpu().numpy()
+        assert np.array_equal(g.view(np.uint32), nr.view(np.uint32)), "normal bits differ"
+        assert vr.mean() > 0.3
+
+
+@pytest.mark.parametrize("solver,iters,mode", [("ceres_lm", 8, 0), ("gn", 10, 1)])
+def test_register_pair_per_step(oracle, dev, solver, iters, mode):
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index, solver=solver, max_iter=iters)
+    clouds = [frame(0, 2, n_az=1875)[0], frame(0, 3, n_az=1875)[0]]
+    pb = _planes(fe, dev, clouds)
+    table = fe.plane_table(pb)
+    last, curr = _sub(pb, [0]), _sub(pb, [1])
+    q0 = np.array([0.0, 0.0, 0.001, 1.0]); q0 /= np.linalg.norm(q0)
+    t0 = np.array([0.9, 0.01, 0.0])
+    pose = torch.tensor([[*q0, *t0]], dtype=torch.float64, device=dev)
+    res = fe.register(last, table, curr, pose, want_log=True, want_nn=True)
+    torch.cuda.synchronize()
+    L = pb.frame(0).cpu().numpy()
+    Cc = pb.frame(1).cpu().numpy()
+    nn_ref = oracle.correspond(L, Cc, q0, t0)
+    o1 = int(pb.h_off[1])
+    assert np.array_equal(res["nn"][o1:o1 + Cc.shape[0]].cpu().numpy(), nn_ref)
+    q, t, log, c = oracle.register_pair(L, Cc, 0.05, mode=mode, max_iter=iters, q_init=q0, t_init=t0)
+    assert int(res["ncorr"][0]) == c
+    nl = int(res["nlog"][0])
+    assert nl == log.shape[0], (nl, log[:, 8])
+    glog = res["log"][0, :nl].cpu().numpy()
+    for k in range(nl):
+        assert glog[k, 8] == log[k, 8], f"step {k} status differs"
+        assert np.abs(glog[k, 4:7] - log[k, 4:7]).max() < TOL_T, k
+        assert _quat_angle(glog[k, :4], log[k, :4]) < TOL_R, k
+        assert abs(glog[k, 7] - log[k, 7]) <= 1e-9 * max(1.0, abs(log[k, 7]))
+    got = res["pose_rel"][0].cpu().numpy()
+    assert np.abs(got[4:] - t).max() < TOL_T and _quat_angle(got[:4], q) < TOL_R
+
+
+def test_register_batch_and_accumulate(oracle, dev):
+    """3 independent pairs in one launch + pose accumulation (publishResult :87-90); one pair
+    whose last frame has <= 10 plane points is skipped (:158) and keeps its warm start."""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index)
+    c = frame(3, 0)[0][:64 * 12]          # 12 azimuth steps of rows 5..12 -> 8 plane points
+    r = np.arange(c.shape[0]) % 64
+    tiny = c[(r >= 5) & (r < 13)]
+    clouds = [frame(1, 0)[0], frame(1, 1)[0], frame(2, 4)[0], frame(2, 5)[0], tiny, frame(3, 1)[0]]
+    pb = _planes(fe, dev, clouds)
+    table = fe.plane_table(pb)
+    last, curr = _sub(pb, [0, 2, 4]), _sub(pb, [1, 3, 5])
+    rel = ssf.identity_poses(3, dev)
+    rel[2, 4] = 0.5
+    ab = ssf.identity_poses(3, dev)
+    ab[:, 4] = 10.0
+    res = fe.register(last, table, curr, rel, ab)
+    torch.cuda.synchronize()
+    for p, (a, b) in enumerate([(0, 1), (2, 3), (4, 5)]):
+        L, Cc = pb.frame(a).cpu().numpy(), pb.frame(b).cpu().numpy()
+        qi = [0, 0, 0, 1]; ti = [0.5 if p == 2 else 0.0, 0, 0]
+        q, t, log, c = oracle.register_pair(L, Cc, 0.05, q_init=qi, t_init=ti)
+        got = rel[p].cpu().numpy()
+        assert int(res["ncorr"][p]) == c
+        assert np.abs(got[4:] - t).max() < TOL_T and _quat_angle(got[:4], q) < TOL_R
+        qa, ta = oracle.accumulate([0, 0, 0, 1], [10.0, 0, 0], q, t)
+        ga = ab[p].cpu().numpy()
+        assert np.abs(ga[4:] - ta).max() < TOL_T and _quat_angle(ga[:4], qa) < TOL_R
+    assert pb.count[4].item() <= 10 and int(res["ncorr"][2]) == -1
+
+
+def test_accumulate_sequence(oracle, dev):
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index)
+    rng = np.random.default_rng(0)
+    rel = np.zeros((20, 7))
+    for i in range(20):
+        q = rng.normal(0, 0.01, 4); q[3] = 1.0; q /= np.linalg.norm(q)
+        rel[i, :4] = q; rel[i, 4:] = rng.normal(0, 1, 3)
+    out = fe.accumulate_sequence(torch.tensor(rel, device=dev)).cpu().numpy()
+    q, t = np.array([0, 0, 0, 1.0]), np.zeros(3)
+    for i in range(20):
+        q, t = oracle.accumulate(q, t, rel[i, :4], rel[i, 4:])
+        assert np.abs(out[i, 4:] - t).max() < 1e-12 and np.abs(out[i, :4] - q).max() < 1e-12

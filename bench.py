@@ -1,0 +1,245 @@
+"""Benchmark: LiDAR front-end frames/sec (mask + feature + GN) on synthetic 64-beam 120k-pt scans.
+
+One step = one new frame for each of B sequences in flight on this GPU, through the whole hot
+path (BASELINE.json north_star):
+  * scene-flow dynamic-point mask: GaussianMixture(2) fit + Kabsch pose + quaternion
+    (PointCloudOdometry_noSeg.py:97-125)                       -> k_mask_pose         [stream A]
+  * frameFeature: ring binning, curvature, planar selection (frameFeature.cpp:45-123)
+                                                               -> k_bin_* / k_curv_select / k_compact
+  * plane table of the new frame (it is the next step's last frame) + registration of the pair
+    (previous frame, new frame): association + 10 Gauss-Newton iterations + pose accumulation
+    (lidarOdometry_onlyPC.cpp:147-252, :87-90)                 -> k_plane_table / k_associate / k_solve
+                                                                                      [stream B]
+  * N > 1: one RCCL all_gather of the step's per-frame 6-DoF poses (weak scaling: every rank
+    owns B sequences, no other data-path collective).
+Inputs are resident in HBM before the timed region.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(REPO, "ssf-slam_amd"), REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="sequences in flight per GPU")
+    ap.add_argument("--n-az", type=int, default=1875, help="azimuth steps (64 x 1875 = 120k pts)")
+    ap.add_argument("--rows", type=int, default=64)
+    ap.add_argument("--solver", default="gn", choices=["gn", "ceres_lm"])
+    ap.add_argument("--iters", type=int, default=None)
+    ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic sequences (tiled)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=12)
+    return ap.parse_args()
+
+
+def make_data(args, dev, n_frames, rank):
+    """[n_frames] batches of B frames: pos/flow packed [B*N, 3] f32, resident in HBM."""
+    from ssf import synth
+    S = max(1, min(args.distinct, args.batch))
+    seqs = []
+    for s in range(S):
+        seq_id = rank * 1000 + s
+        sc = synth.Scene(seq_id)
+        fr = [synth.scan(seq_id, k, n_rows=args.rows, n_az=args.n_az, device=dev, scene=sc)
+              for k in range(n_frames)]
+        seqs.append(fr)
+    batches = []
+    for k in range(n_frames):
+        pos = torch.cat([seqs[b % S][k]["pos1"] for b in range(args.batch)]).contiguous()
+        flow = torch.cat([seqs[b % S][k]["flow"] for b in range(args.batch)]).contiguous()
+        batches.append((pos, flow))
+    del seqs
+    return batches
+
+
+def cpu_baseline(args):
+    """The CPU oracle (C restatement of the reference path, single thread) on a bounded sample:
+    `cpu_frames` consecutive frames of one sequence through mask + features + plane table +
+    registration, timed on this host."""
+    from oracle import oracle as O
+    from ssf import synth
+    O.lib()
+    sc = synth.Scene(0)
+    fr = [synth.scan(0, k, n_rows=args.rows, n_az=args.n_az, scene=sc) for k in range(args.cpu_frames + 1)]
+    prof = O.profile(args.rows)
+    mode = O.MODE_GN if args.solver == "gn" else O.MODE_CERES_LM
+    iters = args.iters or (10 if args.solver == "gn" else 8)
+    last = O.extract_planes(fr[0]["pos1"].numpy(), args.rows)
+    q, t = np.array([0, 0, 0, 1.0]), np.zeros(3)
+    t0 = time.perf_counter()
+    for k in range(1, args.cpu_frames + 1):
+        p, f = fr[k]["pos1"].numpy(), fr[k]["flow"].numpy()
+        O.mask_and_pose(p, f, [0.3, 0.6, 0.9])
+        curr = O.extract_planes(p, args.rows)
+        q, t, _, _ = O.register_pair(last, curr, prof.plane_max, mode=mode, max_iter=iters, q_init=q, t_init=t)
+        last = curr
+    el = time.perf_counter() - t0
+    return dict(value=args.cpu_frames / el, unit="frames/s", cores=1, kind="port",
+                sample=f"{args.cpu_frames} consecutive {args.rows}-beam {args.rows * args.n_az}-pt frames "
+                       f"(mask+features+plane table+{args.solver} x{iters}) through oracle/ssf_oracle.c, "
+                       f"1 thread, {el:.2f} s")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.warmup < 1:
+        args.warmup = 1  # the first frame of a sequence has no last frame to register against
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    import ssf
+    iters = args.iters or (10 if args.solver == "gn" else 8)
+    B, N = args.batch, args.rows * args.n_az
+    n_frames = args.warmup + args.steps + 1
+    batches = make_data(args, dev, n_frames, rank)
+    off, h_off = ssf.frame_offsets([N] * B, dev)
+    fe_mask = ssf.Frontend(args.rows, device=local)
+    fe_feat = ssf.Frontend(args.rows, device=local, solver=args.solver, max_iter=iters)
+    fe_mask.reserve(B, N)
+    fe_feat.reserve(B, N)
+    fe_mask.seed(20240000 + rank)
+    s_mask = torch.cuda.Stream(dev)
+    s_feat = torch.cuda.Stream(dev)
+    # per-step outputs (double-buffered plane clouds: last <- curr)
+    pose_rel = ssf.identity_poses(B, dev)
+    pose_abs = ssf.identity_poses(B, dev)
+    mask_out = [None] * n_frames
+    gathered = []
+    ev = {k: [] for k in ("mask", "feat", "table", "reg")}
+    state = {"last": None, "last_table": None}
+
+    def step(k, timing):
+        pos, flow = batches[k]
+        with torch.cuda.stream(s_mask):
+            e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(s_mask)
+            out, bg = fe_mask.mask_pose(pos, flow, off, h_off, mode="gmm", want_mask=True)
+            e1.record(s_mask)
+            mask_out[k] = out
+        with torch.cuda.stream(s_feat):
+            es = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            es[0].record(s_feat)
+            pb = fe_feat.extract_planes_batch(pos, off, h_off, max_points=N)
+            es[1].record(s_feat)
+            table = fe_feat.plane_table(pb)
+            es[2].record(s_feat)
+            if state["last"] is not None:
+                fe_feat.register(state["last"], state["last_table"], pb, pose_rel, pose_abs)
+            es[3].record(s_feat)
+        state["last"], state["last_table"] = pb, table
+        cur = torch.cuda.current_stream(dev)
+        cur.wait_stream(s_mask)
+        cur.wait_stream(s_feat)
+        if world > 1:
+            poses = torch.cat([pose_abs, mask_out[k][:, 0:7]], 1).contiguous()  # [B, 14]
+            bufs = [torch.empty_like(poses) for _ in range(world)]
+            dist.all_gather(bufs, poses)
+            gathered.append(bufs)
+        if timing:
+            ev["mask"].append((e0, e1)); ev["feat"].append((es[0], es[1]))
+            ev["table"].append((es[1], es[2])); ev["reg"].append((es[2], es[3]))
+
+    for k in range(args.warmup):
+        step(k, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.warmup, args.warmup + args.steps):
+        step(k, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- per-kernel timing (HIP events on the launching streams) + algorithmic bytes
+    def avg_ms(pairs):
+        return float(np.mean([a.elapsed_time(b) for a, b in pairs]))
+
+    mask_ms = avg_ms(ev["mask"])
+    feat_ms = avg_ms(ev["feat"])
+    table_ms = avg_ms(ev["table"])
+    reg_ms = avg_ms(ev["reg"])
+    passes = torch.stack([mask_out[k][:, 25] for k in range(args.warmup, args.warmup + args.steps)])
+    status = torch.stack([mask_out[k][:, 16] for k in range(args.warmup, args.warmup + args.steps)])
+    mean_passes = float(passes.mean())
+    # k_mask_pose: every pass streams [flow, xyz] float32 (24 B/pt); + 1 B/pt mask write
+    mask_bytes = B * N * (24.0 * mean_passes + 1.0)
+    # frameFeature chain: bin_count 12 R + 1 W, bin_scatter 13 R + 16 W, curv_select 16 R + 4 W(sel)
+    feat_bytes = B * N * (12 + 1 + 13 + 16 + 16) * 1.0
+    kernels = {
+        "k_mask_pose": dict(ms=mask_ms, bytes=mask_bytes, gbs=mask_bytes / mask_ms / 1e6,
+                            passes_per_frame=mean_passes),
+        "features(5 kernels)": dict(ms=feat_ms, bytes=feat_bytes, gbs=feat_bytes / feat_ms / 1e6),
+        "plane_table": dict(ms=table_ms),
+        "register(assoc+solve)": dict(ms=reg_ms),
+    }
+    dom = max(kernels, key=lambda k: kernels[k]["ms"])
+    total_frames = B * args.steps * world
+    value = total_frames / elapsed
+    line = {
+        "metric": "LiDAR front-end frames/sec (mask+feature+GN), 64-beam 120k pts, 1/2/4/8 GPUs",
+        "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32 features / f64 mask+solve",
+        "data": "synthetic (seeded ray-cast 64-beam scans, ssf/synth.py)",
+        "config": {"workload": f"{B} sequences in flight per GPU x {args.rows}-beam {N}-pt scans; "
+                               f"mask(GMM+Kabsch) + features + plane table + {args.solver} x{iters}",
+                   "sequences_per_gpu": B, "points_per_frame": N, "solver": args.solver,
+                   "iters": iters, "parallelism": f"sequence-sharded x{world}"},
+        "roofline": None, "cpu_baseline": None, "kernels": kernels,
+        "mask_status_nonzero": int((status != 0).sum()),
+    }
+    if "k_mask_pose" == dom:
+        achieved = mask_bytes / (mask_ms * 1e-3) / 1e9
+        line["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_mask_pose"}
+    else:
+        k = kernels[dom]
+        b = k.get("bytes")
+        if b:
+            achieved = b / (k["ms"] * 1e-3) / 1e9
+            line["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                                "kernel": dom}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

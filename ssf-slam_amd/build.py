@@ -18,6 +18,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: no FMA contraction, so float stages match the reference's x86 arithmetic
 # (and the CPU oracle) bit for bit.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-Wall"]
+# The f64 GMM/Kabsch kernel is compared with tolerances (labels, iteration counts, 1e-5 m), not
+# bit for bit, so it may contract multiply-adds into FMAs (half the f64 instructions).
+FILE_FLAGS = {"mask_pose.hip": ["-ffp-contract=fast"]}
 
 
 def _stale(target, deps):
@@ -37,7 +40,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         o = os.path.join(OBJ_DIR, src.replace(".hip", ".o"))
         objs.append(o)
         if force or _stale(o, [s] + hdrs):
-            jobs.append([HIPCC, *FLAGS, "-c", s, "-o", o])
+            jobs.append([HIPCC, *FLAGS, *FILE_FLAGS.get(src, []), "-c", s, "-o", o])
 
     def run(cmd):
         if verbose:

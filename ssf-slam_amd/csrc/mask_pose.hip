@@ -26,17 +26,21 @@ constexpr int kMaskThreads = 512;
 constexpr int kNW = kMaskThreads / 64;
 constexpr double kPi = 3.14159265358979323846;
 
+// packed upper-triangular index of a 6x6 matrix (row i <= col j)
+SSF_DEV constexpr int up(int i, int j) { return i * 6 - (i * (i - 1)) / 2 + (j - i); }
+
+// Everything lane 0 touches between passes lives here, in LDS: no private arrays, so the
+// streaming passes keep the whole VGPR budget (1024 threads -> <= 128 VGPRs per lane).
 struct MaskShared {
     double mean[6], tol;
+    double tot[28];            // {N, sum(x-mean)[6], sum(x-mean)(x-mean)^T [21 packed]}
     double cen[12], csn[2];
-    double mu[12], U[72], logdet[2], logw[2];
-    double rand1, rand2, pot;
-    double lb, prev_lb;
-    double kab[32];
-    int64_t c0, cand[2], c1;
-    int64_t n1;
+    double mu[12], U[42], cU[12], logdet[2], logw[2];  // U: packed upper precision Cholesky per comp; cU = mu U
+    double rand1, rand2;
+    double lb;
+    double C[36], L[36], Li[36];  // lane-0 scratch for the 6x6 algebra
+    int64_t c0, c1;
     int km_iter, em_iter, strict, converged, done, status, passes, label0, bg;
-    double red_tmp[64];
 };
 
 SSF_DEV void load_x(const float* __restrict__ P, const float* __restrict__ Fl, int64_t i, double x[6]) {
@@ -44,10 +48,11 @@ SSF_DEV void load_x(const float* __restrict__ P, const float* __restrict__ Fl, i
     x[3] = (double)P[3 * i];  x[4] = (double)P[3 * i + 1];  x[5] = (double)P[3 * i + 2];
 }
 
-// lane-0 helpers -----------------------------------------------------------------------------
-SSF_DEV int prec_chol6(const double C[36], double U[36], double* logdet) {
-    double L[36];
-    for (int k = 0; k < 36; ++k) L[k] = 0.0;
+// lane-0: covariance S.C (6x6) -> precision Cholesky (packed upper) U_out, log det.
+// scipy linalg.cholesky(lower) + solve_triangular(L, I).T as sklearn _compute_precision_cholesky.
+__device__ __noinline__ int prec_chol6(MaskShared& S, double* U_out, double* logdet) {
+    double* C = S.C; double* L = S.L; double* Li = S.Li;
+    for (int k = 0; k < 36; ++k) { L[k] = 0.0; Li[k] = 0.0; }
     for (int j = 0; j < 6; ++j) {
         double s = C[j * 6 + j];
         for (int k = 0; k < j; ++k) s -= L[j * 6 + k] * L[j * 6 + k];
@@ -59,8 +64,6 @@ SSF_DEV int prec_chol6(const double C[36], double U[36], double* logdet) {
             L[i * 6 + j] = v / L[j * 6 + j];
         }
     }
-    double Li[36];
-    for (int k = 0; k < 36; ++k) Li[k] = 0.0;
     for (int c = 0; c < 6; ++c)
         for (int i = c; i < 6; ++i) {
             double v = (i == c) ? 1.0 : 0.0;
@@ -69,58 +72,81 @@ SSF_DEV int prec_chol6(const double C[36], double U[36], double* logdet) {
         }
     double ld = 0.0;
     for (int i = 0; i < 6; ++i)
-        for (int j = 0; j < 6; ++j) U[i * 6 + j] = Li[j * 6 + i];
-    for (int i = 0; i < 6; ++i) ld += log(U[i * 6 + i]);
+        for (int j = i; j < 6; ++j) U_out[up(i, j)] = Li[j * 6 + i];
+    for (int i = 0; i < 6; ++i) ld += log(Li[i * 6 + i]);
     *logdet = ld;
     return 0;
 }
 
-// sklearn _estimate_gaussian_parameters from shifted moments: per component k the block
-// acc[k*28 + ...] = {sum r, S1[6] = sum r (x - s), S2[21] = sum r (x - s)(x - s)^T (packed)}.
-SSF_DEV int gmm_params(MaskShared& S, const double* acc, const double* shift, int init, int64_t n) {
+// lane-0: sklearn _estimate_gaussian_parameters from moments about the common shift s = S.mean.
+// comp1 = {sum r1, sum r1 (x-s), sum r1 (x-s)(x-s)^T};  comp0 = S.tot - comp1 (r0 = 1 - r1).
+__device__ __noinline__ int gmm_params(MaskShared& S, const double* comp1, int init, int64_t n) {
     const double eps10 = 10.0 * DBL_EPSILON;
     double nk[2];
     for (int k = 0; k < 2; ++k) {
-        const double* a = acc + 28 * k;
-        const double* s = shift + 6 * k;
+        double a[28];
+        for (int i = 0; i < 28; ++i) a[i] = k == 1 ? comp1[i] : S.tot[i] - comp1[i];
         nk[k] = a[0] + eps10;
-        double mu[6], d[6];
+        double d[6];
         for (int i = 0; i < 6; ++i) {
-            mu[i] = (a[0] * s[i] + a[1 + i]) / nk[k];
-            d[i] = mu[i] - s[i];
+            const double mu = (a[0] * S.mean[i] + a[1 + i]) / nk[k];
+            S.mu[6 * k + i] = mu;
+            d[i] = mu - S.mean[i];
         }
-        double C[36];
-        int p = 0;
         for (int i = 0; i < 6; ++i)
-            for (int j = i; j < 6; ++j, ++p) {
-                double v = a[7 + p] - a[1 + i] * d[j] - d[i] * a[1 + j] + a[0] * d[i] * d[j];
+            for (int j = i; j < 6; ++j) {
+                double v = a[7 + up(i, j)] - a[1 + i] * d[j] - d[i] * a[1 + j] + a[0] * d[i] * d[j];
                 v = v / nk[k];
-                C[i * 6 + j] = v; C[j * 6 + i] = v;
+                S.C[i * 6 + j] = v; S.C[j * 6 + i] = v;
             }
-        for (int i = 0; i < 6; ++i) C[i * 6 + i] += 1e-6;
-        if (prec_chol6(C, S.U + 36 * k, &S.logdet[k]) != 0) return -1;
-        for (int i = 0; i < 6; ++i) S.mu[6 * k + i] = mu[i];
+        for (int i = 0; i < 6; ++i) S.C[i * 6 + i] += 1e-6;
+        if (prec_chol6(S, S.U + 21 * k, &S.logdet[k]) != 0) return -1;
     }
     double w0, w1;
     if (init) { w0 = nk[0] / (double)n; w1 = nk[1] / (double)n; }
     else { const double s = nk[0] + nk[1]; w0 = nk[0] / s; w1 = nk[1] / s; }
     S.logw[0] = log(w0); S.logw[1] = log(w1);
+    for (int k = 0; k < 2; ++k)
+        for (int j = 0; j < 6; ++j) {
+            double c = 0.0;
+            for (int i = 0; i <= j; ++i) c += S.mu[6 * k + i] * S.U[21 * k + up(i, j)];
+            S.cU[6 * k + j] = c;
+        }
     return 0;
 }
 
-// U is read straight from LDS on every use (volatile): keeping both 6x6 precision factors in
-// registers next to the 57 moment accumulators would overflow the 256-VGPR budget.
-SSF_DEV double wlp(const double x[6], const double* mu, const volatile double* U, double logdet,
-                   double logw) {
+// weighted log probability, sklearn _estimate_log_gaussian_prob form: y = x U - (mu U), with
+// c = mu U precomputed by lane 0 (S.cU); U packed upper.
+SSF_DEV double wlp(const double x[6], const double* U, const double* c, double logdet, double logw) {
     double lp = 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
         double y = 0.0;
 #pragma unroll
-        for (int i = 0; i <= j; ++i) y += (x[i] - mu[i]) * U[i * 6 + j];
+        for (int i = 0; i <= j; ++i) y += x[i] * U[up(i, j)];
+        y -= c[j];
         lp += y * y;
     }
     return -0.5 * (6.0 * log(2.0 * kPi) + lp) + logdet + logw;
+}
+
+// Streams the frame's points through f(i, x): every thread keeps the NEXT point's loads in
+// flight while it computes the current one (one wave per SIMD pair cannot hide HBM latency
+// otherwise).
+template <class Fn>
+SSF_DEV void for_points(const float* __restrict__ P, const float* __restrict__ Fl, int64_t n, Fn&& fn) {
+    const int64_t T = blockDim.x;
+    int64_t i = threadIdx.x;
+    if (i >= n) return;
+    double xn[6];
+    load_x(P, Fl, i, xn);
+    for (; i < n; i += T) {
+        double x[6];
+#pragma unroll
+        for (int d = 0; d < 6; ++d) x[d] = xn[d];
+        if (i + T < n) load_x(P, Fl, i + T, xn);
+        fn(i, x);
+    }
 }
 
 SSF_DEV double lse2(double a, double b) {  // scipy 1.15 logsumexp on two terms
@@ -130,7 +156,7 @@ SSF_DEV double lse2(double a, double b) {  // scipy 1.15 logsumexp on two terms
     return log1p(exp(mn - mx)) + mx;
 }
 
-SSF_DEV void svd3(const double A[9], double U[9], double Sv[3], double Vt[9]) {
+__device__ __noinline__ void svd3(const double A[9], double U[9], double Sv[3], double Vt[9]) {
     double a[3][3], v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
     for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) a[i][j] = A[i * 3 + j];
     for (int sweep = 0; sweep < 60; ++sweep) {
@@ -182,7 +208,7 @@ SSF_DEV void svd3(const double A[9], double U[9], double Sv[3], double Vt[9]) {
 }
 
 // Kabsch from shifted sums k[16] = {cnt, sum(s-cs)[3], sum(d-cd)[3], sum (s-cs)(d-cd)^T [9]}.
-SSF_DEV int kabsch_finish(const double* k, const double cs[3], const double cd[3], int reflection,
+__device__ __noinline__ int kabsch_finish(const double* k, const double cs[3], const double cd[3], int reflection,
                           double* out) {
     const double n = k[0];
     if (!(n > 0.0)) return SSF_POSE_EMPTY;
@@ -261,7 +287,7 @@ SSF_DEV int kabsch_finish(const double* k, const double cs[3], const double cd[3
     return status;
 }
 
-SSF_DEV void accum_kabsch(double (&k)[16], const double x[6], const double cs[3], const double cd[3]) {
+SSF_DEV void accum_kabsch(double (&k)[16], const double* x, const double cs[3], const double cd[3]) {
     double s[3], d[3];
     for (int i = 0; i < 3; ++i) { d[i] = x[3 + i] - cd[i]; s[i] = (x[3 + i] + x[i]) - cs[i]; }
     k[0] += 1.0;
@@ -279,9 +305,9 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     const double* __restrict__ draws, int reflection, uint8_t* __restrict__ bg_mask,
     double* __restrict__ out_all, double* __restrict__ dist, uint8_t* __restrict__ lab) {
     __shared__ MaskShared S;
-    __shared__ double red[kNW * 60];
+    __shared__ double red[kNW * 32];
     __shared__ int ired[kNW];
-    __shared__ int64_t cand_lds[2];
+    __shared__ unsigned long long cand_lds[2];
     const int f = blockIdx.x, tid = threadIdx.x;
     const int64_t fb = frame_off[f], n = frame_off[f + 1] - fb;
     const float* P = pts + 3 * fb;
@@ -330,26 +356,35 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         return;
     }
 
-    // ---- pass 0: column means / variances (shift by point 0 for accuracy)
+    // ---- pass 0: column means, variances (KMeans tol) and the total first/second moments
+    //      about point 0, converted by lane 0 to moments about the mean (the common shift of
+    //      every later moment sum).
     {
         double x0[6];
         load_x(P, Fl, 0, x0);
-        double a[12];
-        for (int i = 0; i < 12; ++i) a[i] = 0.0;
-        for (int64_t i = tid; i < n; i += blockDim.x) {
-            double x[6];
-            load_x(P, Fl, i, x);
+        double a[27];
 #pragma unroll
-            for (int d = 0; d < 6; ++d) { const double v = x[d] - x0[d]; a[d] += v; a[6 + d] += v * v; }
-        }
-        block_sum<12>(a, red);
+        for (int i = 0; i < 27; ++i) a[i] = 0.0;
+        for_points(P, Fl, n, [&](int64_t i, const double* x) {
+            double v[6];
+#pragma unroll
+            for (int d = 0; d < 6; ++d) { v[d] = x[d] - x0[d]; a[d] += v[d]; }
+#pragma unroll
+            for (int r = 0; r < 6; ++r)
+#pragma unroll
+                for (int c = r; c < 6; ++c) a[6 + up(r, c)] += v[r] * v[c];
+        });
+        block_sum<27>(a, red);
         if (tid == 0) {
+            const double nn = (double)n;
+            double m[6];
             double tol = 0.0;
-            for (int d = 0; d < 6; ++d) {
-                const double m = a[d] / (double)n;
-                S.mean[d] = x0[d] + m;
-                tol += a[6 + d] / (double)n - m * m;
-            }
+            for (int d = 0; d < 6; ++d) { m[d] = a[d] / nn; S.mean[d] = x0[d] + m[d]; }
+            S.tot[0] = nn;
+            for (int d = 0; d < 6; ++d) S.tot[1 + d] = a[d] - nn * m[d];
+            for (int r = 0; r < 6; ++r)
+                for (int c = r; c < 6; ++c) S.tot[7 + up(r, c)] = a[6 + up(r, c)] - nn * m[r] * m[c];
+            for (int d = 0; d < 6; ++d) tol += S.tot[7 + up(d, d)] / nn;
             S.tol = tol / 6.0 * 1e-4;
             S.c0 = (int64_t)draws[3 * f];
             if (S.c0 < 0) S.c0 = 0;
@@ -371,21 +406,20 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             for (int d = 0; d < 6; ++d) { c0[d] = x[d] - mean[d]; cn0 += c0[d] * c0[d]; }
         }
         double pot = 0.0;
-        for (int64_t i = tid; i < n; i += blockDim.x) {
-            double x[6], dt = 0.0, xs = 0.0;
-            load_x(P, Fl, i, x);
+        for_points(P, Fl, n, [&](int64_t i, const double* x) {
+            double dt = 0.0, xs = 0.0;
 #pragma unroll
             for (int d = 0; d < 6; ++d) { const double v = x[d] - mean[d]; dt += c0[d] * v; xs += v * v; }
             double v = (-2.0 * dt + cn0) + xs;
             v = v > 0.0 ? v : 0.0;
             D[i] = v;
             pot += v;
-        }
+        });
         pot = block_sum_scalar<double>(pot, red);
         if (tid == 0) {
             S.rand1 = draws[3 * f + 1] * pot;
             S.rand2 = draws[3 * f + 2] * pot;
-            cand_lds[0] = n; cand_lds[1] = n;
+            cand_lds[0] = (unsigned long long)n; cand_lds[1] = (unsigned long long)n;
             S.passes += 1;
         }
         __syncthreads();
@@ -409,15 +443,16 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             double tot = carry;
             for (int k = 0; k < kNW; ++k) tot += red[k];
             if (i < n) {
-                if (incl >= r1) atomicMin((unsigned long long*)&cand_lds[0], (unsigned long long)i);
-                if (incl >= r2) atomicMin((unsigned long long*)&cand_lds[1], (unsigned long long)i);
+                if (incl >= r1) atomicMin(&cand_lds[0], (unsigned long long)i);
+                if (incl >= r2) atomicMin(&cand_lds[1], (unsigned long long)i);
             }
             __syncthreads();
             carry = tot;
-            if (cand_lds[0] < n && cand_lds[1] < n) break;  // uniform (read after barrier)
+            if (cand_lds[0] < (unsigned long long)n && cand_lds[1] < (unsigned long long)n) break;
         }
         __syncthreads();
-        int64_t cand[2] = {cand_lds[0] < n ? cand_lds[0] : n - 1, cand_lds[1] < n ? cand_lds[1] : n - 1};
+        const int64_t cand[2] = {cand_lds[0] < (unsigned long long)n ? (int64_t)cand_lds[0] : n - 1,
+                                 cand_lds[1] < (unsigned long long)n ? (int64_t)cand_lds[1] : n - 1};
         double cc[2][6], ccn[2] = {0.0, 0.0};
         for (int j = 0; j < 2; ++j) {
             double x[6];
@@ -425,9 +460,8 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             for (int d = 0; d < 6; ++d) { cc[j][d] = x[d] - mean[d]; ccn[j] += cc[j][d] * cc[j][d]; }
         }
         double cp[2] = {0.0, 0.0};
-        for (int64_t i = tid; i < n; i += blockDim.x) {
-            double x[6], xs = 0.0, dt0 = 0.0, dt1 = 0.0;
-            load_x(P, Fl, i, x);
+        for_points(P, Fl, n, [&](int64_t i, const double* x) {
+            double xs = 0.0, dt0 = 0.0, dt1 = 0.0;
 #pragma unroll
             for (int d = 0; d < 6; ++d) {
                 const double v = x[d] - mean[d];
@@ -438,7 +472,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             const double di = D[i];
             cp[0] += v0 < di ? v0 : di;
             cp[1] += v1 < di ? v1 : di;
-        }
+        });
         block_sum<2>(cp, red);
         if (tid == 0) {
             const int best = cp[1] < cp[0] ? 1 : 0;
@@ -460,16 +494,16 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             }
         }
         __syncthreads();
-        double cen[12], csn0 = S.csn[0], csn1 = S.csn[1];
+        double cen[12];
+        const double csn0 = S.csn[0], csn1 = S.csn[1];
 #pragma unroll
         for (int k = 0; k < 12; ++k) cen[k] = S.cen[k];
         double acc[14];
 #pragma unroll
         for (int k = 0; k < 14; ++k) acc[k] = 0.0;
         int changed = 0;
-        for (int64_t i = tid; i < n; i += blockDim.x) {
-            double x[6], v[6], dt0 = 0.0, dt1 = 0.0;
-            load_x(P, Fl, i, x);
+        for_points(P, Fl, n, [&](int64_t i, const double* x) {
+            double v[6], dt0 = 0.0, dt1 = 0.0;
 #pragma unroll
             for (int d = 0; d < 6; ++d) {
                 v[d] = x[d] - mean[d];
@@ -479,16 +513,11 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             const int l = e1 < e0 ? 1 : 0;
             changed += (Lb[i] != (uint8_t)l) || it == 0;
             Lb[i] = (uint8_t)l;
-            if (l == 0) {
-                acc[0] += 1.0;
+            const double w1 = (double)l, w0 = 1.0 - w1;
+            acc[0] += w0; acc[7] += w1;
 #pragma unroll
-                for (int d = 0; d < 6; ++d) acc[1 + d] += v[d];
-            } else {
-                acc[7] += 1.0;
-#pragma unroll
-                for (int d = 0; d < 6; ++d) acc[8 + d] += v[d];
-            }
-        }
+            for (int d = 0; d < 6; ++d) { acc[1 + d] += w0 * v[d]; acc[8 + d] += w1 * v[d]; }
+        });
         block_sum<14>(acc, red);
         changed = block_sum_scalar<int>(changed, ired);
         if (tid == 0) {
@@ -514,109 +543,92 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         if (S.done) break;
     }
 
-    // ---- GMM init from one-hot k-means labels (relabel first if not strictly converged)
+    // ---- GMM init from one-hot k-means labels (relabel first if not strictly converged);
+    //      only cluster 1's moments are summed, cluster 0 = total - cluster 1.
     {
         const int strict = S.strict;
-        double cen[12], csn0 = 0.0, csn1 = 0.0, sh[12];
+        double cen[12], csn0 = 0.0, csn1 = 0.0;
 #pragma unroll
         for (int k = 0; k < 12; ++k) cen[k] = S.cen[k];
         for (int d = 0; d < 6; ++d) { csn0 += cen[d] * cen[d]; csn1 += cen[6 + d] * cen[6 + d]; }
-        for (int k = 0; k < 2; ++k) for (int d = 0; d < 6; ++d) sh[6 * k + d] = cen[6 * k + d] + mean[d];
-        double acc[56];
+        double acc[28];
 #pragma unroll
-        for (int k = 0; k < 56; ++k) acc[k] = 0.0;
-        for (int64_t i = tid; i < n; i += blockDim.x) {
-            double x[6];
-            load_x(P, Fl, i, x);
+        for (int k = 0; k < 28; ++k) acc[k] = 0.0;
+        for_points(P, Fl, n, [&](int64_t i, const double* x) {
+            double v[6];
+#pragma unroll
+            for (int d = 0; d < 6; ++d) v[d] = x[d] - mean[d];
             int l;
             if (strict) {
                 l = Lb[i];
             } else {
                 double dt0 = 0.0, dt1 = 0.0;
 #pragma unroll
-                for (int d = 0; d < 6; ++d) { const double v = x[d] - mean[d]; dt0 += v * cen[d]; dt1 += v * cen[6 + d]; }
+                for (int d = 0; d < 6; ++d) { dt0 += v[d] * cen[d]; dt1 += v[d] * cen[6 + d]; }
                 l = (-2.0 * dt1 + csn1) < (-2.0 * dt0 + csn0) ? 1 : 0;
             }
-            double v[6];
-            const int o = l ? 28 : 0;
-            const double* s = l ? sh + 6 : sh;
+            const double w1 = (double)l;
+            acc[0] += w1;
 #pragma unroll
-            for (int d = 0; d < 6; ++d) v[d] = x[d] - s[d];
-            if (l == 0) {
-                acc[0] += 1.0;
-                int p = 0;
+            for (int a = 0; a < 6; ++a) {
+                const double wv = w1 * v[a];
+                acc[1 + a] += wv;
 #pragma unroll
-                for (int a = 0; a < 6; ++a) {
-                    acc[1 + a] += v[a];
-#pragma unroll
-                    for (int b = a; b < 6; ++b, ++p) acc[7 + p] += v[a] * v[b];
-                }
-            } else {
-                acc[28] += 1.0;
-                int p = 0;
-#pragma unroll
-                for (int a = 0; a < 6; ++a) {
-                    acc[29 + a] += v[a];
-#pragma unroll
-                    for (int b = a; b < 6; ++b, ++p) acc[35 + p] += v[a] * v[b];
-                }
+                for (int b = a; b < 6; ++b) acc[7 + up(a, b)] += wv * v[b];
             }
-            (void)o;
-        }
-        block_sum<56>(acc, red);
+        });
+        block_sum<28>(acc, red);
         if (tid == 0) {
             S.passes += 1;
-            if (gmm_params(S, acc, sh, 1, n) != 0) S.status = SSF_POSE_GMM_FAILED;
+            if (gmm_params(S, acc, 1, n) != 0) S.status = SSF_POSE_GMM_FAILED;
             S.lb = -__builtin_inf();
             S.done = 0;
         }
         __syncthreads();
     }
 
-    // ---- EM: fused E-step + next M-step moments, one pass per iteration
+    // ---- EM: one fused pass per iteration -- E-step with the current parameters and the
+    //      M-step moments of component 1 (component 0 = total - component 1).
+    //      r_max = 1/(1+e), r_min = e/(1+e), lse = max + log1p(e), e = exp(min - max): the
+    //      scipy logsumexp expression, one exp + one log1p per point.
     for (int it = 1; it <= 100 && S.status == 0; ++it) {
-        double mu[12];
         const double ld0 = S.logdet[0], lw0 = S.logw[0], ld1 = S.logdet[1], lw1 = S.logw[1];
-        const volatile double* U = S.U;
+        double acc[29];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) mu[k] = S.mu[k];
-        double acc[57];
+        for (int k = 0; k < 29; ++k) acc[k] = 0.0;
+        for_points(P, Fl, n, [&](int64_t, const double* x) {
+            // U / cU are re-read from LDS (broadcast ds_reads) for every point: the laundered
+            // offset stops the compiler hoisting 54 loop-invariant doubles into VGPRs.
+            int z = 0;
+            asm volatile("" : "+s"(z));
+            const double* U = S.U + z;
+            const double* cU = S.cU + z;
+            const double a0 = wlp(x, U, cU, ld0, lw0);
+            const double a1 = wlp(x, U + 21, cU + 6, ld1, lw1);
+            const double mx = a0 > a1 ? a0 : a1, mn = a0 > a1 ? a1 : a0;
+            const double e = exp(mn - mx);
+            acc[28] += mx + log1p(e);
+            const double inv = 1.0 / (1.0 + e);
+            const double r1 = a1 > a0 ? inv : e * inv;
+            acc[0] += r1;
+            double v[6];
 #pragma unroll
-        for (int k = 0; k < 57; ++k) acc[k] = 0.0;
-        for (int64_t i = tid; i < n; i += blockDim.x) {
-            double x[6];
-            load_x(P, Fl, i, x);
-            const double a0 = wlp(x, mu, U, ld0, lw0);
-            const double a1 = wlp(x, mu + 6, U + 36, ld1, lw1);
-            const double l = lse2(a0, a1);
-            acc[56] += l;
-            const double r[2] = {exp(a0 - l), exp(a1 - l)};
+            for (int a = 0; a < 6; ++a) v[a] = x[a] - mean[a];
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                double v[6];
+            for (int a = 0; a < 6; ++a) {
+                const double rv = r1 * v[a];
+                acc[1 + a] += rv;
 #pragma unroll
-                for (int d = 0; d < 6; ++d) v[d] = x[d] - mu[6 * k + d];
-                double* A = acc + 28 * k;
-                A[0] += r[k];
-                int p = 0;
-#pragma unroll
-                for (int a = 0; a < 6; ++a) {
-                    const double rv = r[k] * v[a];
-                    A[1 + a] += rv;
-#pragma unroll
-                    for (int b = a; b < 6; ++b, ++p) A[7 + p] += rv * v[b];
-                }
+                for (int b = a; b < 6; ++b) acc[7 + up(a, b)] += rv * v[b];
             }
-        }
-        block_sum<57>(acc, red);
+        });
+        block_sum<29>(acc, red);
         if (tid == 0) {
             S.passes += 1;
             S.em_iter = it;
             const double prev = S.lb;
-            S.lb = acc[56] / (double)n;
-            double shift[12];
-            for (int k = 0; k < 12; ++k) shift[k] = S.mu[k];
-            if (gmm_params(S, acc, shift, 0, n) != 0) S.status = SSF_POSE_GMM_FAILED;
+            S.lb = acc[28] / (double)n;
+            if (gmm_params(S, acc, 0, n) != 0) S.status = SSF_POSE_GMM_FAILED;
             if (fabs(S.lb - prev) < 1e-3) { S.converged = 1; S.done = 1; }
         }
         __syncthreads();
@@ -625,28 +637,28 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
 
     // ---- final E-step labels + per-label Kabsch sums
     {
-        double mu[12];
         const double ld0 = S.logdet[0], lw0 = S.logw[0], ld1 = S.logdet[1], lw1 = S.logw[1];
-        const volatile double* U = S.U;
-#pragma unroll
-        for (int k = 0; k < 12; ++k) mu[k] = S.mu[k];
         double cs[6], cd[6];
         for (int k = 0; k < 2; ++k)
-            for (int i = 0; i < 3; ++i) { cd[3 * k + i] = mu[6 * k + 3 + i]; cs[3 * k + i] = mu[6 * k + 3 + i] + mu[6 * k + i]; }
+            for (int i = 0; i < 3; ++i) { cd[3 * k + i] = S.mu[6 * k + 3 + i]; cs[3 * k + i] = S.mu[6 * k + 3 + i] + S.mu[6 * k + i]; }
         double k0[16], k1[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) { k0[i] = 0.0; k1[i] = 0.0; }
-        for (int64_t i = tid; i < n; i += blockDim.x) {
-            double x[6];
-            load_x(P, Fl, i, x);
-            const double a0 = wlp(x, mu, U, ld0, lw0);
-            const double a1 = wlp(x, mu + 6, U + 36, ld1, lw1);
+        for_points(P, Fl, n, [&](int64_t i, const double* x) {
+            // U / cU are re-read from LDS (broadcast ds_reads) for every point: the laundered
+            // offset stops the compiler hoisting 54 loop-invariant doubles into VGPRs.
+            int z = 0;
+            asm volatile("" : "+s"(z));
+            const double* U = S.U + z;
+            const double* cU = S.cU + z;
+            const double a0 = wlp(x, U, cU, ld0, lw0);
+            const double a1 = wlp(x, U + 21, cU + 6, ld1, lw1);
             const int l = a1 > a0 ? 1 : 0;
             Lb[i] = (uint8_t)l;
             if (i == 0) S.label0 = l;
             if (l) accum_kabsch(k1, x, cs + 3, cd + 3);
             else accum_kabsch(k0, x, cs, cd);
-        }
+        });
         block_sum<16>(k0, red);
         block_sum<16>(k1, red);
         if (tid == 0) {

@@ -46,7 +46,9 @@ def parse():
     ap.add_argument("--iters", type=int, default=None)
     ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic sequences (tiled)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=12)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="CPU baseline sample: run the oracle for at least this long (bounded)")
+    ap.add_argument("--serial", action="store_true", help="one stream (per-kernel timing without overlap)")
     return ap.parse_args()
 
 
@@ -72,28 +74,34 @@ def make_data(args, dev, n_frames, rank):
 
 def cpu_baseline(args):
     """The CPU oracle (C restatement of the reference path, single thread) on a bounded sample:
-    `cpu_frames` consecutive frames of one sequence through mask + features + plane table +
-    registration, timed on this host."""
+    frames of one synthetic sequence through mask + features + plane table + registration
+    (warm-started pairs, frames cycled), timed on this host until >= cpu_seconds have elapsed."""
     from oracle import oracle as O
     from ssf import synth
     O.lib()
     sc = synth.Scene(0)
-    fr = [synth.scan(0, k, n_rows=args.rows, n_az=args.n_az, scene=sc) for k in range(args.cpu_frames + 1)]
+    n_src = 4
+    fr = [synth.scan(0, k, n_rows=args.rows, n_az=args.n_az, scene=sc) for k in range(n_src)]
+    fr = [(f["pos1"].numpy(), f["flow"].numpy()) for f in fr]
     prof = O.profile(args.rows)
     mode = O.MODE_GN if args.solver == "gn" else O.MODE_CERES_LM
     iters = args.iters or (10 if args.solver == "gn" else 8)
-    last = O.extract_planes(fr[0]["pos1"].numpy(), args.rows)
+    last = O.extract_planes(fr[0][0], args.rows)
     q, t = np.array([0, 0, 0, 1.0]), np.zeros(3)
+    done = 0
     t0 = time.perf_counter()
-    for k in range(1, args.cpu_frames + 1):
-        p, f = fr[k]["pos1"].numpy(), fr[k]["flow"].numpy()
+    while True:
+        p, f = fr[1 + done % (n_src - 1)]
         O.mask_and_pose(p, f, [0.3, 0.6, 0.9])
         curr = O.extract_planes(p, args.rows)
         q, t, _, _ = O.register_pair(last, curr, prof.plane_max, mode=mode, max_iter=iters, q_init=q, t_init=t)
         last = curr
-    el = time.perf_counter() - t0
-    return dict(value=args.cpu_frames / el, unit="frames/s", cores=1, kind="port",
-                sample=f"{args.cpu_frames} consecutive {args.rows}-beam {args.rows * args.n_az}-pt frames "
+        done += 1
+        el = time.perf_counter() - t0
+        if (el >= args.cpu_seconds and done >= 2) or el > 30.0:
+            break
+    return dict(value=done / el, unit="frames/s", cores=1, kind="port",
+                sample=f"{done} frames of {args.rows}-beam {args.rows * args.n_az}-pt synthetic scans "
                        f"(mask+features+plane table+{args.solver} x{iters}) through oracle/ssf_oracle.c, "
                        f"1 thread, {el:.2f} s")
 
@@ -123,7 +131,7 @@ def main():
     fe_feat.reserve(B, N)
     fe_mask.seed(20240000 + rank)
     s_mask = torch.cuda.Stream(dev)
-    s_feat = torch.cuda.Stream(dev)
+    s_feat = s_mask if args.serial else torch.cuda.Stream(dev)
     # per-step outputs (double-buffered plane clouds: last <- curr)
     pose_rel = ssf.identity_poses(B, dev)
     pose_abs = ssf.identity_poses(B, dev)

@@ -101,17 +101,25 @@ int32_t ssf_extract_planes(ssf_ctx* ctx, void* stream, const float* d_pts, int64
  * coplanarity gate of src/lidarOdometry_onlyPC.cpp:173-232 (which depend only on the last
  * frame and a, so they are computed once per frame instead of once per correspondence x2).
  *   d_normal  out float32 x3 per plane point (frame offsets), d_valid out uint8 per point.
+ *   d_sorted_xyzi / d_sorted_idx  out (nullable): the frame's plane points sorted by (x, index)
+ *             and the permutation, the search index the k-NN walks use; pass them back to
+ *             ssf_register_batch when this frame is the last frame.  When they are NULL, or
+ *             max_plane_points exceeds SSF_SORTED_MAX, both calls fall back to brute-force k-NN.
+ *             Use the same max_plane_points bound for a frame's table and its registration.
  */
+#define SSF_SORTED_MAX 16384
 int32_t ssf_plane_table_batch(ssf_ctx* ctx, void* stream, int32_t n_frames,
                               const float* d_plane_xyzi, const int64_t* d_frame_off,
                               const int32_t* d_plane_count, int64_t max_plane_points,
-                              float* d_normal, uint8_t* d_valid);
+                              float* d_normal, uint8_t* d_valid, float* d_sorted_xyzi,
+                              int32_t* d_sorted_idx);
 
 /* ---------------------------------------------------------------------------------------
  * lidarOdometry_onlyPC: replaces frameRegistration() (src/lidarOdometry_onlyPC.cpp:147-252)
  * plus the pose accumulation of publishResult() (:87-90) for P independent pairs.
  *   last / curr      plane clouds (x,y,z,intensity) with their own offsets + counts
- *   d_last_normal/valid  plane table of the last frames (ssf_plane_table_batch)
+ *   d_last_normal/valid/sorted_*  plane table + search index of the last frames
+ *                        (ssf_plane_table_batch); the sorted arrays are nullable (brute force)
  *   curr_total_points    host copy of d_curr_off[P] (correspondence scratch extent)
  *   max_plane_points     host upper bound of plane points in any frame (grid sizing)
  *   d_pose_rel [P*7] in: warm start q_last_curr/t_last_curr (the previous pair's solution,
@@ -125,7 +133,8 @@ int32_t ssf_plane_table_batch(ssf_ctx* ctx, void* stream, int32_t n_frames,
 int32_t ssf_register_batch(ssf_ctx* ctx, void* stream, int32_t n_pairs,
                            const float* d_last_xyzi, const int64_t* d_last_off,
                            const int32_t* d_last_count, const float* d_last_normal,
-                           const uint8_t* d_last_valid, const float* d_curr_xyzi,
+                           const uint8_t* d_last_valid, const float* d_last_sorted_xyzi,
+                           const int32_t* d_last_sorted_idx, const float* d_curr_xyzi,
                            const int64_t* d_curr_off, const int32_t* d_curr_count,
                            int64_t curr_total_points, int64_t max_plane_points,
                            double* d_pose_rel, double* d_pose_abs,

@@ -247,7 +247,8 @@ int32_t ssf_extract_planes(ssf_ctx* c, void* stream, const float* d_pts, int64_t
 
 int32_t ssf_plane_table_batch(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_plane_xyzi,
                               const int64_t* d_frame_off, const int32_t* d_plane_count,
-                              int64_t max_plane_points, float* d_normal, uint8_t* d_valid) {
+                              int64_t max_plane_points, float* d_normal, uint8_t* d_valid,
+                              float* d_sorted_xyzi, int32_t* d_sorted_idx) {
     if (!c) return SSF_E_ARG;
     if (n_frames < 0 || max_plane_points < 0 ||
         (n_frames > 0 && (!d_plane_xyzi || !d_frame_off || !d_plane_count || !d_normal || !d_valid)))
@@ -256,7 +257,8 @@ int32_t ssf_plane_table_batch(ssf_ctx* c, void* stream, int32_t n_frames, const 
     SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
     hipError_t e = ssf::launch_plane_table((hipStream_t)stream, c->cfg, n_frames,
                                            reinterpret_cast<const float4*>(d_plane_xyzi), d_frame_off,
-                                           d_plane_count, max_plane_points, d_normal, d_valid);
+                                           d_plane_count, max_plane_points, d_normal, d_valid,
+                                           reinterpret_cast<float4*>(d_sorted_xyzi), d_sorted_idx);
     if (e != hipSuccess) return hip_fail(c, e, "plane_table launch");
     return SSF_OK;
 }
@@ -264,6 +266,7 @@ int32_t ssf_plane_table_batch(ssf_ctx* c, void* stream, int32_t n_frames, const 
 int32_t ssf_register_batch(ssf_ctx* c, void* stream, int32_t n_pairs, const float* d_last_xyzi,
                            const int64_t* d_last_off, const int32_t* d_last_count,
                            const float* d_last_normal, const uint8_t* d_last_valid,
+                           const float* d_last_sorted_xyzi, const int32_t* d_last_sorted_idx,
                            const float* d_curr_xyzi, const int64_t* d_curr_off,
                            const int32_t* d_curr_count, int64_t curr_total_points,
                            int64_t max_plane_points, double* d_pose_rel, double* d_pose_abs,
@@ -278,7 +281,8 @@ int32_t ssf_register_batch(ssf_ctx* c, void* stream, int32_t n_pairs, const floa
     SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(curr_total_points, 1)), "alloc corr");
     hipError_t e = ssf::launch_register(
         (hipStream_t)stream, c->cfg, n_pairs, reinterpret_cast<const float4*>(d_last_xyzi), d_last_off,
-        d_last_count, d_last_normal, d_last_valid, reinterpret_cast<const float4*>(d_curr_xyzi), d_curr_off,
+        d_last_count, d_last_normal, d_last_valid, reinterpret_cast<const float4*>(d_last_sorted_xyzi),
+        d_last_sorted_idx, reinterpret_cast<const float4*>(d_curr_xyzi), d_curr_off,
         d_curr_count, max_plane_points, c->corr.as<ssf::CorrRec>(), d_pose_rel, d_pose_abs, d_log,
         d_nlog, d_ncorr, d_nn);
     if (e != hipSuccess) return hip_fail(c, e, "register launch");

@@ -126,10 +126,85 @@ SSF_DEV void qr_solve_5x3(float m[3][5], float x[3]) {
 constexpr int kKnnTile = 2048;
 constexpr int kK = 30;
 
+SSF_DEV bool lex_less(float ka, int ia, float kb, int ib) { return ka < kb || (ka == kb && ia < ib); }
+
 SSF_DEV float l2_simple(const float4& q, const float4& p) {
     const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
     float d = dx * dx + dy * dy;
     return d + dz * dz;
+}
+
+// Ring-diverse 5-point pick (:180-205), gate d2[n] < 1 (:207), 5x3 least-squares plane
+// (:208-220) and coplanarity gate (:222-232) from the sorted 30-NN list (kd, ki) of a point.
+SSF_DEV void plane_from_knn(const float4* __restrict__ P, const float (&kd)[30], const int (&ki)[30],
+                            int m, float plane_max, float nrm[3], uint8_t& ok) {
+    const int K = m < 30 ? m : 30;
+    nrm[0] = nrm[1] = nrm[2] = 0.f;
+    ok = 0;
+    if (K < 5) return;                                                 // :177
+    int v5[5];
+    int prow = -1, vr0 = -1, vr1 = -1, nvr = 0, n = 5;
+#pragma unroll
+    for (int ik = 0; ik < 30; ++ik) {                                  // :180-198
+        if (ik < K && nvr < 2) {
+            const float fi = P[ki[ik]].w;
+            const int ii = (int)fi;
+            const int row = (int)(100.0 * ((double)(fi - (float)ii) + 0.002));
+            if (ik == 0) prow = row;
+            if (ik < 5) {
+                v5[ik] = ki[ik];
+            } else if (row != prow && row >= 0 && row <= 63) {
+                if (nvr == 0) vr0 = ki[ik]; else vr1 = ki[ik];
+                nvr++;
+                n = ik;
+            }
+        }
+    }
+    if (nvr == 1) v5[4] = vr0;                                         // :199-205
+    if (nvr == 2) { v5[3] = vr0; v5[4] = vr1; }
+    float dn = kd[0];
+#pragma unroll
+    for (int ik = 0; ik < 30; ++ik) if (ik == n) dn = kd[ik];
+    if (!(dn < 1.0f)) return;                                          // :207
+    float Am[3][5];
+    float pts[5][3];
+    for (int j = 0; j < 5; ++j) {
+        const float4 p = P[v5[j]];
+        pts[j][0] = p.x; pts[j][1] = p.y; pts[j][2] = p.z;
+        Am[0][j] = p.x; Am[1][j] = p.y; Am[2][j] = p.z;
+    }
+    qr_solve_5x3(Am, nrm);                                             // :219
+    float z = nrm[0] * nrm[0] + nrm[1] * nrm[1];
+    z = z + nrm[2] * nrm[2];
+    if (z > 0.0f) {                                                    // :220
+        const float sq = sqrtf(z);
+        nrm[0] = nrm[0] / sq; nrm[1] = nrm[1] / sq; nrm[2] = nrm[2] / sq;
+    }
+    ok = 1;
+    for (int k = 0; k < 4; ++k) {                                      // :222-232
+        const double vx = (double)(pts[k][0] - pts[k + 1][0]);
+        const double vy = (double)(pts[k][1] - pts[k + 1][1]);
+        const double vz = (double)(pts[k][2] - pts[k + 1][2]);
+        double dd = (double)nrm[0] * vx + (double)nrm[1] * vy;
+        dd = dd + (double)nrm[2] * vz;
+        if (fabs(dd) > (double)plane_max) { ok = 0; break; }
+    }
+}
+
+// sorted insertion into a (distance, index)-ordered top-K list: ties go to the lower index,
+// independent of the order candidates are visited in.
+template <int K>
+SSF_DEV void knn_insert(float (&kd)[K], int (&ki)[K], float d, int id) {
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        const bool sw = d < kd[s] || (d == kd[s] && id < ki[s]);
+        const float td = kd[s];
+        const int ti = ki[s];
+        kd[s] = sw ? d : td;
+        ki[s] = sw ? id : ti;
+        d = sw ? td : d;
+        id = sw ? ti : id;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_plane_table(const float4* __restrict__ plane,
@@ -148,7 +223,7 @@ __global__ __launch_bounds__(256) void k_plane_table(const float4* __restrict__ 
     float kd[kK];
     int ki[kK];
 #pragma unroll
-    for (int k = 0; k < kK; ++k) { kd[k] = __builtin_inff(); ki[k] = -1; }
+    for (int k = 0; k < kK; ++k) { kd[k] = __builtin_inff(); ki[k] = 0x7fffffff; }
     for (int t0 = 0; t0 < m; t0 += kKnnTile) {
         const int nt = min(kKnnTile, m - t0);
         for (int k = threadIdx.x; k < nt; k += blockDim.x) tile[k] = P[t0 + k];
@@ -156,77 +231,16 @@ __global__ __launch_bounds__(256) void k_plane_table(const float4* __restrict__ 
         if (active) {
             for (int k = 0; k < nt; ++k) {
                 float d = l2_simple(q, tile[k]);
-                if (d < kd[kK - 1]) {
-                    int id = t0 + k;
-#pragma unroll
-                    for (int s = 0; s < kK; ++s) {
-                        const bool sw = d < kd[s];
-                        const float td = kd[s];
-                        const int ti = ki[s];
-                        kd[s] = sw ? d : td;
-                        ki[s] = sw ? id : ti;
-                        d = sw ? td : d;
-                        id = sw ? ti : id;
-                    }
-                }
+                const int id = t0 + k;
+                if (lex_less(d, id, kd[kK - 1], ki[kK - 1])) knn_insert<kK>(kd, ki, d, id);
             }
         }
         __syncthreads();
     }
     if (!active) return;
-    const int K = m < kK ? m : kK;
-    float nrm[3] = {0.f, 0.f, 0.f};
-    uint8_t ok = 0;
-    if (K >= 5) {                                                      // :177
-        int v5[5];
-        int prow = -1, vr0 = -1, vr1 = -1, nvr = 0, n = 5;
-#pragma unroll
-        for (int ik = 0; ik < kK; ++ik) {                               // :180-198
-            if (ik < K && nvr < 2) {
-                const float fi = P[ki[ik]].w;
-                const int ii = (int)fi;
-                const int row = (int)(100.0 * ((double)(fi - (float)ii) + 0.002));
-                if (ik == 0) prow = row;
-                if (ik < 5) {
-                    v5[ik] = ki[ik];
-                } else if (row != prow && row >= 0 && row <= 63) {
-                    if (nvr == 0) vr0 = ki[ik]; else vr1 = ki[ik];
-                    nvr++;
-                    n = ik;
-                }
-            }
-        }
-        if (nvr == 1) v5[4] = vr0;                                      // :199-205
-        if (nvr == 2) { v5[3] = vr0; v5[4] = vr1; }
-        float dn = kd[0];
-#pragma unroll
-        for (int ik = 0; ik < kK; ++ik) if (ik == n) dn = kd[ik];
-        if (dn < 1.0f) {                                                // :207
-            float Am[3][5];
-            float pts[5][3];
-            for (int j = 0; j < 5; ++j) {
-                const float4 p = P[v5[j]];
-                pts[j][0] = p.x; pts[j][1] = p.y; pts[j][2] = p.z;
-                Am[0][j] = p.x; Am[1][j] = p.y; Am[2][j] = p.z;
-            }
-            qr_solve_5x3(Am, nrm);                                      // :219
-            float z = nrm[0] * nrm[0] + nrm[1] * nrm[1];
-            z = z + nrm[2] * nrm[2];
-            if (z > 0.0f) {                                             // :220
-                const float s = sqrtf(z);
-                nrm[0] = nrm[0] / s; nrm[1] = nrm[1] / s; nrm[2] = nrm[2] / s;
-            }
-            ok = 1;
-            for (int k = 0; k < 4; ++k) {                               // :222-232
-                const double vx = (double)(pts[k][0] - pts[k + 1][0]);
-                const double vy = (double)(pts[k][1] - pts[k + 1][1]);
-                const double vz = (double)(pts[k][2] - pts[k + 1][2]);
-                double dd = (double)nrm[0] * vx + (double)nrm[1] * vy;
-                dd = dd + (double)nrm[2] * vz;
-                if (fabs(dd) > (double)plane_max) { ok = 0; break; }
-            }
-        }
-    }
+    float nrm[3];
+    uint8_t ok;
+    plane_from_knn(P, kd, ki, m, plane_max, nrm, ok);
     const int64_t o = frame_off[f] + a;
     normal[3 * o] = nrm[0]; normal[3 * o + 1] = nrm[1]; normal[3 * o + 2] = nrm[2];
     valid[o] = ok;
@@ -284,6 +298,153 @@ __global__ __launch_bounds__(256) void k_associate(const float4* __restrict__ la
     rec.po[0] = pc.x; rec.po[1] = pc.y; rec.po[2] = pc.z; rec.valid = ok ? 1.0f : 0.0f;
     rec.pa[0] = pa.x; rec.pa[1] = pa.y; rec.pa[2] = pa.z; rec.pad0 = 0.f;
     const float* nr = last_normal + 3 * (lo + (bi >= 0 ? bi : 0));
+    rec.n[0] = nr[0]; rec.n[1] = nr[1]; rec.n[2] = nr[2]; rec.pad1 = 0.f;
+    corr[co + i] = rec;
+    if (nn_out) nn_out[co + i] = bi;
+}
+
+// ------------------------------------------------------------------------------------------
+// x-sorted exact k-NN.  One work-group per frame bitonic-sorts the frame's plane points by
+// (x, index) in LDS; every query then walks outward from its own position in x order and stops a
+// direction once fl(dx*dx) exceeds its current K-th distance: since the float distance
+// ((dx*dx + dy*dy) + dz*dz) >= fl(dx*dx) and fl(dx*dx) grows monotonically along the sorted
+// order, no point beyond the stop can enter the list.  Lists are ordered by (distance, original
+// index), so the result is exactly the brute-force (index-order) result.  Typical frames touch a
+// few hundred candidates per query instead of all M.  The sorted points / permutation are
+// written out and reused as the LAST frame of the next pair's association.
+constexpr int kSortMax = 16384;           // plane points per frame sorted in LDS (128 KiB)
+constexpr int kTableThreads = 1024;
+
+__global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
+    const float4* __restrict__ plane, const int64_t* __restrict__ frame_off,
+    const int32_t* __restrict__ count, float plane_max, float* __restrict__ normal,
+    uint8_t* __restrict__ valid, float4* __restrict__ sorted_xyzi, int32_t* __restrict__ sorted_idx) {
+    __shared__ float key[kSortMax];
+    __shared__ int idx[kSortMax];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int m = count[f];
+    const int64_t base = frame_off[f];
+    const float4* P = plane + base;
+    if (m <= 0) return;
+    int np = 1;
+    while (np < m) np <<= 1;
+    for (int r = tid; r < np; r += blockDim.x) {
+        key[r] = r < m ? P[r].x : __builtin_inff();
+        idx[r] = r;
+    }
+    __syncthreads();
+    for (int k = 2; k <= np; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = tid; t < np; t += blockDim.x) {
+                const int u = t ^ j;
+                if (u > t) {
+                    const float ka = key[t], kb = key[u];
+                    const int ia = idx[t], ib = idx[u];
+                    const bool asc = (t & k) == 0;
+                    if (asc ? lex_less(kb, ib, ka, ia) : lex_less(ka, ia, kb, ib)) {
+                        key[t] = kb; key[u] = ka; idx[t] = ib; idx[u] = ia;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    float4* SP = sorted_xyzi + base;
+    int32_t* SI = sorted_idx + base;
+    for (int r = tid; r < m; r += blockDim.x) {
+        SP[r] = P[idx[r]];
+        SI[r] = idx[r];
+    }
+    __syncthreads();
+    for (int r = tid; r < m; r += blockDim.x) {
+        const int a = idx[r];
+        const float4 q = SP[r];
+        float kd[kK];
+        int ki[kK];
+#pragma unroll
+        for (int k = 0; k < kK; ++k) { kd[k] = __builtin_inff(); ki[k] = 0x7fffffff; }
+        for (int c = r; c < m; ++c) {                     // rightwards (x non-decreasing)
+            const float dx = q.x - key[c];
+            if (dx * dx > kd[kK - 1]) break;
+            const float4 p = SP[c];
+            const float d = l2_simple(q, p);
+            const int id = idx[c];
+            if (lex_less(d, id, kd[kK - 1], ki[kK - 1])) knn_insert<kK>(kd, ki, d, id);
+        }
+        for (int c = r - 1; c >= 0; --c) {                // leftwards
+            const float dx = q.x - key[c];
+            if (dx * dx > kd[kK - 1]) break;
+            const float4 p = SP[c];
+            const float d = l2_simple(q, p);
+            const int id = idx[c];
+            if (lex_less(d, id, kd[kK - 1], ki[kK - 1])) knn_insert<kK>(kd, ki, d, id);
+        }
+        float nrm[3];
+        uint8_t ok;
+        plane_from_knn(P, kd, ki, m, plane_max, nrm, ok);
+        const int64_t o = base + a;
+        normal[3 * o] = nrm[0]; normal[3 * o + 1] = nrm[1]; normal[3 * o + 2] = nrm[2];
+        valid[o] = ok;
+    }
+}
+
+// Association against an x-sorted last frame: binary search of the query's x, then the same
+// outward walk with a 1-element list (ties to the lower original index, as the brute force).
+__global__ __launch_bounds__(256) void k_associate_sorted(
+    const float4* __restrict__ last, const int64_t* __restrict__ last_off,
+    const int32_t* __restrict__ last_count, const float* __restrict__ last_normal,
+    const uint8_t* __restrict__ last_valid, const float4* __restrict__ last_sorted,
+    const int32_t* __restrict__ last_sidx, const float4* __restrict__ curr,
+    const int64_t* __restrict__ curr_off, const int32_t* __restrict__ curr_count,
+    const double* __restrict__ pose_rel, CorrRec* __restrict__ corr, int32_t* __restrict__ nn_out) {
+    const int p = blockIdx.y;
+    const int mc = curr_count[p], ml = last_count[p];
+    if ((int)(blockIdx.x * blockDim.x) >= mc || ml <= 10) return;    // uniform (:158)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= mc) return;
+    const int64_t lo = last_off[p], co = curr_off[p];
+    const float4* SL = last_sorted + lo;
+    const int32_t* SI = last_sidx + lo;
+    const double q[4] = {pose_rel[7 * p], pose_rel[7 * p + 1], pose_rel[7 * p + 2], pose_rel[7 * p + 3]};
+    const double t[3] = {pose_rel[7 * p + 4], pose_rel[7 * p + 5], pose_rel[7 * p + 6]};
+    const float4 pc = curr[co + i];
+    float4 qs;
+    {
+        const double v[3] = {(double)pc.x, (double)pc.y, (double)pc.z};
+        double r[3];
+        quat_rotate(q, v, r);                                          // :74-82
+        qs.x = (float)(r[0] + t[0]); qs.y = (float)(r[1] + t[1]); qs.z = (float)(r[2] + t[2]); qs.w = 0.f;
+    }
+    int lo_i = 0, hi_i = ml;                                            // first x >= qs.x
+    while (lo_i < hi_i) {
+        const int mid = (lo_i + hi_i) >> 1;
+        if (SL[mid].x < qs.x) lo_i = mid + 1; else hi_i = mid;
+    }
+    float best = __builtin_inff();
+    int bi = 0x7fffffff;
+    for (int c = lo_i; c < ml; ++c) {
+        const float4 pl = SL[c];
+        const float dx = qs.x - pl.x;
+        if (dx * dx > best) break;
+        const float d = l2_simple(qs, pl);
+        const int id = SI[c];
+        if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+    }
+    for (int c = lo_i - 1; c >= 0; --c) {
+        const float4 pl = SL[c];
+        const float dx = qs.x - pl.x;
+        if (dx * dx > best) break;
+        const float d = l2_simple(qs, pl);
+        const int id = SI[c];
+        if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+    }
+    const float4* L = last + lo;
+    CorrRec rec;
+    const bool ok = last_valid[lo + bi] != 0;
+    const float4 pa = L[bi];
+    rec.po[0] = pc.x; rec.po[1] = pc.y; rec.po[2] = pc.z; rec.valid = ok ? 1.0f : 0.0f;
+    rec.pa[0] = pa.x; rec.pa[1] = pa.y; rec.pa[2] = pa.z; rec.pad0 = 0.f;
+    const float* nr = last_normal + 3 * (lo + bi);
     rec.n[0] = nr[0]; rec.n[1] = nr[1]; rec.n[2] = nr[2]; rec.pad1 = 0.f;
     corr[co + i] = rec;
     if (nn_out) nn_out[co + i] = bi;
@@ -614,26 +775,39 @@ __global__ void k_accumulate(int n, const double* __restrict__ rel, const double
 
 hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames,
                               const float4* plane, const int64_t* frame_off, const int32_t* count,
-                              int64_t max_m, float* normal, uint8_t* valid) {
+                              int64_t max_m, float* normal, uint8_t* valid, float4* sorted_xyzi,
+                              int32_t* sorted_idx) {
     if (n_frames <= 0 || max_m <= 0) return hipSuccess;
-    const int bx = (int)((max_m + 255) / 256);
-    hipLaunchKernelGGL(k_plane_table, dim3(bx, n_frames), dim3(256), 0, s, plane, frame_off, count,
-                       cfg.plane_max, normal, valid);
+    if (max_m <= kSortMax && sorted_xyzi && sorted_idx) {
+        hipLaunchKernelGGL(k_plane_table_sorted, dim3(n_frames), dim3(kTableThreads), 0, s, plane,
+                           frame_off, count, cfg.plane_max, normal, valid, sorted_xyzi, sorted_idx);
+    } else {
+        const int bx = (int)((max_m + 255) / 256);
+        hipLaunchKernelGGL(k_plane_table, dim3(bx, n_frames), dim3(256), 0, s, plane, frame_off,
+                           count, cfg.plane_max, normal, valid);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, const float4* last,
                            const int64_t* last_off, const int32_t* last_count,
-                           const float* last_normal, const uint8_t* last_valid, const float4* curr,
+                           const float* last_normal, const uint8_t* last_valid,
+                           const float4* last_sorted, const int32_t* last_sidx, const float4* curr,
                            const int64_t* curr_off, const int32_t* curr_count, int64_t max_m,
                            CorrRec* corr, double* pose_rel, double* pose_abs, double* log,
                            int32_t* nlog, int32_t* ncorr, int32_t* nn) {
     if (n_pairs <= 0) return hipSuccess;
     if (max_m > 0) {
         const int bx = (int)((max_m + 255) / 256);
-        hipLaunchKernelGGL(k_associate, dim3(bx, n_pairs), dim3(256), 0, s, last, last_off,
-                           last_count, last_normal, last_valid, curr, curr_off, curr_count,
-                           pose_rel, corr, nn);
+        if (max_m <= kSortMax && last_sorted && last_sidx) {
+            hipLaunchKernelGGL(k_associate_sorted, dim3(bx, n_pairs), dim3(256), 0, s, last, last_off,
+                               last_count, last_normal, last_valid, last_sorted, last_sidx, curr,
+                               curr_off, curr_count, pose_rel, corr, nn);
+        } else {
+            hipLaunchKernelGGL(k_associate, dim3(bx, n_pairs), dim3(256), 0, s, last, last_off,
+                               last_count, last_normal, last_valid, curr, curr_off, curr_count,
+                               pose_rel, corr, nn);
+        }
     }
     hipLaunchKernelGGL(k_solve, dim3(n_pairs), dim3(kSolveThreads), 0, s, corr, curr_off,
                        curr_count, last_count, cfg.solver, cfg.max_iter, pose_rel, pose_abs, log,

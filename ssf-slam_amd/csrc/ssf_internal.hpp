@@ -50,10 +50,12 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
 // ---- launchers (registration.hip) ----
 hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames,
                               const float4* plane, const int64_t* frame_off, const int32_t* count,
-                              int64_t max_m, float* normal, uint8_t* valid);
+                              int64_t max_m, float* normal, uint8_t* valid, float4* sorted_xyzi,
+                              int32_t* sorted_idx);
 hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, const float4* last,
                            const int64_t* last_off, const int32_t* last_count,
-                           const float* last_normal, const uint8_t* last_valid, const float4* curr,
+                           const float* last_normal, const uint8_t* last_valid,
+                           const float4* last_sorted, const int32_t* last_sidx, const float4* curr,
                            const int64_t* curr_off, const int32_t* curr_count, int64_t max_m,
                            CorrRec* corr, double* pose_rel, double* pose_abs, double* log,
                            int32_t* nlog, int32_t* ncorr, int32_t* nn);

@@ -70,10 +70,10 @@ def lib():
     L.ssf_extract_planes_batch.restype = i32
     L.ssf_extract_planes.argtypes = [vp, vp, vp, i64, i32, i32, vp, C.POINTER(i64), i64]
     L.ssf_extract_planes.restype = i32
-    L.ssf_plane_table_batch.argtypes = [vp, vp, i32, vp, vp, vp, i64, vp, vp]
+    L.ssf_plane_table_batch.argtypes = [vp, vp, i32, vp, vp, vp, i64, vp, vp, vp, vp]
     L.ssf_plane_table_batch.restype = i32
-    L.ssf_register_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp,
-                                     vp, vp, vp, vp, vp]
+    L.ssf_register_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64,
+                                     vp, vp, vp, vp, vp, vp]
     L.ssf_register_batch.restype = i32
     L.ssf_mask_pose_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, i32, vp, vp]
     L.ssf_mask_pose_batch.restype = i32

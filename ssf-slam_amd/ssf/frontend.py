@@ -128,7 +128,9 @@ class Frontend:
             self._h, _stream(self.device), F, _ptr(pts), stride, _ptr(off), total, mx,
             _ptr(plane), _ptr(count), _ptr(ring), _ptr(roff), _ptr(curv))
         self._check(rc, "ssf_extract_planes_batch")
-        pb = PlaneBatch(plane, count[:F], off, h_off, mx)
+        # plane points per frame <= sum over rows of ceil(n_r / planeSpan) <= n/span + rows
+        pb = PlaneBatch(plane, count[:F], off, h_off,
+                        min(mx, mx // max(1, self.cfg.plane_span) + self.n_rows + 1))
         if debug:
             return pb, ring, roff.view(max(F, 1), self.n_rows + 1)[:F], curv
         return pb
@@ -145,15 +147,23 @@ class Frontend:
         return out[:m.value]
 
     # ------------------------------------------------------------------ lidarOdometry_onlyPC
-    def plane_table(self, pb: PlaneBatch):
+    def plane_table(self, pb: PlaneBatch, brute_force: bool = False):
+        """-> (normal [total,3] f32, valid [total] u8, sorted_xyzi, sorted_idx) -- the plane table
+        of frames that will be LAST frames, plus their x-sorted search index (None, None when
+        brute_force=True)."""
         total = pb.xyzi.shape[0]
         normal = torch.empty((total, 3), dtype=torch.float32, device=self.device)
         valid = torch.empty(total, dtype=torch.uint8, device=self.device)
+        sx = si = None
+        if not brute_force:
+            sx = torch.empty((total, 4), dtype=torch.float32, device=self.device)
+            si = torch.empty(total, dtype=torch.int32, device=self.device)
         rc = _abi.lib().ssf_plane_table_batch(self._h, _stream(self.device), pb.count.numel(),
                                               _ptr(pb.xyzi), _ptr(pb.off), _ptr(pb.count),
-                                              pb.max_points, _ptr(normal), _ptr(valid))
+                                              pb.max_points, _ptr(normal), _ptr(valid), _ptr(sx),
+                                              _ptr(si))
         self._check(rc, "ssf_plane_table_batch")
-        return normal, valid
+        return normal, valid, sx, si
 
     def register(self, last: PlaneBatch, last_table, curr: PlaneBatch, pose_rel, pose_abs=None,
                  want_log=False, want_nn=False):
@@ -163,7 +173,7 @@ class Frontend:
         pose_rel = self._dev(pose_rel, torch.float64)
         if pose_abs is not None:
             pose_abs = self._dev(pose_abs, torch.float64)
-        normal, valid = last_table
+        normal, valid, sx, si = last_table
         log = nlog = nn = None
         ncorr = torch.empty(P, dtype=torch.int32, device=self.device)
         if want_log:
@@ -174,7 +184,8 @@ class Frontend:
         mx = max(last.max_points, curr.max_points)
         rc = _abi.lib().ssf_register_batch(
             self._h, _stream(self.device), P, _ptr(last.xyzi), _ptr(last.off), _ptr(last.count),
-            _ptr(normal), _ptr(valid), _ptr(curr.xyzi), _ptr(curr.off), _ptr(curr.count),
+            _ptr(normal), _ptr(valid), _ptr(sx), _ptr(si), _ptr(curr.xyzi), _ptr(curr.off),
+            _ptr(curr.count),
             int(curr.h_off[-1]), mx, _ptr(pose_rel), _ptr(pose_abs), _ptr(log), _ptr(nlog),
             _ptr(ncorr), _ptr(nn))
         self._check(rc, "ssf_register_batch")

@@ -40,13 +40,22 @@ def _sub(pb, idx):
     return ssf.PlaneBatch(pb.xyzi, pb.count[idx].contiguous(), o, h_st, pb.max_points)
 
 
-def test_plane_table_bitexact(oracle, dev):
+@pytest.mark.parametrize("brute", [False, True])
+def test_plane_table_bitexact(oracle, dev, brute):
+    """x-sorted walk (default) and brute-force k-NN both reproduce the oracle bit for bit"""
     import ssf
     fe = ssf.Frontend(64, device=dev.index)
-    clouds = [frame(0, 0)[0], frame(1, 1)[0]]
+    clouds = [frame(0, 0)[0], frame(1, 1)[0], frame(2, 2, n_az=1875)[0]]
     pb = _planes(fe, dev, clouds)
-    normal, valid = fe.plane_table(pb)
-    for f in range(2):
+    normal, valid, sx, si = fe.plane_table(pb, brute_force=brute)
+    if not brute:
+        for f in range(3):
+            o, m = int(pb.h_off[f]), int(pb.count[f])
+            perm = si[o:o + m].cpu().numpy()
+            xs = sx[o:o + m, 0].cpu().numpy()
+            assert np.all(np.diff(xs) >= 0) and sorted(perm.tolist()) == list(range(m))
+            assert np.array_equal(sx[o:o + m].cpu().numpy(), pb.frame(f).cpu().numpy()[perm])
+    for f in range(3):
         P = pb.frame(f).cpu().numpy()
         nr, vr, _, _ = oracle.plane_table(P, 0.05)
         o, m = int(pb.h_off[f]), P.shape[0]
@@ -56,13 +65,14 @@ def test_plane_table_bitexact(oracle, dev):
         assert vr.mean() > 0.3
 
 
-@pytest.mark.parametrize("solver,iters,mode", [("ceres_lm", 8, 0), ("gn", 10, 1)])
-def test_register_pair_per_step(oracle, dev, solver, iters, mode):
+@pytest.mark.parametrize("solver,iters,mode,brute", [("ceres_lm", 8, 0, False), ("gn", 10, 1, False),
+                                                     ("ceres_lm", 8, 0, True)])
+def test_register_pair_per_step(oracle, dev, solver, iters, mode, brute):
     import ssf
     fe = ssf.Frontend(64, device=dev.index, solver=solver, max_iter=iters)
     clouds = [frame(0, 2, n_az=1875)[0], frame(0, 3, n_az=1875)[0]]
     pb = _planes(fe, dev, clouds)
-    table = fe.plane_table(pb)
+    table = fe.plane_table(pb, brute_force=brute)
     last, curr = _sub(pb, [0]), _sub(pb, [1])
     q0 = np.array([0.0, 0.0, 0.001, 1.0]); q0 /= np.linalg.norm(q0)
     t0 = np.array([0.9, 0.01, 0.0])

@@ -120,6 +120,7 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     import ssf
+    from ssf import dist as sd
     iters = args.iters or (10 if args.solver == "gn" else 8)
     B, N = args.batch, args.rows * args.n_az
     n_frames = args.warmup + args.steps + 1
@@ -162,11 +163,8 @@ def main():
         cur = torch.cuda.current_stream(dev)
         cur.wait_stream(s_mask)
         cur.wait_stream(s_feat)
-        if world > 1:
-            poses = torch.cat([pose_abs, mask_out[k][:, 0:7]], 1).contiguous()  # [B, 14]
-            bufs = [torch.empty_like(poses) for _ in range(world)]
-            dist.all_gather(bufs, poses)
-            gathered.append(bufs)
+        if world > 1:   # the one exchange step: per-frame 6-DoF poses of every rank (RCCL)
+            gathered.append(sd.gather_poses(sd.pose_record(pose_abs, mask_out[k])))
         if timing:
             ev["mask"].append((e0, e1)); ev["feat"].append((es[0], es[1]))
             ev["table"].append((es[1], es[2])); ev["reg"].append((es[2], es[3]))

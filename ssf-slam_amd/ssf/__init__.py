@@ -6,5 +6,7 @@ fallback anywhere in this package.
 """
 from ._abi import SSFError  # noqa: F401
 from .frontend import Frontend, PlaneBatch, frame_offsets, identity_poses  # noqa: F401
+from .pose import mask_and_pose, slove_RT_by_SVD  # noqa: F401
 
-__all__ = ["Frontend", "PlaneBatch", "frame_offsets", "identity_poses", "SSFError"]
+__all__ = ["Frontend", "PlaneBatch", "frame_offsets", "identity_poses", "SSFError",
+           "mask_and_pose", "slove_RT_by_SVD"]

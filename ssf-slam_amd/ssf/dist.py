@@ -1,0 +1,39 @@
+"""Multi-GPU layout: one process per GPU, sequences sharded across ranks.
+
+The path shards naturally -- frames are independent for the mask and the features, and a
+sequence's registration chain is serial (warm start, src/lidarOdometry_onlyPC.cpp:164,251-252)
+-- so every rank owns whole sequences and there is no data-path collective.  The one exchange
+step is an all-gather of the per-frame 6-DoF poses (RCCL over xGMI on the GPU, gloo in the
+CPU tests), done once per batch: it is latency-bound (B x 14 doubles per rank), not
+bandwidth-bound, so it is never split into smaller messages.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def sequence_shard(n_sequences: int, world: int, rank: int) -> range:
+    """Contiguous block of sequence ids owned by `rank` (sizes differ by at most one)."""
+    base, extra = divmod(n_sequences, world)
+    start = rank * base + min(rank, extra)
+    return range(start, start + base + (1 if rank < extra else 0))
+
+
+def pose_record(pose_abs: torch.Tensor, mask_out: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-frame record exchanged between ranks: accumulated registration pose [q xyzw, t]
+    (7 doubles) and, if given, the SSF Kabsch pose [t, q xyzw] (7 doubles)."""
+    parts = [pose_abs.to(torch.float64)]
+    if mask_out is not None:
+        parts.append(mask_out[:, 0:7].to(torch.float64))
+    return torch.cat(parts, 1).contiguous()
+
+
+def gather_poses(local: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather equal-shaped per-rank pose records -> [world * n, k] in rank order."""
+    if not dist.is_available() or not dist.is_initialized():
+        return local
+    world = dist.get_world_size(group)
+    bufs = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(bufs, local.contiguous(), group=group)
+    return torch.cat(bufs, 0)

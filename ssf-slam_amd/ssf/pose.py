@@ -1,0 +1,104 @@
+"""Reference-named Python entry points of the SSF pose block, GPU-backed.
+
+scripts/PointCloudOdometry_noSeg.py (and PointCloudOdometry.py, main_sju_occ_ros.py:256-284)
+computes, per frame:
+
+    X = concatenate((move_gt, points), axis=1)                 # :97
+    all_label = GaussianMixture(n_components=2).fit_predict(X) # :98-101
+    bg_label = Counter(all_label).most_common(1)[0][0]         # :102
+    R, t = slove_RT_by_SVD(points[bg] + move_gt[bg], points[bg])   # :114-118
+    q = Quaternion(matrix=R); publish [t, q.x, q.y, q.z, q.w]  # :119-125
+
+`mask_and_pose` runs that whole block in one HIP kernel (k_mask_pose) for one or many frames;
+`slove_RT_by_SVD` keeps the reference signature.  Error behaviour: the reference raises
+TypeError when det(R) < 0 (`Vt.T & U.T`, :33) and pyquaternion raises ValueError for a
+non-orthogonal R; here both raise ValueError (reflection='fix' applies the evident intent of
+:32-33 instead).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _abi
+from .frontend import Frontend, frame_offsets
+
+_FE: dict = {}
+
+
+def _frontend(device) -> Frontend:
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else
+                       (device.index if isinstance(device, torch.device) else int(device)))
+    fe = _FE.get(dev.index)
+    if fe is None:
+        fe = _FE[dev.index] = Frontend(64, device=dev.index)
+    return fe
+
+
+def _as_f32_dev(a, dev):
+    if isinstance(a, torch.Tensor):
+        return a.to(dev, torch.float32).contiguous()
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(a), dtype=np.float32)).to(dev)
+
+
+def _raise_status(st):
+    st = int(st)
+    if st == _abi.POSE_REFLECTION:
+        raise ValueError("slove_RT_by_SVD: reflection (det(R) < 0); the reference raises TypeError here")
+    if st == _abi.POSE_NOT_ORTHOGONAL:
+        raise ValueError("Matrix must be orthogonal, i.e. its transpose should be its inverse")
+    if st == _abi.POSE_EMPTY:
+        raise ValueError("no background points")
+    if st == _abi.POSE_GMM_FAILED:
+        raise ValueError("Fitting the mixture model failed (ill-defined empirical covariance)")
+
+
+def slove_RT_by_SVD(src, dst, reflection: str = "raise", device=None):
+    """R (3,3), t (3,1) minimising |R src + t - dst| (reference signature, float64 results).
+    Inputs are LiDAR float32 coordinates on the device (float64 inputs are rounded to float32)."""
+    fe = _frontend(device)
+    dst_t = _as_f32_dev(dst, fe.device)
+    src_t = _as_f32_dev(src, fe.device)
+    flow = (src_t - dst_t).contiguous()
+    off, h_off = frame_offsets([dst_t.shape[0]], fe.device)
+    ones = torch.ones(dst_t.shape[0], dtype=torch.uint8, device=fe.device)
+    out, _ = fe.mask_pose(dst_t, flow, off, h_off, mode="given", mask_in=ones,
+                          reflection=1 if reflection == "fix" else 0, want_mask=False)
+    o = out[0].cpu().numpy()
+    if int(o[_abi.POSE_OUT["STATUS"]]) == _abi.POSE_REFLECTION and reflection != "fix":
+        _raise_status(o[_abi.POSE_OUT["STATUS"]])
+    R = o[7:16].reshape(3, 3).copy()
+    t = o[0:3].reshape(3, 1).copy()
+    return R, t
+
+
+def mask_and_pose(points, flow, mode: str = "gmm", gt_mask=None, seed: int | None = None,
+                  draws=None, reflection: str = "raise", device=None, frame_sizes=None):
+    """The PointCloudOdometry_noSeg.py:97-125 block for one frame (or F frames packed back to
+    back with `frame_sizes`).  mode 'gmm' (GaussianMixture on [flow, xyz]), 'gt'
+    (background = s_fg_mask == 0, PointCloudOdometry.py:91) or 'given' (background = mask != 0).
+    -> dict(R [F,3,3], t [F,3], q_xyzw [F,4], para_t_q [F,7], bg_mask (device u8), info)."""
+    fe = _frontend(device)
+    pts = _as_f32_dev(points, fe.device)
+    fl = _as_f32_dev(flow, fe.device)
+    sizes = [pts.shape[0]] if frame_sizes is None else list(frame_sizes)
+    off, h_off = frame_offsets(sizes, fe.device)
+    if seed is not None:
+        fe.seed(seed)
+    m = None
+    if mode != "gmm":
+        if gt_mask is None:
+            raise ValueError(f"mode {mode!r} needs gt_mask")
+        m = torch.as_tensor(np.asarray(gt_mask) if not isinstance(gt_mask, torch.Tensor) else gt_mask)
+        m = m.to(fe.device, torch.uint8).contiguous()
+    out, bg = fe.mask_pose(pts, fl, off, h_off, mode=mode, mask_in=m, draws=draws,
+                           reflection=1 if reflection == "fix" else 0)
+    o = out.cpu().numpy()
+    for st in o[:, _abi.POSE_OUT["STATUS"]]:
+        if int(st) != 0:
+            _raise_status(st)
+    return dict(R=o[:, 7:16].reshape(-1, 3, 3), t=o[:, 0:3], q_xyzw=o[:, 3:7],
+                para_t_q=o[:, 0:7], bg_mask=bg,
+                info=dict(bg_label=o[:, 18], n_bg=o[:, 17], kmeans_iter=o[:, 19], em_iter=o[:, 20],
+                          converged=o[:, 21], centers=o[:, 22:24], lower_bound=o[:, 24],
+                          passes=o[:, 25]))

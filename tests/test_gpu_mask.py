@@ -119,3 +119,23 @@ def test_kabsch_golden(dev):
         assert out[0, 16] == 0
         assert np.abs(out[0, 7:16].reshape(3, 3) - g[f"R{c}"]).max() < 1e-5
         assert np.abs(out[0, 0:3] - g[f"t{c}"]).max() < 1e-4
+
+
+def test_reference_named_python_api(dev):
+    """ssf.slove_RT_by_SVD / ssf.mask_and_pose keep the reference signatures and errors"""
+    import ssf
+    g = np.load(os.path.join(GOLDEN, "kabsch_ref.npz"))
+    R, t = ssf.slove_RT_by_SVD(g["src2"], g["dst2"])
+    assert R.shape == (3, 3) and t.shape == (3, 1)
+    assert np.abs(R - g["R2"]).max() < 1e-5 and np.abs(t.ravel() - g["t2"]).max() < 1e-4
+    with pytest.raises(ValueError):
+        ssf.slove_RT_by_SVD(g["refl_src"], g["refl_dst"])
+    R2, _ = ssf.slove_RT_by_SVD(g["refl_src"], g["refl_dst"], reflection="fix")
+    assert abs(np.linalg.det(R2) - 1) < 1e-9
+    c = np.load(os.path.join(GOLDEN, "gmm_noseg_case0.npz"))
+    res = ssf.mask_and_pose(c["pos1"], c["flow"], seed=int(c["seed"]))
+    assert np.abs(res["para_t_q"][0] - c["para_t_q"]).max() < 1e-6
+    bg_ref = (c["labels"] == int(c["bg_label"])).astype(np.uint8)
+    assert np.array_equal(res["bg_mask"].cpu().numpy(), bg_ref)
+    gt = ssf.mask_and_pose(c["pos1"], c["flow"], mode="gt", gt_mask=c["s_fg_mask"])
+    assert gt["bg_mask"].cpu().numpy().sum() == int((c["s_fg_mask"] == 0).sum())

@@ -57,5 +57,23 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+def build_diag() -> str:
+    """Diagnostic library (phase stamps in k_mask_pose, -DSSF_MASK_STAMPS) for
+    tools/diag_mask_phases.py; never loaded by the product path unless SSF_LIB points at it."""
+    out = os.path.join(OUT_DIR, "libssf_frontend_diag.so")
+    objs = []
+    for src in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(OBJ_DIR, src.replace(".hip", "_diag.o"))
+        extra = ["-DSSF_MASK_STAMPS"] if src == "mask_pose.hip" else []
+        subprocess.run([HIPCC, *FLAGS, *FILE_FLAGS.get(src, []), *extra, "-c", s, "-o", o], check=True)
+        objs.append(o)
+    subprocess.run([HIPCC, *FLAGS, "-shared", *objs, "-o", out], check=True)
+    return out
+
+
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    if "--diag" in sys.argv:
+        print(build_diag())
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

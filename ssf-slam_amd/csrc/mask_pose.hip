@@ -23,6 +23,21 @@
 namespace ssf {
 
 constexpr int kMaskThreads = 512;
+
+// Diagnostic build only (-DSSF_MASK_STAMPS, libssf_frontend_diag.so): lane 0 records the
+// s_memtime cycle count at each phase boundary into the frame's unused out slots 26..31.
+// The product library is compiled without it; no product output is computed from a stamp.
+#ifdef SSF_MASK_STAMPS
+#define SSF_STAMP(slot)                                                                   \
+    do {                                                                                  \
+        if (threadIdx.x == 0) {                                                           \
+            const unsigned long long _t = __builtin_amdgcn_s_memtime();                   \
+            out[26 + (slot)] = (double)(_t - stamp0);                                     \
+        }                                                                                 \
+    } while (0)
+#else
+#define SSF_STAMP(slot) do { } while (0)
+#endif
 constexpr int kNW = kMaskThreads / 64;
 constexpr double kPi = 3.14159265358979323846;
 
@@ -34,13 +49,14 @@ SSF_DEV constexpr int up(int i, int j) { return i * 6 - (i * (i - 1)) / 2 + (j -
 struct MaskShared {
     double mean[6], tol;
     double tot[28];            // {N, sum(x-mean)[6], sum(x-mean)(x-mean)^T [21 packed]}
-    double cen[12], csn[2];
+    double cen[12], csn[2], cenp[12], csnp[2];   // current / previous Lloyd centres
+    double x0[6], ktot[16];    // pass-0 shift (point 0) and total Kabsch sums about it
     double mu[12], U[42], cU[12], logdet[2], logw[2];  // U: packed upper precision Cholesky per comp; cU = mu U
     double rand1, rand2;
     double lb;
     double C[36], L[36], Li[36];  // lane-0 scratch for the 6x6 algebra
     int64_t c0, c1;
-    int km_iter, em_iter, strict, converged, done, status, passes, label0, bg;
+    int km_iter, em_iter, strict, converged, done, status, passes, label0, bg, bg_pred;
 };
 
 SSF_DEV void load_x(const float* __restrict__ P, const float* __restrict__ Fl, int64_t i, double x[6]) {
@@ -113,6 +129,30 @@ __device__ __noinline__ int gmm_params(MaskShared& S, const double* comp1, int i
             S.cU[6 * k + j] = c;
         }
     return 0;
+}
+
+// Same, two points per iteration (i, i + T): two independent f64 dependency chains per wave to
+// hide the exp / log1p / divide latencies at 2 waves per SIMD.  The second point of the last
+// pair may not exist (w1 == 0): it is computed on a duplicate and weighted out.
+template <class Fn>
+SSF_DEV void for_point_pairs(const float* __restrict__ P, const float* __restrict__ Fl, int64_t n, Fn&& fn) {
+    const int64_t T = blockDim.x;
+    int64_t i = threadIdx.x;
+    if (i >= n) return;
+    double xa[6], xb[6];
+    load_x(P, Fl, i, xa);
+    load_x(P, Fl, i + T < n ? i + T : i, xb);
+    for (; i < n; i += 2 * T) {
+        double x0[6], x1[6];
+#pragma unroll
+        for (int d = 0; d < 6; ++d) { x0[d] = xa[d]; x1[d] = xb[d]; }
+        const double w1 = (i + T < n) ? 1.0 : 0.0;
+        if (i + 2 * T < n) {
+            load_x(P, Fl, i + 2 * T, xa);
+            load_x(P, Fl, i + 3 * T < n ? i + 3 * T : i + 2 * T, xb);
+        }
+        fn(x0, x1, w1);
+    }
 }
 
 // weighted log probability, sklearn _estimate_log_gaussian_prob form: y = x U - (mu U), with
@@ -313,9 +353,15 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     const float* P = pts + 3 * fb;
     const float* Fl = flow + 3 * fb;
     double* D = dist + fb;
-    uint8_t* Lb = lab + fb;
+    (void)lab;
     double* out = out_all + (int64_t)f * SSF_POSE_OUT_STRIDE;
-    if (tid == 0) { S.passes = 0; S.status = 0; S.km_iter = 0; S.em_iter = 0; S.converged = 0; }
+    if (tid == 0) {
+        S.passes = 0; S.status = 0; S.km_iter = 0; S.em_iter = 0; S.converged = 0;
+        for (int i = 26; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
+    }
+#ifdef SSF_MASK_STAMPS
+    const unsigned long long stamp0 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
 
     if (mode != SSF_MASK_GMM) {
@@ -386,6 +432,18 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
                 for (int c = r; c < 6; ++c) S.tot[7 + up(r, c)] = a[6 + up(r, c)] - nn * m[r] * m[c];
             for (int d = 0; d < 6; ++d) tol += S.tot[7 + up(d, d)] / nn;
             S.tol = tol / 6.0 * 1e-4;
+            // Kabsch sums over ALL points about (cs, cd) = (x0_p + x0_f, x0_p), from the raw
+            // moments about x0: s - cs = v_f + v_p, d - cd = v_p  (v = x - x0; f = 0..2, p = 3..5)
+            for (int d = 0; d < 6; ++d) S.x0[d] = x0[d];
+            S.ktot[0] = nn;
+            for (int r = 0; r < 3; ++r) { S.ktot[1 + r] = a[r] + a[3 + r]; S.ktot[4 + r] = a[3 + r]; }
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) {
+                    const int fr = r, pr = 3 + r, pc = 3 + c;
+                    const double sfp = a[6 + (fr <= pc ? up(fr, pc) : up(pc, fr))];
+                    const double spp = a[6 + (pr <= pc ? up(pr, pc) : up(pc, pr))];
+                    S.ktot[7 + r * 3 + c] = sfp + spp;
+                }
             S.c0 = (int64_t)draws[3 * f];
             if (S.c0 < 0) S.c0 = 0;
             if (S.c0 >= n) S.c0 = n - 1;
@@ -393,6 +451,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         }
         __syncthreads();
     }
+    SSF_STAMP(0);
     double mean[6];
 #pragma unroll
     for (int d = 0; d < 6; ++d) mean[d] = S.mean[d];
@@ -405,50 +464,53 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             load_x(P, Fl, S.c0, x);
             for (int d = 0; d < 6; ++d) { c0[d] = x[d] - mean[d]; cn0 += c0[d] * c0[d]; }
         }
-        double pot = 0.0;
-        for_points(P, Fl, n, [&](int64_t i, const double* x) {
-            double dt = 0.0, xs = 0.0;
+        // distances to the first centre, stored in D; each wave owns a contiguous segment so the
+        // in-order cumulative sum needs only one block-level exchange of wave totals
+        const int nw = blockDim.x >> 6, w = tid >> 6, lane = lane_id();
+        const int64_t seg = (((n + nw - 1) / nw) + 63) / 64 * 64;
+        const int64_t ws = (int64_t)w * seg, we = ws + seg < n ? ws + seg : n;
+        double wsum = 0.0;
+#pragma unroll 4
+        for (int64_t b = ws; b < we; b += 64) {
+            const int64_t i = b + lane;
+            if (i < we) {
+                double x[6], dt = 0.0, xs = 0.0;
+                load_x(P, Fl, i, x);
 #pragma unroll
-            for (int d = 0; d < 6; ++d) { const double v = x[d] - mean[d]; dt += c0[d] * v; xs += v * v; }
-            double v = (-2.0 * dt + cn0) + xs;
-            v = v > 0.0 ? v : 0.0;
-            D[i] = v;
-            pot += v;
-        });
-        pot = block_sum_scalar<double>(pot, red);
+                for (int d = 0; d < 6; ++d) { const double v = x[d] - mean[d]; dt += c0[d] * v; xs += v * v; }
+                double v = (-2.0 * dt + cn0) + xs;
+                v = v > 0.0 ? v : 0.0;
+                D[i] = v;
+                wsum += v;
+            }
+        }
+        wsum = wave_sum(wsum);
+        if (lane == 0) red[w] = wsum;
+        if (tid == 0) { cand_lds[0] = (unsigned long long)n; cand_lds[1] = (unsigned long long)n; }
+        __syncthreads();
+        double pot = 0.0, carry = 0.0;
+        for (int k = 0; k < nw; ++k) { if (k == w) carry = pot; pot += red[k]; }
         if (tid == 0) {
             S.rand1 = draws[3 * f + 1] * pot;
             S.rand2 = draws[3 * f + 2] * pot;
-            cand_lds[0] = (unsigned long long)n; cand_lds[1] = (unsigned long long)n;
             S.passes += 1;
         }
-        __syncthreads();
-        // in-order inclusive scan of D in chunks of blockDim; first index with cumsum >= rand
-        const double r1 = S.rand1, r2 = S.rand2;
-        double carry = 0.0;
-        const int w = tid >> 6;
-        for (int64_t c = 0; c < n; c += blockDim.x) {
-            const int64_t i = c + tid;
-            double v = i < n ? D[i] : 0.0;
+        const double r1 = draws[3 * f + 1] * pot, r2 = draws[3 * f + 2] * pot;
+        // wave-local in-order inclusive scan of its segment; first index with cumsum >= rand
+        bool f1 = false, f2 = false;
+        for (int64_t b = ws; b < we && !(f1 && f2); b += 64) {
+            const int64_t i = b + lane;
+            double v = i < we ? D[i] : 0.0;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const double y = __shfl_up(v, o, 64);
-                if (lane_id() >= o) v += y;
+                if (lane >= o) v += y;
             }
-            if (lane_id() == 63) red[w] = v;
-            __syncthreads();
-            double pre = carry;
-            for (int k = 0; k < w; ++k) pre += red[k];
-            const double incl = pre + v;
-            double tot = carry;
-            for (int k = 0; k < kNW; ++k) tot += red[k];
-            if (i < n) {
-                if (incl >= r1) atomicMin(&cand_lds[0], (unsigned long long)i);
-                if (incl >= r2) atomicMin(&cand_lds[1], (unsigned long long)i);
-            }
-            __syncthreads();
-            carry = tot;
-            if (cand_lds[0] < (unsigned long long)n && cand_lds[1] < (unsigned long long)n) break;
+            const double incl = carry + v;
+            const uint64_t m1 = __ballot(i < we && incl >= r1), m2 = __ballot(i < we && incl >= r2);
+            if (!f1 && m1) { f1 = true; if (lane == 0) atomicMin(&cand_lds[0], (unsigned long long)(b + __ffsll((unsigned long long)m1) - 1)); }
+            if (!f2 && m2) { f2 = true; if (lane == 0) atomicMin(&cand_lds[1], (unsigned long long)(b + __ffsll((unsigned long long)m2) - 1)); }
+            carry += __shfl(v, 63, 64);
         }
         __syncthreads();
         const int64_t cand[2] = {cand_lds[0] < (unsigned long long)n ? (int64_t)cand_lds[0] : n - 1,
@@ -460,59 +522,69 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             for (int d = 0; d < 6; ++d) { cc[j][d] = x[d] - mean[d]; ccn[j] += cc[j][d] * cc[j][d]; }
         }
         double cp[2] = {0.0, 0.0};
-        for_points(P, Fl, n, [&](int64_t i, const double* x) {
-            double xs = 0.0, dt0 = 0.0, dt1 = 0.0;
+#pragma unroll 4
+        for (int64_t b = ws; b < we; b += 64) {
+            const int64_t i = b + lane;
+            if (i < we) {
+                double x[6], xs = 0.0, dt0 = 0.0, dt1 = 0.0;
+                load_x(P, Fl, i, x);
+                const double di = D[i];
 #pragma unroll
-            for (int d = 0; d < 6; ++d) {
-                const double v = x[d] - mean[d];
-                xs += v * v; dt0 += cc[0][d] * v; dt1 += cc[1][d] * v;
+                for (int d = 0; d < 6; ++d) {
+                    const double v = x[d] - mean[d];
+                    xs += v * v; dt0 += cc[0][d] * v; dt1 += cc[1][d] * v;
+                }
+                double v0 = (-2.0 * dt0 + ccn[0]) + xs, v1 = (-2.0 * dt1 + ccn[1]) + xs;
+                v0 = v0 > 0.0 ? v0 : 0.0; v1 = v1 > 0.0 ? v1 : 0.0;
+                cp[0] += v0 < di ? v0 : di;
+                cp[1] += v1 < di ? v1 : di;
             }
-            double v0 = (-2.0 * dt0 + ccn[0]) + xs, v1 = (-2.0 * dt1 + ccn[1]) + xs;
-            v0 = v0 > 0.0 ? v0 : 0.0; v1 = v1 > 0.0 ? v1 : 0.0;
-            const double di = D[i];
-            cp[0] += v0 < di ? v0 : di;
-            cp[1] += v1 < di ? v1 : di;
-        });
+        }
         block_sum<2>(cp, red);
         if (tid == 0) {
             const int best = cp[1] < cp[0] ? 1 : 0;
             S.c1 = cand[best];
             for (int d = 0; d < 6; ++d) { S.cen[d] = c0[d]; S.cen[6 + d] = cc[best][d]; }
+            for (int d = 0; d < 12; ++d) S.cenp[d] = 0.0;
+            S.csnp[0] = S.csnp[1] = 0.0;
             S.passes += 2;
         }
         __syncthreads();
     }
 
-    // ---- Lloyd iterations (_kmeans_single_lloyd, max_iter 300)
+    SSF_STAMP(1);
+    // ---- Lloyd iterations (_kmeans_single_lloyd, max_iter 300).  The previous iteration's label
+    //      of a point is recomputed from the previous centres (2 dot products) instead of being
+    //      stored and re-loaded: the pass is a pure prefetched stream of [flow, xyz].
     if (tid == 0) { S.strict = 0; S.done = 0; }
     for (int it = 0; it < 300; ++it) {
         if (tid == 0) {
             for (int k = 0; k < 2; ++k) {
-                double s = 0.0;
-                for (int d = 0; d < 6; ++d) s += S.cen[6 * k + d] * S.cen[6 * k + d];
-                S.csn[k] = s;
+                double sn = 0.0;
+                for (int d = 0; d < 6; ++d) sn += S.cen[6 * k + d] * S.cen[6 * k + d];
+                S.csn[k] = sn;
             }
         }
         __syncthreads();
-        double cen[12];
-        const double csn0 = S.csn[0], csn1 = S.csn[1];
+        double cen[12], cenp[12];
+        const double csn0 = S.csn[0], csn1 = S.csn[1], cpn0 = S.csnp[0], cpn1 = S.csnp[1];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) cen[k] = S.cen[k];
+        for (int k = 0; k < 12; ++k) { cen[k] = S.cen[k]; cenp[k] = S.cenp[k]; }
         double acc[14];
 #pragma unroll
         for (int k = 0; k < 14; ++k) acc[k] = 0.0;
         int changed = 0;
-        for_points(P, Fl, n, [&](int64_t i, const double* x) {
-            double v[6], dt0 = 0.0, dt1 = 0.0;
+        for_points(P, Fl, n, [&](int64_t, const double* x) {
+            double v[6], dt0 = 0.0, dt1 = 0.0, dp0 = 0.0, dp1 = 0.0;
 #pragma unroll
             for (int d = 0; d < 6; ++d) {
                 v[d] = x[d] - mean[d];
                 dt0 += v[d] * cen[d]; dt1 += v[d] * cen[6 + d];
+                dp0 += v[d] * cenp[d]; dp1 += v[d] * cenp[6 + d];
             }
-            const double e0 = -2.0 * dt0 + csn0, e1 = -2.0 * dt1 + csn1;
-            const int l = e1 < e0 ? 1 : 0;
-            changed += (Lb[i] != (uint8_t)l) || it == 0;
-            Lb[i] = (uint8_t)l;
+            const int l = (-2.0 * dt1 + csn1) < (-2.0 * dt0 + csn0) ? 1 : 0;
+            const int lp = (-2.0 * dp1 + cpn1) < (-2.0 * dp0 + cpn0) ? 1 : 0;
+            changed += (it == 0) || (l != lp);
             const double w1 = (double)l, w0 = 1.0 - w1;
             acc[0] += w0; acc[7] += w1;
 #pragma unroll
@@ -523,6 +595,8 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         if (tid == 0) {
             S.passes += 1;
             S.km_iter = it + 1;
+            for (int k = 0; k < 12; ++k) S.cenp[k] = S.cen[k];
+            S.csnp[0] = S.csn[0]; S.csnp[1] = S.csn[1];
             double shift = 0.0;
             for (int k = 0; k < 2; ++k) {
                 const double wgt = acc[7 * k];
@@ -543,30 +617,30 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         if (S.done) break;
     }
 
-    // ---- GMM init from one-hot k-means labels (relabel first if not strictly converged);
-    //      only cluster 1's moments are summed, cluster 0 = total - cluster 1.
+    SSF_STAMP(2);
+    // ---- GMM init from one-hot k-means labels: strict convergence keeps the labels of the last
+    //      pass (centres S.cenp), otherwise sklearn relabels with the final centres (S.cen).
+    //      Only cluster 1's moments are summed, cluster 0 = total - cluster 1.
     {
-        const int strict = S.strict;
-        double cen[12], csn0 = 0.0, csn1 = 0.0;
+        double cen[12], csn0, csn1;
+        if (S.strict) {
 #pragma unroll
-        for (int k = 0; k < 12; ++k) cen[k] = S.cen[k];
-        for (int d = 0; d < 6; ++d) { csn0 += cen[d] * cen[d]; csn1 += cen[6 + d] * cen[6 + d]; }
+            for (int k = 0; k < 12; ++k) cen[k] = S.cenp[k];
+            csn0 = S.csnp[0]; csn1 = S.csnp[1];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) cen[k] = S.cen[k];
+            csn0 = 0.0; csn1 = 0.0;
+            for (int d = 0; d < 6; ++d) { csn0 += cen[d] * cen[d]; csn1 += cen[6 + d] * cen[6 + d]; }
+        }
         double acc[28];
 #pragma unroll
         for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-        for_points(P, Fl, n, [&](int64_t i, const double* x) {
-            double v[6];
+        for_points(P, Fl, n, [&](int64_t, const double* x) {
+            double v[6], dt0 = 0.0, dt1 = 0.0;
 #pragma unroll
-            for (int d = 0; d < 6; ++d) v[d] = x[d] - mean[d];
-            int l;
-            if (strict) {
-                l = Lb[i];
-            } else {
-                double dt0 = 0.0, dt1 = 0.0;
-#pragma unroll
-                for (int d = 0; d < 6; ++d) { dt0 += v[d] * cen[d]; dt1 += v[d] * cen[6 + d]; }
-                l = (-2.0 * dt1 + csn1) < (-2.0 * dt0 + csn0) ? 1 : 0;
-            }
+            for (int d = 0; d < 6; ++d) { v[d] = x[d] - mean[d]; dt0 += v[d] * cen[d]; dt1 += v[d] * cen[6 + d]; }
+            const int l = (-2.0 * dt1 + csn1) < (-2.0 * dt0 + csn0) ? 1 : 0;
             const double w1 = (double)l;
             acc[0] += w1;
 #pragma unroll
@@ -587,6 +661,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         __syncthreads();
     }
 
+    SSF_STAMP(3);
     // ---- EM: one fused pass per iteration -- E-step with the current parameters and the
     //      M-step moments of component 1 (component 0 = total - component 1).
     //      r_max = 1/(1+e), r_min = e/(1+e), lse = max + log1p(e), e = exp(min - max): the
@@ -596,30 +671,38 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         double acc[29];
 #pragma unroll
         for (int k = 0; k < 29; ++k) acc[k] = 0.0;
-        for_points(P, Fl, n, [&](int64_t, const double* x) {
-            // U / cU are re-read from LDS (broadcast ds_reads) for every point: the laundered
+        for_point_pairs(P, Fl, n, [&](const double* xa, const double* xb, double wb) {
+            // U / cU are re-read from LDS (broadcast ds_reads) for every pair: the laundered
             // offset stops the compiler hoisting 54 loop-invariant doubles into VGPRs.
             int z = 0;
             asm volatile("" : "+s"(z));
             const double* U = S.U + z;
             const double* cU = S.cU + z;
-            const double a0 = wlp(x, U, cU, ld0, lw0);
-            const double a1 = wlp(x, U + 21, cU + 6, ld1, lw1);
-            const double mx = a0 > a1 ? a0 : a1, mn = a0 > a1 ? a1 : a0;
-            const double e = exp(mn - mx);
-            acc[28] += mx + log1p(e);
-            const double inv = 1.0 / (1.0 + e);
-            const double r1 = a1 > a0 ? inv : e * inv;
-            acc[0] += r1;
-            double v[6];
+            const double a0a = wlp(xa, U, cU, ld0, lw0), a0b = wlp(xb, U, cU, ld0, lw0);
+            const double a1a = wlp(xa, U + 21, cU + 6, ld1, lw1), a1b = wlp(xb, U + 21, cU + 6, ld1, lw1);
+            const double mxa = a0a > a1a ? a0a : a1a, mna = a0a > a1a ? a1a : a0a;
+            const double mxb = a0b > a1b ? a0b : a1b, mnb = a0b > a1b ? a1b : a0b;
+            const double ea = exp(mna - mxa), eb = exp(mnb - mxb);
+            acc[28] += mxa + log1p(ea);
+            acc[28] += wb * (mxb + log1p(eb));
+            const double inva = 1.0 / (1.0 + ea), invb = 1.0 / (1.0 + eb);
+            const double ra = a1a > a0a ? inva : ea * inva;
+            const double rb = wb * (a1b > a0b ? invb : eb * invb);
+            acc[0] += ra;
+            acc[0] += rb;
+            double va[6], vb[6];
 #pragma unroll
-            for (int a = 0; a < 6; ++a) v[a] = x[a] - mean[a];
+            for (int a = 0; a < 6; ++a) { va[a] = xa[a] - mean[a]; vb[a] = xb[a] - mean[a]; }
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
-                const double rv = r1 * v[a];
-                acc[1 + a] += rv;
+                const double rva = ra * va[a], rvb = rb * vb[a];
+                acc[1 + a] += rva;
+                acc[1 + a] += rvb;
 #pragma unroll
-                for (int b = a; b < 6; ++b) acc[7 + up(a, b)] += rv * v[b];
+                for (int b = a; b < 6; ++b) {
+                    acc[7 + up(a, b)] += rva * va[b];
+                    acc[7 + up(a, b)] += rvb * vb[b];
+                }
             }
         });
         block_sum<29>(acc, red);
@@ -635,15 +718,19 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         if (S.done) break;
     }
 
-    // ---- final E-step labels + per-label Kabsch sums
+    SSF_STAMP(4);
+    // ---- final E-step labels + label-1 Kabsch sums (label 0 = totals from pass 0 - label 1).
+    //      The mask is written in the same pass against a predicted background label (the
+    //      heavier component); the rare frame whose majority disagrees gets one flip pass.
     {
         const double ld0 = S.logdet[0], lw0 = S.logw[0], ld1 = S.logdet[1], lw1 = S.logw[1];
-        double cs[6], cd[6];
-        for (int k = 0; k < 2; ++k)
-            for (int i = 0; i < 3; ++i) { cd[3 * k + i] = S.mu[6 * k + 3 + i]; cs[3 * k + i] = S.mu[6 * k + 3 + i] + S.mu[6 * k + i]; }
-        double k0[16], k1[16];
+        const int pred = lw1 > lw0 ? 1 : 0;
+        double x0[6];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) { k0[i] = 0.0; k1[i] = 0.0; }
+        for (int d = 0; d < 6; ++d) x0[d] = S.x0[d];
+        double k1[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) k1[i] = 0.0;
         for_points(P, Fl, n, [&](int64_t i, const double* x) {
             // U / cU are re-read from LDS (broadcast ds_reads) for every point: the laundered
             // offset stops the compiler hoisting 54 loop-invariant doubles into VGPRs.
@@ -654,27 +741,42 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             const double a0 = wlp(x, U, cU, ld0, lw0);
             const double a1 = wlp(x, U + 21, cU + 6, ld1, lw1);
             const int l = a1 > a0 ? 1 : 0;
-            Lb[i] = (uint8_t)l;
+            if (bg_mask) bg_mask[fb + i] = (uint8_t)(l == pred);
             if (i == 0) S.label0 = l;
-            if (l) accum_kabsch(k1, x, cs + 3, cd + 3);
-            else accum_kabsch(k0, x, cs, cd);
+            const double w1 = (double)l;
+            double sv[3], dv[3];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) { dv[r] = x[3 + r] - x0[3 + r]; sv[r] = dv[r] + (x[r] - x0[r]); }
+            k1[0] += w1;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const double ws = w1 * sv[r];
+                k1[1 + r] += ws;
+                k1[4 + r] += w1 * dv[r];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) k1[7 + r * 3 + c] += ws * dv[c];
+            }
         });
-        block_sum<16>(k0, red);
         block_sum<16>(k1, red);
         if (tid == 0) {
             S.passes += 1;
-            for (int i = 0; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
+            for (int i = 0; i < 26; ++i) out[i] = 0.0;
             const double n1 = k1[0];
             int bg;
             if (n1 * 2.0 > (double)n) bg = 1;
             else if (n1 * 2.0 < (double)n) bg = 0;
             else bg = S.label0;                     // Counter.most_common tie -> first seen
             S.bg = bg;
+            S.bg_pred = pred;
+            double kb[16];
+            for (int i = 0; i < 16; ++i) kb[i] = bg ? k1[i] : S.ktot[i] - k1[i];
+            const double cs[3] = {S.x0[3] + S.x0[0], S.x0[4] + S.x0[1], S.x0[5] + S.x0[2]};
+            const double cd[3] = {S.x0[3], S.x0[4], S.x0[5]};
             int st = S.status;
-            if (st == 0) st = kabsch_finish(bg ? k1 : k0, bg ? cs + 3 : cs, bg ? cd + 3 : cd, reflection, out);
+            if (st == 0) st = kabsch_finish(kb, cs, cd, reflection, out);
             out[SSF_POSE_OUT_STATUS] = st;
             out[SSF_POSE_OUT_BGLABEL] = bg;
-            out[SSF_POSE_OUT_NBG] = bg ? k1[0] : k0[0];
+            out[SSF_POSE_OUT_NBG] = kb[0];
             out[SSF_POSE_OUT_KM_ITER] = S.km_iter;
             out[SSF_POSE_OUT_EM_ITER] = S.em_iter;
             out[SSF_POSE_OUT_CONVERGED] = S.converged;
@@ -685,10 +787,10 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         }
         __syncthreads();
     }
-    if (bg_mask) {
-        const uint8_t bg = (uint8_t)S.bg;
-        for (int64_t i = tid; i < n; i += blockDim.x) bg_mask[fb + i] = Lb[i] == bg ? 1 : 0;
+    if (bg_mask && S.bg != S.bg_pred) {
+        for (int64_t i = tid; i < n; i += blockDim.x) bg_mask[fb + i] ^= 1;
     }
+    SSF_STAMP(5);
 }
 
 hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,

@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the dlopen below, see module docstring)
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
-LIB_PATH = os.path.join(LIB_DIR, "libssf_frontend.so")
+LIB_PATH = os.environ.get("SSF_LIB", os.path.join(LIB_DIR, "libssf_frontend.so"))
 
 SSF_OK, SSF_E_ARG, SSF_E_HIP, SSF_E_NOMEM, SSF_E_CAPACITY, SSF_E_NODEV = 0, -1, -2, -3, -4, -5
 SOLVER_CERES_LM, SOLVER_GN = 0, 1

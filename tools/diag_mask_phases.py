@@ -1,0 +1,45 @@
+"""Per-phase cycle shares of k_mask_pose from the diagnostic build (SSF_LIB=.../libssf_frontend_diag.so).
+Read the SHARES, not the absolute time (stamps perturb the kernel)."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "ssf-slam_amd"), REPO]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    import ssf
+    from ssf import synth
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    dev = torch.device("cuda", 0)
+    fr = [synth.scan(s, 0, device=dev) for s in range(8)]
+    pts = torch.cat([fr[b % 8]["pos1"] for b in range(B)]).contiguous()
+    flow = torch.cat([fr[b % 8]["flow"] for b in range(B)]).contiguous()
+    N = fr[0]["pos1"].shape[0]
+    off, h_off = ssf.frame_offsets([N] * B, dev)
+    fe = ssf.Frontend(64, device=0)
+    fe.seed(1)
+    fe.mask_pose(pts, flow, off, h_off)
+    torch.cuda.synchronize()
+    out, _ = fe.mask_pose(pts, flow, off, h_off)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    st = o[:, 26:32]
+    names = ["pass0", "kmeans++", "lloyd", "gmm_init", "em", "final+mask"]
+    d = np.diff(np.concatenate([np.zeros((B, 1)), st], 1), axis=1)
+    tot = st[:, 5].mean()
+    print(f"B={B} mean cycles/frame {tot:.3e}; km_iter {o[:, 19].mean():.1f} em_iter {o[:, 20].mean():.1f} "
+          f"passes {o[:, 25].mean():.1f}")
+    for k, nme in enumerate(names):
+        per = ""
+        if nme == "lloyd":
+            per = f"  per pass {d[:, k].mean() / o[:, 19].mean():.3e}"
+        if nme == "em":
+            per = f"  per pass {d[:, k].mean() / o[:, 20].mean():.3e}"
+        print(f"  {nme:12s} {d[:, k].mean():.3e} cyc  {100 * d[:, k].mean() / tot:5.1f} %{per}")
+
+
+if __name__ == "__main__":
+    main()

@@ -147,6 +147,7 @@ SSF_DEV void plane_from_knn(const float4* __restrict__ P, const float (&kd)[30],
 #pragma unroll
     for (int ik = 0; ik < 30; ++ik) {                                  // :180-198
         if (ik < K && nvr < 2) {
+            if ((unsigned)ki[ik] >= (unsigned)m) { ok = 0; return; }   // never reached: lists are complete
             const float fi = P[ki[ik]].w;
             const int ii = (int)fi;
             const int row = (int)(100.0 * ((double)(fi - (float)ii) + 0.002));
@@ -315,17 +316,151 @@ __global__ __launch_bounds__(256) void k_associate(const float4* __restrict__ la
 constexpr int kSortMax = 16384;           // plane points per frame sorted in LDS (128 KiB)
 constexpr int kTableThreads = 1024;
 
+constexpr int kLdsWalkMax = 6144;         // after the sort, frames up to this size walk in LDS
+
+// Diagnostic build only (-DSSF_TABLE_STAMPS): lane 0 writes s_memtime deltas after the sort,
+// the bounded walks and the deferred walks into sorted_idx[m .. m+3] (frame padding, read by
+// tools/diag_table_phases.py); the product library never executes it.
+#ifdef SSF_TABLE_STAMPS
+#define SSF_TSTAMP(k) do { __syncthreads(); if (threadIdx.x == 0) SI[m + (k)] = (int32_t)((__builtin_amdgcn_s_memtime() - tstamp0) >> 4); } while (0)
+#else
+#define SSF_TSTAMP(k) do { } while (0)
+#endif
+
+// Outward x-walk from sorted rank r.  bounded: stop once dx^2 >= 1 as well (only points with
+// d2 < 1 are needed to decide most queries, see table_query).
+template <bool kLds>
+SSF_DEV void knn_walk(const float4* __restrict__ SPg, const float4* __restrict__ SPl,
+                      const int* __restrict__ idx, int m, int r, const float4& q, bool bounded,
+                      float (&kd)[kK], int (&ki)[kK]) {
+#pragma unroll
+    for (int k = 0; k < kK; ++k) { kd[k] = __builtin_inff(); ki[k] = 0x7fffffff; }
+    for (int c = r; c < m; ++c) {                         // rightwards (x non-decreasing)
+        const float4 p = kLds ? SPl[c] : SPg[c];
+        const float dx = q.x - p.x;
+        const float dx2 = dx * dx;
+        if (dx2 > kd[kK - 1] || (bounded && dx2 >= 1.0f)) break;
+        const float d = l2_simple(q, p);
+        const int id = idx[c];
+        if (lex_less(d, id, kd[kK - 1], ki[kK - 1])) knn_insert<kK>(kd, ki, d, id);
+    }
+    for (int c = r - 1; c >= 0; --c) {                    // leftwards
+        const float4 p = kLds ? SPl[c] : SPg[c];
+        const float dx = q.x - p.x;
+        const float dx2 = dx * dx;
+        if (dx2 > kd[kK - 1] || (bounded && dx2 >= 1.0f)) break;
+        const float d = l2_simple(q, p);
+        const int id = idx[c];
+        if (lex_less(d, id, kd[kK - 1], ki[kK - 1])) knn_insert<kK>(kd, ki, d, id);
+    }
+}
+
+SSF_DEV int row_of(float fi) {                           // lidarOdometry_onlyPC.cpp:181-183
+    const int ii = (int)fi;
+    return (int)(100.0 * ((double)(fi - (float)ii) + 0.002));
+}
+
+// Is the 1-m-bounded list (kd, ki) enough to reproduce :177-232 exactly?  Let K1 = #points with
+// d2 < 1 (all of them are in the list: they have |dx| < 1).  The gate d2[n] < 1 (:207) holds iff
+// n < K1.  K1 <= 5 -> n >= 5 fails;  K1 >= 30 -> the list is the exact 30-NN;  two qualifying
+// different-row points among ranks 5..K1-1 -> n < K1 and only ranks < K1 are used.  Otherwise
+// the answer depends on ranks beyond 1 m and the query takes the full walk.
+// returns 0 undecided, 1 decided (the list is exact for every rank the pick uses), 2 decided
+// invalid (K1 <= 5: the list may be short, the plane is rejected without reading it).
+SSF_DEV int bounded_decides(const float4* __restrict__ P, int m, const float (&kd)[kK],
+                            const int (&ki)[kK]) {
+    if (m <= kK) return 0;
+    int K1 = 0;
+#pragma unroll
+    for (int k = 0; k < kK; ++k) K1 += kd[k] < 1.0f;
+    if (K1 <= 5) return 2;
+    if (K1 >= kK) return 1;
+    const int prow = row_of(P[ki[0]].w);
+    int nq = 0;
+#pragma unroll
+    for (int k = 5; k < kK; ++k)
+        if (k < K1) {
+            const int row = row_of(P[ki[k]].w);
+            nq += (row != prow && row >= 0 && row <= 63);
+        }
+    return nq >= 2 ? 1 : 0;
+}
+
+template <bool kLds>
+SSF_DEV void table_finish(const float4* __restrict__ P, int m, float plane_max, int64_t o,
+                          const float (&kd)[kK], const int (&ki)[kK], float* __restrict__ normal,
+                          uint8_t* __restrict__ valid) {
+    float nrm[3];
+    uint8_t ok;
+    plane_from_knn(P, kd, ki, m, plane_max, nrm, ok);
+    normal[3 * o] = nrm[0]; normal[3 * o + 1] = nrm[1]; normal[3 * o + 2] = nrm[2];
+    valid[o] = ok;
+}
+
+// Queries in sorted order (adjacent lanes ~ adjacent x): 1-m-bounded walk for everyone; the
+// undecided few go to an LDS queue and are re-walked in full afterwards, one per lane, so a
+// handful of long walks no longer stalls whole waves.  queue == nullptr: walk in full at once.
+template <bool kLds>
+SSF_DEV void table_walks(const float4* __restrict__ P, const float4* __restrict__ SPg,
+                         const float4* __restrict__ SPl, const int* __restrict__ idx, int m,
+                         float plane_max, int64_t base, float* __restrict__ normal,
+                         uint8_t* __restrict__ valid, int* queue, int qcap, int* qlen,
+                         int32_t* stamp_out = nullptr, unsigned long long stamp0 = 0) {
+    for (int r = threadIdx.x; r < m; r += blockDim.x) {
+        const float4 q = kLds ? SPl[r] : SPg[r];
+        float kd[kK];
+        int ki[kK];
+        knn_walk<kLds>(SPg, SPl, idx, m, r, q, true, kd, ki);
+        const int dec = bounded_decides(P, m, kd, ki);
+        if (dec == 2) {                                   // gate d2[n] < 1 fails for any n >= 5
+            const int64_t o = base + idx[r];
+            normal[3 * o] = 0.f; normal[3 * o + 1] = 0.f; normal[3 * o + 2] = 0.f;
+            valid[o] = 0;
+            continue;
+        }
+        if (dec == 0) {
+            const int slot = queue ? atomicAdd(qlen, 1) : qcap;
+            if (slot < qcap) { queue[slot] = r; continue; }
+            knn_walk<kLds>(SPg, SPl, idx, m, r, q, false, kd, ki);
+        }
+        table_finish<kLds>(P, m, plane_max, base + idx[r], kd, ki, normal, valid);
+    }
+    if (!queue) return;
+    __syncthreads();
+#ifdef SSF_TABLE_STAMPS
+    if (threadIdx.x == 0 && stamp_out) *stamp_out = (int32_t)((__builtin_amdgcn_s_memtime() - stamp0) >> 4);
+    if (threadIdx.x == 0 && stamp_out) stamp_out[1] = *qlen;
+#endif
+    const int nq = min(*qlen, qcap);
+    for (int k = threadIdx.x; k < nq; k += blockDim.x) {
+        const int r = queue[k];
+        const float4 q = kLds ? SPl[r] : SPg[r];
+        float kd[kK];
+        int ki[kK];
+        knn_walk<kLds>(SPg, SPl, idx, m, r, q, false, kd, ki);
+        table_finish<kLds>(P, m, plane_max, base + idx[r], kd, ki, normal, valid);
+    }
+}
+
 __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
     const float4* __restrict__ plane, const int64_t* __restrict__ frame_off,
     const int32_t* __restrict__ count, float plane_max, float* __restrict__ normal,
     uint8_t* __restrict__ valid, float4* __restrict__ sorted_xyzi, int32_t* __restrict__ sorted_idx) {
-    __shared__ float key[kSortMax];
-    __shared__ int idx[kSortMax];
+    // 160 KiB of LDS: [0, 64K) keys, [64K, 128K) permutation, [128K, 160K) spare.  After the
+    // sort, frames <= kLdsWalkMax move the permutation to the spare region and put the sorted
+    // points (<= 96 KiB) over the keys and the old permutation.
+    __shared__ __attribute__((aligned(16))) char lds[kSortMax * 8 + 32768];
+    float* key = reinterpret_cast<float*>(lds);
+    int* idx = reinterpret_cast<int*>(lds + kSortMax * 4);
+    float4* SPl = reinterpret_cast<float4*>(lds);
     const int f = blockIdx.x, tid = threadIdx.x;
     const int m = count[f];
     const int64_t base = frame_off[f];
     const float4* P = plane + base;
     if (m <= 0) return;
+#ifdef SSF_TABLE_STAMPS
+    const unsigned long long tstamp0 = __builtin_amdgcn_s_memtime();
+#endif
     int np = 1;
     while (np < m) np <<= 1;
     for (int r = tid; r < np; r += blockDim.x) {
@@ -356,35 +491,28 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
         SI[r] = idx[r];
     }
     __syncthreads();
-    for (int r = tid; r < m; r += blockDim.x) {
-        const int a = idx[r];
-        const float4 q = SP[r];
-        float kd[kK];
-        int ki[kK];
-#pragma unroll
-        for (int k = 0; k < kK; ++k) { kd[k] = __builtin_inff(); ki[k] = 0x7fffffff; }
-        for (int c = r; c < m; ++c) {                     // rightwards (x non-decreasing)
-            const float dx = q.x - key[c];
-            if (dx * dx > kd[kK - 1]) break;
-            const float4 p = SP[c];
-            const float d = l2_simple(q, p);
-            const int id = idx[c];
-            if (lex_less(d, id, kd[kK - 1], ki[kK - 1])) knn_insert<kK>(kd, ki, d, id);
-        }
-        for (int c = r - 1; c >= 0; --c) {                // leftwards
-            const float dx = q.x - key[c];
-            if (dx * dx > kd[kK - 1]) break;
-            const float4 p = SP[c];
-            const float d = l2_simple(q, p);
-            const int id = idx[c];
-            if (lex_less(d, id, kd[kK - 1], ki[kK - 1])) knn_insert<kK>(kd, ki, d, id);
-        }
-        float nrm[3];
-        uint8_t ok;
-        plane_from_knn(P, kd, ki, m, plane_max, nrm, ok);
-        const int64_t o = base + a;
-        normal[3 * o] = nrm[0]; normal[3 * o + 1] = nrm[1]; normal[3 * o + 2] = nrm[2];
-        valid[o] = ok;
+    SSF_TSTAMP(0);
+    int* qlen = reinterpret_cast<int*>(lds + sizeof(lds) - 4);   // last word of the LDS image
+    if (tid == 0) *qlen = 0;
+    if (m <= kLdsWalkMax) {
+        // spare region: [128K, 128K + 4m) permutation, the rest (>= 8 KiB) the deferred queue
+        int* idx2 = reinterpret_cast<int*>(lds + kSortMax * 8);
+        int* queue = idx2 + m;
+        const int qcap = (32768 - 4 * m - 4) / 4;
+        for (int r = tid; r < m; r += blockDim.x) idx2[r] = idx[r];
+        __syncthreads();
+        for (int r = tid; r < m; r += blockDim.x) SPl[r] = P[idx2[r]];
+        __syncthreads();
+        #ifdef SSF_TABLE_STAMPS
+        table_walks<true>(P, SP, SPl, idx2, m, plane_max, base, normal, valid, queue, qcap, qlen, SI + m + 1, tstamp0);
+#else
+        table_walks<true>(P, SP, SPl, idx2, m, plane_max, base, normal, valid, queue, qcap, qlen);
+#endif
+        SSF_TSTAMP(3);
+    } else {
+        // queue in the (now unused) key region
+        int* queue = reinterpret_cast<int*>(lds);
+        table_walks<false>(P, SP, SPl, idx, m, plane_max, base, normal, valid, queue, kSortMax, qlen);
     }
 }
 

@@ -1,0 +1,34 @@
+"""Phase shares of k_plane_table_sorted (diagnostic build, SSF_LIB=.../libssf_frontend_diag.so)."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "ssf-slam_amd"), REPO]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    import ssf
+    from ssf import synth
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    dev = torch.device("cuda", 0)
+    fr = [synth.scan(s, 0, device=dev)["pos1"] for s in range(8)]
+    pts = torch.cat([fr[b % 8] for b in range(B)]).contiguous()
+    N = fr[0].shape[0]
+    off, h_off = ssf.frame_offsets([N] * B, dev)
+    fe = ssf.Frontend(64, device=0)
+    pb = fe.extract_planes_batch(pts, off, h_off)
+    for _ in range(2):
+        t = fe.plane_table(pb)
+        torch.cuda.synchronize()
+    si = t[3].cpu().numpy()
+    cnt = pb.count.cpu().numpy()
+    st = np.array([si[int(h_off[f]) + cnt[f]: int(h_off[f]) + cnt[f] + 4] for f in range(B)]).astype(np.float64)
+    st[:, [0, 1, 3]] *= 16
+    print(f"B={B} m mean {cnt.mean():.0f}; cycles: sort {st[:,0].mean():.3e}  bounded-walks-end {st[:,1].mean():.3e} "
+          f"(queue {st[:,2].mean():.0f})  end {st[:,3].mean():.3e}")
+
+
+if __name__ == "__main__":
+    main()

@@ -134,9 +134,30 @@ SSF_DEV float l2_simple(const float4& q, const float4& p) {
     return d + dz * dz;
 }
 
+// A (distance, index) pair packed into one f64: high word = the non-negative f32 distance
+// bits, low word = the index.  For non-negative, non-NaN values the f64 order is the u64 order
+// of the bits, i.e. exactly the lexicographic (distance, index) order, so a sorted insertion is
+// one v_min_f64 + one v_max_f64 per slot.  (Keys with distance 0 are f64 denormals; the kernel
+// keeps f64 denormals, the default, so they compare correctly.)
+SSF_DEV double knn_key(float d, int id) { return __hiloint2double(__float_as_int(d), id); }
+SSF_DEV float key_dist(double k) { return __int_as_float(__double2hiint(k)); }
+SSF_DEV int key_index(double k) { return __double2loint(k); }
+
+template <int K>
+SSF_DEV void key_insert(double (&kk)[K], double key) {
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        // plain v_max/v_min (keys are never NaN: no canonicalisation), the slot updated in place
+        double hi;
+        asm("v_max_f64 %0, %1, %2" : "=v"(hi) : "v"(kk[s]), "v"(key));
+        asm("v_min_f64 %0, %0, %1" : "+v"(kk[s]) : "v"(key));
+        key = hi;
+    }
+}
+
 // Ring-diverse 5-point pick (:180-205), gate d2[n] < 1 (:207), 5x3 least-squares plane
-// (:208-220) and coplanarity gate (:222-232) from the sorted 30-NN list (kd, ki) of a point.
-SSF_DEV void plane_from_knn(const float4* __restrict__ P, const float (&kd)[30], const int (&ki)[30],
+// (:208-220) and coplanarity gate (:222-232) from the sorted 30-NN key list kk of a point.
+SSF_DEV void plane_from_knn(const float4* __restrict__ P, const double (&kk)[30],
                             int m, float plane_max, float nrm[3], uint8_t& ok) {
     const int K = m < 30 ? m : 30;
     nrm[0] = nrm[1] = nrm[2] = 0.f;
@@ -147,15 +168,16 @@ SSF_DEV void plane_from_knn(const float4* __restrict__ P, const float (&kd)[30],
 #pragma unroll
     for (int ik = 0; ik < 30; ++ik) {                                  // :180-198
         if (ik < K && nvr < 2) {
-            if ((unsigned)ki[ik] >= (unsigned)m) { ok = 0; return; }   // never reached: lists are complete
-            const float fi = P[ki[ik]].w;
+            const int id = key_index(kk[ik]);
+            if ((unsigned)id >= (unsigned)m) { ok = 0; return; }       // never reached: lists are complete
+            const float fi = P[id].w;
             const int ii = (int)fi;
             const int row = (int)(100.0 * ((double)(fi - (float)ii) + 0.002));
             if (ik == 0) prow = row;
             if (ik < 5) {
-                v5[ik] = ki[ik];
+                v5[ik] = id;
             } else if (row != prow && row >= 0 && row <= 63) {
-                if (nvr == 0) vr0 = ki[ik]; else vr1 = ki[ik];
+                if (nvr == 0) vr0 = id; else vr1 = id;
                 nvr++;
                 n = ik;
             }
@@ -163,9 +185,9 @@ SSF_DEV void plane_from_knn(const float4* __restrict__ P, const float (&kd)[30],
     }
     if (nvr == 1) v5[4] = vr0;                                         // :199-205
     if (nvr == 2) { v5[3] = vr0; v5[4] = vr1; }
-    float dn = kd[0];
+    float dn = key_dist(kk[0]);
 #pragma unroll
-    for (int ik = 0; ik < 30; ++ik) if (ik == n) dn = kd[ik];
+    for (int ik = 0; ik < 30; ++ik) if (ik == n) dn = key_dist(kk[ik]);
     if (!(dn < 1.0f)) return;                                          // :207
     float Am[3][5];
     float pts[5][3];
@@ -192,22 +214,6 @@ SSF_DEV void plane_from_knn(const float4* __restrict__ P, const float (&kd)[30],
     }
 }
 
-// sorted insertion into a (distance, index)-ordered top-K list: ties go to the lower index,
-// independent of the order candidates are visited in.
-template <int K>
-SSF_DEV void knn_insert(float (&kd)[K], int (&ki)[K], float d, int id) {
-#pragma unroll
-    for (int s = 0; s < K; ++s) {
-        const bool sw = d < kd[s] || (d == kd[s] && id < ki[s]);
-        const float td = kd[s];
-        const int ti = ki[s];
-        kd[s] = sw ? d : td;
-        ki[s] = sw ? id : ti;
-        d = sw ? td : d;
-        id = sw ? ti : id;
-    }
-}
-
 __global__ __launch_bounds__(256) void k_plane_table(const float4* __restrict__ plane,
                                                      const int64_t* __restrict__ frame_off,
                                                      const int32_t* __restrict__ count,
@@ -221,19 +227,17 @@ __global__ __launch_bounds__(256) void k_plane_table(const float4* __restrict__ 
     const bool active = a < m;
     const float4* P = plane + frame_off[f];
     const float4 q = active ? P[a] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float kd[kK];
-    int ki[kK];
+    double kk[kK];
 #pragma unroll
-    for (int k = 0; k < kK; ++k) { kd[k] = __builtin_inff(); ki[k] = 0x7fffffff; }
+    for (int k = 0; k < kK; ++k) kk[k] = knn_key(__builtin_inff(), 0x7fffffff);
     for (int t0 = 0; t0 < m; t0 += kKnnTile) {
         const int nt = min(kKnnTile, m - t0);
         for (int k = threadIdx.x; k < nt; k += blockDim.x) tile[k] = P[t0 + k];
         __syncthreads();
         if (active) {
             for (int k = 0; k < nt; ++k) {
-                float d = l2_simple(q, tile[k]);
-                const int id = t0 + k;
-                if (lex_less(d, id, kd[kK - 1], ki[kK - 1])) knn_insert<kK>(kd, ki, d, id);
+                const double key = knn_key(l2_simple(q, tile[k]), t0 + k);
+                if (key < kk[kK - 1]) key_insert<kK>(kk, key);
             }
         }
         __syncthreads();
@@ -241,7 +245,7 @@ __global__ __launch_bounds__(256) void k_plane_table(const float4* __restrict__ 
     if (!active) return;
     float nrm[3];
     uint8_t ok;
-    plane_from_knn(P, kd, ki, m, plane_max, nrm, ok);
+    plane_from_knn(P, kk, m, plane_max, nrm, ok);
     const int64_t o = frame_off[f] + a;
     normal[3 * o] = nrm[0]; normal[3 * o + 1] = nrm[1]; normal[3 * o + 2] = nrm[2];
     valid[o] = ok;
@@ -327,31 +331,31 @@ constexpr int kLdsWalkMax = 6144;         // after the sort, frames up to this s
 #define SSF_TSTAMP(k) do { } while (0)
 #endif
 
-// Outward x-walk from sorted rank r.  bounded: stop once dx^2 >= 1 as well (only points with
-// d2 < 1 are needed to decide most queries, see table_query).
+// Outward x-walk from sorted rank r.  bounded: the list is seeded with the sentinel distance 1,
+// so only points with d2 < 1 enter it, and the walk stops once dx^2 >= 1 (only those points are
+// needed to decide most queries, see bounded_decides).
 template <bool kLds>
 SSF_DEV void knn_walk(const float4* __restrict__ SPg, const float4* __restrict__ SPl,
                       const int* __restrict__ idx, int m, int r, const float4& q, bool bounded,
-                      float (&kd)[kK], int (&ki)[kK]) {
+                      double (&kk)[kK]) {
+    const float lim = bounded ? 1.0f : __builtin_inff();
 #pragma unroll
-    for (int k = 0; k < kK; ++k) { kd[k] = __builtin_inff(); ki[k] = 0x7fffffff; }
+    for (int k = 0; k < kK; ++k) kk[k] = knn_key(lim, 0x7fffffff);
     for (int c = r; c < m; ++c) {                         // rightwards (x non-decreasing)
         const float4 p = kLds ? SPl[c] : SPg[c];
         const float dx = q.x - p.x;
         const float dx2 = dx * dx;
-        if (dx2 > kd[kK - 1] || (bounded && dx2 >= 1.0f)) break;
-        const float d = l2_simple(q, p);
-        const int id = idx[c];
-        if (lex_less(d, id, kd[kK - 1], ki[kK - 1])) knn_insert<kK>(kd, ki, d, id);
+        if (dx2 > key_dist(kk[kK - 1]) || dx2 >= lim) break;
+        const double key = knn_key(l2_simple(q, p), idx[c]);
+        key_insert<kK>(kk, key);              // branch-free: a key >= kk[K-1] passes through
     }
     for (int c = r - 1; c >= 0; --c) {                    // leftwards
         const float4 p = kLds ? SPl[c] : SPg[c];
         const float dx = q.x - p.x;
         const float dx2 = dx * dx;
-        if (dx2 > kd[kK - 1] || (bounded && dx2 >= 1.0f)) break;
-        const float d = l2_simple(q, p);
-        const int id = idx[c];
-        if (lex_less(d, id, kd[kK - 1], ki[kK - 1])) knn_insert<kK>(kd, ki, d, id);
+        if (dx2 > key_dist(kk[kK - 1]) || dx2 >= lim) break;
+        const double key = knn_key(l2_simple(q, p), idx[c]);
+        key_insert<kK>(kk, key);              // branch-free: a key >= kk[K-1] passes through
     }
 }
 
@@ -367,20 +371,19 @@ SSF_DEV int row_of(float fi) {                           // lidarOdometry_onlyPC
 // the answer depends on ranks beyond 1 m and the query takes the full walk.
 // returns 0 undecided, 1 decided (the list is exact for every rank the pick uses), 2 decided
 // invalid (K1 <= 5: the list may be short, the plane is rejected without reading it).
-SSF_DEV int bounded_decides(const float4* __restrict__ P, int m, const float (&kd)[kK],
-                            const int (&ki)[kK]) {
+SSF_DEV int bounded_decides(const float4* __restrict__ P, int m, const double (&kk)[kK]) {
     if (m <= kK) return 0;
     int K1 = 0;
 #pragma unroll
-    for (int k = 0; k < kK; ++k) K1 += kd[k] < 1.0f;
+    for (int k = 0; k < kK; ++k) K1 += key_dist(kk[k]) < 1.0f;
     if (K1 <= 5) return 2;
     if (K1 >= kK) return 1;
-    const int prow = row_of(P[ki[0]].w);
+    const int prow = row_of(P[key_index(kk[0])].w);
     int nq = 0;
 #pragma unroll
     for (int k = 5; k < kK; ++k)
         if (k < K1) {
-            const int row = row_of(P[ki[k]].w);
+            const int row = row_of(P[key_index(kk[k])].w);
             nq += (row != prow && row >= 0 && row <= 63);
         }
     return nq >= 2 ? 1 : 0;
@@ -388,11 +391,11 @@ SSF_DEV int bounded_decides(const float4* __restrict__ P, int m, const float (&k
 
 template <bool kLds>
 SSF_DEV void table_finish(const float4* __restrict__ P, int m, float plane_max, int64_t o,
-                          const float (&kd)[kK], const int (&ki)[kK], float* __restrict__ normal,
+                          const double (&kk)[kK], float* __restrict__ normal,
                           uint8_t* __restrict__ valid) {
     float nrm[3];
     uint8_t ok;
-    plane_from_knn(P, kd, ki, m, plane_max, nrm, ok);
+    plane_from_knn(P, kk, m, plane_max, nrm, ok);
     normal[3 * o] = nrm[0]; normal[3 * o + 1] = nrm[1]; normal[3 * o + 2] = nrm[2];
     valid[o] = ok;
 }
@@ -408,22 +411,25 @@ SSF_DEV void table_walks(const float4* __restrict__ P, const float4* __restrict_
                          int32_t* stamp_out = nullptr, unsigned long long stamp0 = 0) {
     for (int r = threadIdx.x; r < m; r += blockDim.x) {
         const float4 q = kLds ? SPl[r] : SPg[r];
-        float kd[kK];
-        int ki[kK];
-        knn_walk<kLds>(SPg, SPl, idx, m, r, q, true, kd, ki);
-        const int dec = bounded_decides(P, m, kd, ki);
+        double kk[kK];
+        bool bounded = true;
+        int dec;
+        for (;;) {                                        // one walk call site: one live list
+            knn_walk<kLds>(SPg, SPl, idx, m, r, q, bounded, kk);
+            if (!bounded) { dec = 1; break; }
+            dec = bounded_decides(P, m, kk);
+            if (dec != 0) break;
+            const int slot = queue ? atomicAdd(qlen, 1) : qcap;
+            if (slot < qcap) { queue[slot] = r; break; }
+            bounded = false;
+        }
         if (dec == 2) {                                   // gate d2[n] < 1 fails for any n >= 5
             const int64_t o = base + idx[r];
             normal[3 * o] = 0.f; normal[3 * o + 1] = 0.f; normal[3 * o + 2] = 0.f;
             valid[o] = 0;
-            continue;
+        } else if (dec == 1) {
+            table_finish<kLds>(P, m, plane_max, base + idx[r], kk, normal, valid);
         }
-        if (dec == 0) {
-            const int slot = queue ? atomicAdd(qlen, 1) : qcap;
-            if (slot < qcap) { queue[slot] = r; continue; }
-            knn_walk<kLds>(SPg, SPl, idx, m, r, q, false, kd, ki);
-        }
-        table_finish<kLds>(P, m, plane_max, base + idx[r], kd, ki, normal, valid);
     }
     if (!queue) return;
     __syncthreads();
@@ -435,10 +441,9 @@ SSF_DEV void table_walks(const float4* __restrict__ P, const float4* __restrict_
     for (int k = threadIdx.x; k < nq; k += blockDim.x) {
         const int r = queue[k];
         const float4 q = kLds ? SPl[r] : SPg[r];
-        float kd[kK];
-        int ki[kK];
-        knn_walk<kLds>(SPg, SPl, idx, m, r, q, false, kd, ki);
-        table_finish<kLds>(P, m, plane_max, base + idx[r], kd, ki, normal, valid);
+        double kk[kK];
+        knn_walk<kLds>(SPg, SPl, idx, m, r, q, false, kk);
+        table_finish<kLds>(P, m, plane_max, base + idx[r], kk, normal, valid);
     }
 }
 

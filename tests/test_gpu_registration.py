@@ -65,6 +65,28 @@ def test_plane_table_bitexact(oracle, dev, brute):
         assert vr.mean() > 0.3
 
 
+def test_plane_table_duplicates_and_sizes(oracle, dev):
+    """Exact duplicate points (zero-distance ties broken by index), a frame above the LDS-walk
+    limit (6144: the walk reads the sorted copy in global memory) and one above the LDS sort
+    limit (16384: brute-force k-NN) -- all bit-exact against the oracle."""
+    import ssf
+    rng = np.random.default_rng(7)
+    base = [oracle.extract_planes(frame(s, 0, n_az=1875)[0], 64) for s in range(5)]
+    dup = np.concatenate([base[0], base[0][rng.choice(len(base[0]), 600, replace=False)]])
+    clouds = [dup[rng.permutation(len(dup))], np.concatenate(base[:2]), np.concatenate(base)]
+    assert len(clouds[1]) > 6144 and len(clouds[2]) > 16384
+    fe = ssf.Frontend(64, device=dev.index)
+    for f, P in enumerate(clouds):          # one launch each: the kernel choice is per launch
+        off, h_off = ssf.frame_offsets([len(P)], dev)
+        xyzi = torch.from_numpy(P.astype(np.float32)).to(dev)
+        pb = ssf.PlaneBatch(xyzi, torch.tensor([len(P)], dtype=torch.int32, device=dev), off, h_off, len(P))
+        normal, valid, _, _ = fe.plane_table(pb)
+        nr, vr, _, _ = oracle.plane_table(P, 0.05)
+        assert np.array_equal(valid.cpu().numpy(), vr.astype(np.uint8)), f
+        g = normal.cpu().numpy()
+        assert np.array_equal(g.view(np.uint32), nr.view(np.uint32)), f
+
+
 @pytest.mark.parametrize("solver,iters,mode,brute", [("ceres_lm", 8, 0, False), ("gn", 10, 1, False),
                                                      ("ceres_lm", 8, 0, True)])
 def test_register_pair_per_step(oracle, dev, solver, iters, mode, brute):

@@ -22,7 +22,10 @@
 
 namespace ssf {
 
-constexpr int kMaskThreads = 512;
+#ifndef SSF_MASK_THREADS
+#define SSF_MASK_THREADS 768
+#endif
+constexpr int kMaskThreads = SSF_MASK_THREADS;   // 12 waves: 3 per SIMD at <= 168 VGPRs
 
 // Diagnostic build only (-DSSF_MASK_STAMPS, libssf_frontend_diag.so): lane 0 records the
 // s_memtime cycle count at each phase boundary into the frame's unused out slots 26..31.
@@ -131,30 +134,6 @@ __device__ __noinline__ int gmm_params(MaskShared& S, const double* comp1, int i
     return 0;
 }
 
-// Same, two points per iteration (i, i + T): two independent f64 dependency chains per wave to
-// hide the exp / log1p / divide latencies at 2 waves per SIMD.  The second point of the last
-// pair may not exist (w1 == 0): it is computed on a duplicate and weighted out.
-template <class Fn>
-SSF_DEV void for_point_pairs(const float* __restrict__ P, const float* __restrict__ Fl, int64_t n, Fn&& fn) {
-    const int64_t T = blockDim.x;
-    int64_t i = threadIdx.x;
-    if (i >= n) return;
-    double xa[6], xb[6];
-    load_x(P, Fl, i, xa);
-    load_x(P, Fl, i + T < n ? i + T : i, xb);
-    for (; i < n; i += 2 * T) {
-        double x0[6], x1[6];
-#pragma unroll
-        for (int d = 0; d < 6; ++d) { x0[d] = xa[d]; x1[d] = xb[d]; }
-        const double w1 = (i + T < n) ? 1.0 : 0.0;
-        if (i + 2 * T < n) {
-            load_x(P, Fl, i + 2 * T, xa);
-            load_x(P, Fl, i + 3 * T < n ? i + 3 * T : i + 2 * T, xb);
-        }
-        fn(x0, x1, w1);
-    }
-}
-
 // weighted log probability, sklearn _estimate_log_gaussian_prob form: y = x U - (mu U), with
 // c = mu U precomputed by lane 0 (S.cU); U packed upper.
 SSF_DEV double wlp(const double x[6], const double* U, const double* c, double logdet, double logw) {
@@ -171,22 +150,43 @@ SSF_DEV double wlp(const double x[6], const double* U, const double* c, double l
 }
 
 // Streams the frame's points through f(i, x): every thread keeps the NEXT point's loads in
-// flight while it computes the current one (one wave per SIMD pair cannot hide HBM latency
-// otherwise).
+// flight (as the raw six floats, converted when used) while it computes the current one.
+SSF_DEV void load_raw(const float* __restrict__ P, const float* __restrict__ Fl, int64_t i, float r[6]) {
+    r[0] = Fl[3 * i]; r[1] = Fl[3 * i + 1]; r[2] = Fl[3 * i + 2];
+    r[3] = P[3 * i];  r[4] = P[3 * i + 1];  r[5] = P[3 * i + 2];
+}
+
 template <class Fn>
 SSF_DEV void for_points(const float* __restrict__ P, const float* __restrict__ Fl, int64_t n, Fn&& fn) {
     const int64_t T = blockDim.x;
     int64_t i = threadIdx.x;
     if (i >= n) return;
-    double xn[6];
-    load_x(P, Fl, i, xn);
+    float rn[6];
+    load_raw(P, Fl, i, rn);
     for (; i < n; i += T) {
         double x[6];
 #pragma unroll
-        for (int d = 0; d < 6; ++d) x[d] = xn[d];
-        if (i + T < n) load_x(P, Fl, i + T, xn);
+        for (int d = 0; d < 6; ++d) x[d] = (double)rn[d];
+        if (i + T < n) load_raw(P, Fl, i + T, rn);
         fn(i, x);
     }
+}
+
+// A wave-uniform LDS value moved to SGPRs: the per-point loops keep their VGPRs for the point
+// data and the accumulators (1024-thread work-groups leave 128 VGPRs per lane).
+SSF_DEV double uni(double v) {
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+
+// 1/d for d in [1, 2] (d = 1 + e, e in (0, 1]): v_rcp_f64 and two Newton steps, ~1 ulp,
+// instead of the IEEE division sequence.
+SSF_DEV double recip_1_2(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-d, r, 1.0);
+    return __builtin_fma(r, e, r);
 }
 
 SSF_DEV double lse2(double a, double b) {  // scipy 1.15 logsumexp on two terms
@@ -454,7 +454,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     SSF_STAMP(0);
     double mean[6];
 #pragma unroll
-    for (int d = 0; d < 6; ++d) mean[d] = S.mean[d];
+    for (int d = 0; d < 6; ++d) mean[d] = uni(S.mean[d]);
 
     // ---- k-means++ (sklearn _kmeans_plusplus, n_local_trials = 2)
     {
@@ -567,9 +567,9 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         }
         __syncthreads();
         double cen[12], cenp[12];
-        const double csn0 = S.csn[0], csn1 = S.csn[1], cpn0 = S.csnp[0], cpn1 = S.csnp[1];
+        const double csn0 = uni(S.csn[0]), csn1 = uni(S.csn[1]), cpn0 = uni(S.csnp[0]), cpn1 = uni(S.csnp[1]);
 #pragma unroll
-        for (int k = 0; k < 12; ++k) { cen[k] = S.cen[k]; cenp[k] = S.cenp[k]; }
+        for (int k = 0; k < 12; ++k) { cen[k] = uni(S.cen[k]); cenp[k] = uni(S.cenp[k]); }
         double acc[14];
 #pragma unroll
         for (int k = 0; k < 14; ++k) acc[k] = 0.0;
@@ -625,11 +625,11 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         double cen[12], csn0, csn1;
         if (S.strict) {
 #pragma unroll
-            for (int k = 0; k < 12; ++k) cen[k] = S.cenp[k];
+            for (int k = 0; k < 12; ++k) cen[k] = uni(S.cenp[k]);
             csn0 = S.csnp[0]; csn1 = S.csnp[1];
         } else {
 #pragma unroll
-            for (int k = 0; k < 12; ++k) cen[k] = S.cen[k];
+            for (int k = 0; k < 12; ++k) cen[k] = uni(S.cen[k]);
             csn0 = 0.0; csn1 = 0.0;
             for (int d = 0; d < 6; ++d) { csn0 += cen[d] * cen[d]; csn1 += cen[6 + d] * cen[6 + d]; }
         }
@@ -667,44 +667,45 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     //      r_max = 1/(1+e), r_min = e/(1+e), lse = max + log1p(e), e = exp(min - max): the
     //      scipy logsumexp expression, one exp + one log1p per point.
     for (int it = 1; it <= 100 && S.status == 0; ++it) {
-        const double ld0 = S.logdet[0], lw0 = S.logw[0], ld1 = S.logdet[1], lw1 = S.logw[1];
+        const double ld0 = uni(S.logdet[0]), lw0 = uni(S.logw[0]), ld1 = uni(S.logdet[1]), lw1 = uni(S.logw[1]);
         double acc[29];
 #pragma unroll
         for (int k = 0; k < 29; ++k) acc[k] = 0.0;
-        for_point_pairs(P, Fl, n, [&](const double* xa, const double* xb, double wb) {
-            // U / cU are re-read from LDS (broadcast ds_reads) for every pair: the laundered
+        // sum of log1p(e) over the thread's points = log of the product of (1 + e), kept as
+        // mantissa * 2^pexp (frexp per point: the product never overflows, one log per thread)
+        double prod = 1.0;
+        int pexp = 0;
+        for_points(P, Fl, n, [&](int64_t, const double* x) {
+            // U / cU are re-read from LDS (broadcast ds_reads) for every point: the laundered
             // offset stops the compiler hoisting 54 loop-invariant doubles into VGPRs.
             int z = 0;
             asm volatile("" : "+s"(z));
             const double* U = S.U + z;
             const double* cU = S.cU + z;
-            const double a0a = wlp(xa, U, cU, ld0, lw0), a0b = wlp(xb, U, cU, ld0, lw0);
-            const double a1a = wlp(xa, U + 21, cU + 6, ld1, lw1), a1b = wlp(xb, U + 21, cU + 6, ld1, lw1);
-            const double mxa = a0a > a1a ? a0a : a1a, mna = a0a > a1a ? a1a : a0a;
-            const double mxb = a0b > a1b ? a0b : a1b, mnb = a0b > a1b ? a1b : a0b;
-            const double ea = exp(mna - mxa), eb = exp(mnb - mxb);
-            acc[28] += mxa + log1p(ea);
-            acc[28] += wb * (mxb + log1p(eb));
-            const double inva = 1.0 / (1.0 + ea), invb = 1.0 / (1.0 + eb);
-            const double ra = a1a > a0a ? inva : ea * inva;
-            const double rb = wb * (a1b > a0b ? invb : eb * invb);
-            acc[0] += ra;
-            acc[0] += rb;
-            double va[6], vb[6];
+            const double a0 = wlp(x, U, cU, ld0, lw0);
+            const double a1 = wlp(x, U + 21, cU + 6, ld1, lw1);
+            const double mx = a0 > a1 ? a0 : a1, mn = a0 > a1 ? a1 : a0;
+            const double e = exp(mn - mx);
+            const double d = 1.0 + e;
+            acc[28] += mx;
+            prod *= d;
+            pexp += __builtin_amdgcn_frexp_exp(prod);
+            prod = __builtin_amdgcn_frexp_mant(prod);
+            const double inv = recip_1_2(d);
+            const double r = a1 > a0 ? inv : e * inv;
+            acc[0] += r;
+            double v[6];
 #pragma unroll
-            for (int a = 0; a < 6; ++a) { va[a] = xa[a] - mean[a]; vb[a] = xb[a] - mean[a]; }
+            for (int a = 0; a < 6; ++a) v[a] = x[a] - mean[a];
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
-                const double rva = ra * va[a], rvb = rb * vb[a];
-                acc[1 + a] += rva;
-                acc[1 + a] += rvb;
+                const double rv = r * v[a];
+                acc[1 + a] += rv;
 #pragma unroll
-                for (int b = a; b < 6; ++b) {
-                    acc[7 + up(a, b)] += rva * va[b];
-                    acc[7 + up(a, b)] += rvb * vb[b];
-                }
+                for (int b = a; b < 6; ++b) acc[7 + up(a, b)] += rv * v[b];
             }
         });
+        acc[28] += log(prod) + (double)pexp * 0.69314718055994530942;
         block_sum<29>(acc, red);
         if (tid == 0) {
             S.passes += 1;
@@ -723,11 +724,11 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     //      The mask is written in the same pass against a predicted background label (the
     //      heavier component); the rare frame whose majority disagrees gets one flip pass.
     {
-        const double ld0 = S.logdet[0], lw0 = S.logw[0], ld1 = S.logdet[1], lw1 = S.logw[1];
+        const double ld0 = uni(S.logdet[0]), lw0 = uni(S.logw[0]), ld1 = uni(S.logdet[1]), lw1 = uni(S.logw[1]);
         const int pred = lw1 > lw0 ? 1 : 0;
         double x0[6];
 #pragma unroll
-        for (int d = 0; d < 6; ++d) x0[d] = S.x0[d];
+        for (int d = 0; d < 6; ++d) x0[d] = uni(S.x0[d]);
         double k1[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) k1[i] = 0.0;

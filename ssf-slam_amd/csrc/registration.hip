@@ -583,6 +583,92 @@ __global__ __launch_bounds__(256) void k_associate_sorted(
     if (nn_out) nn_out[co + i] = bi;
 }
 
+// Same association with the last frame's sorted cloud staged in LDS (x, y, z, original index
+// in .w: 16 B per point, dynamic LDS sized by the launch's plane-point bound).  Each
+// work-group handles kAssocQ queries of one pair; the binary search and both walks then run at
+// LDS latency instead of a dependent L2 load per candidate.
+constexpr int kAssocThreads = 1024;
+constexpr int kAssocQ = 2048;              // queries per work-group (2 per thread)
+constexpr int kAssocLdsMax = 6144;         // last-frame plane points staged in LDS (96 KiB)
+
+__global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
+    const float4* __restrict__ last, const int64_t* __restrict__ last_off,
+    const int32_t* __restrict__ last_count, const float* __restrict__ last_normal,
+    const uint8_t* __restrict__ last_valid, const float4* __restrict__ last_sorted,
+    const int32_t* __restrict__ last_sidx, const float4* __restrict__ curr,
+    const int64_t* __restrict__ curr_off, const int32_t* __restrict__ curr_count,
+    const double* __restrict__ pose_rel, CorrRec* __restrict__ corr, int32_t* __restrict__ nn_out,
+    int lds_cap) {
+    extern __shared__ float4 SLl[];
+    const int p = blockIdx.y;
+    const int mc = curr_count[p], ml = last_count[p];
+    const int i0 = blockIdx.x * kAssocQ;
+    if (i0 >= mc || ml <= 10) return;                                   // uniform (:158)
+    const int64_t lo = last_off[p], co = curr_off[p];
+    // a last frame above the caller's plane-point bound (the LDS size) walks global memory
+    const bool in_lds = ml <= lds_cap;
+    if (in_lds) {
+        for (int r = threadIdx.x; r < ml; r += blockDim.x) {
+            float4 v = last_sorted[lo + r];
+            v.w = __int_as_float(last_sidx[lo + r]);
+            SLl[r] = v;
+        }
+    }
+    __syncthreads();
+    auto ld = [&](int c) -> float4 {
+        if (in_lds) return SLl[c];
+        float4 v = last_sorted[lo + c];
+        v.w = __int_as_float(last_sidx[lo + c]);
+        return v;
+    };
+    const double q[4] = {pose_rel[7 * p], pose_rel[7 * p + 1], pose_rel[7 * p + 2], pose_rel[7 * p + 3]};
+    const double t[3] = {pose_rel[7 * p + 4], pose_rel[7 * p + 5], pose_rel[7 * p + 6]};
+    const int i1 = min(mc, i0 + kAssocQ);
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+        const float4 pc = curr[co + i];
+        float4 qs;
+        {
+            const double v[3] = {(double)pc.x, (double)pc.y, (double)pc.z};
+            double r[3];
+            quat_rotate(q, v, r);                                       // :74-82
+            qs.x = (float)(r[0] + t[0]); qs.y = (float)(r[1] + t[1]); qs.z = (float)(r[2] + t[2]); qs.w = 0.f;
+        }
+        int lo_i = 0, hi_i = ml;                                        // first x >= qs.x
+        while (lo_i < hi_i) {
+            const int mid = (lo_i + hi_i) >> 1;
+            if (ld(mid).x < qs.x) lo_i = mid + 1; else hi_i = mid;
+        }
+        float best = __builtin_inff();
+        int bi = 0x7fffffff;
+        for (int c = lo_i; c < ml; ++c) {
+            const float4 pl = ld(c);
+            const float dx = qs.x - pl.x;
+            if (dx * dx > best) break;
+            const float d = l2_simple(qs, pl);
+            const int id = __float_as_int(pl.w);
+            if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+        }
+        for (int c = lo_i - 1; c >= 0; --c) {
+            const float4 pl = ld(c);
+            const float dx = qs.x - pl.x;
+            if (dx * dx > best) break;
+            const float d = l2_simple(qs, pl);
+            const int id = __float_as_int(pl.w);
+            if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+        }
+        const float4* L = last + lo;
+        CorrRec rec;
+        const bool ok = last_valid[lo + bi] != 0;
+        const float4 pa = L[bi];
+        rec.po[0] = pc.x; rec.po[1] = pc.y; rec.po[2] = pc.z; rec.valid = ok ? 1.0f : 0.0f;
+        rec.pa[0] = pa.x; rec.pa[1] = pa.y; rec.pa[2] = pa.z; rec.pad0 = 0.f;
+        const float* nr = last_normal + 3 * (lo + bi);
+        rec.n[0] = nr[0]; rec.n[1] = nr[1]; rec.n[2] = nr[2]; rec.pad1 = 0.f;
+        corr[co + i] = rec;
+        if (nn_out) nn_out[co + i] = bi;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Residual + local Jacobian of PlaneFeatureCost (:25-43) composed with the
 // EigenQuaternionParameterization 4x3 Jacobian (same algebra as the oracle's residual_jac).
@@ -932,7 +1018,13 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
     if (n_pairs <= 0) return hipSuccess;
     if (max_m > 0) {
         const int bx = (int)((max_m + 255) / 256);
-        if (max_m <= kSortMax && last_sorted && last_sidx) {
+        if (max_m <= kAssocLdsMax && last_sorted && last_sidx) {
+            const int qx = (int)((max_m + kAssocQ - 1) / kAssocQ);
+            hipLaunchKernelGGL(k_associate_lds, dim3(qx, n_pairs), dim3(kAssocThreads),
+                               (size_t)max_m * sizeof(float4), s, last, last_off, last_count,
+                               last_normal, last_valid, last_sorted, last_sidx, curr, curr_off,
+                               curr_count, pose_rel, corr, nn, (int)max_m);
+        } else if (max_m <= kSortMax && last_sorted && last_sidx) {
             hipLaunchKernelGGL(k_associate_sorted, dim3(bx, n_pairs), dim3(256), 0, s, last, last_off,
                                last_count, last_normal, last_valid, last_sorted, last_sidx, curr,
                                curr_off, curr_count, pose_rel, corr, nn);

@@ -120,6 +120,28 @@ def test_register_pair_per_step(oracle, dev, solver, iters, mode, brute):
     assert np.abs(got[4:] - t).max() < TOL_T and _quat_angle(got[:4], q) < TOL_R
 
 
+def test_associate_large_frames(oracle, dev):
+    """1-NN indices exact when the frames exceed the LDS staging size (6144 plane points): the
+    association walks the sorted last frame in global memory."""
+    import ssf
+    base = [oracle.extract_planes(frame(s, 0, n_az=1875)[0], 64) for s in range(3)]
+    L, Cc = np.concatenate(base[:2]), np.concatenate(base[1:])
+    assert len(L) > 6144 and len(Cc) > 6144
+    fe = ssf.Frontend(64, device=dev.index)
+    sizes = [len(L), len(Cc)]
+    off, h_off = ssf.frame_offsets(sizes, dev)
+    xyzi = torch.from_numpy(np.concatenate([L, Cc]).astype(np.float32)).to(dev)
+    pb = ssf.PlaneBatch(xyzi, torch.tensor(sizes, dtype=torch.int32, device=dev), off, h_off, max(sizes))
+    table = fe.plane_table(pb)
+    q0 = np.array([0.0, 0.0, 0.002, 1.0]); q0 /= np.linalg.norm(q0)
+    t0 = np.array([0.5, -0.02, 0.01])
+    pose = torch.tensor([[*q0, *t0]], dtype=torch.float64, device=dev)
+    res = fe.register(_sub(pb, [0]), table, _sub(pb, [1]), pose, want_nn=True)
+    torch.cuda.synchronize()
+    o1 = int(h_off[1])
+    assert np.array_equal(res["nn"][o1:o1 + len(Cc)].cpu().numpy(), oracle.correspond(L, Cc, q0, t0))
+
+
 def test_register_batch_and_accumulate(oracle, dev):
     """3 independent pairs in one launch + pose accumulation (publishResult :87-90); one pair
     whose last frame has <= 10 plane points is skipped (:158) and keeps its warm start."""

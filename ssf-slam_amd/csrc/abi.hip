@@ -26,7 +26,7 @@ struct ssf_ctx {
     // registration scratch
     DevBuf corr;
     // mask scratch
-    DevBuf dist, labels, draws, start1;
+    DevBuf draws, start1;
     // host RandomState (MT19937, numpy legacy seeding)
     uint32_t mt[624];
     int mt_pos = 625;
@@ -152,7 +152,7 @@ void ssf_destroy(ssf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     DevBuf* bufs[] = {&c->rid, &c->hist, &c->ring_off, &c->ring_xyzi, &c->sel, &c->sel_cnt,
-                      &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->dist, &c->labels, &c->draws, &c->start1};
+                      &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->draws, &c->start1};
     for (DevBuf* b : bufs) b->release();
     if (c->draws_done) { (void)hipEventSynchronize(c->draws_done); (void)hipEventDestroy(c->draws_done); }
     if (c->h_draws) (void)hipHostFree(c->h_draws);
@@ -186,8 +186,6 @@ int32_t ssf_reserve(ssf_ctx* c, int32_t max_frames, int64_t max_points_per_frame
     int32_t rc = ensure_features(c, max_frames, total, max_points_per_frame);
     if (rc) return rc;
     SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(total, 1)), "alloc corr");
-    SSF_TRY_HIP(c, c->dist.ensure(sizeof(double) * (size_t)std::max<int64_t>(total, 1)), "alloc dist");
-    SSF_TRY_HIP(c, c->labels.ensure((size_t)std::max<int64_t>(total, 1)), "alloc labels");
     SSF_TRY_HIP(c, c->draws.ensure(sizeof(double) * 3 * (size_t)std::max(max_frames, 1)), "alloc draws");
     return SSF_OK;
 }
@@ -305,8 +303,6 @@ int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const fl
         if (h_frame_off[f + 1] < h_frame_off[f]) return fail(c, SSF_E_ARG, "mask_pose_batch: offsets not monotone");
     hipStream_t s = (hipStream_t)stream;
     SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
-    SSF_TRY_HIP(c, c->dist.ensure(sizeof(double) * (size_t)std::max<int64_t>(total, 1)), "alloc dist");
-    SSF_TRY_HIP(c, c->labels.ensure((size_t)std::max<int64_t>(total, 1)), "alloc labels");
     SSF_TRY_HIP(c, c->draws.ensure(sizeof(double) * 3 * (size_t)n_frames), "alloc draws");
     if (c->draws_done) SSF_TRY_HIP(c, hipEventSynchronize(c->draws_done), "draws event");
     else SSF_TRY_HIP(c, hipEventCreateWithFlags(&c->draws_done, hipEventDisableTiming), "draws event");
@@ -332,8 +328,7 @@ int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const fl
                                   hipMemcpyHostToDevice, s), "H2D draws");
     SSF_TRY_HIP(c, hipEventRecord(c->draws_done, s), "draws record");
     hipError_t e = ssf::launch_mask_pose(s, n_frames, d_pts, d_flow, d_frame_off, mode, d_mask_in,
-                                         c->draws.as<double>(), reflection, d_bg_mask, d_out,
-                                         c->dist.as<double>(), c->labels.as<uint8_t>());
+                                         c->draws.as<double>(), reflection, d_bg_mask, d_out);
     if (e != hipSuccess) return hip_fail(c, e, "mask_pose launch");
     return SSF_OK;
 }

@@ -58,6 +58,7 @@ struct MaskShared {
     double rand1, rand2;
     double lb;
     double C[36], L[36], Li[36];  // lane-0 scratch for the 6x6 algebra
+    double sums[29];           // lane 0's copy of a pass's block sums (never a per-lane array)
     int64_t c0, c1;
     int km_iter, em_iter, strict, converged, done, status, passes, label0, bg, bg_pred;
 };
@@ -343,7 +344,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     const float* __restrict__ pts, const float* __restrict__ flow,
     const int64_t* __restrict__ frame_off, int mode, const uint8_t* __restrict__ mask_in,
     const double* __restrict__ draws, int reflection, uint8_t* __restrict__ bg_mask,
-    double* __restrict__ out_all, double* __restrict__ dist, uint8_t* __restrict__ lab) {
+    double* __restrict__ out_all) {
     __shared__ MaskShared S;
     __shared__ double red[kNW * 32];
     __shared__ int ired[kNW];
@@ -352,8 +353,6 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     const int64_t fb = frame_off[f], n = frame_off[f + 1] - fb;
     const float* P = pts + 3 * fb;
     const float* Fl = flow + 3 * fb;
-    double* D = dist + fb;
-    (void)lab;
     double* out = out_all + (int64_t)f * SSF_POSE_OUT_STRIDE;
     if (tid == 0) {
         S.passes = 0; S.status = 0; S.km_iter = 0; S.em_iter = 0; S.converged = 0;
@@ -386,7 +385,8 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         block_sum<16>(k, red);
         if (tid == 0) {
             for (int i = 0; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
-            const int st = kabsch_finish(k, cs, cd, reflection, out);
+            for (int i = 0; i < 16; ++i) S.sums[i] = k[i];
+            const int st = kabsch_finish(S.sums, cs, cd, reflection, out);
             out[SSF_POSE_OUT_STATUS] = st;
             out[SSF_POSE_OUT_BGLABEL] = -1;
             out[SSF_POSE_OUT_PASSES] = 1;
@@ -464,25 +464,26 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             load_x(P, Fl, S.c0, x);
             for (int d = 0; d < 6; ++d) { c0[d] = x[d] - mean[d]; cn0 += c0[d] * c0[d]; }
         }
-        // distances to the first centre, stored in D; each wave owns a contiguous segment so the
+        // distances to the first centre; each wave owns a contiguous segment so the
         // in-order cumulative sum needs only one block-level exchange of wave totals
         const int nw = blockDim.x >> 6, w = tid >> 6, lane = lane_id();
         const int64_t seg = (((n + nw - 1) / nw) + 63) / 64 * 64;
         const int64_t ws = (int64_t)w * seg, we = ws + seg < n ? ws + seg : n;
+        // D(i) = squared distance to the first centre; recomputed (same expression, same bits)
+        // wherever it is needed instead of being stored
+        auto dist0 = [&](int64_t i) {
+            double x[6], dt = 0.0, xs = 0.0;
+            load_x(P, Fl, i, x);
+#pragma unroll
+            for (int d = 0; d < 6; ++d) { const double v = x[d] - mean[d]; dt += c0[d] * v; xs += v * v; }
+            const double v = (-2.0 * dt + cn0) + xs;
+            return v > 0.0 ? v : 0.0;
+        };
         double wsum = 0.0;
 #pragma unroll 4
         for (int64_t b = ws; b < we; b += 64) {
             const int64_t i = b + lane;
-            if (i < we) {
-                double x[6], dt = 0.0, xs = 0.0;
-                load_x(P, Fl, i, x);
-#pragma unroll
-                for (int d = 0; d < 6; ++d) { const double v = x[d] - mean[d]; dt += c0[d] * v; xs += v * v; }
-                double v = (-2.0 * dt + cn0) + xs;
-                v = v > 0.0 ? v : 0.0;
-                D[i] = v;
-                wsum += v;
-            }
+            if (i < we) wsum += dist0(i);
         }
         wsum = wave_sum(wsum);
         if (lane == 0) red[w] = wsum;
@@ -496,11 +497,14 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             S.passes += 1;
         }
         const double r1 = draws[3 * f + 1] * pot, r2 = draws[3 * f + 2] * pot;
-        // wave-local in-order inclusive scan of its segment; first index with cumsum >= rand
-        bool f1 = false, f2 = false;
+        // wave-local in-order inclusive scan of its segment; first index with cumsum >= rand.
+        // A wave whose whole segment ends below both draws cannot hold either index and skips
+        // the scan (1e-9 slack >> the scan's rounding); the others stop once both are found.
+        const double wtot = red[w];
+        bool f1 = carry + wtot < r1 * (1.0 - 1e-9), f2 = carry + wtot < r2 * (1.0 - 1e-9);
         for (int64_t b = ws; b < we && !(f1 && f2); b += 64) {
             const int64_t i = b + lane;
-            double v = i < we ? D[i] : 0.0;
+            double v = i < we ? dist0(i) : 0.0;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const double y = __shfl_up(v, o, 64);
@@ -526,14 +530,15 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         for (int64_t b = ws; b < we; b += 64) {
             const int64_t i = b + lane;
             if (i < we) {
-                double x[6], xs = 0.0, dt0 = 0.0, dt1 = 0.0;
+                double x[6], xs = 0.0, dt0 = 0.0, dt1 = 0.0, dtc = 0.0;
                 load_x(P, Fl, i, x);
-                const double di = D[i];
 #pragma unroll
                 for (int d = 0; d < 6; ++d) {
                     const double v = x[d] - mean[d];
-                    xs += v * v; dt0 += cc[0][d] * v; dt1 += cc[1][d] * v;
+                    dtc += c0[d] * v; xs += v * v; dt0 += cc[0][d] * v; dt1 += cc[1][d] * v;
                 }
+                double di = (-2.0 * dtc + cn0) + xs;             // = dist0(i), bit for bit
+                di = di > 0.0 ? di : 0.0;
                 double v0 = (-2.0 * dt0 + ccn[0]) + xs, v1 = (-2.0 * dt1 + ccn[1]) + xs;
                 v0 = v0 > 0.0 ? v0 : 0.0; v1 = v1 > 0.0 ? v1 : 0.0;
                 cp[0] += v0 < di ? v0 : di;
@@ -654,7 +659,8 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         block_sum<28>(acc, red);
         if (tid == 0) {
             S.passes += 1;
-            if (gmm_params(S, acc, 1, n) != 0) S.status = SSF_POSE_GMM_FAILED;
+            for (int k = 0; k < 28; ++k) S.sums[k] = acc[k];
+            if (gmm_params(S, S.sums, 1, n) != 0) S.status = SSF_POSE_GMM_FAILED;
             S.lb = -__builtin_inf();
             S.done = 0;
         }
@@ -712,7 +718,8 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             S.em_iter = it;
             const double prev = S.lb;
             S.lb = acc[28] / (double)n;
-            if (gmm_params(S, acc, 0, n) != 0) S.status = SSF_POSE_GMM_FAILED;
+            for (int k = 0; k < 29; ++k) S.sums[k] = acc[k];
+            if (gmm_params(S, S.sums, 0, n) != 0) S.status = SSF_POSE_GMM_FAILED;
             if (fabs(S.lb - prev) < 1e-3) { S.converged = 1; S.done = 1; }
         }
         __syncthreads();
@@ -769,7 +776,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             else bg = S.label0;                     // Counter.most_common tie -> first seen
             S.bg = bg;
             S.bg_pred = pred;
-            double kb[16];
+            double* kb = S.sums;
             for (int i = 0; i < 16; ++i) kb[i] = bg ? k1[i] : S.ktot[i] - k1[i];
             const double cs[3] = {S.x0[3] + S.x0[0], S.x0[4] + S.x0[1], S.x0[5] + S.x0[2]};
             const double cd[3] = {S.x0[3], S.x0[4], S.x0[5]};
@@ -796,11 +803,10 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
 
 hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,
                             const int64_t* frame_off, int mode, const uint8_t* mask_in,
-                            const double* draws, int reflection, uint8_t* bg_mask, double* out,
-                            double* dist_scratch, uint8_t* label_scratch) {
+                            const double* draws, int reflection, uint8_t* bg_mask, double* out) {
     if (n_frames <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_mask_pose, dim3(n_frames), dim3(kMaskThreads), 0, s, pts, flow, frame_off,
-                       mode, mask_in, draws, reflection, bg_mask, out, dist_scratch, label_scratch);
+                       mode, mask_in, draws, reflection, bg_mask, out);
     return hipGetLastError();
 }
 

@@ -32,6 +32,21 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# HBM bytes per k_mask_pose launch measured with rocprofv3 PMC passes on this bench command
+# (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE); used when its workload config matches.
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "r01_k_mask_pose_traffic.json")
+
+
+def mask_traffic(B, N):
+    try:
+        with open(TRAFFIC_JSON) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    cfg = t.get("config", {})
+    if cfg.get("sequences_per_gpu") != B or cfg.get("points_per_frame") != N:
+        return None
+    return t.get("traffic_bytes_per_launch")
 
 
 def parse():
@@ -230,7 +245,8 @@ def main():
     if "k_mask_pose" == dom:
         achieved = mask_bytes / (mask_ms * 1e-3) / 1e9
         line["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_mask_pose"}
+                            "frac": achieved / HBM_PEAK_GBS, "traffic": mask_traffic(B, N),
+                            "kernel": "k_mask_pose"}
     else:
         k = kernels[dom]
         b = k.get("bytes")

@@ -135,14 +135,15 @@ class Frontend:
             return pb, ring, roff.view(max(F, 1), self.n_rows + 1)[:F], curv
         return pb
 
-    def extract_planes(self, pts):
-        """Single frame, PointCloud2-style packed xyz [n, 3] -> plane cloud [m, 4]."""
+    def extract_planes(self, pts, xyz_offset: int = 0):
+        """Single frame, PointCloud2-style points [n, k] f32 (point_step = 4k bytes, x/y/z at
+        byte offsets xyz_offset + 0/4/8) -> plane cloud [m, 4]."""
         pts = self._dev(pts, torch.float32)
         n = pts.shape[0]
         out = torch.empty((max(n, 1), 4), dtype=torch.float32, device=self.device)
         m = C.c_int64(0)
         rc = _abi.lib().ssf_extract_planes(self._h, _stream(self.device), _ptr(pts), n,
-                                           4 * pts.shape[1], 0, _ptr(out), C.byref(m), n)
+                                           4 * pts.shape[1], int(xyz_offset), _ptr(out), C.byref(m), n)
         self._check(rc, "ssf_extract_planes")
         return out[:m.value]
 

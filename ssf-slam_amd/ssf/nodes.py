@@ -1,0 +1,217 @@
+"""Node shims around the device front-end that keep the reference's topics and message layouts
+(SURVEY.md §8(f) row 1), plus an in-process runner that replays an npz dataset directory the
+way `launch/*.launch` wires the nodes and writes the odometry as a TUM trajectory (row 2).
+
+  PointCloudOdometryNode   scripts/PointCloudOdometry_noSeg.py:62-127
+      per npz frame -> /velodyne_points (PointCloud2, xyz @ 0/4/8, step 12)
+                    -> /frame_odom1    (Float64MultiArray data = [tx, ty, tz, qx, qy, qz, qw])
+  FrameFeatureNode         src/frameFeature.cpp:35-139
+      /velodyne_points -> /plane_frame_cloud1 (PointXYZI layout, stamp copied, frame "map")
+                       -> /org_frame_cloud1   (the input, frame "map")
+  LidarOdometryNode        src/lidarOdometry_onlyPC.cpp:85-124, 147-311
+      /plane_frame_cloud1 -> /frame_odom2 (Odometry, frame "map", child "map_child")
+                          -> /frame_odom_path2 (Path of every pose so far)
+                          -> /plane_frame_cloud2 (the current plane cloud, frame "map")
+
+rospy, sensor_msgs and nav_msgs are not in this image: messages are the plain stand-ins of
+`ssf.io` / below, and a `Bus` delivers them in-process.  Subscribed callbacks are duck-typed
+(any object with the sensor_msgs/PointCloud2 attributes works), so wiring a node to rospy is
+`rospy.Subscriber(topic, PointCloud2, node.on_cloud)` plus a publish callable that converts
+the stand-in to the real message class.
+"""
+from __future__ import annotations
+
+import copy
+from collections import defaultdict
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import io as sio
+from .frontend import Frontend, PlaneBatch, frame_offsets, identity_poses
+
+
+@dataclass
+class Float64MultiArray:
+    data: list = field(default_factory=list)
+
+
+@dataclass
+class Pose:
+    position: tuple = (0.0, 0.0, 0.0)
+    orientation: tuple = (0.0, 0.0, 0.0, 1.0)      # x, y, z, w
+
+
+@dataclass
+class Odometry:
+    header: sio.Header = field(default_factory=sio.Header)
+    child_frame_id: str = ""
+    pose: Pose = field(default_factory=Pose)
+
+
+@dataclass
+class Path:
+    header: sio.Header = field(default_factory=sio.Header)
+    poses: list = field(default_factory=list)      # (Header, Pose) pairs (geometry_msgs/PoseStamped)
+
+
+class Bus:
+    """In-process topic bus: publish(topic, msg) calls every subscriber in subscription order
+    and keeps the last `keep` messages per topic."""
+
+    def __init__(self, keep: int = 0):
+        self.subs = defaultdict(list)
+        self.keep = keep
+        self.log = defaultdict(list)
+
+    def subscribe(self, topic, cb):
+        self.subs[topic].append(cb)
+
+    def publish(self, topic, msg):
+        if self.keep:
+            lg = self.log[topic]
+            lg.append(msg)
+            del lg[:-self.keep]
+        for cb in self.subs[topic]:
+            cb(msg)
+
+
+def _single_batch(xyzi: torch.Tensor, device) -> PlaneBatch:
+    m = int(xyzi.shape[0])
+    off, h_off = frame_offsets([m], device)
+    return PlaneBatch(xyzi, torch.tensor([m], dtype=torch.int32, device=device), off, h_off, max(m, 1))
+
+
+class FrameFeatureNode:
+    """src/frameFeature.cpp cloudHandler on the device (k_bin_* / k_curv_select / k_compact)."""
+
+    def __init__(self, publish, n_rows: int = 64, device=None, frontend: Frontend | None = None):
+        self.fe = frontend or Frontend(n_rows, device=device)
+        self.publish = publish
+
+    def on_cloud(self, msg):
+        view, ox = sio.cloud_points(msg)
+        pts = torch.from_numpy(np.array(view, dtype=np.float32)).to(self.fe.device)  # msg bytes are read-only
+        planes = self.fe.extract_planes(pts, xyz_offset=ox)                 # :45-123
+        stamp = sio.stamp_of(msg.header)
+        self.publish("/plane_frame_cloud1", sio.xyzi_to_cloud(planes, stamp, "map"))   # :129-133
+        org = copy.copy(msg)                                                  # :135-138
+        org.header = sio.Header(stamp[0], stamp[1], "map")
+        self.publish("/org_frame_cloud1", org)
+        return planes
+
+
+class LidarOdometryNode:
+    """src/lidarOdometry_onlyPC.cpp: the first plane cloud only becomes the last frame; every
+    later one is registered against it (association, plane table, Ceres-style LM or GN) and the
+    accumulated pose is published.  para_q/para_t (the warm start) and q_0_curr/t_0_curr stay on
+    the device between frames."""
+
+    def __init__(self, publish, n_rows: int = 64, device=None, solver: str = "ceres_lm",
+                 max_iter: int | None = None, frontend: Frontend | None = None):
+        self.fe = frontend or Frontend(n_rows, device=device, solver=solver, max_iter=max_iter)
+        self.publish = publish
+        dev = self.fe.device
+        self.pose_rel = identity_poses(1, dev)      # para_q, para_t (:49-50)
+        self.pose_abs = identity_poses(1, dev)      # q_0_last / t_0_last (:87-90)
+        self.last = None
+        self.last_table = None
+        self.path = Path(sio.Header(0, 0, "map"))
+        self.num_frame = 0
+
+    def on_plane_cloud(self, msg):
+        self.num_frame += 1
+        xyzi = torch.from_numpy(sio.cloud_xyzi(msg)).to(self.fe.device)
+        curr = _single_batch(xyzi, self.fe.device)
+        table = self.fe.plane_table(curr)            # this frame's 30-NN planes, used next frame
+        stamp = sio.stamp_of(msg.header)
+        result = None
+        if self.last is not None:                    # flagStart (:301-306)
+            self.fe.register(self.last, self.last_table, curr, self.pose_rel, self.pose_abs)
+            result = self._publish_result(stamp, xyzi)
+        self.last, self.last_table = curr, table     # *lastFramePlanePtr = *currFramePlanePtr (:307)
+        return result
+
+    def _publish_result(self, stamp, xyzi):
+        p = self.pose_abs[0].cpu().numpy()
+        hdr = sio.Header(stamp[0], stamp[1], "map")
+        pose = Pose(tuple(float(v) for v in p[4:7]), tuple(float(v) for v in p[0:4]))
+        odom = Odometry(hdr, "map_child", pose)
+        self.publish("/frame_odom2", odom)                                    # :98-109
+        self.path.poses.append((hdr, pose))                                   # :111-118
+        self.path.header = sio.Header(stamp[0], stamp[1], "map")
+        self.publish("/frame_odom_path2", self.path)
+        self.publish("/plane_frame_cloud2", sio.xyzi_to_cloud(xyzi, stamp, "map"))   # :120-124
+        return odom
+
+
+class PointCloudOdometryNode:
+    """scripts/PointCloudOdometry_noSeg.py main loop body for one npz frame: publish the cloud,
+    then the GMM mask + Kabsch pose as [t, q] (or the ground-truth mask of
+    PointCloudOdometry.py:91 with mode='gt')."""
+
+    def __init__(self, publish, device=None, frontend: Frontend | None = None, mode: str = "gmm",
+                 seed: int | None = None):
+        self.fe = frontend or Frontend(64, device=device)
+        self.publish = publish
+        self.mode = mode
+        if seed is not None:
+            self.fe.seed(seed)
+
+    def on_frame(self, pos1, flow, stamp=(0, 0), gt_mask=None):
+        dev = self.fe.device
+        pos = pos1 if isinstance(pos1, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(pos1, np.float32))
+        fl = flow if isinstance(flow, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(flow, np.float32))
+        pos = pos.to(dev, torch.float32).contiguous()
+        fl = fl.to(dev, torch.float32).contiguous()
+        self.publish("/velodyne_points", sio.xyz_to_cloud(pos.cpu().numpy(), stamp, "livox_frame"))   # :73-94
+        off, h_off = frame_offsets([pos.shape[0]], dev)
+        m = None
+        if self.mode != "gmm":
+            m = torch.as_tensor(np.asarray(gt_mask) if not isinstance(gt_mask, torch.Tensor) else gt_mask)
+            m = m.to(dev, torch.uint8).contiguous()
+        out, _ = self.fe.mask_pose(pos, fl, off, h_off, mode=self.mode, mask_in=m, want_mask=False)
+        o = out[0].cpu().numpy()
+        msg = Float64MultiArray([float(v) for v in o[0:7]])                   # hstack((t, q)) :123-125
+        self.publish("/frame_odom1", msg)
+        return o
+
+
+def run_sequence(root: str, tum_path: str | None = None, n_rows: int = 64, device=None,
+                 solver: str = "ceres_lm", max_iter: int | None = None, seed: int | None = None,
+                 rate_hz: float = 10.0, keys=("pos1", "gt")):
+    """Replay a DATASET_PATH directory through PointCloudOdometry -> frameFeature ->
+    lidarOdometry_onlyPC as the launch files wire them.  Stamps are synthetic and monotone
+    (frame k at k / rate_hz; the reference uses wall-clock ros::Time::now()).  Writes the
+    /frame_odom2 poses as TUM lines when `tum_path` is given.
+    -> dict(odom1 [F, 7] f64 [t, q], odom2 [F-1, 7] f64 [t, q], stamps)"""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    bus = Bus()
+    pco = PointCloudOdometryNode(bus.publish, device=dev, seed=seed)
+    ff = FrameFeatureNode(bus.publish, n_rows=n_rows, device=dev)
+    lo = LidarOdometryNode(bus.publish, n_rows=n_rows, device=dev, solver=solver, max_iter=max_iter)
+    bus.subscribe("/velodyne_points", ff.on_cloud)
+    bus.subscribe("/plane_frame_cloud1", lo.on_plane_cloud)
+    odom1, odom2, stamps = [], [], []
+    writer = sio.TumWriter(tum_path) if tum_path else None
+
+    def on_odom1(msg):
+        odom1.append(list(msg.data))
+
+    def on_odom2(msg):
+        odom2.append(list(msg.pose.position) + list(msg.pose.orientation))
+        if writer:
+            writer.write((msg.header.stamp_sec, msg.header.stamp_nsec), msg.pose.position,
+                         msg.pose.orientation)
+
+    bus.subscribe("/frame_odom1", on_odom1)
+    bus.subscribe("/frame_odom2", on_odom2)
+    period_ns = int(round(1e9 / rate_hz))
+    for fr in sio.NpzSequence(root, keys=keys, device=dev):
+        t_ns = fr["index"] * period_ns
+        stamp = (t_ns // 1_000_000_000, t_ns % 1_000_000_000)
+        stamps.append(stamp)
+        pco.on_frame(fr[keys[0]], fr[keys[1]], stamp)
+    return dict(odom1=np.asarray(odom1, np.float64).reshape(-1, 7),
+                odom2=np.asarray(odom2, np.float64).reshape(-1, 7), stamps=stamps)

@@ -42,6 +42,14 @@ constexpr int kMaskThreads = SSF_MASK_THREADS;   // 12 waves: 3 per SIMD at <= 1
 #define SSF_STAMP(slot) do { } while (0)
 #endif
 constexpr int kNW = kMaskThreads / 64;
+#ifndef SSF_LLOYD_DEEP
+#define SSF_LLOYD_DEEP 2
+#endif
+#ifndef SSF_EM_DEEP
+#define SSF_EM_DEEP 1
+#endif
+constexpr int kLloydDeep = SSF_LLOYD_DEEP;   // points in flight per thread in the Lloyd passes
+constexpr int kEmDeep = SSF_EM_DEEP;         // ... and in the EM passes
 constexpr double kPi = 3.14159265358979323846;
 
 // packed upper-triangular index of a 6x6 matrix (row i <= col j)
@@ -168,7 +176,7 @@ SSF_DEV void for_points(const float* __restrict__ P, const float* __restrict__ F
         double x[6];
 #pragma unroll
         for (int d = 0; d < 6; ++d) x[d] = (double)rn[d];
-        if (i + T < n) load_raw(P, Fl, i + T, rn);
+        load_raw(P, Fl, min(i + T, n - 1), rn);     // unconditional (clamped): a counted wait
         fn(i, x);
     }
 }
@@ -178,6 +186,30 @@ SSF_DEV void for_points(const float* __restrict__ P, const float* __restrict__ F
 SSF_DEV double uni(double v) {
     return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
                             __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+
+// Lloyd only: D points in flight per thread (a rolling register buffer of raw floats).  Each
+// thread visits its points in the same order as for_points, so every sum is bit-identical.
+template <int D, class Fn>
+SSF_DEV void for_points_deep(const float* __restrict__ P, const float* __restrict__ Fl, int64_t n, Fn&& fn) {
+    const int64_t T = blockDim.x;
+    const int64_t i0 = threadIdx.x;
+    // loads are unconditional (indices clamped to the last point): the compiler can then count
+    // them and wait with vmcnt(N) instead of draining every prefetch at a conditional join
+    float buf[D][6];
+#pragma unroll
+    for (int d = 0; d < D; ++d) load_raw(P, Fl, min(i0 + d * T, n - 1), buf[d]);
+    for (int64_t base = i0; base < n; base += D * T) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int64_t i = base + d * T;
+            double x[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) x[k] = (double)buf[d][k];
+            load_raw(P, Fl, min(i + D * T, n - 1), buf[d]);
+            if (i < n) fn(i, x);
+        }
+    }
 }
 
 // 1/d for d in [1, 2] (d = 1 + e, e in (0, 1]): v_rcp_f64 and two Newton steps, ~1 ulp,
@@ -572,14 +604,14 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         }
         __syncthreads();
         double cen[12], cenp[12];
-        const double csn0 = uni(S.csn[0]), csn1 = uni(S.csn[1]), cpn0 = uni(S.csnp[0]), cpn1 = uni(S.csnp[1]);
+        const double csn0 = S.csn[0], csn1 = S.csn[1], cpn0 = S.csnp[0], cpn1 = S.csnp[1];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) { cen[k] = uni(S.cen[k]); cenp[k] = uni(S.cenp[k]); }
+        for (int k = 0; k < 12; ++k) { cen[k] = S.cen[k]; cenp[k] = S.cenp[k]; }
         double acc[14];
 #pragma unroll
         for (int k = 0; k < 14; ++k) acc[k] = 0.0;
         int changed = 0;
-        for_points(P, Fl, n, [&](int64_t, const double* x) {
+        for_points_deep<kLloydDeep>(P, Fl, n, [&](int64_t, const double* x) {
             double v[6], dt0 = 0.0, dt1 = 0.0, dp0 = 0.0, dp1 = 0.0;
 #pragma unroll
             for (int d = 0; d < 6; ++d) {
@@ -681,7 +713,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         // mantissa * 2^pexp (frexp per point: the product never overflows, one log per thread)
         double prod = 1.0;
         int pexp = 0;
-        for_points(P, Fl, n, [&](int64_t, const double* x) {
+        for_points_deep<kEmDeep>(P, Fl, n, [&](int64_t, const double* x) {
             // U / cU are re-read from LDS (broadcast ds_reads) for every point: the laundered
             // offset stops the compiler hoisting 54 loop-invariant doubles into VGPRs.
             int z = 0;

@@ -145,7 +145,20 @@ __device__ __noinline__ int gmm_params(MaskShared& S, const double* comp1, int i
 
 // weighted log probability, sklearn _estimate_log_gaussian_prob form: y = x U - (mu U), with
 // c = mu U precomputed by lane 0 (S.cU); U packed upper.
-SSF_DEV double wlp(const double x[6], const double* U, const double* c, double logdet, double logw) {
+typedef __attribute__((address_space(3))) const double LdsDouble;
+
+// The LDS address of U / cU laundered through a VGPR once per point: the compiler can neither
+// hoist the 54 loop-invariant doubles into VGPRs nor has to rebuild each address in an SGPR
+// (one VGPR base, immediate ds_read2 offsets).  The low 32 bits of a generic LDS pointer are
+// its LDS offset.
+SSF_DEV const LdsDouble* lds_laundered(const double* p) {
+    uint32_t a = (uint32_t)(uintptr_t)p;
+    asm volatile("" : "+v"(a));
+    return (const LdsDouble*)(uintptr_t)a;
+}
+
+template <class Ptr>
+SSF_DEV double wlp(const double x[6], Ptr U, Ptr c, double logdet, double logw) {
     double lp = 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
@@ -714,12 +727,9 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         double prod = 1.0;
         int pexp = 0;
         for_points_deep<kEmDeep>(P, Fl, n, [&](int64_t, const double* x) {
-            // U / cU are re-read from LDS (broadcast ds_reads) for every point: the laundered
-            // offset stops the compiler hoisting 54 loop-invariant doubles into VGPRs.
-            int z = 0;
-            asm volatile("" : "+s"(z));
-            const double* U = S.U + z;
-            const double* cU = S.cU + z;
+            // U / cU are re-read from LDS (broadcast ds_reads) for every point (lds_laundered)
+            const LdsDouble* U = lds_laundered(S.U);
+            const LdsDouble* cU = lds_laundered(S.cU);
             const double a0 = wlp(x, U, cU, ld0, lw0);
             const double a1 = wlp(x, U + 21, cU + 6, ld1, lw1);
             const double mx = a0 > a1 ? a0 : a1, mn = a0 > a1 ? a1 : a0;
@@ -772,12 +782,9 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
 #pragma unroll
         for (int i = 0; i < 16; ++i) k1[i] = 0.0;
         for_points(P, Fl, n, [&](int64_t i, const double* x) {
-            // U / cU are re-read from LDS (broadcast ds_reads) for every point: the laundered
-            // offset stops the compiler hoisting 54 loop-invariant doubles into VGPRs.
-            int z = 0;
-            asm volatile("" : "+s"(z));
-            const double* U = S.U + z;
-            const double* cU = S.cU + z;
+            // U / cU are re-read from LDS (broadcast ds_reads) for every point (lds_laundered)
+            const LdsDouble* U = lds_laundered(S.U);
+            const LdsDouble* cU = lds_laundered(S.cU);
             const double a0 = wlp(x, U, cU, ld0, lw0);
             const double a1 = wlp(x, U + 21, cU + 6, ld1, lw1);
             const int l = a1 > a0 ? 1 : 0;

@@ -4,13 +4,14 @@
 //   k_bin_count   ring id per point (frameFeature.cpp:57-72) + per-chunk ring histogram
 //   k_bin_scan    per-frame exclusive scans -> per-(chunk,row) bases and row offsets
 //   k_bin_scatter stable per-row partition (:73-80): wave ballot "match" on the 6-bit row id
-//                 gives each point its rank among same-row points of its wave; waves are
-//                 ordered through LDS -> the reference's push_back order is reproduced exactly.
-//                 intensity = indexInRow + row/100.0 (:77)
-//   k_curv_select one work-group per (frame,row): the row is streamed through LDS in tiles with
-//                 a 5-point halo, the 11-tap stencil (:84-107) is evaluated left to right in
-//                 float, and wave 0 runs the greedy spacing rule (:110-123) with a 64-bit ballot
-//                 of candidates per 64 points (jstart is wave-uniform).
+//                 gives each point its rank among same-row points; waves own contiguous
+//                 quarters of the chunk and are prefixed in order -> the reference's push_back
+//                 order exactly.  The chunk is regrouped by row in LDS and stored in contiguous
+//                 per-row runs.  intensity = indexInRow + row/100.0 (:77)
+//   k_curv_select one wave per (frame,row): the row streams through a circular LDS window, the
+//                 11-tap stencil (:84-107) is evaluated left to right in float, and the same
+//                 wave runs the greedy spacing rule (:110-123) with a 64-bit ballot of
+//                 candidates per 64 points (jstart is wave-uniform).
 //   k_compact     row-major concatenation of the selected points (framePlanePtr order).
 #include "ssf_device.hpp"
 #include "ssf_internal.hpp"
@@ -83,6 +84,15 @@ __global__ __launch_bounds__(64) void k_bin_scan(int n_rows, int n_chunks, int32
     if (r == n_rows - 1) ro[n_rows] = incl;
 }
 
+// Stable per-row partition of one 4096-point chunk.  Wave w owns the chunk's points
+// [1024 w, 1024 w + 1024) in 16 steps of 64: a 7-ballot "match" on the 6-bit row id gives each
+// point its rank among same-row lanes, and a wave-private running count per row (LDS, no
+// barrier) turns that into its rank among the wave's same-row points.  One barrier later the
+// per-wave counts are prefixed (waves in order, then rows), every point lands in a row-grouped
+// LDS tile, and the tile leaves in contiguous per-row runs: coalesced 16-B stores instead of
+// one scattered store per point (a LiDAR scan interleaves the rows point by point).
+constexpr int kScatterSteps = kBinChunk / 256;   // 16 points per thread
+
 __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ pts, int stride,
                                                      const int64_t* __restrict__ frame_off,
                                                      int n_rows, int n_chunks,
@@ -90,23 +100,36 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
                                                      const int32_t* __restrict__ chunk_base,
                                                      const int32_t* __restrict__ ring_off,
                                                      float4* __restrict__ out) {
-    __shared__ int run[kMaxRows];
-    __shared__ int wcnt[4][kMaxRows];
+    __shared__ float4 tile[kBinChunk];            // 64 KiB
+    __shared__ uint8_t row_of[kBinChunk];
+    __shared__ int wrun[4][kMaxRows];
+    __shared__ int roff[kMaxRows + 1];            // chunk-local row offsets
+    __shared__ int64_t rbase[kMaxRows];           // global index of row r's first chunk point - roff[r]
     const int f = blockIdx.y, c = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
     const int64_t fb = frame_off[f], e = frame_off[f + 1];
     const int64_t s = fb + (int64_t)c * kBinChunk;
     if (s >= e) return;  // uniform
     const int64_t t = min(e, s + (int64_t)kBinChunk);
-    if (tid < kMaxRows) {
-        run[tid] = 0;
-        wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
-    }
+    if (tid < kMaxRows) wrun[0][tid] = wrun[1][tid] = wrun[2][tid] = wrun[3][tid] = 0;
     __syncthreads();
-    const int32_t* cb = chunk_base + ((int64_t)f * n_chunks + c) * n_rows;
-    const int32_t* ro = ring_off + (int64_t)f * (n_rows + 1);
-    for (int64_t base = s; base < t; base += 256) {
-        const int64_t i = base + tid;
-        const int id = (i < t) ? (int)rid[i] : -1;
+    // all loads first (ids, then points at clamped indices, unconditionally): one wait for the
+    // whole 16-point batch instead of one load latency per step
+    int idr[kScatterSteps];       // row id, then row id | rank-in-wave << 8
+    float px[kScatterSteps], py[kScatterSteps], pz[kScatterSteps];
+    const int64_t i0 = s + 1024 * w + (tid & 63);
+#pragma unroll
+    for (int st = 0; st < kScatterSteps; ++st) {
+        const int64_t i = i0 + 64 * st;
+        idr[st] = (i < t) ? (int)rid[i] : -1;
+    }
+#pragma unroll
+    for (int st = 0; st < kScatterSteps; ++st) {
+        const float* p = pts + min(i0 + 64 * st, t - 1) * stride;
+        px[st] = p[0]; py[st] = p[1]; pz[st] = p[2];
+    }
+#pragma unroll
+    for (int st = 0; st < kScatterSteps; ++st) {
+        const int id = idr[st];
         uint64_t m = __ballot(id >= 0);
 #pragma unroll
         for (int bit = 0; bit < 6; ++bit) {
@@ -114,41 +137,77 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
             const uint64_t bb = __ballot(on);
             m &= on ? bb : ~bb;
         }
-        const int rank = __popcll(m & lanemask_lt());
-        if (id >= 0 && rank == 0) wcnt[w][id] = __popcll(m);
-        __syncthreads();
+        const int rin = __popcll(m & lanemask_lt());
+        int rank = 0;
         if (id >= 0) {
-            int pre = run[id];
-            for (int k = 0; k < w; ++k) pre += wcnt[k][id];
-            const int idx_in_row = cb[id] + pre + rank;
-            const float* p = pts + i * stride;
-            float4 v;
-            v.x = p[0]; v.y = p[1]; v.z = p[2];
-            v.w = (float)((double)idx_in_row + (double)id / 100.0);
-            out[fb + ro[id] + idx_in_row] = v;
+            const int before = wrun[w][id];                  // read by every lane first,
+            rank = before + rin;
+            if (rin == 0) wrun[w][id] = before + __popcll(m);   // then the group leader adds
         }
-        __syncthreads();
-        if (tid < kMaxRows) {
-            run[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
-            wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
-        }
-        __syncthreads();
+        idr[st] = (id & 0xff) | (rank << 8);
     }
+    __syncthreads();
+    const int32_t* cb = chunk_base + ((int64_t)f * n_chunks + c) * n_rows;
+    const int32_t* ro = ring_off + (int64_t)f * (n_rows + 1);
+    if (tid < 64) {                                          // rows on the lanes of wave 0
+        const int r = tid;
+        int tot = 0;
+        if (r < n_rows) {
+            int acc = 0;
+            for (int k = 0; k < 4; ++k) { const int v = wrun[k][r]; wrun[k][r] = acc; acc += v; }
+            tot = acc;
+        }
+        int incl = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (r >= o) incl += y;
+        }
+        if (r < n_rows) {
+            roff[r] = incl - tot;
+            rbase[r] = fb + ro[r] + cb[r] - (incl - tot);
+        }
+        if (r == 63) roff[kMaxRows] = incl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < kScatterSteps; ++st) {
+        const int id = (int)(int8_t)(idr[st] & 0xff);
+        if (id >= 0) {
+            const int in_row = wrun[w][id] + (idr[st] >> 8);    // rank among the chunk's row-id points
+            const int loc = roff[id] + in_row;
+            float4 v;
+            v.x = px[st]; v.y = py[st]; v.z = pz[st];
+            v.w = (float)((double)(cb[id] + in_row) + (double)id / 100.0);   // frameFeature.cpp:77
+            tile[loc] = v;
+            row_of[loc] = (uint8_t)id;
+        }
+    }
+    __syncthreads();
+    const int total = roff[kMaxRows];
+    for (int k = tid; k < total; k += 256) out[rbase[row_of[k]] + k] = tile[k];
 }
 
-constexpr int kCurvTile = 2048;
+// One WAVE per (frame, row), four rows per work-group, no block barrier.  The wave streams its
+// row in 64-point groups (one coalesced float4 load per lane, three groups in flight) into a
+// 192-point circular LDS window (3 groups; point p at p % 192); group g-1's 11-tap stencil
+// (:84-107, evaluated left to right in float exactly as the reference) is computed once group g
+// has landed, and the greedy spacing rule (:110-123) runs on the same wave with a 64-bit ballot
+// of candidates per group (jstart is wave-uniform).
+constexpr int kCurvRowsPerWG = 4;
 
-SSF_DEV float stencil11(const float* a, int k) {  // a[k] is point j-5 ... a[k+10] is j+5
-    float s = a[k] + a[k + 1];
-    s = s + a[k + 2];
-    s = s + a[k + 3];
-    s = s + a[k + 4];
-    s = s - 10.0f * a[k + 5];
-    s = s + a[k + 6];
-    s = s + a[k + 7];
-    s = s + a[k + 8];
-    s = s + a[k + 9];
-    s = s + a[k + 10];
+SSF_DEV float stencil11w(const float* a, int j) {   // a is the 192-point window, j the centre
+    auto at = [&](int d) { return a[(j + d) % 192]; };
+    float s = at(-5) + at(-4);
+    s = s + at(-3);
+    s = s + at(-2);
+    s = s + at(-1);
+    s = s - 10.0f * at(0);
+    s = s + at(1);
+    s = s + at(2);
+    s = s + at(3);
+    s = s + at(4);
+    s = s + at(5);
     return s;
 }
 
@@ -160,66 +219,65 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
                                                      float* __restrict__ curv,
                                                      int32_t* __restrict__ sel,
                                                      int32_t* __restrict__ sel_cnt) {
-    __shared__ float sx[kCurvTile + 16], sy[kCurvTile + 16], sz[kCurvTile + 16];
-    __shared__ float cv[kCurvTile];
-    const int r = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    __shared__ float win[kCurvRowsPerWG][3][192];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = blockIdx.x * kCurvRowsPerWG + w, f = blockIdx.y;
+    if (r >= n_rows) return;                                   // wave-uniform
     const int32_t* ro = ring_off + (int64_t)f * (n_rows + 1);
     const int rs = ro[r], n_r = ro[r + 1] - rs;
     const int64_t base = frame_off[f] + rs;
     const bool in_rows = (r >= row_start) && (r < n_rows - row_end);
     if (!in_rows) {
         if (curv)
-            for (int j = tid; j < n_r; j += blockDim.x) curv[base + j] = 0.0f;
-        if (tid == 0) sel_cnt[(int64_t)f * n_rows + r] = 0;
+            for (int j = lane; j < n_r; j += 64) curv[base + j] = 0.0f;
+        if (lane == 0) sel_cnt[(int64_t)f * n_rows + r] = 0;
         return;
     }
-    int cnt = 0;     // wave-0 uniform
-    int jstart = 0;  // wave-0 uniform
-    for (int t0 = 0; t0 < n_r; t0 += kCurvTile) {
-        for (int k = tid; k < kCurvTile + 10; k += blockDim.x) {
-            const int j = t0 - 5 + k;
-            if (j >= 0 && j < n_r) {
-                const float4 v = rxyzi[base + j];
-                sx[k] = v.x; sy[k] = v.y; sz[k] = v.z;
-            }
+    float* wx = win[w][0];
+    float* wy = win[w][1];
+    float* wz = win[w][2];
+    const float4* src = rxyzi + base;
+    const int ng = (n_r + 63) >> 6;
+    auto load = [&](int g) {                                   // clamped: always a valid point
+        const int p = min(64 * g + lane, max(n_r - 1, 0));
+        return src[p];
+    };
+    float4 cur = n_r > 0 ? load(0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 nxt = n_r > 0 ? load(1 < ng ? 1 : 0) : cur;
+    float4 nx2 = n_r > 0 ? load(2 < ng ? 2 : 0) : cur;
+    int cnt = 0, jstart = 0;                                   // wave-uniform
+    for (int g = 0; g <= ng; ++g) {
+        if (g < ng) {                                          // group g into the window
+            const int p = 64 * g + lane;
+            wx[p % 192] = cur.x; wy[p % 192] = cur.y; wz[p % 192] = cur.z;
+            cur = nxt;
+            nxt = nx2;
+            nx2 = load(g + 3 < ng ? g + 3 : ng - 1);
         }
-        __syncthreads();
-        for (int k = tid; k < kCurvTile; k += blockDim.x) {
-            const int j = t0 + k;
-            if (j >= n_r) break;
-            float v = 0.0f;
-            if (j >= 5 && j < n_r - 5) {
-                const float dx = stencil11(sx, k), dy = stencil11(sy, k), dz = stencil11(sz, k);
-                v = dx * dx + dy * dy;
-                v = v + dz * dz;
-            }
-            cv[k] = v;
-            if (curv) curv[base + j] = v;
+        if (g == 0) continue;
+        const int j = 64 * (g - 1) + lane;                     // group g-1: its stencil is complete
+        float v = 0.0f;
+        if (j >= 5 && j < n_r - 5) {
+            const float dx = stencil11w(wx, j), dy = stencil11w(wy, j), dz = stencil11w(wz, j);
+            v = dx * dx + dy * dy;
+            v = v + dz * dz;
         }
-        __syncthreads();
-        if (tid < 64) {
-            const int lim = min(kCurvTile, n_r - t0);
-            for (int sub = 0; sub < lim; sub += 64) {
-                const int k = sub + tid;
-                const bool cand = (k < lim) && (cv[k] < plane_min);
-                uint64_t m = __ballot(cand);
-                const int j0 = t0 + sub;
-                while (true) {
-                    const int lo = jstart - j0;
-                    if (lo >= 64) break;
-                    if (lo > 0) m &= ~((1ull << lo) - 1ull);
-                    if (!m) break;
-                    const int l = __ffsll((unsigned long long)m) - 1;
-                    const int jj = j0 + l;
-                    if (tid == 0) sel[base + cnt] = jj;
-                    cnt++;
-                    jstart = jj + plane_span;
-                }
-            }
+        if (curv && j < n_r) curv[base + j] = v;
+        uint64_t m = __ballot(j < n_r && v < plane_min);
+        const int j0 = 64 * (g - 1);
+        while (true) {
+            const int lo = jstart - j0;
+            if (lo >= 64) break;
+            if (lo > 0) m &= ~((1ull << lo) - 1ull);
+            if (!m) break;
+            const int l = __ffsll((unsigned long long)m) - 1;
+            const int jj = j0 + l;
+            if (lane == 0) sel[base + cnt] = jj;
+            cnt++;
+            jstart = jj + plane_span;
         }
-        __syncthreads();
     }
-    if (tid == 0) sel_cnt[(int64_t)f * n_rows + r] = cnt;
+    if (lane == 0) sel_cnt[(int64_t)f * n_rows + r] = cnt;
 }
 
 __global__ __launch_bounds__(256) void k_compact(const int64_t* __restrict__ frame_off, int n_rows,
@@ -257,7 +315,8 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
         hipLaunchKernelGGL(k_bin_scatter, dim3(n_chunks, n_frames), dim3(256), 0, s, pts, stride,
                            frame_off, R, n_chunks, rid, hist, ring_off, ring_xyzi);
     }
-    hipLaunchKernelGGL(k_curv_select, dim3(R, n_frames), dim3(256), 0, s, frame_off, R,
+    hipLaunchKernelGGL(k_curv_select, dim3((R + kCurvRowsPerWG - 1) / kCurvRowsPerWG, n_frames),
+                       dim3(64 * kCurvRowsPerWG), 0, s, frame_off, R,
                        cfg.row_start, cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off,
                        ring_xyzi, curv, sel, sel_cnt);
     hipLaunchKernelGGL(k_compact, dim3(R, n_frames), dim3(256), 0, s, frame_off, R, ring_off,

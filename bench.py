@@ -64,6 +64,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU baseline sample: run the oracle for at least this long (bounded)")
     ap.add_argument("--serial", action="store_true", help="one stream (per-kernel timing without overlap)")
+    ap.add_argument("--mask-streams", type=int, default=2,
+                    help="mask launches of consecutive steps alternate over this many streams: the "
+                         "GMM of a frame depends on no other frame, so a step's slow frames overlap "
+                         "the next step's mask instead of idling the other CUs")
     return ap.parse_args()
 
 
@@ -146,8 +150,9 @@ def main():
     fe_mask.reserve(B, N)
     fe_feat.reserve(B, N)
     fe_mask.seed(20240000 + rank)
-    s_mask = torch.cuda.Stream(dev)
-    s_feat = s_mask if args.serial else torch.cuda.Stream(dev)
+    n_ms = 1 if args.serial else max(1, args.mask_streams)
+    s_masks = [torch.cuda.Stream(dev) for _ in range(n_ms)]
+    s_feat = s_masks[0] if args.serial else torch.cuda.Stream(dev)
     # per-step outputs (double-buffered plane clouds: last <- curr)
     pose_rel = ssf.identity_poses(B, dev)
     pose_abs = ssf.identity_poses(B, dev)
@@ -158,6 +163,7 @@ def main():
 
     def step(k, timing):
         pos, flow = batches[k]
+        s_mask = s_masks[k % n_ms]
         with torch.cuda.stream(s_mask):
             e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
             e0.record(s_mask)
@@ -175,10 +181,10 @@ def main():
                 fe_feat.register(state["last"], state["last_table"], pb, pose_rel, pose_abs)
             es[3].record(s_feat)
         state["last"], state["last_table"] = pb, table
-        cur = torch.cuda.current_stream(dev)
-        cur.wait_stream(s_mask)
-        cur.wait_stream(s_feat)
         if world > 1:   # the one exchange step: per-frame 6-DoF poses of every rank (RCCL)
+            cur = torch.cuda.current_stream(dev)
+            cur.wait_stream(s_mask)
+            cur.wait_stream(s_feat)
             gathered.append(sd.gather_poses(sd.pose_record(pose_abs, mask_out[k])))
         if timing:
             ev["mask"].append((e0, e1)); ev["feat"].append((es[0], es[1]))
@@ -219,8 +225,12 @@ def main():
     # frameFeature chain: bin_count 12 R + 1 W, bin_scatter 13 R + 16 W, curv_select 16 R + 4 W(sel)
     feat_bytes = B * N * (12 + 1 + 13 + 16 + 16) * 1.0
     kernels = {
+        # gbs: per launch (launches of consecutive steps overlap on two streams, so a launch's
+        # duration includes time shared with the next one); aggregate_gbs: all mask bytes of the
+        # timed steps over the timed wall time
         "k_mask_pose": dict(ms=mask_ms, bytes=mask_bytes, gbs=mask_bytes / mask_ms / 1e6,
-                            passes_per_frame=mean_passes),
+                            aggregate_gbs=mask_bytes * args.steps / elapsed / 1e9,
+                            passes_per_frame=mean_passes, streams=n_ms),
         "features(5 kernels)": dict(ms=feat_ms, bytes=feat_bytes, gbs=feat_bytes / feat_ms / 1e6),
         "plane_table": dict(ms=table_ms),
         "register(assoc+solve)": dict(ms=reg_ms),

@@ -25,15 +25,23 @@ struct ssf_ctx {
     DevBuf rid, hist, ring_off, ring_xyzi, sel, sel_cnt, plane1, off1, cnt1;
     // registration scratch
     DevBuf corr;
-    // mask scratch
-    DevBuf draws, start1;
+    // mask: k-means++ draws staged per launch through a ring of slots, so launches on different
+    // streams (e.g. consecutive batches overlapping their slow frames) never share a buffer
+    struct DrawSlot {
+        DevBuf d;
+        double* h = nullptr;           // pinned staging
+        int64_t hcap = 0;
+        hipEvent_t copied = nullptr;   // this slot's H2D finished: the staging may be rewritten
+        hipEvent_t used = nullptr;     // the kernel that read this slot finished
+    };
+    static constexpr int kDrawSlots = 4;
+    DrawSlot dslot[kDrawSlots];
+    int dnext = 0;
+    DevBuf start1;
     // host RandomState (MT19937, numpy legacy seeding)
     uint32_t mt[624];
     int mt_pos = 625;
     std::map<int64_t, std::vector<double>> cdf_cache;  // choice(n, p=1/n) cumulative table
-    double* h_draws = nullptr;        // pinned staging for the per-frame k-means++ draws
-    int64_t h_draws_cap = 0;
-    hipEvent_t draws_done = nullptr;  // guards reuse of the pinned staging buffer
 };
 
 namespace {
@@ -152,10 +160,14 @@ void ssf_destroy(ssf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     DevBuf* bufs[] = {&c->rid, &c->hist, &c->ring_off, &c->ring_xyzi, &c->sel, &c->sel_cnt,
-                      &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->draws, &c->start1};
+                      &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->start1};
+    for (auto& ds : c->dslot) {
+        if (ds.used) { (void)hipEventSynchronize(ds.used); (void)hipEventDestroy(ds.used); }
+        if (ds.copied) { (void)hipEventSynchronize(ds.copied); (void)hipEventDestroy(ds.copied); }
+        if (ds.h) (void)hipHostFree(ds.h);
+        ds.d.release();
+    }
     for (DevBuf* b : bufs) b->release();
-    if (c->draws_done) { (void)hipEventSynchronize(c->draws_done); (void)hipEventDestroy(c->draws_done); }
-    if (c->h_draws) (void)hipHostFree(c->h_draws);
     delete c;
 }
 
@@ -186,7 +198,8 @@ int32_t ssf_reserve(ssf_ctx* c, int32_t max_frames, int64_t max_points_per_frame
     int32_t rc = ensure_features(c, max_frames, total, max_points_per_frame);
     if (rc) return rc;
     SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(total, 1)), "alloc corr");
-    SSF_TRY_HIP(c, c->draws.ensure(sizeof(double) * 3 * (size_t)std::max(max_frames, 1)), "alloc draws");
+    for (auto& ds : c->dslot)
+        SSF_TRY_HIP(c, ds.d.ensure(sizeof(double) * 3 * (size_t)std::max(max_frames, 1)), "alloc draws");
     return SSF_OK;
 }
 
@@ -303,32 +316,44 @@ int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const fl
         if (h_frame_off[f + 1] < h_frame_off[f]) return fail(c, SSF_E_ARG, "mask_pose_batch: offsets not monotone");
     hipStream_t s = (hipStream_t)stream;
     SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
-    SSF_TRY_HIP(c, c->draws.ensure(sizeof(double) * 3 * (size_t)n_frames), "alloc draws");
-    if (c->draws_done) SSF_TRY_HIP(c, hipEventSynchronize(c->draws_done), "draws event");
-    else SSF_TRY_HIP(c, hipEventCreateWithFlags(&c->draws_done, hipEventDisableTiming), "draws event");
-    if (c->h_draws_cap < 3 * (int64_t)n_frames) {
-        if (c->h_draws) SSF_TRY_HIP(c, hipHostFree(c->h_draws), "free pinned");
-        c->h_draws = nullptr; c->h_draws_cap = 0;
-        SSF_TRY_HIP(c, hipHostMalloc((void**)&c->h_draws, sizeof(double) * 3 * (size_t)n_frames), "pinned draws");
-        c->h_draws_cap = 3 * (int64_t)n_frames;
+    ssf_ctx::DrawSlot& ds = c->dslot[c->dnext];
+    c->dnext = (c->dnext + 1) % ssf_ctx::kDrawSlots;
+    const size_t need = 3 * (size_t)n_frames;
+    if (!ds.copied) {
+        SSF_TRY_HIP(c, hipEventCreateWithFlags(&ds.copied, hipEventDisableTiming), "draws event");
+        SSF_TRY_HIP(c, hipEventCreateWithFlags(&ds.used, hipEventDisableTiming), "draws event");
+    } else {
+        SSF_TRY_HIP(c, hipEventSynchronize(ds.copied), "draws event");   // staging reusable
     }
-    std::memset(c->h_draws, 0, sizeof(double) * 3 * (size_t)n_frames);
+    if (ds.d.bytes < sizeof(double) * need) {                      // growing frees the old buffer
+        SSF_TRY_HIP(c, hipEventSynchronize(ds.used), "draws event");
+        SSF_TRY_HIP(c, ds.d.ensure(sizeof(double) * need), "alloc draws");
+    } else {
+        SSF_TRY_HIP(c, hipStreamWaitEvent(s, ds.used, 0), "draws wait");   // device-side: no host stall
+    }
+    if (ds.hcap < (int64_t)need) {
+        if (ds.h) SSF_TRY_HIP(c, hipHostFree(ds.h), "free pinned");
+        ds.h = nullptr; ds.hcap = 0;
+        SSF_TRY_HIP(c, hipHostMalloc((void**)&ds.h, sizeof(double) * need), "pinned draws");
+        ds.hcap = (int64_t)need;
+    }
+    std::memset(ds.h, 0, sizeof(double) * need);
     if (mode == SSF_MASK_GMM) {
         for (int f = 0; f < n_frames; ++f) {
             const int64_t nf = h_frame_off[f + 1] - h_frame_off[f];
             double u0, u1, u2;
             if (h_draws) { u0 = h_draws[3 * f]; u1 = h_draws[3 * f + 1]; u2 = h_draws[3 * f + 2]; }
             else { u0 = mt_random_sample(c); u1 = mt_random_sample(c); u2 = mt_random_sample(c); }
-            c->h_draws[3 * f] = nf > 0 ? (double)choice_uniform(c, nf, u0) : 0.0;
-            c->h_draws[3 * f + 1] = u1;
-            c->h_draws[3 * f + 2] = u2;
+            ds.h[3 * f] = nf > 0 ? (double)choice_uniform(c, nf, u0) : 0.0;
+            ds.h[3 * f + 1] = u1;
+            ds.h[3 * f + 2] = u2;
         }
     }
-    SSF_TRY_HIP(c, hipMemcpyAsync(c->draws.p, c->h_draws, sizeof(double) * 3 * n_frames,
-                                  hipMemcpyHostToDevice, s), "H2D draws");
-    SSF_TRY_HIP(c, hipEventRecord(c->draws_done, s), "draws record");
+    SSF_TRY_HIP(c, hipMemcpyAsync(ds.d.p, ds.h, sizeof(double) * need, hipMemcpyHostToDevice, s), "H2D draws");
+    SSF_TRY_HIP(c, hipEventRecord(ds.copied, s), "draws record");
     hipError_t e = ssf::launch_mask_pose(s, n_frames, d_pts, d_flow, d_frame_off, mode, d_mask_in,
-                                         c->draws.as<double>(), reflection, d_bg_mask, d_out);
+                                         ds.d.as<double>(), reflection, d_bg_mask, d_out);
+    if (e == hipSuccess) e = hipEventRecord(ds.used, s);
     if (e != hipSuccess) return hip_fail(c, e, "mask_pose launch");
     return SSF_OK;
 }

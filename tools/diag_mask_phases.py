@@ -23,8 +23,12 @@ def main():
     fe.seed(1)
     fe.mask_pose(pts, flow, off, h_off)
     torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     out, _ = fe.mask_pose(pts, flow, off, h_off)
+    e1.record()
     torch.cuda.synchronize()
+    wall_ms = e0.elapsed_time(e1)
     o = out.cpu().numpy()
     st = o[:, 26:32]
     names = ["pass0", "kmeans++", "lloyd", "gmm_init", "em", "final+mask"]
@@ -32,6 +36,10 @@ def main():
     tot = st[:, 5].mean()
     print(f"B={B} mean cycles/frame {tot:.3e}; km_iter {o[:, 19].mean():.1f} em_iter {o[:, 20].mean():.1f} "
           f"passes {o[:, 25].mean():.1f}")
+    slow = int(np.argmax(st[:, 5]))
+    print(f"  frame cycles min {st[:, 5].min():.3e} max {st[:, 5].max():.3e} (slowest: km_iter "
+          f"{o[slow, 19]:.0f} em_iter {o[slow, 20]:.0f}); kernel wall {wall_ms:.3f} ms -> "
+          f"{st[:, 5].max() / wall_ms / 1e6:.2f} G stamp-cycles/s over the slowest frame")
     for k, nme in enumerate(names):
         per = ""
         if nme == "lloyd":

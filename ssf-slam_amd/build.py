@@ -65,7 +65,7 @@ def build_diag() -> str:
     for src in SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(OBJ_DIR, src.replace(".hip", "_diag.o"))
-        extra = {"mask_pose.hip": ["-DSSF_MASK_STAMPS"], "registration.hip": ["-DSSF_TABLE_STAMPS"]}.get(src, [])
+        extra = {"mask_pose.hip": ["-DSSF_MASK_STAMPS"], "registration.hip": ["-DSSF_TABLE_STAMPS", "-DSSF_ASSOC_STAMPS"]}.get(src, [])
         subprocess.run([HIPCC, *FLAGS, *FILE_FLAGS.get(src, []), *extra, "-c", s, "-o", o], check=True)
         objs.append(o)
     subprocess.run([HIPCC, *FLAGS, "-shared", *objs, "-o", out], check=True)

@@ -585,11 +585,143 @@ __global__ __launch_bounds__(256) void k_associate_sorted(
 
 // Same association with the last frame's sorted cloud staged in LDS (x, y, z, original index
 // in .w: 16 B per point, dynamic LDS sized by the launch's plane-point bound).  Each
-// work-group handles kAssocQ queries of one pair; the binary search and both walks then run at
-// LDS latency instead of a dependent L2 load per candidate.
+// work-group handles kAssocQ queries of one pair in two phases:
+//   1. every query walks outward in x only while dx^2 < R^2 (and dx^2 <= best), R = 1 m.  If
+//      the best squared distance found is < R^2 the answer is exact: any closer point has
+//      dx^2 < R^2 and was visited.  About 95 % of queries finish here.
+//   2. the rest (no point within R: sparse, far regions, where an x-band walk would cover
+//      most of the frame) were queued in LDS; after a barrier they are answered 64 at a time by
+//      an exhaustive scan split over all waves (disjoint slices, merged in LDS).
+// Candidates are compared as (distance, original index), so visit order never changes the result.
 constexpr int kAssocThreads = 1024;
 constexpr int kAssocQ = 2048;              // queries per work-group (2 per thread)
 constexpr int kAssocLdsMax = 6144;         // last-frame plane points staged in LDS (96 KiB)
+#ifndef SSF_ASSOC_BAND2
+#define SSF_ASSOC_BAND2 1.0f
+#endif
+constexpr float kAssocBand2 = SSF_ASSOC_BAND2;   // phase-1 band: dx^2 < 1 (R = 1 m; 0.5 / 0.7 m measured slower)
+
+SSF_DEV float4 assoc_query_point(const float4& pc, const double q[4], const double t[3]) {
+    const double v[3] = {(double)pc.x, (double)pc.y, (double)pc.z};
+    double r[3];
+    quat_rotate(q, v, r);                                               // :74-82
+    float4 qs;
+    qs.x = (float)(r[0] + t[0]); qs.y = (float)(r[1] + t[1]); qs.z = (float)(r[2] + t[2]); qs.w = 0.f;
+    return qs;
+}
+
+template <class Ld>
+SSF_DEV void assoc_walk(Ld ld, int ml, const float4& qs, float lim, float& best, int& bi) {
+    int lo_i = 0, hi_i = ml;                                            // first x >= qs.x
+    while (lo_i < hi_i) {
+        const int mid = (lo_i + hi_i) >> 1;
+        if (ld(mid).x < qs.x) lo_i = mid + 1; else hi_i = mid;
+    }
+    for (int c = lo_i; c < ml; ++c) {
+        const float4 pl = ld(c);
+        const float dx = qs.x - pl.x;
+        const float dx2 = dx * dx;
+        if (dx2 > best || dx2 >= lim) break;
+        const float d = l2_simple(qs, pl);
+        const int id = __float_as_int(pl.w);
+        if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+    }
+    for (int c = lo_i - 1; c >= 0; --c) {
+        const float4 pl = ld(c);
+        const float dx = qs.x - pl.x;
+        const float dx2 = dx * dx;
+        if (dx2 > best || dx2 >= lim) break;
+        const float d = l2_simple(qs, pl);
+        const int id = __float_as_int(pl.w);
+        if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+    }
+}
+
+SSF_DEV void assoc_finish(const float4* __restrict__ L, int64_t lo, const float* __restrict__ last_normal,
+                          const uint8_t* __restrict__ last_valid, const float4& pc, int bi,
+                          CorrRec* __restrict__ corr, int32_t* __restrict__ nn_out, int64_t ci) {
+    CorrRec rec;
+    const bool ok = last_valid[lo + bi] != 0;
+    const float4 pa = L[bi];
+    rec.po[0] = pc.x; rec.po[1] = pc.y; rec.po[2] = pc.z; rec.valid = ok ? 1.0f : 0.0f;
+    rec.pa[0] = pa.x; rec.pa[1] = pa.y; rec.pa[2] = pa.z; rec.pad0 = 0.f;
+    const float* nr = last_normal + 3 * (lo + bi);
+    rec.n[0] = nr[0]; rec.n[1] = nr[1]; rec.n[2] = nr[2]; rec.pad1 = 0.f;
+    corr[ci] = rec;
+    if (nn_out) nn_out[ci] = bi;
+}
+
+// phases 1 and 2 for one work-group; Ld reads sorted point c as (x, y, z, original index)
+template <class Ld>
+SSF_DEV void assoc_phases(Ld ld, int ml, int mc, int i0, int64_t lo, int64_t co,
+                          const double* __restrict__ pose_rel, int p, const float4* __restrict__ curr,
+                          const float4* __restrict__ L, const float* __restrict__ last_normal,
+                          const uint8_t* __restrict__ last_valid, CorrRec* __restrict__ corr,
+                          int32_t* __restrict__ nn_out, int* queue, int* qlen, float* red_d,
+                          int* red_i, unsigned long long* stamp1) {
+    const double q[4] = {pose_rel[7 * p], pose_rel[7 * p + 1], pose_rel[7 * p + 2], pose_rel[7 * p + 3]};
+    const double t[3] = {pose_rel[7 * p + 4], pose_rel[7 * p + 5], pose_rel[7 * p + 6]};
+    const int i1 = min(mc, i0 + kAssocQ);
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {           // phase 1: the x band
+        const float4 pc = curr[co + i];
+        const float4 qs = assoc_query_point(pc, q, t);
+        float best = __builtin_inff();
+        int bi = 0x7fffffff;
+        assoc_walk(ld, ml, qs, kAssocBand2, best, bi);
+        if (best < kAssocBand2) assoc_finish(L, lo, last_normal, last_valid, pc, bi, corr, nn_out, co + i);
+        else queue[atomicAdd(qlen, 1)] = i;                             // <= kAssocQ entries
+    }
+    __syncthreads();
+#ifdef SSF_ASSOC_STAMPS
+    *stamp1 = __builtin_amdgcn_s_memtime();
+#endif
+    // phase 2: the queued queries in groups of 64 (one per lane); for each group all waves scan
+    // disjoint slices of the last frame (broadcast LDS reads, 8 in flight, no divergence) and the
+    // per-slice (distance, index) bests are merged in LDS -- lexicographic, so exact
+    const int nq = *qlen;
+    const int nw = blockDim.x >> 6, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int chunk = (ml + nw - 1) / nw;
+    const int c0 = min(ml, w * chunk), c1 = min(ml, c0 + chunk);
+    for (int g0 = 0; g0 < nq; g0 += 64) {
+        const int k = g0 + lane;
+        const bool act = k < nq;
+        const int i = queue[act ? k : g0];
+        const float4 pc = curr[co + i];
+        const float4 qs = assoc_query_point(pc, q, t);
+        float best = __builtin_inff();
+        int bi = 0x7fffffff;
+        int c = c0;
+        for (; c + 8 <= c1; c += 8) {
+            float4 pl[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) pl[u] = ld(c + u);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const float d = l2_simple(qs, pl[u]);
+                const int id = __float_as_int(pl[u].w);
+                if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+            }
+        }
+        for (; c < c1; ++c) {
+            const float4 pl = ld(c);
+            const float d = l2_simple(qs, pl);
+            const int id = __float_as_int(pl.w);
+            if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+        }
+        red_d[w * 64 + lane] = best;
+        red_i[w * 64 + lane] = bi;
+        __syncthreads();
+        if (w == 0 && act) {
+            for (int v = 1; v < nw; ++v) {
+                const float d = red_d[v * 64 + lane];
+                const int id = red_i[v * 64 + lane];
+                if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+            }
+            assoc_finish(L, lo, last_normal, last_valid, pc, bi, corr, nn_out, co + i);
+        }
+        __syncthreads();
+    }
+}
 
 __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
     const float4* __restrict__ last, const int64_t* __restrict__ last_off,
@@ -599,74 +731,52 @@ __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
     const int64_t* __restrict__ curr_off, const int32_t* __restrict__ curr_count,
     const double* __restrict__ pose_rel, CorrRec* __restrict__ corr, int32_t* __restrict__ nn_out,
     int lds_cap) {
-    extern __shared__ float4 SLl[];
+    extern __shared__ float4 SLl[];                 // [lds_cap] points, then the queue
+    int* queue = reinterpret_cast<int*>(SLl + lds_cap);
+    __shared__ int qlen;
+    __shared__ float red_d[kAssocThreads];          // phase-2 per-slice bests
+    __shared__ int red_i[kAssocThreads];
     const int p = blockIdx.y;
     const int mc = curr_count[p], ml = last_count[p];
     const int i0 = blockIdx.x * kAssocQ;
     if (i0 >= mc || ml <= 10) return;                                   // uniform (:158)
     const int64_t lo = last_off[p], co = curr_off[p];
-    // a last frame above the caller's plane-point bound (the LDS size) walks global memory
-    const bool in_lds = ml <= lds_cap;
-    if (in_lds) {
+    unsigned long long st1 = 0;
+#ifdef SSF_ASSOC_STAMPS
+    // diagnostic build only: work-group lifetime (s_memtime) into nn_out[co + i0 .. +3]
+    const unsigned long long st0 = __builtin_amdgcn_s_memtime();
+#endif
+    if (threadIdx.x == 0) qlen = 0;
+    const float4* L = last + lo;
+    if (ml <= lds_cap) {
         for (int r = threadIdx.x; r < ml; r += blockDim.x) {
             float4 v = last_sorted[lo + r];
             v.w = __int_as_float(last_sidx[lo + r]);
             SLl[r] = v;
         }
+        __syncthreads();
+        assoc_phases([&](int c) { return SLl[c]; }, ml, mc, i0, lo, co, pose_rel, p, curr, L,
+                     last_normal, last_valid, corr, nn_out, queue, &qlen, red_d, red_i, &st1);
+    } else {  // a last frame above the caller's plane-point bound (the LDS size): global memory
+        __syncthreads();
+        const float4* SG = last_sorted + lo;
+        const int32_t* SI = last_sidx + lo;
+        assoc_phases([&](int c) { float4 v = SG[c]; v.w = __int_as_float(SI[c]); return v; },
+                     ml, mc, i0, lo, co, pose_rel, p, curr, L, last_normal, last_valid, corr, nn_out,
+                     queue, &qlen, red_d, red_i, &st1);
     }
+#ifdef SSF_ASSOC_STAMPS
     __syncthreads();
-    auto ld = [&](int c) -> float4 {
-        if (in_lds) return SLl[c];
-        float4 v = last_sorted[lo + c];
-        v.w = __int_as_float(last_sidx[lo + c]);
-        return v;
-    };
-    const double q[4] = {pose_rel[7 * p], pose_rel[7 * p + 1], pose_rel[7 * p + 2], pose_rel[7 * p + 3]};
-    const double t[3] = {pose_rel[7 * p + 4], pose_rel[7 * p + 5], pose_rel[7 * p + 6]};
-    const int i1 = min(mc, i0 + kAssocQ);
-    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-        const float4 pc = curr[co + i];
-        float4 qs;
-        {
-            const double v[3] = {(double)pc.x, (double)pc.y, (double)pc.z};
-            double r[3];
-            quat_rotate(q, v, r);                                       // :74-82
-            qs.x = (float)(r[0] + t[0]); qs.y = (float)(r[1] + t[1]); qs.z = (float)(r[2] + t[2]); qs.w = 0.f;
-        }
-        int lo_i = 0, hi_i = ml;                                        // first x >= qs.x
-        while (lo_i < hi_i) {
-            const int mid = (lo_i + hi_i) >> 1;
-            if (ld(mid).x < qs.x) lo_i = mid + 1; else hi_i = mid;
-        }
-        float best = __builtin_inff();
-        int bi = 0x7fffffff;
-        for (int c = lo_i; c < ml; ++c) {
-            const float4 pl = ld(c);
-            const float dx = qs.x - pl.x;
-            if (dx * dx > best) break;
-            const float d = l2_simple(qs, pl);
-            const int id = __float_as_int(pl.w);
-            if (lex_less(d, id, best, bi)) { best = d; bi = id; }
-        }
-        for (int c = lo_i - 1; c >= 0; --c) {
-            const float4 pl = ld(c);
-            const float dx = qs.x - pl.x;
-            if (dx * dx > best) break;
-            const float d = l2_simple(qs, pl);
-            const int id = __float_as_int(pl.w);
-            if (lex_less(d, id, best, bi)) { best = d; bi = id; }
-        }
-        const float4* L = last + lo;
-        CorrRec rec;
-        const bool ok = last_valid[lo + bi] != 0;
-        const float4 pa = L[bi];
-        rec.po[0] = pc.x; rec.po[1] = pc.y; rec.po[2] = pc.z; rec.valid = ok ? 1.0f : 0.0f;
-        rec.pa[0] = pa.x; rec.pa[1] = pa.y; rec.pa[2] = pa.z; rec.pad0 = 0.f;
-        const float* nr = last_normal + 3 * (lo + bi);
-        rec.n[0] = nr[0]; rec.n[1] = nr[1]; rec.n[2] = nr[2]; rec.pad1 = 0.f;
-        corr[co + i] = rec;
-        if (nn_out) nn_out[co + i] = bi;
+    if (threadIdx.x == 0 && nn_out) {
+        const unsigned long long st2 = __builtin_amdgcn_s_memtime();
+        nn_out[co + i0] = qlen;
+        nn_out[co + i0 + 1] = (int32_t)((st1 - st0) >> 4);
+        nn_out[co + i0 + 2] = (int32_t)((st2 - st0) >> 4);
+        nn_out[co + i0 + 3] = qlen;
     }
+#else
+    (void)st1;
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1021,7 +1131,8 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
         if (max_m <= kAssocLdsMax && last_sorted && last_sidx) {
             const int qx = (int)((max_m + kAssocQ - 1) / kAssocQ);
             hipLaunchKernelGGL(k_associate_lds, dim3(qx, n_pairs), dim3(kAssocThreads),
-                               (size_t)max_m * sizeof(float4), s, last, last_off, last_count,
+                               (size_t)max_m * sizeof(float4) + kAssocQ * sizeof(int), s, last,
+                               last_off, last_count,
                                last_normal, last_valid, last_sorted, last_sidx, curr, curr_off,
                                curr_count, pose_rel, corr, nn, (int)max_m);
         } else if (max_m <= kSortMax && last_sorted && last_sidx) {

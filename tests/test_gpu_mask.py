@@ -78,6 +78,36 @@ def test_full_size_batch_vs_oracle(oracle, dev):
         assert np.abs(o[7:16].reshape(3, 3) - ref["R"]).max() < 1e-6
 
 
+def test_concurrent_streams_one_context(dev):
+    """ssf_mask_pose_batch from one context on two streams back to back (the bench overlaps
+    consecutive batches this way): every launch stages its draws in its own slot, so each result
+    equals the same launch run alone."""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index)
+    batches = []
+    for k in range(3):
+        fr = [frame(8 + k, 0, n_az=900), frame(9 + k, 1, n_az=900)]
+        pts = torch.from_numpy(np.concatenate([f[0] for f in fr])).to(dev)
+        fl = torch.from_numpy(np.concatenate([f[1] for f in fr])).to(dev)
+        off, h_off = ssf.frame_offsets([f[0].shape[0] for f in fr], dev)
+        draws = np.array([[0.1 + 0.2 * k, 0.3, 0.6], [0.9 - 0.1 * k, 0.5, 0.2]])
+        batches.append((pts, fl, off, h_off, draws))
+    ref = []
+    for b in batches:
+        o, bg = fe.mask_pose(b[0], b[1], b[2], b[3], draws=b[4])
+        torch.cuda.synchronize()
+        ref.append((o.cpu().numpy(), bg.cpu().numpy()))
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    outs = []
+    for k, b in enumerate(batches):
+        with torch.cuda.stream(streams[k % 2]):
+            outs.append(fe.mask_pose(b[0], b[1], b[2], b[3], draws=b[4]))
+    torch.cuda.synchronize()
+    for (o, bg), (ro, rbg) in zip(outs, ref):
+        assert np.array_equal(o.cpu().numpy()[:, :26], ro[:, :26])
+        assert np.array_equal(bg.cpu().numpy(), rbg)
+
+
 def test_gt_and_given_masks(oracle, dev):
     import ssf
     fe = ssf.Frontend(64, device=dev.index)

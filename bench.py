@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU baseline sample: run the oracle for at least this long (bounded)")
     ap.add_argument("--serial", action="store_true", help="one stream (per-kernel timing without overlap)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N>1 rehearsal on a one-GPU box: every rank on cuda:0, gloo collectives "
+                         "(the printed line is marked rehearsal; not a scaling measurement)")
     ap.add_argument("--mask-streams", type=int, default=2,
                     help="mask launches of consecutive steps alternate over this many streams: the "
                          "GMM of a frame depends on no other frame, so a step's slow frames overlap "
@@ -132,11 +135,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.warmup < 1:
         args.warmup = 1  # the first frame of a sequence has no last frame to register against
+    if args.rehearse_one_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     import ssf
     from ssf import dist as sd
@@ -205,7 +213,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.rehearse_one_gpu else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -248,7 +256,8 @@ def main():
         "config": {"workload": f"{B} sequences in flight per GPU x {args.rows}-beam {N}-pt scans; "
                                f"mask(GMM+Kabsch) + features + plane table + {args.solver} x{iters}",
                    "sequences_per_gpu": B, "points_per_frame": N, "solver": args.solver,
-                   "iters": iters, "parallelism": f"sequence-sharded x{world}"},
+                   "iters": iters, "parallelism": f"sequence-sharded x{world}",
+                   **({"rehearsal": "all ranks on one GPU, gloo"} if args.rehearse_one_gpu else {})},
         "roofline": None, "cpu_baseline": None, "kernels": kernels,
         "mask_status_nonzero": int((status != 0).sum()),
     }

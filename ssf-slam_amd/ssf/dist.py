@@ -33,6 +33,8 @@ def gather_poses(local: torch.Tensor, group=None) -> torch.Tensor:
     """All-gather equal-shaped per-rank pose records -> [world * n, k] in rank order."""
     if not dist.is_available() or not dist.is_initialized():
         return local
+    if local.is_cuda and dist.get_backend(group) == "gloo":     # gloo gathers host tensors
+        return gather_poses(local.cpu(), group).to(local.device)
     world = dist.get_world_size(group)
     bufs = [torch.empty_like(local) for _ in range(world)]
     dist.all_gather(bufs, local.contiguous(), group=group)

@@ -818,17 +818,22 @@ SSF_DEV int pk(int u, int v) {
 
 // All threads: evaluate Huber(0.1)-corrected normal equations at (q, t) over the pair's
 // records; result (x2 for the reference's duplicated residual blocks) in ne[] of every thread.
-SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4], const double t[3],
-                      double (&ne)[kNE], double* lds) {
+// Valid correspondences of a pair compacted (original order) into LDS once per solve, SoA floats:
+// every evaluation of the LM/GN loop then reads LDS instead of re-streaming the 48-byte records.
+constexpr int kSolveLdsCap = 4096;
+struct CorrLds {
+    float po[3][kSolveLdsCap], pa[3][kSolveLdsCap], n[3][kSolveLdsCap];
+};
+
+template <class Get>
+SSF_DEV void evaluate_with(Get get, int n, const double q[4], const double t[3],
+                           double (&ne)[kNE], double* lds) {
 #pragma unroll
     for (int k = 0; k < kNE; ++k) ne[k] = 0.0;
     const double a = 0.1, b = 0.1 * 0.1;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const CorrRec c = rec[i];
-        if (c.valid == 0.0f) continue;
-        const double po[3] = {c.po[0], c.po[1], c.po[2]};
-        const double pa[3] = {c.pa[0], c.pa[1], c.pa[2]};
-        const double nn[3] = {c.n[0], c.n[1], c.n[2]};
+        double po[3], pa[3], nn[3];
+        if (!get(i, po, pa, nn)) continue;
         double J[6];
         const double r = residual_jac(q, t, po, pa, nn, J);
         const double s = r * r;
@@ -853,6 +858,27 @@ SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4],
     block_sum<kNE>(ne, lds);
 #pragma unroll
     for (int k = 0; k < kNE; ++k) ne[k] *= 2.0;
+}
+
+SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4], const double t[3],
+                      double (&ne)[kNE], double* lds) {
+    evaluate_with([&](int i, double* po, double* pa, double* nn) {
+        const CorrRec c = rec[i];
+        if (c.valid == 0.0f) return false;
+        po[0] = c.po[0]; po[1] = c.po[1]; po[2] = c.po[2];
+        pa[0] = c.pa[0]; pa[1] = c.pa[1]; pa[2] = c.pa[2];
+        nn[0] = c.n[0]; nn[1] = c.n[1]; nn[2] = c.n[2];
+        return true;
+    }, n, q, t, ne, lds);
+}
+
+SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double t[3],
+                      double (&ne)[kNE], double* lds) {
+    evaluate_with([&](int i, double* po, double* pa, double* nn) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) { po[d] = C.po[d][i]; pa[d] = C.pa[d][i]; nn[d] = C.n[d][i]; }
+        return true;
+    }, nv, q, t, ne, lds);
 }
 
 SSF_DEV int chol_solve6(double M[6][6], const double b[6], double y[6]) {
@@ -912,6 +938,8 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
                                                          int32_t* __restrict__ ncorr_out) {
     __shared__ SolveShared S;
     __shared__ double red[(kSolveThreads / 64) * kNE];
+    __shared__ CorrLds C;
+    __shared__ int wtot[kSolveThreads / 64];
     const int p = blockIdx.x, tid = threadIdx.x;
     const int n = curr_count[p];
     const CorrRec* rec = corr + curr_off[p];
@@ -923,15 +951,45 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
     __syncthreads();
     const bool skip = last_count[p] <= 10;                              // :158
     if (!skip) {
-        int nv = 0;
-        for (int i = tid; i < n; i += blockDim.x) nv += rec[i].valid != 0.0f;
-        nv = block_sum_scalar<int>(nv, reinterpret_cast<int*>(red));
+        // order-preserving compaction of the valid records: thread tid owns a contiguous chunk,
+        // an exclusive scan of the chunk counts gives its first output slot
+        const int per = (n + blockDim.x - 1) / blockDim.x;
+        const int r0 = min(n, tid * per), r1 = min(n, r0 + per);
+        int mine = 0;
+        for (int i = r0; i < r1; ++i) mine += rec[i].valid != 0.0f;
+        const int lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+        int incl = mine;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wtot[w] = incl;
+        __syncthreads();
+        int before = 0, nv = 0;
+        for (int k = 0; k < nw; ++k) { const int v = wtot[k]; if (k < w) before += v; nv += v; }
+        const bool in_lds = nv <= kSolveLdsCap;                        // uniform
+        if (in_lds) {
+            int pos = before + incl - mine;
+            for (int i = r0; i < r1; ++i) {
+                const CorrRec c = rec[i];
+                if (c.valid == 0.0f) continue;
+#pragma unroll
+                for (int d = 0; d < 3; ++d) { C.po[d][pos] = c.po[d]; C.pa[d][pos] = c.pa[d]; C.n[d][pos] = c.n[d]; }
+                ++pos;
+            }
+        }
+        __syncthreads();
         if (tid == 0 && ncorr_out) ncorr_out[p] = nv;
+        auto eval_at = [&](const double* qq, const double* tt, double (&ne_)[kNE]) {
+            if (in_lds) evaluate(C, nv, qq, tt, ne_, red);
+            else evaluate(rec, n, qq, tt, ne_, red);
+        };
         double ne[kNE];
         double q[4], t[3];
         for (int k = 0; k < 4; ++k) q[k] = S.q[k];
         for (int k = 0; k < 3; ++k) t[k] = S.t[k];
-        evaluate(rec, n, q, t, ne, red);
+        eval_at(q, t, ne);
         if (tid == 0) {
             for (int k = 0; k < kNE; ++k) S.ne[k] = ne[k];
             for (int u = 0; u < 6; ++u) S.s[u] = 1.0 / (1.0 + sqrt(ne[pk(u, u)]));
@@ -960,7 +1018,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
                 if (S.done) break;
                 for (int k = 0; k < 4; ++k) q[k] = S.q[k];
                 for (int k = 0; k < 3; ++k) t[k] = S.t[k];
-                evaluate(rec, n, q, t, ne, red);
+                eval_at(q, t, ne);
                 if (tid == 0) {
                     for (int k = 0; k < kNE; ++k) S.ne[k] = ne[k];
                     write_log(log, max_iter, p, S.nlog++, S.q, S.t, ne[27], 6, 0);
@@ -1017,7 +1075,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
                 double qc[4], tc[3];
                 for (int k = 0; k < 4; ++k) qc[k] = S.qc[k];
                 for (int k = 0; k < 3; ++k) tc[k] = S.tc[k];
-                evaluate(rec, n, qc, tc, ne, red);
+                eval_at(qc, tc, ne);
                 if (tid == 0) {
                     double xn = 0.0, sn = 0.0;
                     for (int u = 0; u < 4; ++u) { xn += S.q[u] * S.q[u]; sn += (S.q[u] - S.qc[u]) * (S.q[u] - S.qc[u]); }

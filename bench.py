@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N>1 rehearsal on a one-GPU box: every rank on cuda:0, gloo collectives "
                          "(the printed line is marked rehearsal; not a scaling measurement)")
+    ap.add_argument("--feat-priority", type=int, default=-1,
+                    help="HIP stream priority of the features/registration stream (lower = higher)")
     ap.add_argument("--mask-streams", type=int, default=2,
                     help="mask launches of consecutive steps alternate over this many streams: the "
                          "GMM of a frame depends on no other frame, so a step's slow frames overlap "
@@ -160,7 +162,9 @@ def main():
     fe_mask.seed(20240000 + rank)
     n_ms = 1 if args.serial else max(1, args.mask_streams)
     s_masks = [torch.cuda.Stream(dev) for _ in range(n_ms)]
-    s_feat = s_masks[0] if args.serial else torch.cuda.Stream(dev)
+    # the registration chain is serial across steps: its stream gets the higher priority so the
+    # mask launches (independent frames) fill the CUs it leaves free
+    s_feat = s_masks[0] if args.serial else torch.cuda.Stream(dev, priority=args.feat_priority)
     # per-step outputs (double-buffered plane clouds: last <- curr)
     pose_rel = ssf.identity_poses(B, dev)
     pose_abs = ssf.identity_poses(B, dev)

@@ -162,10 +162,9 @@ SSF_DEV double wlp(const double x[6], Ptr U, Ptr c, double logdet, double logw) 
     double lp = 0.0;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-        double y = 0.0;
-#pragma unroll
-        for (int i = 0; i <= j; ++i) y += x[i] * U[up(i, j)];
-        y -= c[j];
+        double y = -c[j];                  // (x U)_j - (mu U)_j with the subtraction folded
+#pragma unroll                             // into the first FMA (sklearn subtracts after the
+        for (int i = 0; i <= j; ++i) y += x[i] * U[up(i, j)];   // product: ~1 ulp apart)
         lp += y * y;
     }
     return -0.5 * (6.0 * log(2.0 * kPi) + lp) + logdet + logw;
@@ -222,6 +221,29 @@ SSF_DEV void for_points_deep(const float* __restrict__ P, const float* __restric
             load_raw(P, Fl, min(i + D * T, n - 1), buf[d]);
             if (i < n) fn(i, x);
         }
+    }
+}
+
+// EM: two points per step (i, i + T) so every U / cU read from LDS serves both (the per-point
+// LDS re-read of the 54 parameter doubles is what bounds the EM pass).  The second point of the
+// last step may not exist (w1 = 0: computed on a duplicate, weighted out).  Loads clamped and
+// unconditional, as in for_points.
+template <class Fn>
+SSF_DEV void for_point_pairs(const float* __restrict__ P, const float* __restrict__ Fl, int64_t n, Fn&& fn) {
+    const int64_t T = blockDim.x;
+    int64_t i = threadIdx.x;
+    if (i >= n) return;
+    float ra[6], rb[6];
+    load_raw(P, Fl, i, ra);
+    load_raw(P, Fl, min(i + T, n - 1), rb);
+    for (; i < n; i += 2 * T) {
+        double xa[6], xb[6];
+#pragma unroll
+        for (int d = 0; d < 6; ++d) { xa[d] = (double)ra[d]; xb[d] = (double)rb[d]; }
+        const double wb = (i + T < n) ? 1.0 : 0.0;
+        load_raw(P, Fl, min(i + 2 * T, n - 1), ra);
+        load_raw(P, Fl, min(i + 3 * T, n - 1), rb);
+        fn(xa, xb, wb);
     }
 }
 
@@ -726,31 +748,39 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         // mantissa * 2^pexp (frexp per point: the product never overflows, one log per thread)
         double prod = 1.0;
         int pexp = 0;
-        for_points_deep<kEmDeep>(P, Fl, n, [&](int64_t, const double* x) {
-            // U / cU are re-read from LDS (broadcast ds_reads) for every point (lds_laundered)
+        for_point_pairs(P, Fl, n, [&](const double* xa, const double* xb, double wb) {
+            // U / cU are re-read from LDS once per PAIR of points (lds_laundered)
             const LdsDouble* U = lds_laundered(S.U);
             const LdsDouble* cU = lds_laundered(S.cU);
-            const double a0 = wlp(x, U, cU, ld0, lw0);
-            const double a1 = wlp(x, U + 21, cU + 6, ld1, lw1);
-            const double mx = a0 > a1 ? a0 : a1, mn = a0 > a1 ? a1 : a0;
-            const double e = exp(mn - mx);
-            const double d = 1.0 + e;
-            acc[28] += mx;
-            prod *= d;
-            pexp += __builtin_amdgcn_frexp_exp(prod);
-            prod = __builtin_amdgcn_frexp_mant(prod);
-            const double inv = recip_1_2(d);
-            const double r = a1 > a0 ? inv : e * inv;
-            acc[0] += r;
-            double v[6];
+            double a0[2], a1[2];
+            a0[0] = wlp(xa, U, cU, ld0, lw0);
+            a0[1] = wlp(xb, U, cU, ld0, lw0);
+            a1[0] = wlp(xa, U + 21, cU + 6, ld1, lw1);
+            a1[1] = wlp(xb, U + 21, cU + 6, ld1, lw1);
 #pragma unroll
-            for (int a = 0; a < 6; ++a) v[a] = x[a] - mean[a];
+            for (int h = 0; h < 2; ++h) {
+                const double* x = h ? xb : xa;
+                const double wgt = h ? wb : 1.0;
+                const double mx = a0[h] > a1[h] ? a0[h] : a1[h], mn = a0[h] > a1[h] ? a1[h] : a0[h];
+                const double e = exp(mn - mx);
+                const double d = 1.0 + e;
+                acc[28] += wgt * mx;
+                prod *= (h ? (wb > 0.0 ? d : 1.0) : d);
+                pexp += __builtin_amdgcn_frexp_exp(prod);
+                prod = __builtin_amdgcn_frexp_mant(prod);
+                const double inv = recip_1_2(d);
+                const double r = wgt * (a1[h] > a0[h] ? inv : e * inv);
+                acc[0] += r;
+                double v[6];
 #pragma unroll
-            for (int a = 0; a < 6; ++a) {
-                const double rv = r * v[a];
-                acc[1 + a] += rv;
+                for (int a = 0; a < 6; ++a) v[a] = x[a] - mean[a];
 #pragma unroll
-                for (int b = a; b < 6; ++b) acc[7 + up(a, b)] += rv * v[b];
+                for (int a = 0; a < 6; ++a) {
+                    const double rv = r * v[a];
+                    acc[1 + a] += rv;
+#pragma unroll
+                    for (int b = a; b < 6; ++b) acc[7 + up(a, b)] += rv * v[b];
+                }
             }
         });
         acc[28] += log(prod) + (double)pexp * 0.69314718055994530942;

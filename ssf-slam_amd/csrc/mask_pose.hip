@@ -50,6 +50,7 @@ constexpr int kNW = kMaskThreads / 64;
 #endif
 constexpr int kLloydDeep = SSF_LLOYD_DEEP;   // points in flight per thread in the Lloyd passes
 constexpr int kEmDeep = SSF_EM_DEEP;         // ... and in the EM passes
+constexpr int kKppBlocks = 4096;             // k-means++ block totals in LDS (frames up to ~262k points)
 constexpr double kPi = 3.14159265358979323846;
 
 // packed upper-triangular index of a 6x6 matrix (row i <= col j)
@@ -416,6 +417,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     __shared__ double red[kNW * 32];
     __shared__ int ired[kNW];
     __shared__ unsigned long long cand_lds[2];
+    __shared__ double bsum[kKppBlocks];   // k-means++ per-64-point-block distance totals
     const int f = blockIdx.x, tid = threadIdx.x;
     const int64_t fb = frame_off[f], n = frame_off[f + 1] - fb;
     const float* P = pts + 3 * fb;
@@ -546,11 +548,25 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             const double v = (-2.0 * dt + cn0) + xs;
             return v > 0.0 ? v : 0.0;
         };
+        // per 64-point block: the in-block inclusive scan's total (lane 63) goes to LDS, so the
+        // draw search below only re-scans the one block that holds the draw
+        const int64_t spw = seg / 64;                            // blocks per wave segment
+        const bool use_blocks = spw * nw <= kKppBlocks;          // uniform
         double wsum = 0.0;
-#pragma unroll 4
+#pragma unroll 2
         for (int64_t b = ws; b < we; b += 64) {
             const int64_t i = b + lane;
-            if (i < we) wsum += dist0(i);
+            const double d = i < we ? dist0(i) : 0.0;
+            wsum += d;
+            if (use_blocks) {
+                double v = d;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const double y = __shfl_up(v, o, 64);
+                    if (lane >= o) v += y;
+                }
+                if (lane == 63) bsum[w * spw + (b - ws) / 64] = v;
+            }
         }
         wsum = wave_sum(wsum);
         if (lane == 0) red[w] = wsum;
@@ -569,6 +585,42 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         // the scan (1e-9 slack >> the scan's rounding); the others stop once both are found.
         const double wtot = red[w];
         bool f1 = carry + wtot < r1 * (1.0 - 1e-9), f2 = carry + wtot < r2 * (1.0 - 1e-9);
+        if (use_blocks) {
+            // walk the wave's block totals with the same carry arithmetic as the full scan
+            // (carry + block total, then carry += total): the first block whose end reaches a
+            // draw is the block the full scan would stop in; only that block is re-scanned
+            int64_t blk1 = -1, blk2 = -1;
+            double cb1 = 0.0, cb2 = 0.0;
+            if (lane == 0 && !(f1 && f2)) {
+                double cr = carry;
+                for (int64_t k = 0; ws + 64 * k < we; ++k) {
+                    const double tot = bsum[w * spw + k];
+                    if (!f1 && blk1 < 0 && cr + tot >= r1) { blk1 = k; cb1 = cr; }
+                    if (!f2 && blk2 < 0 && cr + tot >= r2) { blk2 = k; cb2 = cr; }
+                    if ((f1 || blk1 >= 0) && (f2 || blk2 >= 0)) break;
+                    cr += tot;
+                }
+            }
+            blk1 = __shfl(blk1, 0, 64); blk2 = __shfl(blk2, 0, 64);
+            cb1 = __shfl(cb1, 0, 64); cb2 = __shfl(cb2, 0, 64);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int64_t blk = j ? blk2 : blk1;
+                if (blk < 0) continue;                           // wave-uniform
+                const int64_t b = ws + 64 * blk;
+                const int64_t i = b + lane;
+                double v = i < we ? dist0(i) : 0.0;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const double y = __shfl_up(v, o, 64);
+                    if (lane >= o) v += y;
+                }
+                const double incl = (j ? cb2 : cb1) + v;
+                const uint64_t mm = __ballot(i < we && incl >= (j ? r2 : r1));
+                if (mm && lane == 0) atomicMin(&cand_lds[j], (unsigned long long)(b + __ffsll((unsigned long long)mm) - 1));
+            }
+            f1 = f2 = true;                                      // skip the sequential scan
+        }
         for (int64_t b = ws; b < we && !(f1 && f2); b += 64) {
             const int64_t i = b + lane;
             double v = i < we ? dist0(i) : 0.0;

@@ -120,6 +120,34 @@ def test_register_pair_per_step(oracle, dev, solver, iters, mode, brute):
     assert np.abs(got[4:] - t).max() < TOL_T and _quat_angle(got[:4], q) < TOL_R
 
 
+def test_16_row_profile_table_and_registration(oracle, dev):
+    """16-beam profile (planeMax 0.15, lidarOdometry_onlyPC.cpp:314-316): plane table bit-exact
+    and an LM pair within the pose bars."""
+    import ssf
+    fe = ssf.Frontend(16, device=dev.index)
+    clouds = [frame(3, 0, n_rows=16, n_az=1800)[0], frame(3, 1, n_rows=16, n_az=1800)[0]]
+    pb = _planes(fe, dev, clouds)
+    table = fe.plane_table(pb)
+    normal, valid = table[0], table[1]
+    for f in range(2):
+        P = pb.frame(f).cpu().numpy()
+        nr, vr, _, _ = oracle.plane_table(P, 0.15)
+        o, m = int(pb.h_off[f]), P.shape[0]
+        assert np.array_equal(valid[o:o + m].cpu().numpy(), vr.astype(np.uint8))
+        assert np.array_equal(normal[o:o + m].cpu().numpy().view(np.uint32), nr.view(np.uint32))
+    q0, t0 = np.array([0.0, 0.0, 0.0, 1.0]), np.array([0.5, 0.0, 0.0])
+    pose = torch.tensor([[*q0, *t0]], dtype=torch.float64, device=dev)
+    res = fe.register(_sub(pb, [0]), table, _sub(pb, [1]), pose, want_nn=True)
+    torch.cuda.synchronize()
+    L, Cc = pb.frame(0).cpu().numpy(), pb.frame(1).cpu().numpy()
+    o1 = int(pb.h_off[1])
+    assert np.array_equal(res["nn"][o1:o1 + len(Cc)].cpu().numpy(), oracle.correspond(L, Cc, q0, t0))
+    q, t, _, c = oracle.register_pair(L, Cc, 0.15, mode=0, max_iter=8, q_init=q0, t_init=t0)
+    got = res["pose_rel"][0].cpu().numpy()
+    assert int(res["ncorr"][0]) == c
+    assert np.abs(got[4:] - t).max() < TOL_T and _quat_angle(got[:4], q) < TOL_R
+
+
 def test_associate_large_frames(oracle, dev):
     """1-NN indices exact when the frames exceed the LDS staging size (6144 plane points): the
     association walks the sorted last frame in global memory."""

@@ -69,7 +69,7 @@ def parse():
                          "(the printed line is marked rehearsal; not a scaling measurement)")
     ap.add_argument("--feat-priority", type=int, default=-1,
                     help="HIP stream priority of the features/registration stream (lower = higher)")
-    ap.add_argument("--mask-streams", type=int, default=2,
+    ap.add_argument("--mask-streams", type=int, default=3,
                     help="mask launches of consecutive steps alternate over this many streams: the "
                          "GMM of a frame depends on no other frame, so a step's slow frames overlap "
                          "the next step's mask instead of idling the other CUs")

@@ -321,6 +321,7 @@ constexpr int kSortMax = 16384;           // plane points per frame sorted in LD
 constexpr int kTableThreads = 1024;
 
 constexpr int kLdsWalkMax = 6144;         // after the sort, frames up to this size walk in LDS
+// (16 m bytes of points + the deferred-query grid (16.6 KiB + 2 m) fit below the permutation)
 
 // Diagnostic build only (-DSSF_TABLE_STAMPS): lane 0 writes s_memtime deltas after the sort,
 // the bounded walks and the deferred walks into sorted_idx[m .. m+3] (frame padding, read by
@@ -400,6 +401,128 @@ SSF_DEV void table_finish(const float4* __restrict__ P, int m, float plane_max, 
     valid[o] = ok;
 }
 
+// Deferred queries (no decision inside 1 m: sparse, far regions) on a 2-D (x, y) grid built in
+// spare LDS: an x band around a far point crosses every LiDAR ring and holds thousands of
+// candidates, the grid cells around it a few hundred at most.  G x G cells over the frame's
+// bounding box, u32 cell ends (count, exclusive scan, atomic scatter) and a u16 list of sorted
+// ranks.  Each query searches rings of cells outward and stops once the squared distance to
+// the unvisited region (minus a 1 mm slack for float cell assignment) exceeds its 30th key's
+// distance; keys are (distance, index), so the list is the exact 30-NN in any visit order.
+constexpr int kGridG = 64;
+constexpr int kGridBytes = 4 * kGridG * kGridG + 256;      // + 2 m bytes of list
+
+SSF_DEV void table_deferred_grid(const float4* __restrict__ P, const float4* __restrict__ SPl,
+                                 const int* __restrict__ idx, int m, float plane_max, int64_t base,
+                                 float* __restrict__ normal, uint8_t* __restrict__ valid,
+                                 const int* queue, int nq, char* gridmem,
+                                 int32_t* stamp_out, unsigned long long stamp0) {
+    constexpr int G = kGridG;
+    uint32_t* cend = reinterpret_cast<uint32_t*>(gridmem);
+    float* scr = reinterpret_cast<float*>(gridmem + 4 * G * G);          // 2 floats per wave
+    uint16_t* list = reinterpret_cast<uint16_t*>(gridmem + kGridBytes);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+    float ymn = __builtin_inff(), ymx = -__builtin_inff();
+    for (int r = tid; r < m; r += blockDim.x) { const float y = SPl[r].y; ymn = fminf(ymn, y); ymx = fmaxf(ymx, y); }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        ymn = fminf(ymn, __shfl_xor(ymn, o, 64));
+        ymx = fmaxf(ymx, __shfl_xor(ymx, o, 64));
+    }
+    if (lane == 0) { scr[2 * w] = ymn; scr[2 * w + 1] = ymx; }
+    for (int c = tid; c < G * G; c += blockDim.x) cend[c] = 0u;
+    __syncthreads();
+    float y0 = __builtin_inff(), y1 = -__builtin_inff();
+    for (int k = 0; k < nw; ++k) { y0 = fminf(y0, scr[2 * k]); y1 = fmaxf(y1, scr[2 * k + 1]); }
+    const float x0 = SPl[0].x, x1 = SPl[m - 1].x;
+    float h = fmaxf(x1 - x0, y1 - y0) / (float)G;
+    if (!(h > 0.0f)) h = 1.0f;
+    const float invh = 1.0f / h;
+    auto cell = [&](const float4& p, int& cx, int& cy) {
+        cx = min(G - 1, max(0, (int)((p.x - x0) * invh)));
+        cy = min(G - 1, max(0, (int)((p.y - y0) * invh)));
+    };
+    for (int r = tid; r < m; r += blockDim.x) {
+        int cx, cy;
+        cell(SPl[r], cx, cy);
+        atomicAdd(&cend[cy * G + cx], 1u);
+    }
+    __syncthreads();
+    {   // exclusive scan of the G*G counts: a contiguous run per thread, then the block
+        const int per = (G * G + blockDim.x - 1) / blockDim.x;
+        const int c0 = min(G * G, tid * per), c1 = min(G * G, c0 + per);
+        uint32_t run = 0;
+        for (int c = c0; c < c1; ++c) run += cend[c];
+        uint32_t incl = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) reinterpret_cast<uint32_t*>(scr)[2 * nw + w] = incl;
+        __syncthreads();
+        uint32_t pre = incl - run;
+        for (int k = 0; k < w; ++k) pre += reinterpret_cast<uint32_t*>(scr)[2 * nw + k];
+        for (int c = c0; c < c1; ++c) { const uint32_t v = cend[c]; cend[c] = pre; pre += v; }
+    }
+    __syncthreads();
+    for (int r = tid; r < m; r += blockDim.x) {               // cend[c]: start -> end of cell c
+        int cx, cy;
+        cell(SPl[r], cx, cy);
+        list[atomicAdd(&cend[cy * G + cx], 1u)] = (uint16_t)r;
+    }
+    __syncthreads();
+    if (tid == 0 && stamp_out) stamp_out[3] = (int32_t)((__builtin_amdgcn_s_memtime() - stamp0) >> 4);
+    const int t2 = (tid & 63) * nw + w;                        // entry k -> wave k % nw
+    for (int k = t2; k < nq; k += blockDim.x) {
+        const int r = queue[k];
+        const float4 q = SPl[r];
+        int cx, cy;
+        cell(q, cx, cy);
+        double kk[kK];
+#pragma unroll
+        for (int j = 0; j < kK; ++j) kk[j] = knn_key(__builtin_inff(), 0x7fffffff);
+        // one candidate per loop trip (lanes hold different queries: nested ring/cell/point loops
+        // would cost the wave the per-cell maximum over lanes at every step)
+        int rr = 0, dy = 0, dx = 0, j = 0, e = 0;
+        {
+            const int c = cy * G + cx;
+            j = c ? (int)cend[c - 1] : 0;
+            e = (int)cend[c];
+        }
+        for (;;) {
+            bool done = false;
+            while (j >= e) {                                   // next non-empty cell of the ring walk
+                const bool edge = dy == -rr || dy == rr;
+                if (edge && dx < rr) ++dx;
+                else if (!edge && dx == -rr) dx = rr;
+                else { ++dy; dx = -rr; }
+                if (dy > rr) {                                 // ring rr complete: stop test
+                    if (cx - rr <= 0 && cy - rr <= 0 && cx + rr >= G - 1 && cy + rr >= G - 1) { done = true; break; }
+                    float dmin = __builtin_inff();
+                    if (cx - rr > 0) dmin = fminf(dmin, q.x - (x0 + (float)(cx - rr) * h));
+                    if (cx + rr < G - 1) dmin = fminf(dmin, (x0 + (float)(cx + rr + 1) * h) - q.x);
+                    if (cy - rr > 0) dmin = fminf(dmin, q.y - (y0 + (float)(cy - rr) * h));
+                    if (cy + rr < G - 1) dmin = fminf(dmin, (y0 + (float)(cy + rr + 1) * h) - q.y);
+                    dmin -= 1e-3f;
+                    if (dmin > 0.0f && dmin * dmin > key_dist(kk[kK - 1])) { done = true; break; }
+                    ++rr; dy = -rr; dx = -rr;
+                }
+                const int xx = cx + dx, yy = cy + dy;
+                if (xx >= 0 && xx < G && yy >= 0 && yy < G) {
+                    const int c = yy * G + xx;
+                    j = c ? (int)cend[c - 1] : 0;
+                    e = (int)cend[c];
+                }
+            }
+            if (done) break;
+            const int rj = list[j++];
+            const double key = knn_key(l2_simple(q, SPl[rj]), idx[rj]);
+            if (key < kk[kK - 1]) key_insert<kK>(kk, key);
+        }
+        table_finish<true>(P, m, plane_max, base + idx[r], kk, normal, valid);
+    }
+}
+
 // Queries in sorted order (adjacent lanes ~ adjacent x): 1-m-bounded walk for everyone; the
 // undecided few go to an LDS queue and are re-walked in full afterwards, one per lane, so a
 // handful of long walks no longer stalls whole waves.  queue == nullptr: walk in full at once.
@@ -408,7 +531,8 @@ SSF_DEV void table_walks(const float4* __restrict__ P, const float4* __restrict_
                          const float4* __restrict__ SPl, const int* __restrict__ idx, int m,
                          float plane_max, int64_t base, float* __restrict__ normal,
                          uint8_t* __restrict__ valid, int* queue, int qcap, int* qlen,
-                         int32_t* stamp_out = nullptr, unsigned long long stamp0 = 0) {
+                         char* gridmem = nullptr, int32_t* stamp_out = nullptr,
+                         unsigned long long stamp0 = 0) {
     for (int r = threadIdx.x; r < m; r += blockDim.x) {
         const float4 q = kLds ? SPl[r] : SPg[r];
         double kk[kK];
@@ -438,6 +562,11 @@ SSF_DEV void table_walks(const float4* __restrict__ P, const float4* __restrict_
     if (threadIdx.x == 0 && stamp_out) stamp_out[1] = *qlen;
 #endif
     const int nq = min(*qlen, qcap);
+    if (kLds && gridmem && nq > 0) {                          // uniform
+        table_deferred_grid(P, SPl, idx, m, plane_max, base, normal, valid, queue, nq, gridmem,
+                            stamp_out, stamp0);
+        return;
+    }
     for (int k = threadIdx.x; k < nq; k += blockDim.x) {
         const int r = queue[k];
         const float4 q = kLds ? SPl[r] : SPg[r];
@@ -508,10 +637,14 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
         __syncthreads();
         for (int r = tid; r < m; r += blockDim.x) SPl[r] = P[idx2[r]];
         __syncthreads();
-        #ifdef SSF_TABLE_STAMPS
-        table_walks<true>(P, SP, SPl, idx2, m, plane_max, base, normal, valid, queue, qcap, qlen, SI + m + 1, tstamp0);
+        // spare LDS between the sorted points and the permutation holds the deferred-query grid
+        char* gridmem = lds + ((16 * m + 15) & ~15);
+#ifdef SSF_TABLE_STAMPS
+        table_walks<true>(P, SP, SPl, idx2, m, plane_max, base, normal, valid, queue, qcap, qlen,
+                          gridmem, SI + m + 1, tstamp0);
 #else
-        table_walks<true>(P, SP, SPl, idx2, m, plane_max, base, normal, valid, queue, qcap, qlen);
+        table_walks<true>(P, SP, SPl, idx2, m, plane_max, base, normal, valid, queue, qcap, qlen,
+                          gridmem);
 #endif
         SSF_TSTAMP(3);
     } else {

@@ -232,7 +232,8 @@ def main():
     passes = torch.stack([mask_out[k][:, 25] for k in range(args.warmup, args.warmup + args.steps)])
     status = torch.stack([mask_out[k][:, 16] for k in range(args.warmup, args.warmup + args.steps)])
     mean_passes = float(passes.mean())
-    # k_mask_pose: every pass streams [flow, xyz] float32 (24 B/pt); + 1 B/pt mask write
+    # k_mask_pose: out[25] counts its algorithmic bytes in units of one [flow, xyz] float32
+    # stream (24 B/pt; Lloyd skip passes count their record/queue bytes); + 1 B/pt mask write
     mask_bytes = B * N * (24.0 * mean_passes + 1.0)
     # frameFeature chain: bin_count 12 R + 1 W, bin_scatter 13 R + 16 W, curv_select 16 R + 4 W(sel)
     feat_bytes = B * N * (12 + 1 + 13 + 16 + 16) * 1.0

@@ -172,7 +172,7 @@ enum {
     SSF_POSE_OUT_CENTER0 = 22, /* k-means++ chosen indices                                   */
     SSF_POSE_OUT_CENTER1 = 23,
     SSF_POSE_OUT_LOWER_BOUND = 24,
-    SSF_POSE_OUT_PASSES = 25   /* full passes over the frame's points (traffic accounting)   */
+    SSF_POSE_OUT_PASSES = 25   /* algorithmic bytes / (24 B x points): full-pass equivalents */
 };
 enum { SSF_POSE_EMPTY = -1, SSF_POSE_REFLECTION = -2, SSF_POSE_NOT_ORTHOGONAL = -3,
        SSF_POSE_GMM_FAILED = -4 };

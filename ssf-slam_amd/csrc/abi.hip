@@ -29,6 +29,7 @@ struct ssf_ctx {
     // streams (e.g. consecutive batches overlapping their slow frames) never share a buffer
     struct DrawSlot {
         DevBuf d;
+        DevBuf rec;                    // Lloyd label/bound records (8 B) + relabel queue (4 B) per point
         double* h = nullptr;           // pinned staging
         int64_t hcap = 0;
         hipEvent_t copied = nullptr;   // this slot's H2D finished: the staging may be rewritten
@@ -166,6 +167,7 @@ void ssf_destroy(ssf_ctx* c) {
         if (ds.copied) { (void)hipEventSynchronize(ds.copied); (void)hipEventDestroy(ds.copied); }
         if (ds.h) (void)hipHostFree(ds.h);
         ds.d.release();
+        ds.rec.release();
     }
     for (DevBuf* b : bufs) b->release();
     delete c;
@@ -198,8 +200,10 @@ int32_t ssf_reserve(ssf_ctx* c, int32_t max_frames, int64_t max_points_per_frame
     int32_t rc = ensure_features(c, max_frames, total, max_points_per_frame);
     if (rc) return rc;
     SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(total, 1)), "alloc corr");
-    for (auto& ds : c->dslot)
+    for (auto& ds : c->dslot) {
         SSF_TRY_HIP(c, ds.d.ensure(sizeof(double) * 3 * (size_t)std::max(max_frames, 1)), "alloc draws");
+        SSF_TRY_HIP(c, ds.rec.ensure(sizeof(uint2) * (size_t)(total + 2 * (int64_t)max_frames + 2) + sizeof(uint32_t) * (size_t)total), "alloc lloyd records");
+    }
     return SSF_OK;
 }
 
@@ -325,9 +329,11 @@ int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const fl
     } else {
         SSF_TRY_HIP(c, hipEventSynchronize(ds.copied), "draws event");   // staging reusable
     }
-    if (ds.d.bytes < sizeof(double) * need) {                      // growing frees the old buffer
+    const size_t rec_need = mode == SSF_MASK_GMM ? sizeof(uint2) * (size_t)(total + 2 * (int64_t)n_frames + 2) + sizeof(uint32_t) * (size_t)total : 0;
+    if (ds.d.bytes < sizeof(double) * need || ds.rec.bytes < rec_need) {   // growing frees the old buffer
         SSF_TRY_HIP(c, hipEventSynchronize(ds.used), "draws event");
         SSF_TRY_HIP(c, ds.d.ensure(sizeof(double) * need), "alloc draws");
+        if (rec_need) SSF_TRY_HIP(c, ds.rec.ensure(rec_need), "alloc lloyd records");
     } else {
         SSF_TRY_HIP(c, hipStreamWaitEvent(s, ds.used, 0), "draws wait");   // device-side: no host stall
     }
@@ -352,7 +358,7 @@ int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const fl
     SSF_TRY_HIP(c, hipMemcpyAsync(ds.d.p, ds.h, sizeof(double) * need, hipMemcpyHostToDevice, s), "H2D draws");
     SSF_TRY_HIP(c, hipEventRecord(ds.copied, s), "draws record");
     hipError_t e = ssf::launch_mask_pose(s, n_frames, d_pts, d_flow, d_frame_off, mode, d_mask_in,
-                                         ds.d.as<double>(), reflection, d_bg_mask, d_out);
+                                         ds.d.as<double>(), ds.rec.as<uint2>(), reflection, d_bg_mask, d_out);
     if (e == hipSuccess) e = hipEventRecord(ds.used, s);
     if (e != hipSuccess) return hip_fail(c, e, "mask_pose launch");
     return SSF_OK;

@@ -8,7 +8,7 @@
 //               draw), in-order chunked prefix scan -> the two local-trial candidates, potentials
 //   Lloyd       one streaming pass per iteration (labels, per-cluster sums, changed-label count)
 //   GMM init    one-hot responsibilities -> shifted first/second moments -> 6x6 Cholesky
-//   EM          ONE fused pass per iteration: E-step (weighted log-prob, logsumexp,
+//   EM          ONE fused pass per iteration: E-step (log-prob difference of the two components,
 //               responsibilities) and the M-step moment sums of the next parameters together
 //   final       argmax labels + per-label Kabsch sums (src = pos + flow, dst = pos) in one pass,
 //               background = majority label, 3x3 SVD (one-sided Jacobi, f64) on one lane,
@@ -19,6 +19,7 @@
 #include "ssf_internal.hpp"
 
 #include <float.h>
+#include <type_traits>
 
 namespace ssf {
 
@@ -45,13 +46,18 @@ constexpr int kNW = kMaskThreads / 64;
 #ifndef SSF_LLOYD_DEEP
 #define SSF_LLOYD_DEEP 2
 #endif
-#ifndef SSF_EM_DEEP
-#define SSF_EM_DEEP 1
-#endif
 constexpr int kLloydDeep = SSF_LLOYD_DEEP;   // points in flight per thread in the Lloyd passes
-constexpr int kEmDeep = SSF_EM_DEEP;         // ... and in the EM passes
 constexpr int kKppBlocks = 4096;             // k-means++ block totals in LDS (frames up to ~262k points)
 constexpr double kPi = 3.14159265358979323846;
+#ifndef SSF_LLOYD_FULL_PASSES
+#define SSF_LLOYD_FULL_PASSES 4
+#endif
+constexpr int kLloydFullPasses = SSF_LLOYD_FULL_PASSES;   // full Lloyd passes before skipping
+#ifndef SSF_LLOYD_REC_DEEP
+#define SSF_LLOYD_REC_DEEP 8
+#endif
+constexpr int kLloydRecDeep = SSF_LLOYD_REC_DEEP;         // 16-byte record loads in flight per lane
+constexpr int kLloydMax = 300;               // sklearn KMeans max_iter (pass index fits 9 bits)
 
 // packed upper-triangular index of a 6x6 matrix (row i <= col j)
 SSF_DEV constexpr int up(int i, int j) { return i * 6 - (i * (i - 1)) / 2 + (j - i); }
@@ -63,13 +69,20 @@ struct MaskShared {
     double tot[28];            // {N, sum(x-mean)[6], sum(x-mean)(x-mean)^T [21 packed]}
     double cen[12], csn[2], cenp[12], csnp[2];   // current / previous Lloyd centres
     double x0[6], ktot[16];    // pass-0 shift (point 0) and total Kabsch sums about it
-    double mu[12], U[42], cU[12], logdet[2], logw[2];  // U: packed upper precision Cholesky per comp; cU = mu U
+    double mu[12], U[42], logdet[2], logw[2];  // U: packed upper precision Cholesky per component
+    double Aq[21], bq[6], cq, C0;  // EM difference form: delta = a1 - a0 = v'A v + b'v + c (v = x - mean)
     double rand1, rand2;
     double lb;
     double C[36], L[36], Li[36];  // lane-0 scratch for the 6x6 algebra
     double sums[29];           // lane 0's copy of a pass's block sums (never a per-lane array)
+    double lsum[14];           // running Lloyd cluster sums {n0, S0[6], n1, S1[6]} about mean
+    double lhist[kLloydMax * 9];   // per labelling pass t: w = c1 - c0 [6], s = csn0 - csn1,
+                                   // |c0| + |c1|, csn0 + csn1 (lloyd_skip_bounds)
+    float lb1[512], lb2[512];   // this pass's drift bounds against pass r (9-bit index)
     int64_t c0, c1;
-    int km_iter, em_iter, strict, converged, done, status, passes, label0, bg, bg_pred;
+    double dg_cyc, dg_n, dg_lab, dg_wfull, dg_full1;   // diagnostic build only
+    double passes;             // algorithmic bytes / (24 B x n): 1 per full pass (see the Lloyd loop)
+    int km_iter, em_iter, strict, converged, done, status, label0, bg, bg_pred, lfull;
 };
 
 SSF_DEV void load_x(const float* __restrict__ P, const float* __restrict__ Fl, int64_t i, double x[6]) {
@@ -107,6 +120,57 @@ __device__ __noinline__ int prec_chol6(MaskShared& S, double* U_out, double* log
     return 0;
 }
 
+// lane-0: the E-step in difference form.  With P_k = U_k U_k^T, v = x - s (s = S.mean) and
+// m_k = mu_k - s, sklearn's weighted log-probabilities a_k = -0.5 (v - m_k)' P_k (v - m_k) + K_k,
+// K_k = -3 log(2 pi) + logdet_k + logw_k, differ by the quadratic
+//     delta = a1 - a0 = v' A v + b' v + c,   A = -0.5 (P1 - P0),  b = P1 m1 - P0 m0,
+//     c = -0.5 (m1' P1 m1 - m0' P0 m0) + K1 - K0,
+// which is all the per-point work needs: resp1 = sigmoid(delta), argmax = [delta > 0], and
+// logsumexp(a0, a1) = a0 + max(delta, 0) + log1p(exp(-|delta|)).  The a0 part of the lower bound
+// is summed over the frame from the pass-0 moments about s (S.tot = {N, M1, M2}):
+//     sum_i a0_i = N K0 - 0.5 (tr(P0 M2) - 2 m0' P0 M1 + N m0' P0 m0).
+// Aq is packed upper with the off-diagonal entries doubled (v'Av = sum_j v_j sum_{k>=j} Aq_jk v_k).
+__device__ __noinline__ void em_diff_form(MaskShared& S) {
+    double* P0 = S.C; double* P1 = S.L; double* m = S.Li;   // lane-0 scratch, free after prec_chol6
+    for (int k = 0; k < 2; ++k) {
+        double* Pk = k ? P1 : P0;
+        for (int a = 0; a < 6; ++a)
+            for (int b = a; b < 6; ++b) {
+                double v = 0.0;
+                for (int j = b; j < 6; ++j) v += S.U[21 * k + up(a, j)] * S.U[21 * k + up(b, j)];
+                Pk[a * 6 + b] = v; Pk[b * 6 + a] = v;
+            }
+        for (int a = 0; a < 6; ++a) m[6 * k + a] = S.mu[6 * k + a] - S.mean[a];
+    }
+    double q[2], Pm[12];
+    for (int k = 0; k < 2; ++k) {
+        const double* Pk = k ? P1 : P0;
+        q[k] = 0.0;
+        for (int a = 0; a < 6; ++a) {
+            double v = 0.0;
+            for (int b = 0; b < 6; ++b) v += Pk[a * 6 + b] * m[6 * k + b];
+            Pm[6 * k + a] = v;
+            q[k] += m[6 * k + a] * v;
+        }
+    }
+    for (int a = 0; a < 6; ++a) {
+        for (int b = a; b < 6; ++b) {
+            const double A = -0.5 * (P1[a * 6 + b] - P0[a * 6 + b]);
+            S.Aq[up(a, b)] = a == b ? A : 2.0 * A;
+        }
+        S.bq[a] = Pm[6 + a] - Pm[a];
+    }
+    S.cq = -0.5 * (q[1] - q[0]) + (S.logdet[1] + S.logw[1]) - (S.logdet[0] + S.logw[0]);
+    const double N = S.tot[0];
+    double tr = 0.0, lin = 0.0;
+    for (int a = 0; a < 6; ++a) {
+        lin += Pm[a] * S.tot[1 + a];
+        for (int b = 0; b < 6; ++b) tr += P0[a * 6 + b] * S.tot[7 + (a <= b ? up(a, b) : up(b, a))];
+    }
+    const double K0 = -3.0 * log(2.0 * kPi) + S.logdet[0] + S.logw[0];
+    S.C0 = N * K0 - 0.5 * (tr - 2.0 * lin + N * q[0]);
+}
+
 // lane-0: sklearn _estimate_gaussian_parameters from moments about the common shift s = S.mean.
 // comp1 = {sum r1, sum r1 (x-s), sum r1 (x-s)(x-s)^T};  comp0 = S.tot - comp1 (r0 = 1 - r1).
 __device__ __noinline__ int gmm_params(MaskShared& S, const double* comp1, int init, int64_t n) {
@@ -135,21 +199,14 @@ __device__ __noinline__ int gmm_params(MaskShared& S, const double* comp1, int i
     if (init) { w0 = nk[0] / (double)n; w1 = nk[1] / (double)n; }
     else { const double s = nk[0] + nk[1]; w0 = nk[0] / s; w1 = nk[1] / s; }
     S.logw[0] = log(w0); S.logw[1] = log(w1);
-    for (int k = 0; k < 2; ++k)
-        for (int j = 0; j < 6; ++j) {
-            double c = 0.0;
-            for (int i = 0; i <= j; ++i) c += S.mu[6 * k + i] * S.U[21 * k + up(i, j)];
-            S.cU[6 * k + j] = c;
-        }
+    em_diff_form(S);
     return 0;
 }
 
-// weighted log probability, sklearn _estimate_log_gaussian_prob form: y = x U - (mu U), with
-// c = mu U precomputed by lane 0 (S.cU); U packed upper.
 typedef __attribute__((address_space(3))) const double LdsDouble;
 
-// The LDS address of U / cU laundered through a VGPR once per point: the compiler can neither
-// hoist the 54 loop-invariant doubles into VGPRs nor has to rebuild each address in an SGPR
+// The LDS address of the E-step parameters laundered through a VGPR once per point: the compiler can neither
+// hoist the 27 loop-invariant doubles into VGPRs nor has to rebuild each address in an SGPR
 // (one VGPR base, immediate ds_read2 offsets).  The low 32 bits of a generic LDS pointer are
 // its LDS offset.
 SSF_DEV const LdsDouble* lds_laundered(const double* p) {
@@ -158,17 +215,32 @@ SSF_DEV const LdsDouble* lds_laundered(const double* p) {
     return (const LdsDouble*)(uintptr_t)a;
 }
 
+// delta = v'A v + b'v + c (em_diff_form) for two points at once: every Aq / bq read from LDS
+// serves both.
 template <class Ptr>
-SSF_DEV double wlp(const double x[6], Ptr U, Ptr c, double logdet, double logw) {
-    double lp = 0.0;
+SSF_DEV void em_delta2(const double va[6], const double vb[6], Ptr Aq, Ptr bq, double cq,
+                       double& da, double& db) {
+    da = cq; db = cq;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-        double y = -c[j];                  // (x U)_j - (mu U)_j with the subtraction folded
-#pragma unroll                             // into the first FMA (sklearn subtracts after the
-        for (int i = 0; i <= j; ++i) y += x[i] * U[up(i, j)];   // product: ~1 ulp apart)
-        lp += y * y;
+        double ta = bq[j], tb = ta;
+#pragma unroll
+        for (int k = j; k < 6; ++k) { const double a = Aq[up(j, k)]; ta += a * va[k]; tb += a * vb[k]; }
+        da += va[j] * ta; db += vb[j] * tb;
     }
-    return -0.5 * (6.0 * log(2.0 * kPi) + lp) + logdet + logw;
+}
+
+template <class Ptr>
+SSF_DEV double em_delta1(const double v[6], Ptr Aq, Ptr bq, double cq) {
+    double d = cq;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        double t = bq[j];
+#pragma unroll
+        for (int k = j; k < 6; ++k) t += Aq[up(j, k)] * v[k];
+        d += v[j] * t;
+    }
+    return d;
 }
 
 // Streams the frame's points through f(i, x): every thread keeps the NEXT point's loads in
@@ -225,8 +297,8 @@ SSF_DEV void for_points_deep(const float* __restrict__ P, const float* __restric
     }
 }
 
-// EM: two points per step (i, i + T) so every U / cU read from LDS serves both (the per-point
-// LDS re-read of the 54 parameter doubles is what bounds the EM pass).  The second point of the
+// EM: two points per step (i, i + T) so every Aq / bq read from LDS serves both (the per-point
+// LDS re-read of the parameter doubles is what bounds the EM pass).  The second point of the
 // last step may not exist (w1 = 0: computed on a duplicate, weighted out).  Loads clamped and
 // unconditional, as in for_points.
 template <class Fn>
@@ -411,8 +483,8 @@ SSF_DEV void accum_kabsch(double (&k)[16], const double* x, const double cs[3], 
 __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     const float* __restrict__ pts, const float* __restrict__ flow,
     const int64_t* __restrict__ frame_off, int mode, const uint8_t* __restrict__ mask_in,
-    const double* __restrict__ draws, int reflection, uint8_t* __restrict__ bg_mask,
-    double* __restrict__ out_all) {
+    const double* __restrict__ draws, uint2* __restrict__ lloyd_rec, int reflection,
+    uint8_t* __restrict__ bg_mask, double* __restrict__ out_all) {
     __shared__ MaskShared S;
     __shared__ double red[kNW * 32];
     __shared__ int ired[kNW];
@@ -677,56 +749,199 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     }
 
     SSF_STAMP(1);
-    // ---- Lloyd iterations (_kmeans_single_lloyd, max_iter 300).  The previous iteration's label
-    //      of a point is recomputed from the previous centres (2 dot products) instead of being
-    //      stored and re-loaded: the pass is a pure prefetched stream of [flow, xyz].
-    if (tid == 0) { S.strict = 0; S.done = 0; }
-    for (int it = 0; it < 300; ++it) {
+    // ---- Lloyd iterations (_kmeans_single_lloyd, max_iter 300) with exact label skipping.
+    //      A point's label at pass t is the sign of g_t = D0 - D1 (D_k = -2 v.c_k + |c_k|^2, the
+    //      expression the label is computed with).  In exact arithmetic g_t(v) = 2 v.w_t + s_t
+    //      (w = c1 - c0, s = |c0|^2 - |c1|^2), so |g_t - g_r| <= 2|v| |w_t - w_r| + |s_t - s_r|.
+    //      Every labelled point leaves an 8-byte record {|g_r| rounded down, |v| rounded up,
+    //      pass r, label}; a later pass t re-reads the point's 24 bytes only when
+    //          |g_r| <= B1(t, r) |v| + B2(t, r)
+    //      (B1/B2: the drift bounds plus 1e-13-relative margins for the f64 rounding of both
+    //      evaluations, >= 50x the dot-product error bound), i.e. whenever the sign could
+    //      differ.  Skipped points keep their label, so the labels, the changed-label count and
+    //      the strict-convergence decision are those of the full pass; the cluster sums are
+    //      updated by the points that changed label.
+    if (tid == 0) { S.strict = 0; S.done = 0; S.lfull = 1; S.dg_cyc = S.dg_n = S.dg_lab = S.dg_wfull = S.dg_full1 = 0.0; }
+    // records at an even offset (16-byte aligned pairs) with at least one spare slot (index n)
+    // after each frame: frame f at ((fb + 2 f + 1) & ~1); the buffer holds total + 2 F + 2
+    // records, then total 4-byte queue entries
+    uint2* __restrict__ LR = lloyd_rec + ((fb + 2 * (int64_t)f + 1) & ~(int64_t)1);
+    // the relabel queues (4 bytes per point) follow the records
+    uint32_t* __restrict__ LQ =
+        reinterpret_cast<uint32_t*>(lloyd_rec + frame_off[gridDim.x] + 2 * (int64_t)gridDim.x + 2) + fb;
+    for (int it = 0; it < kLloydMax; ++it) {
         if (tid == 0) {
+            double* h = S.lhist + 9 * it;
             for (int k = 0; k < 2; ++k) {
                 double sn = 0.0;
                 for (int d = 0; d < 6; ++d) sn += S.cen[6 * k + d] * S.cen[6 * k + d];
                 S.csn[k] = sn;
             }
+            for (int d = 0; d < 6; ++d) h[d] = S.cen[6 + d] - S.cen[d];
+            h[6] = S.csn[0] - S.csn[1];
+            h[7] = sqrt(S.csn[0]) + sqrt(S.csn[1]);
+            h[8] = S.csn[0] + S.csn[1];
         }
         __syncthreads();
-        double cen[12], cenp[12];
-        const double csn0 = S.csn[0], csn1 = S.csn[1], cpn0 = S.csnp[0], cpn1 = S.csnp[1];
+        if (tid < it) {   // drift bounds of this pass against every earlier labelling pass
+            const double* h = S.lhist + 9 * it;
+            const double* g = S.lhist + 9 * tid;
+            double dw = 0.0;
+            for (int d = 0; d < 6; ++d) dw += (h[d] - g[d]) * (h[d] - g[d]);
+            S.lb1[tid] = __double2float_ru(2.0 * sqrt(dw) + 2e-13 * (h[7] + g[7]));
+            S.lb2[tid] = __double2float_ru(fabs(h[6] - g[6]) + 1e-13 * (h[8] + g[8]));
+        }
+        __syncthreads();
+        double cen[12];
+        const double csn0 = uni(S.csn[0]), csn1 = uni(S.csn[1]);
 #pragma unroll
-        for (int k = 0; k < 12; ++k) { cen[k] = S.cen[k]; cenp[k] = S.cenp[k]; }
+        for (int k = 0; k < 12; ++k) cen[k] = uni(S.cen[k]);
         double acc[14];
 #pragma unroll
         for (int k = 0; k < 14; ++k) acc[k] = 0.0;
-        int changed = 0;
-        for_points_deep<kLloydDeep>(P, Fl, n, [&](int64_t, const double* x) {
-            double v[6], dt0 = 0.0, dt1 = 0.0, dp0 = 0.0, dp1 = 0.0;
+        int changed = 0, nlab = 0;
+        const bool full = S.lfull != 0;
+#ifdef SSF_MASK_STAMPS
+        const unsigned long long pass_t0 = __builtin_amdgcn_s_memtime();
+#endif
+        const bool wrec = it >= kLloydFullPasses - 1;   // a skip pass may follow this full pass
+        // exact labelling of one point (the expression of every earlier version of this pass):
+        // sums (full pass) or sum deltas (skip pass), changed count, new record
+        // (val = 0: a pipeline slot with no point -- computed, weighted out, record written to
+        // the frame's spare slot n)
+        auto label = [&](auto wrec_c, int64_t i, const double* x, int lp, bool val) {
+            double v[6], dt0 = 0.0, dt1 = 0.0, vn = 0.0;
 #pragma unroll
             for (int d = 0; d < 6; ++d) {
                 v[d] = x[d] - mean[d];
-                dt0 += v[d] * cen[d]; dt1 += v[d] * cen[6 + d];
-                dp0 += v[d] * cenp[d]; dp1 += v[d] * cenp[6 + d];
+                dt0 += v[d] * cen[d]; dt1 += v[d] * cen[6 + d]; vn += v[d] * v[d];
             }
-            const int l = (-2.0 * dt1 + csn1) < (-2.0 * dt0 + csn0) ? 1 : 0;
-            const int lp = (-2.0 * dp1 + cpn1) < (-2.0 * dp0 + cpn0) ? 1 : 0;
-            changed += (it == 0) || (l != lp);
-            const double w1 = (double)l, w0 = 1.0 - w1;
-            acc[0] += w0; acc[7] += w1;
+            const double D0 = -2.0 * dt0 + csn0, D1 = -2.0 * dt1 + csn1;
+            const int l = D1 < D0 ? 1 : 0;
+            double d1 = full ? (double)l : (double)(l - lp), d0 = full ? 1.0 - d1 : -d1;
+            d1 = val ? d1 : 0.0; d0 = val ? d0 : 0.0;
+            changed += val && (it == 0 || l != lp);
+            acc[0] += d0; acc[7] += d1;
 #pragma unroll
-            for (int d = 0; d < 6; ++d) { acc[1 + d] += w0 * v[d]; acc[8 + d] += w1 * v[d]; }
-        });
+            for (int d = 0; d < 6; ++d) { acc[1 + d] += d0 * v[d]; acc[8 + d] += d1 * v[d]; }
+            // |g| one f32 ulp below its nearest float (<= |g|); |v| from an f32 sqrt, 4 ulps up,
+            // then up to the 2^-14-relative grid that leaves the low 9 bits for the pass index
+            const uint32_t gb = __float_as_uint((float)fabs(D0 - D1));
+            const uint32_t nvb = (__float_as_uint(__builtin_sqrtf((float)vn)) + 4u + 0x1FFu) & 0x7FFFFE00u;
+            if constexpr (decltype(wrec_c)::value) LR[val ? i : n] = make_uint2(gb ? gb - 1u : 0u, nvb | (uint32_t)it | ((uint32_t)l << 31));
+        };
+        if (full) {
+            // every point: a prefetched stream of [flow, xyz]; the previous label is recomputed
+            // from the previous centres (the pass that wrote it used the same expression)
+            double cenp[12];
+            const double cpn0 = uni(S.csnp[0]), cpn1 = uni(S.csnp[1]);
+#pragma unroll
+            for (int k = 0; k < 12; ++k) cenp[k] = uni(S.cenp[k]);
+            auto full_pass = [&](auto wrec_c) {
+                for_points_deep<kLloydDeep>(P, Fl, n, [&](int64_t i, const double* x) {
+                    double dp0 = 0.0, dp1 = 0.0;
+#pragma unroll
+                    for (int d = 0; d < 6; ++d) {
+                        const double v = x[d] - mean[d];
+                        dp0 += v * cenp[d]; dp1 += v * cenp[6 + d];
+                    }
+                    const int lp = (-2.0 * dp1 + cpn1) < (-2.0 * dp0 + cpn0) ? 1 : 0;
+                    label(wrec_c, i, x, lp, true);
+                });
+            };
+            if (wrec) full_pass(std::true_type{});    // two loop bodies: no branch per point
+            else full_pass(std::false_type{});
+            nlab = (int)((n - tid + blockDim.x - 1) / blockDim.x);
+        } else {
+            // skip pass, two streams per wave over its own segment.  (1) the records, 16 bytes
+            // (two records) per lane per load, 8 loads in flight: the points whose sign could
+            // change are appended (ballot compaction, label in bit 31) to the wave's queue in
+            // global memory.  (2) the queue, 512 entries at a time: every entry load, then every
+            // point gather, then the relabelling -- two round trips per 512 queued points.
+            const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = lane_id();
+            const int64_t seg = ((n + kNW - 1) / kNW + 127) / 128 * 128;
+            const int64_t ws = (int64_t)w * seg, we = ws + seg < n ? ws + seg : n;
+            uint32_t* __restrict__ WQ = LQ + ws;        // capacity seg >= the wave's points
+            const uint4* __restrict__ LR4 = reinterpret_cast<const uint4*>(LR);
+            const int64_t plast = (n - 1) >> 1;
+            int qc = 0;
+            constexpr int D = kLloydRecDeep;
+            uint4 buf[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) buf[d] = LR4[min((ws >> 1) + d * 64 + lane, plast)];
+            for (int64_t base = ws; base < we; base += D * 128) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    const int64_t b = base + d * 128;
+                    const uint4 q = buf[d];
+                    buf[d] = LR4[min(((b + D * 128) >> 1) + lane, plast)];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t gx = h ? q.z : q.x, gy = h ? q.w : q.y;
+                        const int64_t i = b + 2 * lane + h;
+                        const int tr = (int)(gy & 0x1FFu);
+                        const float nv = __uint_as_float(gy & 0x7FFFFE00u);
+                        const bool skip = __uint_as_float(gx) > __builtin_fmaf(S.lb1[tr], nv, S.lb2[tr]) * 1.00001f;
+#ifdef SSF_LLOYD_EXP_NOQUEUE
+                        const bool nd = (i < we) & !skip & (gx == 0x7FFFFFFFu);
+#else
+                        const bool nd = (i < we) & !skip;
+#endif
+                        const uint64_t m = __ballot(nd);
+                        if (nd) WQ[qc + __popcll(m & lanemask_lt())] = (uint32_t)i | (gy & 0x80000000u);
+                        qc += __popcll(m);
+                    }
+                }
+            }
+            __threadfence_block();   // the wave's queue stores are visible to its loads below
+            for (int j0 = 0; j0 < qc; j0 += 512) {
+                uint32_t e[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) e[k] = WQ[min(j0 + k * 64 + lane, qc - 1)];
+                float px[8][6];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) load_raw(P, Fl, (int64_t)(e[k] & 0x7FFFFFFFu), px[k]);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    double x[6];
+#pragma unroll
+                    for (int d = 0; d < 6; ++d) x[d] = (double)px[k][d];
+                    const bool val = j0 + k * 64 + lane < qc;
+                    label(std::true_type{}, (int64_t)(e[k] & 0x7FFFFFFFu), x, (int)(e[k] >> 31), val);
+                    nlab += val ? 1 : 0;
+                }
+            }
+        }
         block_sum<14>(acc, red);
         changed = block_sum_scalar<int>(changed, ired);
+        nlab = block_sum_scalar<int>(nlab, ired);
         if (tid == 0) {
-            S.passes += 1;
+            // traffic accounting in 24-byte-per-point units: a full pass reads [flow, xyz] (+8 B
+            // of records written when wrec); a skip pass reads 8 B of records per point and
+            // 24 B per relabelled point, and writes (reads) 8 B of record + 4 (4) B of queue
+            // per relabel
+            S.passes += full ? 1.0 + (wrec ? 8.0 / 24.0 : 0.0)
+                             : (8.0 * (double)n + 40.0 * (double)nlab) / (24.0 * (double)n);
             S.km_iter = it + 1;
+            for (int k = 0; k < 14; ++k) S.lsum[k] = full ? acc[k] : S.lsum[k] + acc[k];
+            // the first passes move the centres most (typically 35-45 % of the points would be
+            // relabelled): full passes through it = 3, then skip passes while they relabel < 1/4
+            S.lfull = full ? it < kLloydFullPasses - 1 : nlab * 4 > n;
+#ifdef SSF_MASK_STAMPS
+            // diagnostic: cycles and relabelled points of the skip passes (k_mask_pose stamps
+            // build only; reported through the k-means++ centre slots, which it overwrites)
+            if (!full) { S.dg_cyc += (double)(__builtin_amdgcn_s_memtime() - pass_t0); S.dg_n += 1.0; S.dg_lab += nlab; }
+            else if (it == kLloydFullPasses - 1) S.dg_wfull = (double)(__builtin_amdgcn_s_memtime() - pass_t0);
+            else if (it == 1) S.dg_full1 = (double)(__builtin_amdgcn_s_memtime() - pass_t0);
+#endif
             for (int k = 0; k < 12; ++k) S.cenp[k] = S.cen[k];
             S.csnp[0] = S.csn[0]; S.csnp[1] = S.csn[1];
             double shift = 0.0;
             for (int k = 0; k < 2; ++k) {
-                const double wgt = acc[7 * k];
+                const double wgt = S.lsum[7 * k];
                 double sh = 0.0;
                 for (int d = 0; d < 6; ++d) {
-                    const double nc = wgt > 0.0 ? acc[7 * k + 1 + d] * (1.0 / wgt) : S.cen[6 * k + d];
+                    const double nc = wgt > 0.0 ? S.lsum[7 * k + 1 + d] * (1.0 / wgt) : S.cen[6 * k + d];
                     const double df = nc - S.cen[6 * k + d];
                     sh += df * df;
                     S.cen[6 * k + d] = nc;
@@ -788,11 +1003,12 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
 
     SSF_STAMP(3);
     // ---- EM: one fused pass per iteration -- E-step with the current parameters and the
-    //      M-step moments of component 1 (component 0 = total - component 1).
-    //      r_max = 1/(1+e), r_min = e/(1+e), lse = max + log1p(e), e = exp(min - max): the
-    //      scipy logsumexp expression, one exp + one log1p per point.
+    //      M-step moments of component 1 (component 0 = total - component 1), in the
+    //      difference form of em_diff_form: per point only delta = a1 - a0 (27 FMAs instead of
+    //      two 27-FMA Mahalanobis forms), e = exp(-|delta|), r1 = 1/(1+e) if delta > 0 else
+    //      e/(1+e), and the lower bound's per-point part max(delta, 0) + log1p(e).
     for (int it = 1; it <= 100 && S.status == 0; ++it) {
-        const double ld0 = uni(S.logdet[0]), lw0 = uni(S.logw[0]), ld1 = uni(S.logdet[1]), lw1 = uni(S.logw[1]);
+        const double cq = uni(S.cq);
         double acc[29];
 #pragma unroll
         for (int k = 0; k < 29; ++k) acc[k] = 0.0;
@@ -801,31 +1017,27 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         double prod = 1.0;
         int pexp = 0;
         for_point_pairs(P, Fl, n, [&](const double* xa, const double* xb, double wb) {
-            // U / cU are re-read from LDS once per PAIR of points (lds_laundered)
-            const LdsDouble* U = lds_laundered(S.U);
-            const LdsDouble* cU = lds_laundered(S.cU);
-            double a0[2], a1[2];
-            a0[0] = wlp(xa, U, cU, ld0, lw0);
-            a0[1] = wlp(xb, U, cU, ld0, lw0);
-            a1[0] = wlp(xa, U + 21, cU + 6, ld1, lw1);
-            a1[1] = wlp(xb, U + 21, cU + 6, ld1, lw1);
+            // Aq / bq are re-read from LDS once per PAIR of points (lds_laundered)
+            const LdsDouble* Aq = lds_laundered(S.Aq);
+            const LdsDouble* bq = lds_laundered(S.bq);
+            double va[6], vb[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) { va[a] = xa[a] - mean[a]; vb[a] = xb[a] - mean[a]; }
+            double dl[2];
+            em_delta2(va, vb, Aq, bq, cq, dl[0], dl[1]);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const double* x = h ? xb : xa;
+                const double* v = h ? vb : va;
                 const double wgt = h ? wb : 1.0;
-                const double mx = a0[h] > a1[h] ? a0[h] : a1[h], mn = a0[h] > a1[h] ? a1[h] : a0[h];
-                const double e = exp(mn - mx);
+                const double e = exp(-fabs(dl[h]));
                 const double d = 1.0 + e;
-                acc[28] += wgt * mx;
+                acc[28] += wgt * (dl[h] > 0.0 ? dl[h] : 0.0);
                 prod *= (h ? (wb > 0.0 ? d : 1.0) : d);
                 pexp += __builtin_amdgcn_frexp_exp(prod);
                 prod = __builtin_amdgcn_frexp_mant(prod);
                 const double inv = recip_1_2(d);
-                const double r = wgt * (a1[h] > a0[h] ? inv : e * inv);
+                const double r = wgt * (dl[h] > 0.0 ? inv : e * inv);
                 acc[0] += r;
-                double v[6];
-#pragma unroll
-                for (int a = 0; a < 6; ++a) v[a] = x[a] - mean[a];
 #pragma unroll
                 for (int a = 0; a < 6; ++a) {
                     const double rv = r * v[a];
@@ -841,7 +1053,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             S.passes += 1;
             S.em_iter = it;
             const double prev = S.lb;
-            S.lb = acc[28] / (double)n;
+            S.lb = (S.C0 + acc[28]) / (double)n;   // C0: the a0 part, from this E-step's parameters
             for (int k = 0; k < 29; ++k) S.sums[k] = acc[k];
             if (gmm_params(S, S.sums, 0, n) != 0) S.status = SSF_POSE_GMM_FAILED;
             if (fabs(S.lb - prev) < 1e-3) { S.converged = 1; S.done = 1; }
@@ -855,8 +1067,8 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     //      The mask is written in the same pass against a predicted background label (the
     //      heavier component); the rare frame whose majority disagrees gets one flip pass.
     {
-        const double ld0 = uni(S.logdet[0]), lw0 = uni(S.logw[0]), ld1 = uni(S.logdet[1]), lw1 = uni(S.logw[1]);
-        const int pred = lw1 > lw0 ? 1 : 0;
+        const int pred = S.logw[1] > S.logw[0] ? 1 : 0;
+        const double cq = uni(S.cq);
         double x0[6];
 #pragma unroll
         for (int d = 0; d < 6; ++d) x0[d] = uni(S.x0[d]);
@@ -864,12 +1076,13 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
 #pragma unroll
         for (int i = 0; i < 16; ++i) k1[i] = 0.0;
         for_points(P, Fl, n, [&](int64_t i, const double* x) {
-            // U / cU are re-read from LDS (broadcast ds_reads) for every point (lds_laundered)
-            const LdsDouble* U = lds_laundered(S.U);
-            const LdsDouble* cU = lds_laundered(S.cU);
-            const double a0 = wlp(x, U, cU, ld0, lw0);
-            const double a1 = wlp(x, U + 21, cU + 6, ld1, lw1);
-            const int l = a1 > a0 ? 1 : 0;
+            // Aq / bq are re-read from LDS (broadcast ds_reads) for every point (lds_laundered)
+            const LdsDouble* Aq = lds_laundered(S.Aq);
+            const LdsDouble* bq = lds_laundered(S.bq);
+            double v[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) v[a] = x[a] - mean[a];
+            const int l = em_delta1(v, Aq, bq, cq) > 0.0 ? 1 : 0;   // a1 > a0
             if (bg_mask) bg_mask[fb + i] = (uint8_t)(l == pred);
             if (i == 0) S.label0 = l;
             const double w1 = (double)l;
@@ -911,6 +1124,12 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             out[SSF_POSE_OUT_CONVERGED] = S.converged;
             out[SSF_POSE_OUT_CENTER0] = (double)S.c0;
             out[SSF_POSE_OUT_CENTER1] = (double)S.c1;
+#ifdef SSF_MASK_STAMPS
+            out[SSF_POSE_OUT_CENTER0] = S.dg_n > 0.0 ? S.dg_cyc / S.dg_n : 0.0;
+            out[SSF_POSE_OUT_CENTER1] = S.dg_n > 0.0 ? S.dg_lab / (S.dg_n * (double)n) : 0.0;
+            out[SSF_POSE_OUT_CONVERGED] = S.dg_wfull;
+            out[SSF_POSE_OUT_NBG] = S.dg_full1;
+#endif
             out[SSF_POSE_OUT_LOWER_BOUND] = S.lb;
             out[SSF_POSE_OUT_PASSES] = S.passes;
         }
@@ -924,10 +1143,11 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
 
 hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,
                             const int64_t* frame_off, int mode, const uint8_t* mask_in,
-                            const double* draws, int reflection, uint8_t* bg_mask, double* out) {
+                            const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
+                            double* out) {
     if (n_frames <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_mask_pose, dim3(n_frames), dim3(kMaskThreads), 0, s, pts, flow, frame_off,
-                       mode, mask_in, draws, reflection, bg_mask, out);
+                       mode, mask_in, draws, lloyd_rec, reflection, bg_mask, out);
     return hipGetLastError();
 }
 

@@ -65,6 +65,7 @@ hipError_t launch_accumulate(hipStream_t s, int n, const double* rel, const doub
 // ---- launchers (mask_pose.hip) ----
 hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,
                             const int64_t* frame_off, int mode, const uint8_t* mask_in,
-                            const double* draws, int reflection, uint8_t* bg_mask, double* out);
+                            const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
+                            double* out);
 
 }  // namespace ssf

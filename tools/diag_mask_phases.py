@@ -36,6 +36,8 @@ def main():
     tot = st[:, 5].mean()
     print(f"B={B} mean cycles/frame {tot:.3e}; km_iter {o[:, 19].mean():.1f} em_iter {o[:, 20].mean():.1f} "
           f"passes {o[:, 25].mean():.1f}")
+    print(f"  lloyd skip passes: {o[:, 22].mean():.3e} cycles each, {100 * o[:, 23].mean():.2f} % of points relabelled;"
+          f" full pass 1 {o[:, 17].mean():.3e}, record-writing full pass {o[:, 21].mean():.3e} cycles")
     slow = int(np.argmax(st[:, 5]))
     print(f"  frame cycles min {st[:, 5].min():.3e} max {st[:, 5].max():.3e} (slowest: km_iter "
           f"{o[slow, 19]:.0f} em_iter {o[slow, 20]:.0f}); kernel wall {wall_ms:.3f} ms -> "

@@ -112,7 +112,7 @@ int64_t choice_uniform(ssf_ctx* c, int64_t n, double u) {
 }
 
 bool valid_cfg(const ssf_config& c) {
-    return (c.n_rows == 16 || c.n_rows == 64) && c.plane_span >= 1 && c.row_start >= 0 &&
+    return (c.n_rows == 16 || c.n_rows == 64) && c.plane_span >= 2 && c.row_start >= 0 &&
            c.row_end >= 0 && c.max_iter >= 0 && c.max_iter <= 64 &&
            (c.solver == SSF_SOLVER_CERES_LM || c.solver == SSF_SOLVER_GN);
 }
@@ -202,7 +202,7 @@ int32_t ssf_reserve(ssf_ctx* c, int32_t max_frames, int64_t max_points_per_frame
     SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(total, 1)), "alloc corr");
     for (auto& ds : c->dslot) {
         SSF_TRY_HIP(c, ds.d.ensure(sizeof(double) * 3 * (size_t)std::max(max_frames, 1)), "alloc draws");
-        SSF_TRY_HIP(c, ds.rec.ensure(sizeof(uint2) * (size_t)(total + 2 * (int64_t)max_frames + 2) + sizeof(uint32_t) * (size_t)total), "alloc lloyd records");
+        SSF_TRY_HIP(c, ds.rec.ensure(sizeof(uint2) * (size_t)(total + 2 * (int64_t)max_frames + 2) + sizeof(uint32_t) * (size_t)(total + 64 * (int64_t)max_frames)), "alloc lloyd records");
     }
     return SSF_OK;
 }
@@ -329,7 +329,7 @@ int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const fl
     } else {
         SSF_TRY_HIP(c, hipEventSynchronize(ds.copied), "draws event");   // staging reusable
     }
-    const size_t rec_need = mode == SSF_MASK_GMM ? sizeof(uint2) * (size_t)(total + 2 * (int64_t)n_frames + 2) + sizeof(uint32_t) * (size_t)total : 0;
+    const size_t rec_need = mode == SSF_MASK_GMM ? sizeof(uint2) * (size_t)(total + 2 * (int64_t)n_frames + 2) + sizeof(uint32_t) * (size_t)(total + 64 * (int64_t)n_frames) : 0;
     if (ds.d.bytes < sizeof(double) * need || ds.rec.bytes < rec_need) {   // growing frees the old buffer
         SSF_TRY_HIP(c, hipEventSynchronize(ds.used), "draws event");
         SSF_TRY_HIP(c, ds.d.ensure(sizeof(double) * need), "alloc draws");

@@ -35,6 +35,10 @@ SSF_DEV int ring_id(float x, float y, float z, int n_rows) {
     return (id > -1 && id < n_rows) ? id : -1;
 }
 
+// Each thread issues all of its 16 point loads (clamped, unconditional) before the first ring
+// id: one load latency per chunk instead of one per point.
+constexpr int kCountSteps = kBinChunk / 256;
+
 __global__ __launch_bounds__(256) void k_bin_count(const float* __restrict__ pts, int stride,
                                                    const int64_t* __restrict__ frame_off,
                                                    int n_rows, int n_chunks,
@@ -48,11 +52,20 @@ __global__ __launch_bounds__(256) void k_bin_count(const float* __restrict__ pts
     const int64_t s = b + (int64_t)c * kBinChunk;
     if (s < e) {
         const int64_t t = min(e, s + (int64_t)kBinChunk);
-        for (int64_t i = s + threadIdx.x; i < t; i += blockDim.x) {
-            const float* p = pts + i * stride;
-            int id = ring_id(p[0], p[1], p[2], n_rows);
-            rid[i] = (int8_t)id;
-            if (id >= 0) atomicAdd(&h[id], 1);
+        float px[kCountSteps], py[kCountSteps], pz[kCountSteps];
+#pragma unroll
+        for (int k = 0; k < kCountSteps; ++k) {
+            const float* p = pts + min(s + threadIdx.x + 256 * k, t - 1) * stride;
+            px[k] = p[0]; py[k] = p[1]; pz[k] = p[2];
+        }
+#pragma unroll
+        for (int k = 0; k < kCountSteps; ++k) {
+            const int64_t i = s + threadIdx.x + 256 * k;
+            if (i < t) {
+                const int id = ring_id(px[k], py[k], pz[k], n_rows);
+                rid[i] = (int8_t)id;
+                if (id >= 0) atomicAdd(&h[id], 1);
+            }
         }
     }
     __syncthreads();
@@ -189,11 +202,14 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
 }
 
 // One WAVE per (frame, row), four rows per work-group, no block barrier.  The wave streams its
-// row in 64-point groups (one coalesced float4 load per lane, three groups in flight) into a
-// 192-point circular LDS window (3 groups; point p at p % 192); group g-1's 11-tap stencil
-// (:84-107, evaluated left to right in float exactly as the reference) is computed once group g
-// has landed, and the greedy spacing rule (:110-123) runs on the same wave with a 64-bit ballot
-// of candidates per group (jstart is wave-uniform).
+// row in 64-point groups (one coalesced float4 load per lane) into a 192-point circular LDS
+// window (3 groups; point p at p % 192); group g-1's 11-tap stencil (:84-107, evaluated left to
+// right in float exactly as the reference) is computed once group g has landed, and the greedy
+// spacing rule (:110-123) runs on the same wave with a 64-bit ballot of candidates per group
+// (jstart is wave-uniform).  Three register buffers with static roles (one loop trip = three
+// groups; loads clamped and unconditional) keep three groups in flight: a rotation by register
+// moves, or a load or store under a branch, makes the compiler wait for every load at each
+// group.  The selected indices collect in LDS and leave once per trip.
 constexpr int kCurvRowsPerWG = 4;
 
 SSF_DEV float stencil11w(const float* a, int j) {   // a is the 192-point window, j the centre
@@ -211,6 +227,7 @@ SSF_DEV float stencil11w(const float* a, int j) {   // a is the 192-point window
     return s;
 }
 
+template <bool kCurv>
 __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__ frame_off,
                                                      int n_rows, int row_start, int row_end,
                                                      float plane_min, int plane_span,
@@ -220,15 +237,18 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
                                                      int32_t* __restrict__ sel,
                                                      int32_t* __restrict__ sel_cnt) {
     __shared__ float win[kCurvRowsPerWG][3][192];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ int32_t slist[kCurvRowsPerWG][128];
+    // the wave index through readfirstlane: the compiler then knows the row, its length and
+    // every loop bound are wave-uniform (scalar loads, no exec-masked loops)
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int r = blockIdx.x * kCurvRowsPerWG + w, f = blockIdx.y;
     if (r >= n_rows) return;                                   // wave-uniform
     const int32_t* ro = ring_off + (int64_t)f * (n_rows + 1);
     const int rs = ro[r], n_r = ro[r + 1] - rs;
     const int64_t base = frame_off[f] + rs;
     const bool in_rows = (r >= row_start) && (r < n_rows - row_end);
-    if (!in_rows) {
-        if (curv)
+    if (!in_rows || n_r == 0) {
+        if (kCurv)
             for (int j = lane; j < n_r; j += 64) curv[base + j] = 0.0f;
         if (lane == 0) sel_cnt[(int64_t)f * n_rows + r] = 0;
         return;
@@ -236,25 +256,18 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
     float* wx = win[w][0];
     float* wy = win[w][1];
     float* wz = win[w][2];
+    int32_t* sl = slist[w];
     const float4* src = rxyzi + base;
     const int ng = (n_r + 63) >> 6;
-    auto load = [&](int g) {                                   // clamped: always a valid point
-        const int p = min(64 * g + lane, max(n_r - 1, 0));
-        return src[p];
-    };
-    float4 cur = n_r > 0 ? load(0) : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 nxt = n_r > 0 ? load(1 < ng ? 1 : 0) : cur;
-    float4 nx2 = n_r > 0 ? load(2 < ng ? 2 : 0) : cur;
-    int cnt = 0, jstart = 0;                                   // wave-uniform
-    for (int g = 0; g <= ng; ++g) {
-        if (g < ng) {                                          // group g into the window
-            const int p = 64 * g + lane;
-            wx[p % 192] = cur.x; wy[p % 192] = cur.y; wz[p % 192] = cur.z;
-            cur = nxt;
-            nxt = nx2;
-            nx2 = load(g + 3 < ng ? g + 3 : ng - 1);
+    auto load = [&](int g) { return src[min(64 * g + lane, n_r - 1)]; };   // clamped
+    int cnt = 0, nl = 0, jstart = 0;                           // wave-uniform
+    auto group = [&](float4& buf, int g) {
+        {                                                      // group g into the window
+            const int p = (64 * g + lane) % 192;
+            wx[p] = buf.x; wy[p] = buf.y; wz[p] = buf.z;
+            buf = load(g + 3);
         }
-        if (g == 0) continue;
+        if (g == 0 || g > ng) return;                          // uniform
         const int j = 64 * (g - 1) + lane;                     // group g-1: its stencil is complete
         float v = 0.0f;
         if (j >= 5 && j < n_r - 5) {
@@ -262,7 +275,7 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
             v = dx * dx + dy * dy;
             v = v + dz * dz;
         }
-        if (curv && j < n_r) curv[base + j] = v;
+        if (kCurv) curv[base + min(j, n_r - 1)] = v;   // lanes past the row write its last value, 0
         uint64_t m = __ballot(j < n_r && v < plane_min);
         const int j0 = 64 * (g - 1);
         while (true) {
@@ -271,11 +284,33 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
             if (lo > 0) m &= ~((1ull << lo) - 1ull);
             if (!m) break;
             const int l = __ffsll((unsigned long long)m) - 1;
-            const int jj = j0 + l;
-            if (lane == 0) sel[base + cnt] = jj;
-            cnt++;
+            const int jj = __builtin_amdgcn_readfirstlane(j0 + l);
+            if (lane == 0) sl[nl] = jj;
+            nl++;
             jstart = jj + plane_span;
         }
+        nl = __builtin_amdgcn_readfirstlane(nl);
+    };
+    // a trip's selections (<= 192 / plane_span + 1 <= 128) leave with two unconditional stores;
+    // lanes without one write the row's last slot, which no selection list reaches (at most
+    // ceil(n_r / 2) entries for plane_span >= 2)
+    const int64_t spare = base + n_r - 1;
+    // prologue loads in buffer order (the loop's waits count on b0 being the oldest)
+    float4 b0 = load(0);
+    asm volatile("" ::: "memory");
+    float4 b1 = load(1);
+    asm volatile("" ::: "memory");
+    float4 b2 = load(2);
+    for (int g = 0; g <= ng; g += 3) {
+        group(b0, g);
+        group(b1, g + 1);
+        group(b2, g + 2);
+        __builtin_amdgcn_wave_barrier();
+        sel[lane < nl ? base + cnt + lane : spare] = sl[lane];
+        sel[lane + 64 < nl ? base + cnt + 64 + lane : spare] = sl[64 + lane];
+        __builtin_amdgcn_wave_barrier();
+        cnt += nl;
+        nl = 0;
     }
     if (lane == 0) sel_cnt[(int64_t)f * n_rows + r] = cnt;
 }
@@ -315,10 +350,15 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
         hipLaunchKernelGGL(k_bin_scatter, dim3(n_chunks, n_frames), dim3(256), 0, s, pts, stride,
                            frame_off, R, n_chunks, rid, hist, ring_off, ring_xyzi);
     }
-    hipLaunchKernelGGL(k_curv_select, dim3((R + kCurvRowsPerWG - 1) / kCurvRowsPerWG, n_frames),
-                       dim3(64 * kCurvRowsPerWG), 0, s, frame_off, R,
-                       cfg.row_start, cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off,
-                       ring_xyzi, curv, sel, sel_cnt);
+    const dim3 cgrid((R + kCurvRowsPerWG - 1) / kCurvRowsPerWG, n_frames);
+    if (curv)
+        hipLaunchKernelGGL(k_curv_select<true>, cgrid, dim3(64 * kCurvRowsPerWG), 0, s, frame_off, R,
+                           cfg.row_start, cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off,
+                           ring_xyzi, curv, sel, sel_cnt);
+    else
+        hipLaunchKernelGGL(k_curv_select<false>, cgrid, dim3(64 * kCurvRowsPerWG), 0, s, frame_off, R,
+                           cfg.row_start, cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off,
+                           ring_xyzi, curv, sel, sel_cnt);
     hipLaunchKernelGGL(k_compact, dim3(R, n_frames), dim3(256), 0, s, frame_off, R, ring_off,
                        ring_xyzi, sel, sel_cnt, plane, plane_count);
     return hipGetLastError();

@@ -57,6 +57,7 @@ constexpr int kLloydFullPasses = SSF_LLOYD_FULL_PASSES;   // full Lloyd passes b
 #define SSF_LLOYD_REC_DEEP 8
 #endif
 constexpr int kLloydRecDeep = SSF_LLOYD_REC_DEEP;         // 16-byte record loads in flight per lane
+constexpr int kLQ = SSF_LLOYD_REC_DEEP * 128;   // a record trip: D loads of two records per lane
 constexpr int kLloydMax = 300;               // sklearn KMeans max_iter (pass index fits 9 bits)
 
 // packed upper-triangular index of a 6x6 matrix (row i <= col j)
@@ -490,6 +491,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     __shared__ int ired[kNW];
     __shared__ unsigned long long cand_lds[2];
     __shared__ double bsum[kKppBlocks];   // k-means++ per-64-point-block distance totals
+    __shared__ uint32_t lq[kNW * kLQ];     // Lloyd skip passes: per-wave relabel entries of a trip
     const int f = blockIdx.x, tid = threadIdx.x;
     const int64_t fb = frame_off[f], n = frame_off[f + 1] - fb;
     const float* P = pts + 3 * fb;
@@ -764,11 +766,12 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     if (tid == 0) { S.strict = 0; S.done = 0; S.lfull = 1; S.dg_cyc = S.dg_n = S.dg_lab = S.dg_wfull = S.dg_full1 = 0.0; }
     // records at an even offset (16-byte aligned pairs) with at least one spare slot (index n)
     // after each frame: frame f at ((fb + 2 f + 1) & ~1); the buffer holds total + 2 F + 2
-    // records, then total 4-byte queue entries
+    // records, then total + 64 F 4-byte queue entries
     uint2* __restrict__ LR = lloyd_rec + ((fb + 2 * (int64_t)f + 1) & ~(int64_t)1);
-    // the relabel queues (4 bytes per point) follow the records
+    // the relabel queues follow the records: frame f's at fb + 64 f, n entries + 64 spare slots
     uint32_t* __restrict__ LQ =
-        reinterpret_cast<uint32_t*>(lloyd_rec + frame_off[gridDim.x] + 2 * (int64_t)gridDim.x + 2) + fb;
+        reinterpret_cast<uint32_t*>(lloyd_rec + frame_off[gridDim.x] + 2 * (int64_t)gridDim.x + 2) + fb +
+        64 * (int64_t)f;
     for (int it = 0; it < kLloydMax; ++it) {
         if (tid == 0) {
             double* h = S.lhist + 9 * it;
@@ -862,9 +865,11 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             const int64_t seg = ((n + kNW - 1) / kNW + 127) / 128 * 128;
             const int64_t ws = (int64_t)w * seg, we = ws + seg < n ? ws + seg : n;
             uint32_t* __restrict__ WQ = LQ + ws;        // capacity seg >= the wave's points
+            const int64_t qspare = n - ws;               // LQ[n, n + 64): spare slots
             const uint4* __restrict__ LR4 = reinterpret_cast<const uint4*>(LR);
             const int64_t plast = (n - 1) >> 1;
-            int qc = 0;
+            uint32_t* Q = lq + w * kLQ;                 // this trip's entries (<= D * 128)
+            int qc = 0, nl = 0;                         // wave-uniform
             constexpr int D = kLloydRecDeep;
             uint4 buf[D];
 #pragma unroll
@@ -874,7 +879,6 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
                 for (int d = 0; d < D; ++d) {
                     const int64_t b = base + d * 128;
                     const uint4 q = buf[d];
-                    buf[d] = LR4[min(((b + D * 128) >> 1) + lane, plast)];
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const uint32_t gx = h ? q.z : q.x, gy = h ? q.w : q.y;
@@ -888,10 +892,24 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
                         const bool nd = (i < we) & !skip;
 #endif
                         const uint64_t m = __ballot(nd);
-                        if (nd) WQ[qc + __popcll(m & lanemask_lt())] = (uint32_t)i | (gy & 0x80000000u);
-                        qc += __popcll(m);
+                        if (nd) Q[nl + __popcll(m & lanemask_lt())] = (uint32_t)i | (gy & 0x80000000u);
+                        nl += __popcll(m);
                     }
+                    // reloaded only after q is consumed: the load can reuse q's registers, so
+                    // the loop-carried buffers need no copies (a copy waits for its load)
+                    buf[d] = LR4[min(((b + D * 128) >> 1) + lane, plast)];
                 }
+                // the trip's queue entries leave LDS: two unconditional 64-entry stores (lanes
+                // without an entry write the frame's spare slots), more only past 128 entries
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    WQ[h * 64 + lane < nl ? qc + h * 64 + lane : qspare + lane] = Q[h * 64 + lane];
+                for (int k = 128; k < nl; k += 64)
+                    if (k + lane < nl) WQ[qc + k + lane] = Q[k + lane];
+                __builtin_amdgcn_wave_barrier();
+                qc += nl;
+                nl = 0;
             }
             __threadfence_block();   // the wave's queue stores are visible to its loads below
             for (int j0 = 0; j0 < qc; j0 += 512) {

@@ -19,9 +19,7 @@
 namespace ssf {
 
 // frameFeature.cpp:57-72 (see oracle/ssf_oracle.c orc_ring_id for the precision choices).
-SSF_DEV int ring_id(float x, float y, float z, int n_rows) {
-    float r2 = x * x + y * y;
-    float ratio = z / sqrtf(r2);
+SSF_DEV int ring_id_exact(float ratio, int n_rows) {
     float angle = (float)(atan((double)ratio) * 180.0 / 3.14159265358979323846);
     int id = -1;
     if (n_rows == 16) {
@@ -32,6 +30,32 @@ SSF_DEV int ring_id(float x, float y, float z, int n_rows) {
         else
             id = n_rows / 2 + (int)((-8.83 - (double)angle) * 2.0 + 0.5);
     }
+    return (id > -1 && id < n_rows) ? id : -1;
+}
+
+// The same id with a float atan (the f64 atan made k_bin_count f64-issue-bound).  The float
+// angle is within ~3e-5 deg of the f64 expression's; whenever it lies within 1e-3 deg of a bin
+// edge (or of the -8.83 switch, or is not finite) the exact f64 path decides, so the id is the
+// exact path's for every input.
+SSF_DEV int ring_id(float x, float y, float z, int n_rows) {
+    float r2 = x * x + y * y;
+    float ratio = z / sqrtf(r2);
+    const float af = atanf(ratio) * 57.29577951308232f;
+    double v;
+    float margin;
+    if (n_rows == 16) {
+        v = (double)((af + 15.0f) / 2.0f) + 0.5;
+        margin = 0.5e-3f;
+    } else {
+        const bool upper = (double)af >= -8.83;
+        v = upper ? (2.0 - (double)af) * 3.0 + 0.5 : (-8.83 - (double)af) * 2.0 + 0.5;
+        margin = upper ? 3e-3f : 2e-3f;
+        if (!(fabsf(af + 8.83f) > 1e-3f)) margin = -1.0f;   // near the switch (or NaN): exact
+    }
+    const float edge = (float)fabs(v - rint(v));
+    if (!(edge > margin)) return ring_id_exact(ratio, n_rows);
+    int id = (n_rows == 16 || (double)af >= -8.83) ? (int)v : n_rows / 2 + (int)v;
+    if (n_rows != 16 && n_rows != 64) id = -1;
     return (id > -1 && id < n_rows) ? id : -1;
 }
 
@@ -118,12 +142,16 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
     __shared__ int wrun[4][kMaxRows];
     __shared__ int roff[kMaxRows + 1];            // chunk-local row offsets
     __shared__ int64_t rbase[kMaxRows];           // global index of row r's first chunk point - roff[r]
+    __shared__ double rfrac[kMaxRows];            // id / 100.0, the f64 division done once per row
     const int f = blockIdx.y, c = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
     const int64_t fb = frame_off[f], e = frame_off[f + 1];
     const int64_t s = fb + (int64_t)c * kBinChunk;
     if (s >= e) return;  // uniform
     const int64_t t = min(e, s + (int64_t)kBinChunk);
-    if (tid < kMaxRows) wrun[0][tid] = wrun[1][tid] = wrun[2][tid] = wrun[3][tid] = 0;
+    if (tid < kMaxRows) {
+        wrun[0][tid] = wrun[1][tid] = wrun[2][tid] = wrun[3][tid] = 0;
+        rfrac[tid] = (double)tid / 100.0;
+    }
     __syncthreads();
     // all loads first (ids, then points at clamped indices, unconditionally): one wait for the
     // whole 16-point batch instead of one load latency per step
@@ -191,7 +219,7 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
             const int loc = roff[id] + in_row;
             float4 v;
             v.x = px[st]; v.y = py[st]; v.z = pz[st];
-            v.w = (float)((double)(cb[id] + in_row) + (double)id / 100.0);   // frameFeature.cpp:77
+            v.w = (float)((double)(cb[id] + in_row) + rfrac[id]);   // frameFeature.cpp:77
             tile[loc] = v;
             row_of[loc] = (uint8_t)id;
         }

@@ -94,3 +94,36 @@ def test_full_size_frame(oracle, dev):
     c = frame(4, 7, n_az=1875)[0]
     out, h_off = _run(fe, [c, c], dev)
     _check_frame(oracle, fe, out, h_off, 1, c, 64)
+
+
+@pytest.mark.parametrize("n_rows", [16, 64])
+def test_ring_ids_near_bin_edges(oracle, dev, n_rows):
+    """Elevations on and within 1e-6..1e-2 deg of every bin edge (and the -8.83 switch), plus a
+    uniform spread: the float-atan fast path of the ring id must fall back to the f64
+    expression wherever the two could disagree (src/frameFeature.cpp:57-72), so the binned
+    cloud is bit-identical to the oracle's."""
+    import ssf
+    O = oracle
+    if n_rows == 64:
+        edges = [2.0 - (k - 0.5) / 3.0 for k in range(-2, 35)] + [-8.83] + \
+                [-8.83 - (m - 0.5) / 2.0 for m in range(0, 34)]
+    else:
+        edges = [-15.0 + 2.0 * k - 1.0 for k in range(0, 18)]
+    rng = np.random.default_rng(7)
+    el = []
+    for e in edges:
+        for d in (0.0, 1e-6, -1e-6, 1e-5, -1e-5, 1e-4, -1e-4, 5e-4, -5e-4, 2e-3, -2e-3, 1e-2, -1e-2):
+            el.append(e + d)
+    el = np.array(el + list(rng.uniform(-32.0, 12.0, 20000)), np.float64)
+    az = rng.uniform(0, 2 * np.pi, el.size)
+    rng_m = rng.uniform(2.0, 90.0, el.size)
+    e = np.radians(el)
+    pts = np.stack([rng_m * np.cos(e) * np.cos(az), rng_m * np.cos(e) * np.sin(az),
+                    rng_m * np.sin(e)], 1).astype(np.float32)
+    fe = ssf.Frontend(n_rows, device=dev.index or 0)
+    out, h_off = _run(fe, [pts], dev)
+    pb, ring, roff, curv = out
+    rx, off_ref, _, _ = O.bin_rings(pts, n_rows)
+    assert np.array_equal(roff[0].cpu().numpy().astype(np.int64), off_ref)
+    kept = int(off_ref[-1])
+    assert np.array_equal(ring[:kept].cpu().numpy(), rx), "ring-ordered cloud differs near bin edges"

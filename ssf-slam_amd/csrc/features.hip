@@ -230,8 +230,8 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
 }
 
 // One WAVE per (frame, row), four rows per work-group, no block barrier.  The wave streams its
-// row in 64-point groups (one coalesced float4 load per lane) into a 192-point circular LDS
-// window (3 groups; point p at p % 192); group g-1's 11-tap stencil (:84-107, evaluated left to
+// row in 64-point groups (one coalesced float4 load per lane) into a 256-point circular LDS
+// window (point p at p & 255, see stencil11w); group g-1's 11-tap stencil (:84-107, evaluated left to
 // right in float exactly as the reference) is computed once group g has landed, and the greedy
 // spacing rule (:110-123) runs on the same wave with a 64-bit ballot of candidates per group
 // (jstart is wave-uniform).  Three register buffers with static roles (one loop trip = three
@@ -239,19 +239,29 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
 // moves, or a load or store under a branch, makes the compiler wait for every load at each
 // group.  The selected indices collect in LDS and leave once per trip.
 constexpr int kCurvRowsPerWG = 4;
+#ifndef SSF_CURV_DEPTH
+#define SSF_CURV_DEPTH 3
+#endif
+constexpr int kCurvDepth = SSF_CURV_DEPTH;   // 64-point groups in flight per wave (one trip)
 
-SSF_DEV float stencil11w(const float* a, int j) {   // a is the 192-point window, j the centre
-    auto at = [&](int d) { return a[(j + d) % 192]; };
-    float s = at(-5) + at(-4);
-    s = s + at(-3);
-    s = s + at(-2);
-    s = s + at(-1);
-    s = s - 10.0f * at(0);
-    s = s + at(1);
-    s = s + at(2);
-    s = s + at(3);
-    s = s + at(4);
-    s = s + at(5);
+// The window holds 256 points (4 groups; point p at p & 255) plus a mirror of its first 16 at
+// [256, 272), so the 11 taps of centre j are the contiguous a[b .. b + 10], b = (j - 5) & 255:
+// one base address, immediate LDS offsets.
+constexpr int kWin = 256;
+constexpr int kWinPad = kWin + 16;
+
+SSF_DEV float stencil11w(const float* a, int j) {
+    const float* t = a + ((j - 5) & (kWin - 1));
+    float s = t[0] + t[1];
+    s = s + t[2];
+    s = s + t[3];
+    s = s + t[4];
+    s = s - 10.0f * t[5];
+    s = s + t[6];
+    s = s + t[7];
+    s = s + t[8];
+    s = s + t[9];
+    s = s + t[10];
     return s;
 }
 
@@ -264,8 +274,8 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
                                                      float* __restrict__ curv,
                                                      int32_t* __restrict__ sel,
                                                      int32_t* __restrict__ sel_cnt) {
-    __shared__ float win[kCurvRowsPerWG][3][192];
-    __shared__ int32_t slist[kCurvRowsPerWG][128];
+    __shared__ float win[kCurvRowsPerWG][3][kWinPad];
+    __shared__ int32_t slist[kCurvRowsPerWG][64 * (kCurvDepth / 2 + 1)];
     // the wave index through readfirstlane: the compiler then knows the row, its length and
     // every loop bound are wave-uniform (scalar loads, no exec-masked loops)
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -291,9 +301,10 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
     int cnt = 0, nl = 0, jstart = 0;                           // wave-uniform
     auto group = [&](float4& buf, int g) {
         {                                                      // group g into the window
-            const int p = (64 * g + lane) % 192;
+            const int p = (64 * g + lane) & (kWin - 1);
             wx[p] = buf.x; wy[p] = buf.y; wz[p] = buf.z;
-            buf = load(g + 3);
+            if (p < kWinPad - kWin) { wx[p + kWin] = buf.x; wy[p + kWin] = buf.y; wz[p + kWin] = buf.z; }
+            buf = load(g + kCurvDepth);
         }
         if (g == 0 || g > ng) return;                          // uniform
         const int j = 64 * (g - 1) + lane;                     // group g-1: its stencil is complete
@@ -319,23 +330,24 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
         }
         nl = __builtin_amdgcn_readfirstlane(nl);
     };
-    // a trip's selections (<= 192 / plane_span + 1 <= 128) leave with two unconditional stores;
+    // a trip's selections (<= 64 kCurvDepth / plane_span + 1 <= 256) leave with unconditional stores;
     // lanes without one write the row's last slot, which no selection list reaches (at most
     // ceil(n_r / 2) entries for plane_span >= 2)
     const int64_t spare = base + n_r - 1;
-    // prologue loads in buffer order (the loop's waits count on b0 being the oldest)
-    float4 b0 = load(0);
-    asm volatile("" ::: "memory");
-    float4 b1 = load(1);
-    asm volatile("" ::: "memory");
-    float4 b2 = load(2);
-    for (int g = 0; g <= ng; g += 3) {
-        group(b0, g);
-        group(b1, g + 1);
-        group(b2, g + 2);
+    // prologue loads in buffer order (the loop's waits count on b[0] being the oldest)
+    float4 b[kCurvDepth];
+#pragma unroll
+    for (int k = 0; k < kCurvDepth; ++k) {
+        b[k] = load(k);
+        asm volatile("" ::: "memory");
+    }
+    for (int g = 0; g <= ng; g += kCurvDepth) {
+#pragma unroll
+        for (int k = 0; k < kCurvDepth; ++k) group(b[k], g + k);
         __builtin_amdgcn_wave_barrier();
-        sel[lane < nl ? base + cnt + lane : spare] = sl[lane];
-        sel[lane + 64 < nl ? base + cnt + 64 + lane : spare] = sl[64 + lane];
+#pragma unroll
+        for (int h = 0; h < kCurvDepth / 2 + 1; ++h)   // >= 64 kCurvDepth / plane_span + 1 entries
+            sel[lane + 64 * h < nl ? base + cnt + 64 * h + lane : spare] = sl[64 * h + lane];
         __builtin_amdgcn_wave_barrier();
         cnt += nl;
         nl = 0;

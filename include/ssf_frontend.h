@@ -195,6 +195,49 @@ int32_t ssf_rng_seed(ssf_ctx* ctx, uint32_t seed);
 int32_t ssf_accumulate_sequence(ssf_ctx* ctx, void* stream, int32_t n, const double* d_rel,
                                 const double* h_start, double* d_abs);
 
+/* ---------------------------------------------------------------------------------------
+ * mapOptmization loop closure.
+ *
+ * ssf_voxel_grid_batch replaces pcl::VoxelGrid<PointXYZI>::filter as downSizeFilterICP
+ * (leaf 0.1, src/mapOptmization.cpp:214-217, 461) and downSizeFilterMap (leaf 0.4, :406-409,
+ * 462) use it: per cloud, the centroid (x, y, z, intensity) of every occupied cube, in voxel
+ * index order.  d_xyzi: float4 points of n_clouds clouds at d_off / h_off (int64, n_clouds + 1);
+ * d_out: float4 at the SAME offsets (a cloud's output never exceeds its input);
+ * d_out_count: int32 per cloud.  Asynchronous on stream.
+ */
+int32_t ssf_voxel_grid_batch(ssf_ctx* ctx, void* stream, int32_t n_clouds, const float* d_xyzi,
+                             const int64_t* d_off, const int64_t* h_off, float leaf,
+                             float* d_out, int32_t* d_out_count);
+
+/* ssf_icp_batch replaces pcl::IterativeClosestPoint<PointXYZI, PointXYZI>::align +
+ * hasConverged + getFitnessScore + getFinalTransformation as addLoopFactor() uses them
+ * (src/mapOptmization.cpp:224-238): n_prob independent (source, target) problems, float4
+ * clouds at int64 offsets (device + host copies).  h_guess: n_prob row-major 4x4 float initial
+ * transforms (nullable = identity).  h_out (host, n_prob * SSF_ICP_OUT_STRIDE doubles): the
+ * final transformation (16, row-major, float values), fitness score, converged, iterations,
+ * convergence state (SSF_ICP_*), correspondences of the last iteration.  Synchronous: the
+ * iteration loop runs on device; the host only polls the per-problem done flags. */
+typedef struct {
+    int32_t max_iter;       /* setMaximumIterations (100)                              */
+    float max_corr_dist;    /* setMaxCorrespondenceDistance (50)                       */
+    double trans_eps;       /* setTransformationEpsilon (1e-6)                         */
+    double fit_eps;         /* setEuclideanFitnessEpsilon (1e-6)                       */
+} ssf_icp_params;
+#define SSF_ICP_OUT_STRIDE 24
+enum {
+    SSF_ICP_OUT_T = 0, SSF_ICP_OUT_FITNESS = 16, SSF_ICP_OUT_CONVERGED = 17,
+    SSF_ICP_OUT_ITERATIONS = 18, SSF_ICP_OUT_STATE = 19, SSF_ICP_OUT_NCORR = 20
+};
+enum {  /* pcl::registration::DefaultConvergenceCriteria::ConvergenceState */
+    SSF_ICP_NOT_CONVERGED = 0, SSF_ICP_ITERATIONS = 1, SSF_ICP_TRANSFORM = 2, SSF_ICP_ABS_MSE = 3,
+    SSF_ICP_REL_MSE = 4, SSF_ICP_NO_CORRESPONDENCES = 5
+};
+int32_t ssf_icp_params_default(ssf_icp_params* out);
+int32_t ssf_icp_batch(ssf_ctx* ctx, void* stream, int32_t n_prob, const float* d_src,
+                      const int64_t* d_src_off, const int64_t* h_src_off, const float* d_tgt,
+                      const int64_t* d_tgt_off, const int64_t* h_tgt_off,
+                      const ssf_icp_params* params, const float* h_guess, double* h_out);
+
 #ifdef __cplusplus
 }
 #endif

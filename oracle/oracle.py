@@ -39,6 +39,20 @@ class Profile(C.Structure):
                 ("row_start", C.c_int32), ("row_end", C.c_int32), ("plane_max", C.c_float)]
 
 
+class IcpParams(C.Structure):
+    _fields_ = [("max_iter", C.c_int32), ("max_corr_dist", C.c_float), ("trans_eps", C.c_double),
+                ("fit_eps", C.c_double)]
+
+
+class IcpResult(C.Structure):
+    _fields_ = [("T", C.c_float * 16), ("fitness", C.c_double), ("converged", C.c_int32),
+                ("iterations", C.c_int32), ("state", C.c_int32), ("n_corr", C.c_int32)]
+
+
+ICP_STATES = {0: "not_converged", 1: "iterations", 2: "transform", 3: "abs_mse", 4: "rel_mse",
+              5: "no_correspondences"}
+
+
 def build():
     """Compile the oracle with its committed Makefile (gcc)."""
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
@@ -80,6 +94,11 @@ def lib():
     L.orc_quat_from_R.argtypes = [f64p, f64p]
     L.orc_quat_from_R.restype = C.c_int32
     L.orc_svd3.argtypes = [f64p, f64p, f64p, f64p]
+    L.orc_voxel_grid.argtypes = [f32p, C.c_int64, C.c_float, f32p]
+    L.orc_voxel_grid.restype = C.c_int64
+    L.orc_icp.argtypes = [f32p, C.c_int64, f32p, C.c_int64, C.POINTER(IcpParams), f32p,
+                          C.POINTER(IcpResult)]
+    L.orc_icp.restype = C.c_int32
     _lib = L
     return L
 
@@ -292,3 +311,26 @@ def mask_and_pose(points, flow, draws):
     qrc, q = quat_from_R(R) if rc == 0 else (rc, np.zeros(4))
     return dict(labels=lab, bg_mask=bg, R=R, t=t, q_xyzw=q, info=info, means=means,
                 rc=rc if rc != 0 else qrc)
+
+
+# ---- mapOptmization loop closure: oracle/loop_oracle.c ----
+def voxel_grid(xyzi, leaf):
+    """pcl::VoxelGrid<PointXYZI> restated (mapOptmization.cpp:214-217): n x 4 -> m x 4."""
+    x = np.ascontiguousarray(xyzi, np.float32).reshape(-1, 4)
+    out = np.zeros_like(x)
+    m = lib().orc_voxel_grid(x.reshape(-1), x.shape[0], float(leaf), out.reshape(-1))
+    return out[:m].copy()
+
+
+def icp(src, tgt, max_corr_dist=50.0, max_iter=100, trans_eps=1e-6, fit_eps=1e-6, guess=None):
+    """pcl::IterativeClosestPoint<PointXYZI, PointXYZI> restated (mapOptmization.cpp:224-236)."""
+    s = np.ascontiguousarray(src, np.float32).reshape(-1, 4)
+    t = np.ascontiguousarray(tgt, np.float32).reshape(-1, 4)
+    g = np.eye(4, dtype=np.float32) if guess is None else np.ascontiguousarray(guess, np.float32)
+    p = IcpParams(int(max_iter), float(max_corr_dist), float(trans_eps), float(fit_eps))
+    r = IcpResult()
+    lib().orc_icp(s.reshape(-1), s.shape[0], t.reshape(-1), t.shape[0], C.byref(p), g.reshape(-1),
+                  C.byref(r))
+    return dict(T=np.array(r.T, np.float32).reshape(4, 4), fitness=r.fitness,
+                converged=bool(r.converged), iterations=r.iterations,
+                state=ICP_STATES[r.state], n_corr=r.n_corr)

@@ -101,6 +101,18 @@ int32_t orc_kabsch(const double* src, const double* dst, int64_t n, const uint8_
 int32_t orc_quat_from_R(const double R[9], double q[4]);
 void orc_svd3(const double A[9], double U[9], double S[3], double Vt[9]);
 
+/* ---- mapOptmization loop closure, oracle/loop_oracle.c ---- */
+/* pcl::VoxelGrid<PointXYZI> (leaf cube), xyzi n x 4 -> centroids m x 4 in voxel order; returns m */
+int64_t orc_voxel_grid(const float* xyzi, int64_t n, float leaf, float* out);
+enum { ORC_ICP_NOT_CONVERGED = 0, ORC_ICP_ITERATIONS = 1, ORC_ICP_TRANSFORM = 2, ORC_ICP_ABS_MSE = 3,
+       ORC_ICP_REL_MSE = 4, ORC_ICP_NO_CORRESPONDENCES = 5 };
+typedef struct { int32_t max_iter; float max_corr_dist; double trans_eps; double fit_eps; } orc_icp_params;
+typedef struct { float T[16]; double fitness; int32_t converged; int32_t iterations; int32_t state;
+                 int32_t n_corr; } orc_icp_result;
+/* pcl::IterativeClosestPoint<PointXYZI, PointXYZI>: T row-major 4x4 float (final transformation) */
+int32_t orc_icp(const float* src, int64_t ns, const float* tgt, int64_t nt, const orc_icp_params* p,
+                const float guess[16], orc_icp_result* r);
+
 #ifdef __cplusplus
 }
 #endif

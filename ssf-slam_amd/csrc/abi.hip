@@ -39,6 +39,9 @@ struct ssf_ctx {
     DrawSlot dslot[kDrawSlots];
     int dnext = 0;
     DevBuf start1;
+    // loop closure (loop.hip): voxel-grid sort scratch; ICP transformed source, 1-NN keys,
+    // per-problem state and guesses
+    DevBuf vg, icp_cur, icp_key, icp_st, icp_guess;
     // host RandomState (MT19937, numpy legacy seeding)
     uint32_t mt[624];
     int mt_pos = 625;
@@ -161,7 +164,8 @@ void ssf_destroy(ssf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     DevBuf* bufs[] = {&c->rid, &c->hist, &c->ring_off, &c->ring_xyzi, &c->sel, &c->sel_cnt,
-                      &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->start1};
+                      &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->start1, &c->vg,
+                      &c->icp_cur, &c->icp_key, &c->icp_st, &c->icp_guess};
     for (auto& ds : c->dslot) {
         if (ds.used) { (void)hipEventSynchronize(ds.used); (void)hipEventDestroy(ds.used); }
         if (ds.copied) { (void)hipEventSynchronize(ds.copied); (void)hipEventDestroy(ds.copied); }
@@ -380,6 +384,109 @@ int32_t ssf_accumulate_sequence(ssf_ctx* c, void* stream, int32_t n, const doubl
     hipError_t e = ssf::launch_accumulate(s, n, d_rel, d_start, d_abs);
     if (e != hipSuccess) return hip_fail(c, e, "accumulate launch");
     if (h_start) SSF_TRY_HIP(c, hipStreamSynchronize(s), "sync start");
+    return SSF_OK;
+}
+
+int32_t ssf_voxel_grid_batch(ssf_ctx* c, void* stream, int32_t n_clouds, const float* d_xyzi,
+                             const int64_t* d_off, const int64_t* h_off, float leaf,
+                             float* d_out, int32_t* d_out_count) {
+    if (!c) return SSF_E_ARG;
+    if (n_clouds < 0 || !(leaf > 0.0f) ||
+        (n_clouds > 0 && (!d_xyzi || !d_off || !h_off || !d_out || !d_out_count)))
+        return fail(c, SSF_E_ARG, "voxel_grid_batch: bad arguments");
+    if (n_clouds == 0) return SSF_OK;
+    int64_t max_pts = 0;
+    for (int k = 0; k < n_clouds; ++k) {
+        const int64_t m = h_off[k + 1] - h_off[k];
+        if (m < 0) return fail(c, SSF_E_ARG, "voxel_grid_batch: offsets not monotone");
+        if (m > (int64_t)INT32_MAX) return fail(c, SSF_E_ARG, "voxel_grid_batch: cloud too large");
+        max_pts = std::max(max_pts, m);
+    }
+    if (h_off[0] != 0) return fail(c, SSF_E_ARG, "voxel_grid_batch: offsets must start at 0");
+    const int64_t n = h_off[n_clouds];
+    if (n > (int64_t)INT32_MAX) return fail(c, SSF_E_ARG, "voxel_grid_batch: too many points");
+    hipStream_t s = (hipStream_t)stream;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    SSF_TRY_HIP(c, c->vg.ensure(ssf::vg_scratch_bytes(n_clouds, n)), "alloc voxel scratch");
+    hipError_t e = ssf::launch_voxel_grid(s, n_clouds, reinterpret_cast<const float4*>(d_xyzi), d_off, n,
+                                          max_pts, leaf, c->vg.p, reinterpret_cast<float4*>(d_out),
+                                          d_out_count);
+    if (e != hipSuccess) return hip_fail(c, e, "voxel_grid launch");
+    return SSF_OK;
+}
+
+int32_t ssf_icp_params_default(ssf_icp_params* out) {
+    if (!out) return SSF_E_ARG;
+    out->max_iter = 100;            // mapOptmization.cpp:225-228
+    out->max_corr_dist = 50.0f;
+    out->trans_eps = 1e-6;
+    out->fit_eps = 1e-6;
+    return SSF_OK;
+}
+
+int32_t ssf_icp_batch(ssf_ctx* c, void* stream, int32_t n_prob, const float* d_src,
+                      const int64_t* d_src_off, const int64_t* h_src_off, const float* d_tgt,
+                      const int64_t* d_tgt_off, const int64_t* h_tgt_off,
+                      const ssf_icp_params* prm, const float* h_guess, double* h_out) {
+    if (!c) return SSF_E_ARG;
+    if (n_prob < 0 || !prm || prm->max_iter < 0 || !(prm->max_corr_dist >= 0.0f) ||
+        (n_prob > 0 && (!d_src || !d_src_off || !h_src_off || !d_tgt || !d_tgt_off || !h_tgt_off || !h_out)))
+        return fail(c, SSF_E_ARG, "icp_batch: bad arguments");
+    if (n_prob == 0) return SSF_OK;
+    int64_t max_ns = 0, max_nt = 0;
+    for (int k = 0; k < n_prob; ++k) {
+        const int64_t a = h_src_off[k + 1] - h_src_off[k], b = h_tgt_off[k + 1] - h_tgt_off[k];
+        if (a < 0 || b < 0) return fail(c, SSF_E_ARG, "icp_batch: offsets not monotone");
+        if (b > (int64_t)INT32_MAX) return fail(c, SSF_E_ARG, "icp_batch: target too large");
+        max_ns = std::max(max_ns, a); max_nt = std::max(max_nt, b);
+    }
+    const int64_t s0 = h_src_off[0], total_ns = h_src_off[n_prob] - s0;
+    hipStream_t s = (hipStream_t)stream;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    SSF_TRY_HIP(c, c->icp_cur.ensure(sizeof(float4) * (size_t)std::max<int64_t>(h_src_off[n_prob], 1)), "alloc icp");
+    SSF_TRY_HIP(c, c->icp_key.ensure(sizeof(unsigned long long) * (size_t)std::max<int64_t>(h_src_off[n_prob], 1)), "alloc icp");
+    SSF_TRY_HIP(c, c->icp_st.ensure(sizeof(ssf::IcpState) * (size_t)n_prob), "alloc icp");
+    SSF_TRY_HIP(c, c->icp_guess.ensure(sizeof(float) * 16 * (size_t)n_prob), "alloc icp");
+    std::vector<float> g(16 * (size_t)n_prob, 0.0f);
+    for (int k = 0; k < n_prob; ++k)
+        for (int i = 0; i < 16; ++i) g[16 * k + i] = h_guess ? h_guess[16 * k + i] : (i % 5 == 0 ? 1.0f : 0.0f);
+    SSF_TRY_HIP(c, hipMemcpyAsync(c->icp_guess.p, g.data(), sizeof(float) * g.size(), hipMemcpyHostToDevice, s), "H2D guess");
+    const float4* src = reinterpret_cast<const float4*>(d_src);
+    const float4* tgt = reinterpret_cast<const float4*>(d_tgt);
+    float4* cur = c->icp_cur.as<float4>();
+    unsigned long long* key = c->icp_key.as<unsigned long long>();
+    ssf::IcpState* st = c->icp_st.as<ssf::IcpState>();
+    hipError_t e = ssf::launch_icp_init(s, n_prob, src, d_src_off, max_ns, c->icp_guess.as<float>(), cur, st, key);
+    if (e != hipSuccess) return hip_fail(c, e, "icp init");
+    // the iteration loop runs on device: every launch is skipped by problems already done; the
+    // host polls the done flags every 8 iterations and stops once all problems have converged
+    std::vector<ssf::IcpState> hs((size_t)n_prob);
+    for (int it = 0; it < prm->max_iter; ++it) {
+        e = ssf::launch_icp_iteration(s, n_prob, cur, d_src_off, max_ns, tgt, d_tgt_off, max_nt, *prm, st, key);
+        if (e != hipSuccess) return hip_fail(c, e, "icp iteration");
+        if ((it & 7) == 7 || it + 1 == prm->max_iter) {
+            SSF_TRY_HIP(c, hipMemcpyAsync(hs.data(), st, sizeof(ssf::IcpState) * hs.size(), hipMemcpyDeviceToHost, s), "D2H icp state");
+            SSF_TRY_HIP(c, hipStreamSynchronize(s), "icp sync");
+            bool all = true;
+            for (const auto& x : hs) all = all && x.done;
+            if (all) break;
+        }
+    }
+    (void)s0; (void)total_ns;
+    e = ssf::launch_icp_fitness(s, n_prob, src, d_src_off, h_src_off[n_prob], max_ns, tgt, d_tgt_off, max_nt, st, key);
+    if (e != hipSuccess) return hip_fail(c, e, "icp fitness");
+    SSF_TRY_HIP(c, hipMemcpyAsync(hs.data(), st, sizeof(ssf::IcpState) * hs.size(), hipMemcpyDeviceToHost, s), "D2H icp state");
+    SSF_TRY_HIP(c, hipStreamSynchronize(s), "icp sync");
+    for (int k = 0; k < n_prob; ++k) {
+        double* o = h_out + (size_t)k * SSF_ICP_OUT_STRIDE;
+        for (int i = 0; i < SSF_ICP_OUT_STRIDE; ++i) o[i] = 0.0;
+        for (int i = 0; i < 16; ++i) o[SSF_ICP_OUT_T + i] = hs[k].fin[i];
+        o[SSF_ICP_OUT_FITNESS] = hs[k].fitness;
+        o[SSF_ICP_OUT_CONVERGED] = hs[k].converged;
+        o[SSF_ICP_OUT_ITERATIONS] = hs[k].it;
+        o[SSF_ICP_OUT_STATE] = hs[k].state;
+        o[SSF_ICP_OUT_NCORR] = hs[k].n_corr;
+    }
     return SSF_OK;
 }
 

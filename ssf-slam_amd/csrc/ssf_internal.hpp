@@ -68,4 +68,28 @@ hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const
                             const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
                             double* out);
 
+// ---- launchers (loop.hip) ----
+struct IcpState {             // one per ICP problem, device-resident across iterations
+    float fin[16];            // final transformation (row-major, float as PCL's Matrix4f)
+    double prev_mse;
+    double fitness;
+    int32_t it, done, state, converged, n_corr, pad;
+};
+typedef ssf_icp_params IcpParams;
+size_t vg_scratch_bytes(int n_clouds, int64_t n);
+hipError_t launch_voxel_grid(hipStream_t s, int n_clouds, const float4* pts, const int64_t* off,
+                             int64_t n, int64_t max_pts, float leaf, void* scratch, float4* out,
+                             int32_t* out_count);
+hipError_t launch_icp_init(hipStream_t s, int n_prob, const float4* src, const int64_t* soff,
+                           int64_t max_ns, const float* guess, float4* cur, IcpState* st,
+                           unsigned long long* key);
+hipError_t launch_icp_iteration(hipStream_t s, int n_prob, float4* cur, const int64_t* soff,
+                                int64_t max_ns, const float4* tgt, const int64_t* toff,
+                                int64_t max_nt, const IcpParams& prm, IcpState* st,
+                                unsigned long long* key);
+hipError_t launch_icp_fitness(hipStream_t s, int n_prob, const float4* src, const int64_t* soff,
+                              int64_t total_ns, int64_t max_ns, const float4* tgt,
+                              const int64_t* toff, int64_t max_nt, IcpState* st,
+                              unsigned long long* key);
+
 }  // namespace ssf

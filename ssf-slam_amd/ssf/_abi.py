@@ -28,7 +28,18 @@ EXPORTS = [
     "ssf_abi_version", "ssf_config_default", "ssf_create", "ssf_destroy", "ssf_last_error",
     "ssf_reserve", "ssf_extract_planes_batch", "ssf_extract_planes", "ssf_plane_table_batch",
     "ssf_register_batch", "ssf_mask_pose_batch", "ssf_rng_seed", "ssf_accumulate_sequence",
+    "ssf_voxel_grid_batch", "ssf_icp_params_default", "ssf_icp_batch",
 ]
+
+ICP_OUT_STRIDE = 24
+ICP_OUT = dict(T=0, FITNESS=16, CONVERGED=17, ITERATIONS=18, STATE=19, NCORR=20)
+ICP_STATES = {0: "not_converged", 1: "iterations", 2: "transform", 3: "abs_mse", 4: "rel_mse",
+              5: "no_correspondences"}
+
+
+class IcpParams(C.Structure):
+    _fields_ = [("max_iter", C.c_int32), ("max_corr_dist", C.c_float), ("trans_eps", C.c_double),
+                ("fit_eps", C.c_double)]
 
 
 class Config(C.Structure):
@@ -79,6 +90,12 @@ def lib():
     L.ssf_mask_pose_batch.restype = i32
     L.ssf_accumulate_sequence.argtypes = [vp, vp, i32, vp, vp, vp]
     L.ssf_accumulate_sequence.restype = i32
+    L.ssf_voxel_grid_batch.argtypes = [vp, vp, i32, vp, vp, vp, C.c_float, vp, vp]
+    L.ssf_voxel_grid_batch.restype = i32
+    L.ssf_icp_params_default.argtypes = [C.POINTER(IcpParams)]
+    L.ssf_icp_params_default.restype = i32
+    L.ssf_icp_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, C.POINTER(IcpParams), vp, vp]
+    L.ssf_icp_batch.restype = i32
     _lib = L
     return L
 

@@ -7,6 +7,7 @@ fallback anywhere in this package.
 from ._abi import SSFError  # noqa: F401
 from .frontend import Frontend, PlaneBatch, frame_offsets, identity_poses  # noqa: F401
 from .pose import mask_and_pose, slove_RT_by_SVD  # noqa: F401
+from . import loop  # noqa: F401  (mapOptmization loop closure: voxel grid, ICP, LoopCloser)
 
 __all__ = ["Frontend", "PlaneBatch", "frame_offsets", "identity_poses", "SSFError",
-           "mask_and_pose", "slove_RT_by_SVD"]
+           "mask_and_pose", "slove_RT_by_SVD", "loop"]

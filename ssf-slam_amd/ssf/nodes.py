@@ -178,9 +178,63 @@ class PointCloudOdometryNode:
         return o
 
 
+class MapOptimizationNode:
+    """src/mapOptmization.cpp cloudThread/mapOptimization (:429-467) for one sequence: pairs
+    /plane_frame_cloud2 with /frame_odom2 (stamps within 5 ms, :434-439), keeps keyframes,
+    detects loops and registers them on the GPU (ssf.loop.LoopCloser), publishes
+    /map_odom_res3 (Odometry "map" / "map_child"), /map_frame_res3 (the frame in the map) and
+    /map_laser_path_res3, and appends TUM lines to RESULT_PATH (:355-374).  GTSAM iSAM2 is not
+    part of this path: the published pose is the loop-adjusted odometry trans_loop_adjust *
+    T_fodom_0_curr (:450) at every frame (the reference publishes its iSAM2 estimate for
+    keyframes only), and the loop constraints are kept in ``closer.constraints``."""
+
+    def __init__(self, publish, device=None, frontend: Frontend | None = None,
+                 tum_path: str | None = None):
+        from .loop import LoopCloser, get_translation_and_euler_angles  # noqa: F401
+        self.publish = publish
+        self.fe = frontend or Frontend(64, device=device)
+        self.closer = LoopCloser(self.fe)
+        self.planes, self.odoms = [], []          # planeQueue / odometryQueue (:65-75)
+        self.path = Path()
+        self.writer = sio.TumWriter(tum_path) if tum_path else None
+
+    def on_plane_cloud(self, msg):
+        self.planes.append(msg)
+        self._drain()
+
+    def on_odom(self, msg):
+        self.odoms.append(msg)
+        self._drain()
+
+    def _drain(self):
+        import numpy as np
+        from .loop import transform_cloud
+        from scipy.spatial.transform import Rotation
+        while self.planes and self.odoms:
+            pm, om = self.planes[0], self.odoms[0]
+            tp, to = sio.stamp_of(pm.header), (om.header.stamp_sec, om.header.stamp_nsec)
+            if abs((tp[0] - to[0]) + (tp[1] - to[1]) * 1e-9) > 0.005:    # time sync (:436-439)
+                return
+            self.planes.pop(0)
+            self.odoms.pop(0)
+            xyzi = torch.from_numpy(sio.cloud_xyzi(pm)).to(self.fe.device)
+            stamp = tp[0] + tp[1] * 1e-9
+            T, _, _ = self.closer.process(xyzi, om.pose.orientation, om.pose.position, stamp)
+            q = Rotation.from_matrix(T[:3, :3]).as_quat()                  # x, y, z, w
+            hdr = sio.Header(tp[0], tp[1], "map")
+            pose = Pose(tuple(float(v) for v in T[:3, 3]), tuple(float(v) for v in q))
+            self.publish("/map_odom_res3", Odometry(hdr, "map_child", pose))
+            if self.writer:
+                self.writer.write(tp, pose.position, pose.orientation)
+            self.path.poses.append((hdr, pose))
+            self.path.header = hdr
+            self.publish("/map_laser_path_res3", self.path)
+            self.publish("/map_frame_res3", sio.xyzi_to_cloud(transform_cloud(xyzi, T), tp, "map"))
+
+
 def run_sequence(root: str, tum_path: str | None = None, n_rows: int = 64, device=None,
                  solver: str = "ceres_lm", max_iter: int | None = None, seed: int | None = None,
-                 rate_hz: float = 10.0, keys=("pos1", "gt")):
+                 rate_hz: float = 10.0, keys=("pos1", "gt"), map_tum_path: str | None = None):
     """Replay a DATASET_PATH directory through PointCloudOdometry -> frameFeature ->
     lidarOdometry_onlyPC as the launch files wire them.  Stamps are synthetic and monotone
     (frame k at k / rate_hz; the reference uses wall-clock ros::Time::now()).  Writes the
@@ -207,6 +261,11 @@ def run_sequence(root: str, tum_path: str | None = None, n_rows: int = 64, devic
 
     bus.subscribe("/frame_odom1", on_odom1)
     bus.subscribe("/frame_odom2", on_odom2)
+    mo = None
+    if map_tum_path is not None:                     # mapOptmization on /plane_frame_cloud2 + /frame_odom2
+        mo = MapOptimizationNode(bus.publish, device=dev, tum_path=map_tum_path or None)
+        bus.subscribe("/plane_frame_cloud2", mo.on_plane_cloud)
+        bus.subscribe("/frame_odom2", mo.on_odom)
     period_ns = int(round(1e9 / rate_hz))
     for fr in sio.NpzSequence(root, keys=keys, device=dev):
         t_ns = fr["index"] * period_ns
@@ -214,4 +273,5 @@ def run_sequence(root: str, tum_path: str | None = None, n_rows: int = 64, devic
         stamps.append(stamp)
         pco.on_frame(fr[keys[0]], fr[keys[1]], stamp)
     return dict(odom1=np.asarray(odom1, np.float64).reshape(-1, 7),
-                odom2=np.asarray(odom2, np.float64).reshape(-1, 7), stamps=stamps)
+                odom2=np.asarray(odom2, np.float64).reshape(-1, 7), stamps=stamps,
+                loops=mo.closer.constraints if mo else [])

@@ -80,3 +80,26 @@ def test_nodes_message_layouts(dev):
     assert od.header.frame_id == "map" and od.child_frame_id == "map_child"
     assert len(bus.log["/frame_odom_path2"][-1].poses) == 1
     assert np.array_equal(sio.cloud_xyzi(bus.log["/plane_frame_cloud2"][0]), ref)
+
+
+def test_map_optimization_node_chain(dev, tmp_path):
+    """mapOptmization on the bus (/plane_frame_cloud2 + /frame_odom2 -> /map_odom_res3 and the
+    RESULT_PATH TUM file, src/mapOptmization.cpp:355-374, 429-467): with no loop in a short
+    forward sequence, trans_loop_adjust stays identity and the map pose is /frame_odom2."""
+    from ssf import io as sio
+    from ssf import nodes
+    frames = [frame(5, k, n_az=900) for k in range(4)]
+    data = tmp_path / "data"
+    data.mkdir()
+    for k, f in enumerate(frames):
+        np.savez(str(data / f"{k:06d}.npz"), pos1=f[0], gt=f[1])
+    tum2, tum3 = str(tmp_path / "odom2.txt"), str(tmp_path / "map.txt")
+    with torch.cuda.device(dev):
+        res = nodes.run_sequence(str(data), tum2, seed=7, map_tum_path=tum3)
+    assert res["loops"] == []
+    s2, t2, q2 = sio.read_tum(tum2)
+    s3, t3, q3 = sio.read_tum(tum3)
+    assert s2 == s3 and len(s3) == 3
+    assert np.abs(t3 - t2).max() <= 1e-6
+    for a, b in zip(q2, q3):
+        assert _angle(a, b) < 1e-6

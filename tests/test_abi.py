@@ -49,6 +49,12 @@ def test_error_paths_without_gpu():
     assert L.ssf_rng_seed(None, 1) == _abi.SSF_E_ARG
     assert L.ssf_extract_planes_batch(None, None, 1, None, 3, None, 0, 0, None, None, None, None, None) == _abi.SSF_E_ARG
     assert L.ssf_last_error(None) == b"null context"
+    assert L.ssf_voxel_grid_batch(None, None, 1, None, None, None, 0.1, None, None) == _abi.SSF_E_ARG
+    prm = _abi.IcpParams()
+    assert L.ssf_icp_params_default(C.byref(prm)) == _abi.SSF_OK
+    assert (prm.max_iter, prm.max_corr_dist, prm.trans_eps, prm.fit_eps) == (100, 50.0, 1e-6, 1e-6)
+    assert L.ssf_icp_params_default(None) == _abi.SSF_E_ARG
+    assert L.ssf_icp_batch(None, None, 1, None, None, None, None, None, None, C.byref(prm), None, None) == _abi.SSF_E_ARG
     cfg = _abi.config_default(64)
     cfg.n_rows = 33
     h = C.c_void_p()

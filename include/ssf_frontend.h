@@ -89,6 +89,19 @@ int32_t ssf_extract_planes_batch(ssf_ctx* ctx, void* stream, int32_t n_frames,
                                  int64_t max_frame_points,
                                  float* d_plane_xyzi, int32_t* d_plane_count,
                                  float* d_ring_xyzi, int32_t* d_ring_off, float* d_curv);
+
+/* Beyond the reference (BASELINE configs[2] "mask applied before features"; parity unpinned,
+ * off unless called): the same extraction on the points whose d_keep byte is non-zero -- e.g.
+ * the background mask of ssf_mask_pose_batch at the same offsets.  Dropped points are treated as
+ * if they were not in the cloud (the reference's frameFeature always receives every point,
+ * scripts/PointCloudOdometry_noSeg.py:92-94), so the result equals ssf_extract_planes_batch on
+ * the stably compacted cloud. */
+int32_t ssf_extract_planes_batch_masked(ssf_ctx* ctx, void* stream, int32_t n_frames,
+                                        const float* d_pts, int32_t point_stride,
+                                        const int64_t* d_frame_off, int64_t total_points,
+                                        int64_t max_frame_points, const uint8_t* d_keep,
+                                        float* d_plane_xyzi, int32_t* d_plane_count,
+                                        float* d_ring_xyzi, int32_t* d_ring_off, float* d_curv);
 /* Single-frame form with the SURVEY §8(b) signature: synchronises, returns the plane count in
  * *h_out_m; SSF_E_CAPACITY if more than out_cap points were selected. */
 int32_t ssf_extract_planes(ssf_ctx* ctx, void* stream, const float* d_pts, int64_t n,

@@ -211,11 +211,12 @@ int32_t ssf_reserve(ssf_ctx* c, int32_t max_frames, int64_t max_points_per_frame
     return SSF_OK;
 }
 
-int32_t ssf_extract_planes_batch(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_pts,
-                                 int32_t point_stride, const int64_t* d_frame_off,
-                                 int64_t total_points, int64_t max_frame_points,
-                                 float* d_plane_xyzi, int32_t* d_plane_count, float* d_ring_xyzi,
-                                 int32_t* d_ring_off, float* d_curv) {
+static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_pts,
+                                   int32_t point_stride, const int64_t* d_frame_off,
+                                   int64_t total_points, int64_t max_frame_points,
+                                   const uint8_t* d_keep, float* d_plane_xyzi,
+                                   int32_t* d_plane_count, float* d_ring_xyzi, int32_t* d_ring_off,
+                                   float* d_curv) {
     if (!c) return SSF_E_ARG;
     if (n_frames < 0 || point_stride < 3 || total_points < 0 || max_frame_points < 0 ||
         (n_frames > 0 && (!d_pts || !d_frame_off || !d_plane_xyzi || !d_plane_count)))
@@ -228,10 +229,32 @@ int32_t ssf_extract_planes_batch(ssf_ctx* c, void* stream, int32_t n_frames, con
     int32_t* roff = d_ring_off ? d_ring_off : c->ring_off.as<int32_t>();
     hipError_t e = ssf::launch_extract_planes(
         (hipStream_t)stream, c->cfg, n_frames, d_pts, point_stride, d_frame_off, max_frame_points,
-        c->rid.as<int8_t>(), c->hist.as<int32_t>(), roff, ring, d_curv, c->sel.as<int32_t>(),
+        d_keep, c->rid.as<int8_t>(), c->hist.as<int32_t>(), roff, ring, d_curv, c->sel.as<int32_t>(),
         c->sel_cnt.as<int32_t>(), reinterpret_cast<float4*>(d_plane_xyzi), d_plane_count);
     if (e != hipSuccess) return hip_fail(c, e, "extract_planes launch");
     return SSF_OK;
+}
+
+int32_t ssf_extract_planes_batch(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_pts,
+                                 int32_t point_stride, const int64_t* d_frame_off,
+                                 int64_t total_points, int64_t max_frame_points,
+                                 float* d_plane_xyzi, int32_t* d_plane_count, float* d_ring_xyzi,
+                                 int32_t* d_ring_off, float* d_curv) {
+    return extract_planes_impl(c, stream, n_frames, d_pts, point_stride, d_frame_off, total_points,
+                               max_frame_points, nullptr, d_plane_xyzi, d_plane_count, d_ring_xyzi,
+                               d_ring_off, d_curv);
+}
+
+int32_t ssf_extract_planes_batch_masked(ssf_ctx* c, void* stream, int32_t n_frames,
+                                        const float* d_pts, int32_t point_stride,
+                                        const int64_t* d_frame_off, int64_t total_points,
+                                        int64_t max_frame_points, const uint8_t* d_keep,
+                                        float* d_plane_xyzi, int32_t* d_plane_count,
+                                        float* d_ring_xyzi, int32_t* d_ring_off, float* d_curv) {
+    if (c && n_frames > 0 && !d_keep) return fail(c, SSF_E_ARG, "extract_planes_batch_masked: null keep mask");
+    return extract_planes_impl(c, stream, n_frames, d_pts, point_stride, d_frame_off, total_points,
+                               max_frame_points, d_keep, d_plane_xyzi, d_plane_count, d_ring_xyzi,
+                               d_ring_off, d_curv);
 }
 
 int32_t ssf_extract_planes(ssf_ctx* c, void* stream, const float* d_pts, int64_t n,

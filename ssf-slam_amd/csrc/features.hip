@@ -66,6 +66,7 @@ constexpr int kCountSteps = kBinChunk / 256;
 __global__ __launch_bounds__(256) void k_bin_count(const float* __restrict__ pts, int stride,
                                                    const int64_t* __restrict__ frame_off,
                                                    int n_rows, int n_chunks,
+                                                   const uint8_t* __restrict__ keep,
                                                    int8_t* __restrict__ rid,
                                                    int32_t* __restrict__ hist) {
     __shared__ int h[kMaxRows];
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(256) void k_bin_count(const float* __restrict__ pts
         for (int k = 0; k < kCountSteps; ++k) {
             const int64_t i = s + threadIdx.x + 256 * k;
             if (i < t) {
-                const int id = ring_id(px[k], py[k], pz[k], n_rows);
+                const int id = (keep && !keep[i]) ? -1 : ring_id(px[k], py[k], pz[k], n_rows);
                 rid[i] = (int8_t)id;
                 if (id >= 0) atomicAdd(&h[id], 1);
             }
@@ -375,15 +376,15 @@ __global__ __launch_bounds__(256) void k_compact(const int64_t* __restrict__ fra
 
 hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_frames,
                                  const float* pts, int stride, const int64_t* frame_off,
-                                 int64_t max_pts, int8_t* rid, int32_t* hist, int32_t* ring_off,
-                                 float4* ring_xyzi, float* curv, int32_t* sel, int32_t* sel_cnt,
-                                 float4* plane, int32_t* plane_count) {
+                                 int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
+                                 int32_t* ring_off, float4* ring_xyzi, float* curv, int32_t* sel,
+                                 int32_t* sel_cnt, float4* plane, int32_t* plane_count) {
     const int R = cfg.n_rows;
     const int n_chunks = (int)((max_pts + kBinChunk - 1) / kBinChunk);
     if (n_frames <= 0) return hipSuccess;
     if (n_chunks > 0) {
         hipLaunchKernelGGL(k_bin_count, dim3(n_chunks, n_frames), dim3(256), 0, s, pts, stride,
-                           frame_off, R, n_chunks, rid, hist);
+                           frame_off, R, n_chunks, keep, rid, hist);
     }
     hipLaunchKernelGGL(k_bin_scan, dim3(n_frames), dim3(64), 0, s, R, n_chunks, hist, ring_off);
     if (n_chunks > 0) {

@@ -43,9 +43,9 @@ struct alignas(16) CorrRec {
 // ---- launchers (features.hip) ----
 hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_frames,
                                  const float* pts, int stride, const int64_t* frame_off,
-                                 int64_t max_pts, int8_t* rid, int32_t* hist, int32_t* ring_off,
-                                 float4* ring_xyzi, float* curv, int32_t* sel, int32_t* sel_cnt,
-                                 float4* plane, int32_t* plane_count);
+                                 int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
+                                 int32_t* ring_off, float4* ring_xyzi, float* curv, int32_t* sel,
+                                 int32_t* sel_cnt, float4* plane, int32_t* plane_count);
 
 // ---- launchers (registration.hip) ----
 hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames,

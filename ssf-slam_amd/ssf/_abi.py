@@ -29,6 +29,7 @@ EXPORTS = [
     "ssf_reserve", "ssf_extract_planes_batch", "ssf_extract_planes", "ssf_plane_table_batch",
     "ssf_register_batch", "ssf_mask_pose_batch", "ssf_rng_seed", "ssf_accumulate_sequence",
     "ssf_voxel_grid_batch", "ssf_icp_params_default", "ssf_icp_batch",
+    "ssf_extract_planes_batch_masked",
 ]
 
 ICP_OUT_STRIDE = 24
@@ -79,6 +80,8 @@ def lib():
     L.ssf_rng_seed.restype = i32
     L.ssf_extract_planes_batch.argtypes = [vp, vp, i32, vp, i32, vp, i64, i64, vp, vp, vp, vp, vp]
     L.ssf_extract_planes_batch.restype = i32
+    L.ssf_extract_planes_batch_masked.argtypes = [vp, vp, i32, vp, i32, vp, i64, i64, vp, vp, vp, vp, vp, vp]
+    L.ssf_extract_planes_batch_masked.restype = i32
     L.ssf_extract_planes.argtypes = [vp, vp, vp, i64, i32, i32, vp, C.POINTER(i64), i64]
     L.ssf_extract_planes.restype = i32
     L.ssf_plane_table_batch.argtypes = [vp, vp, i32, vp, vp, vp, i64, vp, vp, vp, vp]

@@ -108,9 +108,11 @@ class Frontend:
 
     # ------------------------------------------------------------------ frameFeature
     def extract_planes_batch(self, pts, off, h_off, max_points=None, point_stride=None,
-                             debug=False):
+                             debug=False, keep=None):
         """cloudHandler for F frames packed in `pts` ([total, stride] f32) at offsets `off`.
-        Returns PlaneBatch (and, with debug=True, ring-ordered points, row offsets, curvature)."""
+        Returns PlaneBatch (and, with debug=True, ring-ordered points, row offsets, curvature).
+        keep (uint8/bool per point, optional, beyond the reference): extract from the kept
+        points only -- e.g. the background mask of mask_pose ("mask applied before features")."""
         pts = self._dev(pts, torch.float32)
         F = h_off.numel() - 1
         total = int(h_off[-1])
@@ -124,10 +126,19 @@ class Frontend:
             ring = torch.zeros((max(total, 1), 4), dtype=torch.float32, device=self.device)
             roff = torch.zeros(max(F, 1) * (self.n_rows + 1), dtype=torch.int32, device=self.device)
             curv = torch.zeros(max(total, 1), dtype=torch.float32, device=self.device)
-        rc = _abi.lib().ssf_extract_planes_batch(
-            self._h, _stream(self.device), F, _ptr(pts), stride, _ptr(off), total, mx,
-            _ptr(plane), _ptr(count), _ptr(ring), _ptr(roff), _ptr(curv))
-        self._check(rc, "ssf_extract_planes_batch")
+        if keep is None:
+            rc = _abi.lib().ssf_extract_planes_batch(
+                self._h, _stream(self.device), F, _ptr(pts), stride, _ptr(off), total, mx,
+                _ptr(plane), _ptr(count), _ptr(ring), _ptr(roff), _ptr(curv))
+            self._check(rc, "ssf_extract_planes_batch")
+        else:
+            keep = self._dev(keep, torch.uint8)
+            if keep.numel() != total:
+                raise ValueError(f"keep has {keep.numel()} entries for {total} points")
+            rc = _abi.lib().ssf_extract_planes_batch_masked(
+                self._h, _stream(self.device), F, _ptr(pts), stride, _ptr(off), total, mx, _ptr(keep),
+                _ptr(plane), _ptr(count), _ptr(ring), _ptr(roff), _ptr(curv))
+            self._check(rc, "ssf_extract_planes_batch_masked")
         # plane points per frame <= sum over rows of ceil(n_r / planeSpan) <= n/span + rows
         pb = PlaneBatch(plane, count[:F], off, h_off,
                         min(mx, mx // max(1, self.cfg.plane_span) + self.n_rows + 1))

@@ -127,3 +127,28 @@ def test_ring_ids_near_bin_edges(oracle, dev, n_rows):
     assert np.array_equal(roff[0].cpu().numpy().astype(np.int64), off_ref)
     kept = int(off_ref[-1])
     assert np.array_equal(ring[:kept].cpu().numpy(), rx), "ring-ordered cloud differs near bin edges"
+
+
+def test_mask_before_features_equals_compacted_cloud(oracle, dev):
+    """Beyond the reference (BASELINE configs[2], flag off by default): extraction from the kept
+    points only equals the reference extraction of the stably compacted cloud -- with the
+    ground-truth background mask and with a random mask, two frames in one batch."""
+    import ssf
+    from helpers import frame as fr
+    O = oracle
+    rng = np.random.default_rng(11)
+    clouds, keeps = [], []
+    for k in range(2):
+        pts, _, fg = fr(2, k)
+        clouds.append(pts)
+        keeps.append((fg == 0).astype(np.uint8) if k == 0 else (rng.random(pts.shape[0]) < 0.8).astype(np.uint8))
+    fe = ssf.Frontend(64, device=dev.index or 0)
+    t = torch.from_numpy(np.concatenate(clouds)).to(dev)
+    keep = torch.from_numpy(np.concatenate(keeps)).to(dev)
+    off, h_off = ssf.frame_offsets([c.shape[0] for c in clouds], dev)
+    pb = fe.extract_planes_batch(t, off, h_off, keep=keep)
+    torch.cuda.synchronize()
+    for f in range(2):
+        ref = O.extract_planes(clouds[f][keeps[f] != 0], 64)
+        got = pb.frame(f).cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), f

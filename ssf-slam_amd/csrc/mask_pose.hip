@@ -745,10 +745,9 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             S.lb2[tid] = __double2float_ru(fabs(h[6] - g[6]) + 1e-13 * (h[8] + g[8]));
         }
         __syncthreads();
-        double cen[12];
+        // the centres are read from LDS (broadcast) at every point through a laundered base,
+        // like the EM parameters: held in registers they spilled to scratch in these loops
         const double csn0 = uni(S.csn[0]), csn1 = uni(S.csn[1]);
-#pragma unroll
-        for (int k = 0; k < 12; ++k) cen[k] = uni(S.cen[k]);
         double acc[14];
 #pragma unroll
         for (int k = 0; k < 14; ++k) acc[k] = 0.0;
@@ -763,6 +762,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         // (val = 0: a pipeline slot with no point -- computed, weighted out, record written to
         // the frame's spare slot n)
         auto label = [&](auto wrec_c, int64_t i, const double* x, int lp, bool val) {
+            const LdsDouble* cen = lds_laundered(S.cen);
             double v[6], dt0 = 0.0, dt1 = 0.0, vn = 0.0;
 #pragma unroll
             for (int d = 0; d < 6; ++d) {
@@ -786,12 +786,10 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         if (full) {
             // every point: a prefetched stream of [flow, xyz]; the previous label is recomputed
             // from the previous centres (the pass that wrote it used the same expression)
-            double cenp[12];
             const double cpn0 = uni(S.csnp[0]), cpn1 = uni(S.csnp[1]);
-#pragma unroll
-            for (int k = 0; k < 12; ++k) cenp[k] = uni(S.cenp[k]);
             auto full_pass = [&](auto wrec_c) {
                 for_points_deep<kLloydDeep>(P, Fl, n, [&](int64_t i, const double* x) {
+                    const LdsDouble* cenp = lds_laundered(S.cenp);
                     double dp0 = 0.0, dp1 = 0.0;
 #pragma unroll
                     for (int d = 0; d < 6; ++d) {

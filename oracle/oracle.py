@@ -334,3 +334,102 @@ def icp(src, tgt, max_corr_dist=50.0, max_iter=100, trans_eps=1e-6, fit_eps=1e-6
     return dict(T=np.array(r.T, np.float32).reshape(4, 4), fitness=r.fitness,
                 converged=bool(r.converged), iterations=r.iterations,
                 state=ICP_STATES[r.state], n_corr=r.n_corr)
+
+
+# ---- TFlow point-set operators: oracle/pn2_oracle.c ----
+def _pn2(L):
+    if not getattr(L, "_pn2_typed", False):
+        L.orc_pn2_fps.argtypes = [f32p, C.c_int64, C.c_int32, C.c_int32, f32p, i32p]
+        L.orc_pn2_knn.argtypes = [f32p, C.c_int64, f32p, C.c_int64, C.c_int32, f32p, i32p]
+        L.orc_pn2_gather.argtypes = [f32p, C.c_int32, C.c_int64, i32p, C.c_int64, f32p]
+        L.orc_pn2_interp3.argtypes = [f32p, C.c_int32, C.c_int64, i32p, f32p, C.c_int64, f32p]
+        L.orc_pn2_upsample.argtypes = [f32p, C.c_int64, f32p, C.c_int64, f32p, C.c_int32,
+                                       C.c_int32, f32p]
+        L._pn2_typed = True
+    return L
+
+
+def pn2_fps(xyz, npoint, start=None):
+    """farthest_point_sample (utils/utils.py:68-89): xyz [B, N, 3] -> int32 [B, npoint]."""
+    L = _pn2(lib())
+    x = np.ascontiguousarray(xyz, np.float32)
+    B, N, _ = x.shape
+    out = np.zeros((B, npoint), np.int32)
+    tmp = np.zeros(N, np.float32)
+    for b in range(B):
+        o = np.zeros(npoint, np.int32)
+        L.orc_pn2_fps(np.ascontiguousarray(x[b]).reshape(-1), N, npoint,
+                      0 if start is None else int(start[b]), tmp, o)
+        out[b] = o
+    return out
+
+
+def pn2_knn(k, query, ref):
+    """knn_point (utils/utils.py:92-108): query [B, S, 3], ref [B, N, 3] -> (dist, idx) [B, S, k]."""
+    L = _pn2(lib())
+    q = np.ascontiguousarray(query, np.float32)
+    r = np.ascontiguousarray(ref, np.float32)
+    B, S, _ = q.shape
+    N = r.shape[1]
+    dist = np.zeros((B, S, k), np.float32)
+    idx = np.zeros((B, S, k), np.int32)
+    for b in range(B):
+        d = np.zeros(S * k, np.float32); i = np.zeros(S * k, np.int32)
+        L.orc_pn2_knn(np.ascontiguousarray(q[b]).reshape(-1), S,
+                      np.ascontiguousarray(r[b]).reshape(-1), N, k, d, i)
+        dist[b] = d.reshape(S, k); idx[b] = i.reshape(S, k)
+    return dist, idx
+
+
+def pn2_gather(feat, idx):
+    """index_points on the [B, C, N] layout: idx [B, ...] -> [B, C, ...]."""
+    L = _pn2(lib())
+    f = np.ascontiguousarray(feat, np.float32)
+    ix = np.ascontiguousarray(idx, np.int32)
+    B, Cc, N = f.shape
+    g = int(np.prod(ix.shape[1:]))
+    out = np.zeros((B, Cc, g), np.float32)
+    for b in range(B):
+        o = np.zeros(Cc * g, np.float32)
+        L.orc_pn2_gather(np.ascontiguousarray(f[b]).reshape(-1), Cc, N,
+                         np.ascontiguousarray(ix[b]).reshape(-1), g, o)
+        out[b] = o.reshape(Cc, g)
+    return out.reshape((B, Cc) + ix.shape[1:])
+
+
+def pn2_three_interpolate(feat, idx, weight):
+    """utils/utils.py:662-663: feat [B, C, M], idx/weight [B, N, 3] -> [B, C, N]."""
+    L = _pn2(lib())
+    f = np.ascontiguousarray(feat, np.float32)
+    ix = np.ascontiguousarray(idx, np.int32)
+    w = np.ascontiguousarray(weight, np.float32)
+    B, Cc, M = f.shape
+    N = ix.shape[1]
+    out = np.zeros((B, Cc, N), np.float32)
+    for b in range(B):
+        o = np.zeros(Cc * N, np.float32)
+        L.orc_pn2_interp3(np.ascontiguousarray(f[b]).reshape(-1), Cc, M,
+                          np.ascontiguousarray(ix[b]).reshape(-1),
+                          np.ascontiguousarray(w[b]).reshape(-1), N, o)
+        out[b] = o.reshape(Cc, N)
+    return out
+
+
+def pn2_upsample_flow(xyz, sparse_xyz, sparse_feat, k=3):
+    """UpsampleFlow.forward (utils/soflow.py:1442-1470): xyz [B, 3, N], sparse_xyz [B, 3, S],
+    sparse_feat [B, C, S] -> [B, C, N]."""
+    L = _pn2(lib())
+    x = np.ascontiguousarray(xyz, np.float32)
+    sx = np.ascontiguousarray(sparse_xyz, np.float32)
+    sf = np.ascontiguousarray(sparse_feat, np.float32)
+    B, _, N = x.shape
+    S = sx.shape[2]
+    Cc = sf.shape[1]
+    out = np.zeros((B, Cc, N), np.float32)
+    for b in range(B):
+        o = np.zeros(Cc * N, np.float32)
+        L.orc_pn2_upsample(np.ascontiguousarray(x[b]).reshape(-1), N,
+                           np.ascontiguousarray(sx[b]).reshape(-1), S,
+                           np.ascontiguousarray(sf[b]).reshape(-1), Cc, int(k), o)
+        out[b] = o.reshape(Cc, N)
+    return out

@@ -12,8 +12,9 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "ssf", "_lib")
 OBJ_DIR = os.path.join(HERE, "build")
 LIB = os.path.join(OUT_DIR, "libssf_frontend.so")
-SOURCES = ["abi.hip", "features.hip", "registration.hip", "mask_pose.hip", "loop.hip"]
-HEADERS = ["ssf_device.hpp", "ssf_internal.hpp", "svd3.hpp", os.path.join("..", "..", "include", "ssf_frontend.h")]
+SOURCES = ["abi.hip", "features.hip", "registration.hip", "mask_pose.hip", "loop.hip", "pointnet2.hip"]
+HEADERS = ["ssf_device.hpp", "ssf_internal.hpp", "svd3.hpp", os.path.join("..", "..", "include", "ssf_frontend.h"),
+           os.path.join("..", "..", "include", "ssf_pointnet2.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: no FMA contraction, so float stages match the reference's x86 arithmetic
 # (and the CPU oracle) bit for bit.

@@ -8,6 +8,7 @@ from ._abi import SSFError  # noqa: F401
 from .frontend import Frontend, PlaneBatch, frame_offsets, identity_poses  # noqa: F401
 from .pose import mask_and_pose, slove_RT_by_SVD  # noqa: F401
 from . import loop  # noqa: F401  (mapOptmization loop closure: voxel grid, ICP, LoopCloser)
+from . import pointnet2  # noqa: F401  (TFlow point-set operators: pointutils surface)
 
 __all__ = ["Frontend", "PlaneBatch", "frame_offsets", "identity_poses", "SSFError",
-           "mask_and_pose", "slove_RT_by_SVD", "loop"]
+           "mask_and_pose", "slove_RT_by_SVD", "loop", "pointnet2"]

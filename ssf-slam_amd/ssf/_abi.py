@@ -31,6 +31,12 @@ EXPORTS = [
     "ssf_voxel_grid_batch", "ssf_icp_params_default", "ssf_icp_batch",
     "ssf_extract_planes_batch_masked",
 ]
+# Every symbol include/ssf_pointnet2.h declares (TFlow point-set operators).
+PN2_EXPORTS = [
+    "ssf_pn2_last_error", "ssf_pn2_furthest_point_sample", "ssf_pn2_knn", "ssf_pn2_three_nn",
+    "ssf_pn2_gather", "ssf_pn2_three_interpolate", "ssf_pn2_upsample_flow",
+]
+PN2_KNN_MAX, PN2_UPSAMPLE_MAX_SPARSE = 32, 4096
 
 ICP_OUT_STRIDE = 24
 ICP_OUT = dict(T=0, FITNESS=16, CONVERGED=17, ITERATIONS=18, STATE=19, NCORR=20)
@@ -99,6 +105,16 @@ def lib():
     L.ssf_icp_params_default.restype = i32
     L.ssf_icp_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, C.POINTER(IcpParams), vp, vp]
     L.ssf_icp_batch.restype = i32
+    L.ssf_pn2_last_error.argtypes = []
+    L.ssf_pn2_last_error.restype = C.c_char_p
+    L.ssf_pn2_furthest_point_sample.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp]
+    L.ssf_pn2_knn.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp]
+    L.ssf_pn2_three_nn.argtypes = [vp, i32, i32, i32, vp, vp, vp, vp]
+    L.ssf_pn2_gather.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp]
+    L.ssf_pn2_three_interpolate.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp]
+    L.ssf_pn2_upsample_flow.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp]
+    for name in PN2_EXPORTS[1:]:
+        getattr(L, name).restype = i32
     _lib = L
     return L
 

@@ -69,3 +69,20 @@ def test_no_cpu_fallback_in_product_package():
             if f.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
                 txt = open(os.path.join(root, f)).read()
                 assert "oracle" not in txt.replace("oracle/ssf_oracle.c", "").replace("CPU oracle", "").replace("the oracle", "") or f == "synth.py", f
+
+
+def test_pointnet2_header_symbols_exported_and_arg_checks():
+    """include/ssf_pointnet2.h: every declared symbol is exported; bad arguments are rejected
+    before any HIP call"""
+    from ssf import _abi
+    L = _abi.lib()
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(REPO, "include", "ssf_pointnet2.h")).read(), flags=re.S)
+    syms = sorted(set(re.findall(r"\b(ssf_[a-z0-9_]+)\s*\(", src)))
+    assert syms == sorted(_abi.PN2_EXPORTS)
+    assert all(hasattr(L, s) for s in syms)
+    assert L.ssf_pn2_knn(None, 1, 4, 8, 33, 1, 1, 1, 1) == _abi.SSF_E_ARG      # k > 32
+    assert b"knn" in L.ssf_pn2_last_error()
+    assert L.ssf_pn2_furthest_point_sample(None, 1, 0, 4, 1, None, None, 1) == _abi.SSF_E_ARG
+    assert L.ssf_pn2_furthest_point_sample(None, 1, 20000, 4, 1, None, None, 1) == _abi.SSF_E_ARG  # no temp
+    assert L.ssf_pn2_upsample_flow(None, 1, 8, 5000, 3, 3, 1, 1, 1, 1) == _abi.SSF_E_ARG  # s > 4096
+    assert L.ssf_pn2_gather(None, 1, 1, 4, 4, 1, 1, 1, None) == _abi.SSF_E_ARG

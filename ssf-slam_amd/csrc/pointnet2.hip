@@ -222,6 +222,63 @@ __global__ __launch_bounds__(256) void k_gather(const float* __restrict__ feat, 
     }
 }
 
+// LDS-staged variants for feature rows that fit: a work-group owns CH consecutive channels of
+// one batch element, loads their rows (CH * n floats) into LDS with coalesced reads, then walks
+// the index list once (coalesced) and answers every channel from LDS.  Random 4-byte gathers
+// from L2 each cost a whole cache line of L2->L1 traffic (the bound of k_gather above); here
+// HBM sees the feature map once, the indices C / CH times and the output once.
+constexpr int kStageThreads = 1024;
+constexpr int kStageFloats = 36864;        // 144 KiB of LDS
+
+__global__ __launch_bounds__(kStageThreads) void k_gather_lds(const float* __restrict__ feat, int c,
+                                                              int n, const int32_t* __restrict__ idx,
+                                                              int g, int ch, float* __restrict__ out,
+                                                              int32_t* __restrict__ bad) {
+    extern __shared__ float rows[];
+    const int b = blockIdx.y, c0 = blockIdx.x * ch;
+    const int nch = min(ch, c - c0);
+    const float* F = feat + ((int64_t)b * c + c0) * n;
+    for (int e = threadIdx.x; e < nch * n; e += kStageThreads) rows[e] = F[e];
+    __syncthreads();
+    const int32_t* I = idx + (int64_t)b * g;
+    float* O = out + ((int64_t)b * c + c0) * g;
+    for (int j = threadIdx.x; j < g; j += kStageThreads) {
+        int i = I[j];
+        if ((unsigned)i >= (unsigned)n) { *bad = 1; i = -1; }
+        for (int k = 0; k < nch; ++k) O[(int64_t)k * g + j] = i >= 0 ? rows[k * n + i] : 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(kStageThreads) void k_three_interp_lds(
+    const float* __restrict__ feat, int c, int m, const int32_t* __restrict__ idx,
+    const float* __restrict__ w, int n, int ch, float* __restrict__ out, int32_t* __restrict__ bad) {
+    extern __shared__ float rows[];
+    const int b = blockIdx.y, c0 = blockIdx.x * ch;
+    const int nch = min(ch, c - c0);
+    const float* F = feat + ((int64_t)b * c + c0) * m;
+    for (int e = threadIdx.x; e < nch * m; e += kStageThreads) rows[e] = F[e];
+    __syncthreads();
+    const int32_t* I = idx + (int64_t)b * n * 3;
+    const float* W = w + (int64_t)b * n * 3;
+    float* O = out + ((int64_t)b * c + c0) * n;
+    for (int j = threadIdx.x; j < n; j += kStageThreads) {
+        int i[3];
+        float wt[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            i[t] = I[3 * j + t];
+            wt[t] = W[3 * j + t];
+            if ((unsigned)i[t] >= (unsigned)m) { *bad = 1; i[t] = -1; }
+        }
+        for (int k = 0; k < nch; ++k) {
+            const float* R = rows + k * m;
+            const float v0 = i[0] >= 0 ? R[i[0]] : 0.0f, v1 = i[1] >= 0 ? R[i[1]] : 0.0f,
+                        v2 = i[2] >= 0 ? R[i[2]] : 0.0f;
+            O[(int64_t)k * n + j] = (wt[0] * v0 + wt[1] * v1) + wt[2] * v2;
+        }
+    }
+}
+
 // three_interpolate (utils.py:662-663 with normalised weights): out[b,c,n] =
 // w0 f[i0] + w1 f[i1] + w2 f[i2], summed in that order.
 __global__ __launch_bounds__(256) void k_three_interp(const float* __restrict__ feat, int c, int m,
@@ -313,6 +370,19 @@ __global__ __launch_bounds__(kUpThreads) void k_upsample(const float* __restrict
     }
 }
 
+// The LDS-staged kernels take up to 144 KiB of dynamic LDS (above the 64 KiB default limit).
+hipError_t allow_stage_lds() {
+    static hipError_t once = [] {
+        hipError_t e = hipFuncSetAttribute((const void*)k_gather_lds,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kStageFloats * 4);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)k_three_interp_lds,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kStageFloats * 4);
+        return e;
+    }();
+    return once;
+}
+
 dim3 grid_rows(int64_t per_row, int64_t rows) {
     const int64_t gx = (per_row + 255) / 256;
     return dim3((unsigned)(gx < 4096 ? (gx > 0 ? gx : 1) : 4096), (unsigned)(rows < 65535 ? rows : 65535));
@@ -369,8 +439,15 @@ int32_t ssf_pn2_gather(void* stream, int32_t b, int32_t c, int32_t n, int32_t g,
         return fail(SSF_PN2_E_ARG, "gather: bad arguments");
     const int64_t total = (int64_t)b * c * g;
     if (total == 0) return SSF_PN2_OK;
-    hipLaunchKernelGGL(k_gather, grid_rows(g, (int64_t)b * c), dim3(256), 0, (hipStream_t)stream, d_feat,
-                       c, n, d_idx, g, (int64_t)b * c, d_out, d_bad);
+    if (n <= kStageFloats && b <= 65535) {
+        if (hipError_t e = allow_stage_lds(); e != hipSuccess) return hip_status(e, "gather: LDS limit");
+        const int ch = min(c, kStageFloats / n);
+        hipLaunchKernelGGL(k_gather_lds, dim3((c + ch - 1) / ch, b), dim3(kStageThreads),
+                           (size_t)ch * n * 4, (hipStream_t)stream, d_feat, c, n, d_idx, g, ch, d_out, d_bad);
+    } else {
+        hipLaunchKernelGGL(k_gather, grid_rows(g, (int64_t)b * c), dim3(256), 0, (hipStream_t)stream, d_feat,
+                           c, n, d_idx, g, (int64_t)b * c, d_out, d_bad);
+    }
     return hip_status(hipGetLastError(), "k_gather");
 }
 
@@ -381,8 +458,16 @@ int32_t ssf_pn2_three_interpolate(void* stream, int32_t b, int32_t c, int32_t m,
         return fail(SSF_PN2_E_ARG, "three_interpolate: bad arguments");
     const int64_t total = (int64_t)b * c * n;
     if (total == 0) return SSF_PN2_OK;
-    hipLaunchKernelGGL(k_three_interp, grid_rows(n, (int64_t)b * c), dim3(256), 0, (hipStream_t)stream,
-                       d_feat, c, m, d_idx, d_weight, n, (int64_t)b * c, d_out, d_bad);
+    if (m <= kStageFloats && b <= 65535) {
+        if (hipError_t e = allow_stage_lds(); e != hipSuccess) return hip_status(e, "three_interpolate: LDS limit");
+        const int ch = min(c, kStageFloats / m);
+        hipLaunchKernelGGL(k_three_interp_lds, dim3((c + ch - 1) / ch, b), dim3(kStageThreads),
+                           (size_t)ch * m * 4, (hipStream_t)stream, d_feat, c, m, d_idx, d_weight, n, ch,
+                           d_out, d_bad);
+    } else {
+        hipLaunchKernelGGL(k_three_interp, grid_rows(n, (int64_t)b * c), dim3(256), 0, (hipStream_t)stream,
+                           d_feat, c, m, d_idx, d_weight, n, (int64_t)b * c, d_out, d_bad);
+    }
     return hip_status(hipGetLastError(), "k_three_interp");
 }
 

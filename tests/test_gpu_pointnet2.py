@@ -138,3 +138,23 @@ def test_upsample_vs_oracle(dev, oracle, k, s, n, c):
     sf = (rng.standard_normal((2, c, s)) * 60).astype(np.float32)   # some sums hit the +-100 clamp
     got = P.upsample_flow(_t(xyz, dev), _t(sxyz, dev), _t(sf, dev), k=k).cpu().numpy()
     assert np.array_equal(got, oracle.pn2_upsample_flow(xyz, sxyz, sf, k=k))
+
+
+@pytest.mark.parametrize("c,n,s,k", [(35, 8192, 2048, 16), (3, 40000, 512, 8), (130, 300, 77, 5)])
+def test_group_staging_paths_vs_oracle(dev, oracle, c, n, s, k):
+    """LDS-staged rows (channel groups not dividing C) and the global fallback (n > 36864)"""
+    from ssf import pointnet2 as P
+    rng = np.random.default_rng(c + n)
+    feat = rng.standard_normal((2, c, n)).astype(np.float32)
+    idx = rng.integers(0, n, (2, s, k)).astype(np.int32)
+    out = P.grouping_operation(_t(feat, dev), _t(idx, dev), check=True).cpu().numpy()
+    assert np.array_equal(out, oracle.pn2_gather(feat, idx))
+    g1 = P.gather_operation(_t(feat, dev), _t(idx[:, :, 0], dev), check=True).cpu().numpy()
+    assert np.array_equal(g1, oracle.pn2_gather(feat, np.ascontiguousarray(idx[:, :, 0])))
+    i3 = rng.integers(0, n, (2, s, 3)).astype(np.int32)
+    w3 = rng.uniform(0, 1, (2, s, 3)).astype(np.float32)
+    got = P.three_interpolate(_t(feat, dev), _t(i3, dev), _t(w3, dev), check=True).cpu().numpy()
+    assert np.array_equal(got, oracle.pn2_three_interpolate(feat, i3, w3))
+    i3[0, 1, 1] = -1
+    with pytest.raises(ValueError):
+        P.three_interpolate(_t(feat, dev), _t(i3, dev), _t(w3, dev), check=True)

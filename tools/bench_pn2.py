@@ -69,9 +69,16 @@ def main():
     ms = timed(lambda: P.knn(K, new_xyz, xyz), a.reps)
     res["knn"] = dict(ms=ms, pairs_per_s=B * S * N / ms * 1e3, bound="VALU (brute force)")
     ms = timed(lambda: P.grouping_operation(feat, idx), a.reps)
-    by = B * C * S * K * 4 * 2 + B * S * K * 4       # gathered reads + writes + indices
+    by = B * C * N * 4 + B * S * K * 4 + B * C * S * K * 4   # feature map + indices read once, output written
     res["grouping_operation"] = dict(ms=ms, bytes=by, gbs=by / ms / 1e6,
                                      frac=by / ms / 1e6 / HBM_PEAK, bound="hbm")
+    i3 = torch.randint(0, S, (B, N, 3), device=dev, dtype=torch.int32)
+    w3 = torch.rand(B, N, 3, device=dev)
+    sfeat = torch.randn(B, 64, S, device=dev)
+    ms = timed(lambda: P.three_interpolate(sfeat, i3, w3), a.reps)
+    by = B * 64 * S * 4 + B * N * 3 * 8 + B * 64 * N * 4
+    res["three_interpolate"] = dict(ms=ms, bytes=by, gbs=by / ms / 1e6, frac=by / ms / 1e6 / HBM_PEAK,
+                                    bound="hbm", shape=f"C=64, {S} -> {N}")
     ms = timed(lambda: P.upsample_flow(xyz_c, sxyz_c, sflow, k=KU), a.reps)
     res["upsample_flow"] = dict(ms=ms, pairs_per_s=B * N * S / ms * 1e3,
                                 bound="VALU (brute force over the LDS-staged sparse cloud)")

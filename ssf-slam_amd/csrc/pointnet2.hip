@@ -149,6 +149,73 @@ __global__ __launch_bounds__(kFpsThreads) void k_fps(const float* __restrict__ x
     }
 }
 
+// Clouds of up to 8192 points: the same iteration with two points per packed-f32 operation
+// (v_pk_add_f32 / v_pk_mul_f32 on the pairs (j, j + 1)), and only (distance, slot) tracked per
+// thread -- the winner's coordinates are read back from an LDS copy of the cloud after the
+// cross-wave pass instead of being carried through three selects per point.
+typedef float f2v __attribute__((ext_vector_type(2)));
+constexpr int kFpsLdsMax = 8192;
+
+template <int PPT>
+__global__ __launch_bounds__(kFpsThreads) void k_fps_pk(const float* __restrict__ xyz, int n,
+                                                        int npoint, const int32_t* __restrict__ start,
+                                                        int32_t* __restrict__ out) {
+    static_assert(PPT % 2 == 0 && PPT * kFpsThreads <= kFpsLdsMax, "PPT");
+    __shared__ float sx[kFpsLdsMax], sy[kFpsLdsMax], sz[kFpsLdsMax];
+    __shared__ unsigned long long slot[2][kFpsWaves];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float* P = xyz + (int64_t)b * n * 3;
+    int32_t* O = out + (int64_t)b * npoint;
+    f2v px[PPT / 2], py[PPT / 2], pz[PPT / 2];
+    float pd[PPT];
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+        const int i = tid + j * kFpsThreads;
+        const int ic = i < n ? i : n - 1;
+        const float x = P[3 * ic], y = P[3 * ic + 1], z = P[3 * ic + 2];
+        px[j / 2][j % 2] = x; py[j / 2][j % 2] = y; pz[j / 2][j % 2] = z;
+        pd[j] = i < n ? 1e10f : -1.0f;                  // padding never wins (distances >= 0)
+        if (i < n) { sx[i] = x; sy[i] = y; sz[i] = z; }
+    }
+    __syncthreads();
+    int far = start ? min(max(start[b], 0), n - 1) : 0;
+    float cx = sx[far], cy = sy[far], cz = sz[far];
+    for (int it = 0; it < npoint; ++it) {
+        if (tid == 0) O[it] = far;                                   // centroids[:, i] (:84)
+        if (it + 1 == npoint) break;
+        const f2v c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
+        float bd = -1.0f;
+        int bj = 0;
+#pragma unroll
+        for (int h = 0; h < PPT / 2; ++h) {
+            const f2v dx = px[h] - c2x, dy = py[h] - c2y, dz = pz[h] - c2z;
+            const f2v d = (dx * dx + dy * dy) + dz * dz;                       // :86
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int j = 2 * h + e;
+                pd[j] = d[e] < pd[j] ? d[e] : pd[j];                           // :87-88
+                if (pd[j] > bd) { bd = pd[j]; bj = j; }
+            }
+        }
+        unsigned long long key = bd >= 0.0f ? fps_key(bd, tid + bj * kFpsThreads) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long k2 = __shfl_xor(key, o, 64);
+            key = k2 > key ? k2 : key;
+        }
+        if (lane == 0) slot[it & 1][w] = key;
+        __syncthreads();
+        unsigned long long best = slot[it & 1][0];
+#pragma unroll
+        for (int k = 1; k < kFpsWaves; ++k) {
+            const unsigned long long s2 = slot[it & 1][k];
+            best = s2 > best ? s2 : best;
+        }
+        far = 0x7fffffff - (int)(unsigned)(best & 0xffffffffu);             // :89
+        cx = sx[far]; cy = sy[far]; cz = sz[far];
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Exact k-NN (knn_point, utils.py:92-108): for each query of [B, S, 3], the k nearest points of
 // [B, N, 3] by f32 squared distance, ascending, ties to the lower index; outputs sqrt(distance)
@@ -163,13 +230,14 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn(const float* __restrict__ q
                                                      const float* __restrict__ ref, int n, int k,
                                                      float* __restrict__ dist,
                                                      int32_t* __restrict__ idx) {
-    __shared__ float tx[kKnnTile], ty[kKnnTile], tz[kKnnTile];
+    __shared__ __attribute__((aligned(8))) float tx[kKnnTile], ty[kKnnTile], tz[kKnnTile];
     const int b = blockIdx.y;
     const int q = blockIdx.x * kKnnThreads + threadIdx.x;
     const float* Q = query + (int64_t)b * s * 3;
     const float* R = ref + (int64_t)b * n * 3;
     const int qc = q < s ? q : s - 1;
     const float qx = Q[3 * qc], qy = Q[3 * qc + 1], qz = Q[3 * qc + 2];
+    const f2v q2x = {qx, qx}, q2y = {qy, qy}, q2z = {qz, qz};
     double kk[KM];
 #pragma unroll
     for (int j = 0; j < KM; ++j) kk[j] = nn_key(__builtin_inff(), 0x7fffffff);
@@ -180,7 +248,17 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn(const float* __restrict__ q
             tx[j] = R[3 * (t0 + j)]; ty[j] = R[3 * (t0 + j) + 1]; tz[j] = R[3 * (t0 + j) + 2];
         }
         __syncthreads();
-        for (int j = 0; j < nt; ++j) {
+        int j = 0;
+        for (; j + 1 < nt; j += 2) {            // two candidates per packed-f32 operation
+            const f2v dx = *reinterpret_cast<const f2v*>(tx + j) - q2x;
+            const f2v dy = *reinterpret_cast<const f2v*>(ty + j) - q2y;
+            const f2v dz = *reinterpret_cast<const f2v*>(tz + j) - q2z;
+            const f2v d = (dx * dx + dy * dy) + dz * dz;
+            const double k0 = nn_key(d[0], t0 + j), k1 = nn_key(d[1], t0 + j + 1);
+            if (k0 < kk[KM - 1]) nn_insert<KM>(kk, k0);
+            if (k1 < kk[KM - 1]) nn_insert<KM>(kk, k1);
+        }
+        if (j < nt) {
             const double key = nn_key(sq3(tx[j] - qx, ty[j] - qy, tz[j] - qz), t0 + j);
             if (key < kk[KM - 1]) nn_insert<KM>(kk, key);
         }
@@ -322,7 +400,7 @@ __global__ __launch_bounds__(kUpThreads) void k_upsample(const float* __restrict
                                                          const float* __restrict__ sxyz, int s,
                                                          const float* __restrict__ sfeat, int c,
                                                          int k, float* __restrict__ out) {
-    __shared__ float tx[kUpMaxSparse], ty[kUpMaxSparse], tz[kUpMaxSparse];
+    __shared__ __attribute__((aligned(8))) float tx[kUpMaxSparse], ty[kUpMaxSparse], tz[kUpMaxSparse];
     const int b = blockIdx.y;
     const int q = blockIdx.x * kUpThreads + threadIdx.x;
     const float* X = xyz + (int64_t)b * 3 * n;       // [B, 3, N] (the module's input layout)
@@ -336,8 +414,19 @@ __global__ __launch_bounds__(kUpThreads) void k_upsample(const float* __restrict
     double kk[KM];
 #pragma unroll
     for (int j = 0; j < KM; ++j) kk[j] = nn_key(__builtin_inff(), 0x7fffffff);
-    for (int j = 0; j < s; ++j) {
-        const double key = nn_key(sq3(tx[j] - qx, ty[j] - qy, tz[j] - qz), j);
+    const f2v q2x = {qx, qx}, q2y = {qy, qy}, q2z = {qz, qz};
+    int j0 = 0;
+    for (; j0 + 1 < s; j0 += 2) {
+        const f2v dx = *reinterpret_cast<const f2v*>(tx + j0) - q2x;
+        const f2v dy = *reinterpret_cast<const f2v*>(ty + j0) - q2y;
+        const f2v dz = *reinterpret_cast<const f2v*>(tz + j0) - q2z;
+        const f2v d = (dx * dx + dy * dy) + dz * dz;
+        const double k0 = nn_key(d[0], j0), k1 = nn_key(d[1], j0 + 1);
+        if (k0 < kk[KM - 1]) nn_insert<KM>(kk, k0);
+        if (k1 < kk[KM - 1]) nn_insert<KM>(kk, k1);
+    }
+    if (j0 < s) {
+        const double key = nn_key(sq3(tx[j0] - qx, ty[j0] - qy, tz[j0] - qz), j0);
         if (key < kk[KM - 1]) nn_insert<KM>(kk, key);
     }
     int id[KM];
@@ -402,9 +491,9 @@ int32_t ssf_pn2_furthest_point_sample(void* stream, int32_t b, int32_t n, int32_
     if (b == 0 || npoint == 0) return SSF_PN2_OK;
     hipStream_t s = (hipStream_t)stream;
     const int ppt = (n + kFpsThreads - 1) / kFpsThreads;
-    if (ppt <= 4) hipLaunchKernelGGL(k_fps<4>, dim3(b), dim3(kFpsThreads), 0, s, d_xyz, n, npoint, d_start, nullptr, d_idx);
-    else if (ppt <= 8) hipLaunchKernelGGL(k_fps<8>, dim3(b), dim3(kFpsThreads), 0, s, d_xyz, n, npoint, d_start, nullptr, d_idx);
-    else if (ppt <= 16) hipLaunchKernelGGL(k_fps<16>, dim3(b), dim3(kFpsThreads), 0, s, d_xyz, n, npoint, d_start, nullptr, d_idx);
+    if (ppt <= 4) hipLaunchKernelGGL(k_fps_pk<4>, dim3(b), dim3(kFpsThreads), 0, s, d_xyz, n, npoint, d_start, d_idx);
+    else if (ppt <= 8) hipLaunchKernelGGL(k_fps_pk<8>, dim3(b), dim3(kFpsThreads), 0, s, d_xyz, n, npoint, d_start, d_idx);
+    else if (ppt <= 16) hipLaunchKernelGGL(k_fps_pk<16>, dim3(b), dim3(kFpsThreads), 0, s, d_xyz, n, npoint, d_start, d_idx);
     else if (ppt <= 32) hipLaunchKernelGGL(k_fps<32>, dim3(b), dim3(kFpsThreads), 0, s, d_xyz, n, npoint, d_start, nullptr, d_idx);
     else {
         if (!d_temp) return fail(SSF_PN2_E_ARG, "fps: n > 16384 needs d_temp (b * n floats)");

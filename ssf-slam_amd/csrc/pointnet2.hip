@@ -65,7 +65,7 @@ SSF_DEV float sq3(float dx, float dy, float dz) { return (dx * dx + dy * dy) + d
 // Furthest point sampling (utils.py:68-89).  One work-group per cloud; PPT points per thread
 // kept in registers (point t + j * kFpsThreads), with their running min distance.  Iteration i:
 // every thread folds the last centroid into its distances and keeps its best (distance, lowest
-// index); a wave reduction of a u64 key (distance bits : ~index) and a cross-wave pass over an
+// index); a wave reduction to a u64 key (distance bits : ~index) and a cross-wave pass over an
 // LDS slot (double-buffered by iteration parity, so one barrier per iteration) give the next
 // centroid, whose coordinates travel with the key.  torch.max returns the FIRST maximum, hence
 // the lowest index on ties.  PPT == 0: distances live in global scratch (N > 16384).
@@ -76,10 +76,6 @@ struct FpsSlot {
     unsigned long long key;
     float x, y, z, pad;
 };
-
-SSF_DEV unsigned long long fps_key(float d, int idx) {
-    return ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)(0x7fffffff - idx);
-}
 
 template <int PPT>
 __global__ __launch_bounds__(kFpsThreads) void k_fps(const float* __restrict__ xyz, int n,
@@ -126,15 +122,14 @@ __global__ __launch_bounds__(kFpsThreads) void k_fps(const float* __restrict__ x
                 if (t > bd) { bd = t; bi = i; bx = x; by = y; bz = z; }
             }
         }
-        unsigned long long key = bd >= 0.0f ? fps_key(bd, bi) : 0ull;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long k2 = __shfl_xor(key, o, 64);
-            key = k2 > key ? k2 : key;
-        }
-        const unsigned long long mine = bd >= 0.0f ? fps_key(bd, bi) : 0ull;
-        const uint64_t ball = __ballot(mine == key);
-        if (lane == (int)(__builtin_ffsll((long long)ball) - 1)) {
+        // wave (max distance, min index): two 32-bit DPP reductions, as in k_fps_pk below; the
+        // one lane holding the winner writes it with its coordinates
+        const unsigned dbits = bd >= 0.0f ? __float_as_uint(bd) : 0u;
+        const unsigned wmax = __ockl_wfred_max_u32(dbits);
+        const unsigned myidx = bd >= 0.0f ? (unsigned)bi : 0x7fffffffu;
+        const unsigned widx = __ockl_wfred_min_u32(dbits == wmax ? myidx : 0x7fffffffu);
+        const unsigned long long key = ((unsigned long long)wmax << 32) | (0x7fffffffu - widx);
+        if (myidx == widx || (widx == 0x7fffffffu && lane == 0)) {
             slot[it & 1][w] = FpsSlot{key, bx, by, bz, 0.f};
         }
         __syncthreads();
@@ -197,13 +192,15 @@ __global__ __launch_bounds__(kFpsThreads) void k_fps_pk(const float* __restrict_
                 if (pd[j] > bd) { bd = pd[j]; bj = j; }
             }
         }
-        unsigned long long key = bd >= 0.0f ? fps_key(bd, tid + bj * kFpsThreads) : 0ull;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long k2 = __shfl_xor(key, o, 64);
-            key = k2 > key ? k2 : key;
-        }
-        if (lane == 0) slot[it & 1][w] = key;
+        // wave (max distance, min index) in two 32-bit DPP reductions (OCKL wave reduce): the
+        // distance bits first (distances >= 0, so their u32 order is their numeric order;
+        // padding lanes enter as 0 with index 0x7fffffff), then the lowest index among the
+        // lanes holding that maximum
+        const unsigned dbits = bd >= 0.0f ? __float_as_uint(bd) : 0u;
+        const unsigned wmax = __ockl_wfred_max_u32(dbits);
+        const unsigned myidx = bd >= 0.0f ? (unsigned)(tid + bj * kFpsThreads) : 0x7fffffffu;
+        const unsigned widx = __ockl_wfred_min_u32(dbits == wmax ? myidx : 0x7fffffffu);
+        if (lane == 0) slot[it & 1][w] = ((unsigned long long)wmax << 32) | (0x7fffffffu - widx);
         __syncthreads();
         unsigned long long best = slot[it & 1][0];
 #pragma unroll

@@ -64,7 +64,7 @@ def _cloud(rng, b, n, scale=20.0):
     return x
 
 
-@pytest.mark.parametrize("n,npoint", [(8192, 2048), (2048, 512), (700, 700), (20000, 256), (5, 1)])
+@pytest.mark.parametrize("n,npoint", [(8192, 2048), (2048, 512), (700, 700), (12000, 1000), (20000, 256), (5, 1)])
 def test_fps_vs_oracle(dev, oracle, n, npoint):
     from ssf import pointnet2 as P
     rng = np.random.default_rng(n)

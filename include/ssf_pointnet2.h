@@ -59,6 +59,14 @@ int32_t ssf_pn2_three_nn(void* stream, int32_t b, int32_t n, int32_t m, const fl
 int32_t ssf_pn2_gather(void* stream, int32_t b, int32_t c, int32_t n, int32_t g,
                        const float* d_feat, const int32_t* d_idx, float* d_out, int32_t* d_bad);
 
+/* The grouping block of PointNetSetAbstraction.forward (utils/utils.py:228-234) in one call:
+ * out [b, 3 + c, s, k] = cat(grouping(xyz, idx) - new_xyz[..., None], grouping(feat, idx)),
+ * with d_xyz [b, 3, n] (n <= 36864), d_new_xyz [b, 3, s], d_feat [b, c, n] (nullable when
+ * c = 0), d_idx [b, s, k]. */
+int32_t ssf_pn2_group_relative(void* stream, int32_t b, int32_t n, int32_t s, int32_t k, int32_t c,
+                               const float* d_xyz, const float* d_new_xyz, const float* d_feat,
+                               const int32_t* d_idx, float* d_out, int32_t* d_bad);
+
 /* pointutils.three_interpolate(features [b, c, m], idx [b, n, 3], weight [b, n, 3]) ->
  * [b, c, n]: w0 f[i0] + w1 f[i1] + w2 f[i2] (the weighted 3-NN sum of
  * PointNetFeaturePropogation, utils/utils.py:658-663). */

@@ -305,9 +305,14 @@ __global__ __launch_bounds__(256) void k_gather(const float* __restrict__ feat, 
 constexpr int kStageThreads = 1024;
 constexpr int kStageFloats = 36864;        // 144 KiB of LDS
 
+// Output rows go to channel out_c0 + (c0 + k) of an out_c-channel output; center (nullable,
+// [B, c, g / kdiv]) is subtracted from every gathered value of its row (grouped xyz minus the
+// centroid, utils.py:232).
 __global__ __launch_bounds__(kStageThreads) void k_gather_lds(const float* __restrict__ feat, int c,
                                                               int n, const int32_t* __restrict__ idx,
                                                               int g, int ch, float* __restrict__ out,
+                                                              int out_c, int out_c0,
+                                                              const float* __restrict__ center, int kdiv,
                                                               int32_t* __restrict__ bad) {
     extern __shared__ float rows[];
     const int b = blockIdx.y, c0 = blockIdx.x * ch;
@@ -316,11 +321,17 @@ __global__ __launch_bounds__(kStageThreads) void k_gather_lds(const float* __res
     for (int e = threadIdx.x; e < nch * n; e += kStageThreads) rows[e] = F[e];
     __syncthreads();
     const int32_t* I = idx + (int64_t)b * g;
-    float* O = out + ((int64_t)b * c + c0) * g;
+    float* O = out + ((int64_t)b * out_c + out_c0 + c0) * g;
+    const int gc = g / kdiv;
+    const float* CT = center ? center + ((int64_t)b * c + c0) * gc : nullptr;
     for (int j = threadIdx.x; j < g; j += kStageThreads) {
         int i = I[j];
         if ((unsigned)i >= (unsigned)n) { *bad = 1; i = -1; }
-        for (int k = 0; k < nch; ++k) O[(int64_t)k * g + j] = i >= 0 ? rows[k * n + i] : 0.0f;
+        const int jc = j / kdiv;
+        for (int k = 0; k < nch; ++k) {
+            const float v = i >= 0 ? rows[k * n + i] : 0.0f;
+            O[(int64_t)k * g + j] = CT ? v - CT[(int64_t)k * gc + jc] : v;
+        }
     }
 }
 
@@ -529,12 +540,36 @@ int32_t ssf_pn2_gather(void* stream, int32_t b, int32_t c, int32_t n, int32_t g,
         if (hipError_t e = allow_stage_lds(); e != hipSuccess) return hip_status(e, "gather: LDS limit");
         const int ch = min(c, kStageFloats / n);
         hipLaunchKernelGGL(k_gather_lds, dim3((c + ch - 1) / ch, b), dim3(kStageThreads),
-                           (size_t)ch * n * 4, (hipStream_t)stream, d_feat, c, n, d_idx, g, ch, d_out, d_bad);
+                           (size_t)ch * n * 4, (hipStream_t)stream, d_feat, c, n, d_idx, g, ch, d_out, c, 0,
+                           (const float*)nullptr, 1, d_bad);
     } else {
         hipLaunchKernelGGL(k_gather, grid_rows(g, (int64_t)b * c), dim3(256), 0, (hipStream_t)stream, d_feat,
                            c, n, d_idx, g, (int64_t)b * c, d_out, d_bad);
     }
     return hip_status(hipGetLastError(), "k_gather");
+}
+
+int32_t ssf_pn2_group_relative(void* stream, int32_t b, int32_t n, int32_t s, int32_t k, int32_t c,
+                               const float* d_xyz, const float* d_new_xyz, const float* d_feat,
+                               const int32_t* d_idx, float* d_out, int32_t* d_bad) {
+    if (b < 0 || n <= 0 || n > kStageFloats || s < 0 || k <= 0 || c < 0 || (c > 0 && !d_feat) ||
+        !d_xyz || !d_new_xyz || !d_idx || !d_out || !d_bad)
+        return fail(SSF_PN2_E_ARG, "group_relative: bad arguments (0 < n <= 36864)");
+    if (b == 0 || s == 0) return SSF_PN2_OK;
+    if (b > 65535) return fail(SSF_PN2_E_ARG, "group_relative: b > 65535");
+    if (hipError_t e = allow_stage_lds(); e != hipSuccess) return hip_status(e, "group_relative: LDS limit");
+    hipStream_t st = (hipStream_t)stream;
+    const int g = s * k, oc = 3 + c;
+    const int chx = min(3, kStageFloats / n);
+    hipLaunchKernelGGL(k_gather_lds, dim3((3 + chx - 1) / chx, b), dim3(kStageThreads), (size_t)chx * n * 4, st,
+                       d_xyz, 3, n, d_idx, g, chx, d_out, oc, 0, d_new_xyz, k, d_bad);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return hip_status(e, "k_gather_lds (xyz)");
+    if (c > 0) {
+        const int ch = min(c, kStageFloats / n);
+        hipLaunchKernelGGL(k_gather_lds, dim3((c + ch - 1) / ch, b), dim3(kStageThreads), (size_t)ch * n * 4, st,
+                           d_feat, c, n, d_idx, g, ch, d_out, oc, 3, (const float*)nullptr, 1, d_bad);
+    }
+    return hip_status(hipGetLastError(), "k_gather_lds (features)");
 }
 
 int32_t ssf_pn2_three_interpolate(void* stream, int32_t b, int32_t c, int32_t m, int32_t n,

@@ -35,6 +35,7 @@ EXPORTS = [
 PN2_EXPORTS = [
     "ssf_pn2_last_error", "ssf_pn2_furthest_point_sample", "ssf_pn2_knn", "ssf_pn2_three_nn",
     "ssf_pn2_gather", "ssf_pn2_three_interpolate", "ssf_pn2_upsample_flow",
+    "ssf_pn2_group_relative",
 ]
 PN2_KNN_MAX, PN2_UPSAMPLE_MAX_SPARSE = 32, 4096
 
@@ -113,6 +114,7 @@ def lib():
     L.ssf_pn2_gather.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp]
     L.ssf_pn2_three_interpolate.argtypes = [vp, i32, i32, i32, i32, vp, vp, vp, vp, vp]
     L.ssf_pn2_upsample_flow.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp]
+    L.ssf_pn2_group_relative.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]
     for name in PN2_EXPORTS[1:]:
         getattr(L, name).restype = i32
     _lib = L

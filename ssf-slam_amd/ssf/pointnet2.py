@@ -11,6 +11,7 @@ Same names, argument order and layouts as the calls in the reference network:
     three_nn(unknown [B,N,3], known [B,M,3])                utils.py:560  -> (dist, idx) [B,N,3]
     three_interpolate(features [B,C,M], idx, weight)        utils.py:662  -> [B,C,N]
     UpsampleFlow()(xyz [B,3,N], sparse_xyz [B,3,S], sparse_flow [B,C,S], k)  soflow.py:1442
+    group_relative(xyz, new_xyz, points, idx)   utils.py:228-234 (grouping block, fused)
 
 Inputs are CUDA tensors (float32 coordinates/features, integer indices); there is no CPU path.
 Invalid arguments raise ValueError; a failing launch raises SSFError.
@@ -23,7 +24,7 @@ from . import _abi
 from .frontend import _ptr, _stream
 
 __all__ = ["furthest_point_sample", "gather_operation", "knn", "grouping_operation", "three_nn",
-           "three_interpolate", "upsample_flow", "UpsampleFlow"]
+           "three_interpolate", "upsample_flow", "UpsampleFlow", "group_relative"]
 
 
 def _check(rc, what):
@@ -125,6 +126,34 @@ def gather_operation(features, idx, check=False):
 def grouping_operation(features, idx, check=False):
     """pointutils.grouping_operation(features [B,C,N], idx [B,S,K]) -> [B,C,S,K]."""
     return _gather(features, idx, check, "grouping_operation")
+
+
+def group_relative(xyz, new_xyz, points, idx, check=False):
+    """The grouping block of PointNetSetAbstraction.forward (utils.py:228-234), one call:
+    cat([grouping_operation(xyz, idx) - new_xyz.unsqueeze(-1), grouping_operation(points, idx)],
+    dim=1).  xyz [B,3,N] (N <= 36864), new_xyz [B,3,S], points [B,C,N] or None, idx [B,S,K]
+    -> [B, 3 + C, S, K]."""
+    x = _f32(xyz, "xyz", 3)
+    nx = _f32(new_xyz, "new_xyz", 3)
+    ix = _i32(idx, "idx")
+    B, c3, N = x.shape
+    if c3 != 3 or nx.shape[:2] != (B, 3) or ix.dim() != 3 or ix.shape[:2] != (B, nx.shape[2]):
+        raise ValueError("xyz [B,3,N], new_xyz [B,3,S] and idx [B,S,K] expected")
+    S, K = ix.shape[1], ix.shape[2]
+    f = None
+    Cc = 0
+    if points is not None:
+        f = _f32(points, "points", 3)
+        if f.shape[0] != B or f.shape[2] != N:
+            raise ValueError("points must be [B, C, N]")
+        Cc = f.shape[1]
+    out = torch.empty((B, 3 + Cc, S, K), dtype=torch.float32, device=x.device)
+    bad = _bad_flag(x.device)
+    _check(_abi.lib().ssf_pn2_group_relative(_stream(x.device), B, N, S, K, Cc, _ptr(x), _ptr(nx),
+                                             _ptr(f), _ptr(ix), _ptr(out), _ptr(bad)),
+           "group_relative")
+    _raise_if_bad(bad, check, "group_relative")
+    return out
 
 
 def three_interpolate(features, idx, weight, check=False):

@@ -86,3 +86,4 @@ def test_pointnet2_header_symbols_exported_and_arg_checks():
     assert L.ssf_pn2_furthest_point_sample(None, 1, 20000, 4, 1, None, None, 1) == _abi.SSF_E_ARG  # no temp
     assert L.ssf_pn2_upsample_flow(None, 1, 8, 5000, 3, 3, 1, 1, 1, 1) == _abi.SSF_E_ARG  # s > 4096
     assert L.ssf_pn2_gather(None, 1, 1, 4, 4, 1, 1, 1, None) == _abi.SSF_E_ARG
+    assert L.ssf_pn2_group_relative(None, 1, 40000, 4, 4, 0, 1, 1, None, 1, 1, 1) == _abi.SSF_E_ARG  # n too big

@@ -158,3 +158,24 @@ def test_group_staging_paths_vs_oracle(dev, oracle, c, n, s, k):
     i3[0, 1, 1] = -1
     with pytest.raises(ValueError):
         P.three_interpolate(_t(feat, dev), _t(i3, dev), _t(w3, dev), check=True)
+
+
+@pytest.mark.parametrize("c,n,s,k", [(32, 8192, 2048, 16), (0, 2048, 512, 16), (128, 512, 256, 8)])
+def test_group_relative_vs_oracle(dev, oracle, c, n, s, k):
+    """PointNetSetAbstraction grouping block (utils.py:228-234): cat(grouped xyz - centroid,
+    grouped features), bit-exact vs the oracle gathers + one f32 subtraction"""
+    from ssf import pointnet2 as P
+    rng = np.random.default_rng(c + s)
+    xyz = _cloud(rng, 2, n).transpose(0, 2, 1).copy()                    # [B, 3, N]
+    fps = oracle.pn2_fps(np.ascontiguousarray(xyz.transpose(0, 2, 1)), s)
+    new_xyz = oracle.pn2_gather(xyz, fps)                                # [B, 3, S]
+    _, idx = oracle.pn2_knn(k, np.ascontiguousarray(new_xyz.transpose(0, 2, 1)),
+                            np.ascontiguousarray(xyz.transpose(0, 2, 1)))
+    feat = rng.standard_normal((2, c, n)).astype(np.float32) if c else None
+    got = P.group_relative(_t(xyz, dev), _t(new_xyz, dev), None if feat is None else _t(feat, dev),
+                           _t(idx, dev), check=True).cpu().numpy()
+    want = oracle.pn2_gather(xyz, idx) - new_xyz[..., None]
+    if c:
+        want = np.concatenate([want, oracle.pn2_gather(feat, idx)], axis=1)
+    assert got.shape == (2, 3 + c, s, k)
+    assert np.array_equal(got, want)

@@ -72,6 +72,11 @@ def main():
     by = B * C * N * 4 + B * S * K * 4 + B * C * S * K * 4   # feature map + indices read once, output written
     res["grouping_operation"] = dict(ms=ms, bytes=by, gbs=by / ms / 1e6,
                                      frac=by / ms / 1e6 / HBM_PEAK, bound="hbm")
+    pts32 = torch.randn(B, 32, N, device=dev)
+    ms = timed(lambda: P.group_relative(xyz_c, sxyz_c, pts32, idx), a.reps)
+    by = B * 35 * N * 4 + B * 3 * S * 4 + B * S * K * 4 * 2 + B * 35 * S * K * 4
+    res["group_relative"] = dict(ms=ms, bytes=by, gbs=by / ms / 1e6, frac=by / ms / 1e6 / HBM_PEAK,
+                                 bound="hbm", shape=f"sa1: [B, 3+32, {S}, {K}] from {N} points")
     i3 = torch.randint(0, S, (B, N, 3), device=dev, dtype=torch.int32)
     w3 = torch.rand(B, N, 3, device=dev)
     sfeat = torch.randn(B, 64, S, device=dev)

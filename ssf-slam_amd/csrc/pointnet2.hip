@@ -222,14 +222,14 @@ __global__ __launch_bounds__(kFpsThreads) void k_fps_pk(const float* __restrict_
 constexpr int kKnnThreads = 256;
 constexpr int kKnnTile = 2048;
 
-template <int KM>
-__global__ __launch_bounds__(kKnnThreads) void k_knn(const float* __restrict__ query, int s,
+template <int KM, int TPB>
+__global__ __launch_bounds__(TPB) void k_knn(const float* __restrict__ query, int s,
                                                      const float* __restrict__ ref, int n, int k,
                                                      float* __restrict__ dist,
                                                      int32_t* __restrict__ idx) {
     __shared__ __attribute__((aligned(8))) float tx[kKnnTile], ty[kKnnTile], tz[kKnnTile];
     const int b = blockIdx.y;
-    const int q = blockIdx.x * kKnnThreads + threadIdx.x;
+    const int q = blockIdx.x * TPB + threadIdx.x;
     const float* Q = query + (int64_t)b * s * 3;
     const float* R = ref + (int64_t)b * n * 3;
     const int qc = q < s ? q : s - 1;
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn(const float* __restrict__ q
     for (int t0 = 0; t0 < n; t0 += kKnnTile) {
         const int nt = min(kKnnTile, n - t0);
         __syncthreads();
-        for (int j = threadIdx.x; j < nt; j += kKnnThreads) {
+        for (int j = threadIdx.x; j < nt; j += TPB) {
             tx[j] = R[3 * (t0 + j)]; ty[j] = R[3 * (t0 + j) + 1]; tz[j] = R[3 * (t0 + j) + 2];
         }
         __syncthreads();
@@ -261,6 +261,74 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn(const float* __restrict__ q
         }
     }
     if (q >= s) return;
+    const int64_t o = ((int64_t)b * s + q) * k;
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+        if (j < k) {
+            const bool have = j < n;
+            dist[o + j] = have ? __builtin_sqrtf(nn_dist(kk[j])) : 0.0f;
+            idx[o + j] = have ? nn_index(kk[j]) : 0;
+        }
+    }
+}
+
+// Small batches (the live node runs one cloud): 64 queries per work-group and W waves that each
+// scan 1/W of every LDS tile, then wave 0 merges the W sorted partial lists from LDS.  Keys
+// order (distance, index) totally, so the merged list is exactly the sequential scan's.
+template <int KM, int W>
+__global__ __launch_bounds__(64 * W) void k_knn_split(const float* __restrict__ query, int s,
+                                                      const float* __restrict__ ref, int n, int k,
+                                                      float* __restrict__ dist,
+                                                      int32_t* __restrict__ idx) {
+    __shared__ __attribute__((aligned(8))) float tx[kKnnTile], ty[kKnnTile], tz[kKnnTile];
+    __shared__ double part[W - 1][KM][64];
+    const int b = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int q = blockIdx.x * 64 + lane;
+    const float* Q = query + (int64_t)b * s * 3;
+    const float* R = ref + (int64_t)b * n * 3;
+    const int qc = q < s ? q : s - 1;
+    const float qx = Q[3 * qc], qy = Q[3 * qc + 1], qz = Q[3 * qc + 2];
+    const f2v q2x = {qx, qx}, q2y = {qy, qy}, q2z = {qz, qz};
+    double kk[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) kk[j] = nn_key(__builtin_inff(), 0x7fffffff);
+    constexpr int kSlice = kKnnTile / W;                     // even: pairs never straddle slices
+    for (int t0 = 0; t0 < n; t0 += kKnnTile) {
+        const int nt = min(kKnnTile, n - t0);
+        __syncthreads();
+        for (int j = threadIdx.x; j < nt; j += 64 * W) {
+            tx[j] = R[3 * (t0 + j)]; ty[j] = R[3 * (t0 + j) + 1]; tz[j] = R[3 * (t0 + j) + 2];
+        }
+        __syncthreads();
+        const int j1 = min(nt, (w + 1) * kSlice);
+        int j = w * kSlice;
+        for (; j + 1 < j1; j += 2) {
+            const f2v dx = *reinterpret_cast<const f2v*>(tx + j) - q2x;
+            const f2v dy = *reinterpret_cast<const f2v*>(ty + j) - q2y;
+            const f2v dz = *reinterpret_cast<const f2v*>(tz + j) - q2z;
+            const f2v d = (dx * dx + dy * dy) + dz * dz;
+            const double k0 = nn_key(d[0], t0 + j), k1 = nn_key(d[1], t0 + j + 1);
+            if (k0 < kk[KM - 1]) nn_insert<KM>(kk, k0);
+            if (k1 < kk[KM - 1]) nn_insert<KM>(kk, k1);
+        }
+        if (j < j1) {
+            const double key = nn_key(sq3(tx[j] - qx, ty[j] - qy, tz[j] - qz), t0 + j);
+            if (key < kk[KM - 1]) nn_insert<KM>(kk, key);
+        }
+    }
+    if (w > 0) {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) part[w - 1][j][lane] = kk[j];
+    }
+    __syncthreads();
+    if (w != 0 || q >= s) return;
+    for (int v = 0; v < W - 1; ++v) {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            const double key = part[v][j][lane];
+            if (key < kk[KM - 1]) nn_insert<KM>(kk, key);
+        }
+    }
     const int64_t o = ((int64_t)b * s + q) * k;
 #pragma unroll
     for (int j = 0; j < KM; ++j) {
@@ -403,17 +471,17 @@ __global__ __launch_bounds__(256) void k_three_interp(const float* __restrict__ 
 constexpr int kUpThreads = 256;
 constexpr int kUpMaxSparse = 4096;
 
-template <int KM>
-__global__ __launch_bounds__(kUpThreads) void k_upsample(const float* __restrict__ xyz, int n,
+template <int KM, int TPB>
+__global__ __launch_bounds__(TPB) void k_upsample(const float* __restrict__ xyz, int n,
                                                          const float* __restrict__ sxyz, int s,
                                                          const float* __restrict__ sfeat, int c,
                                                          int k, float* __restrict__ out) {
     __shared__ __attribute__((aligned(8))) float tx[kUpMaxSparse], ty[kUpMaxSparse], tz[kUpMaxSparse];
     const int b = blockIdx.y;
-    const int q = blockIdx.x * kUpThreads + threadIdx.x;
+    const int q = blockIdx.x * TPB + threadIdx.x;
     const float* X = xyz + (int64_t)b * 3 * n;       // [B, 3, N] (the module's input layout)
     const float* SX = sxyz + (int64_t)b * 3 * s;     // [B, 3, S]
-    for (int j = threadIdx.x; j < s; j += kUpThreads) {
+    for (int j = threadIdx.x; j < s; j += TPB) {
         tx[j] = SX[j]; ty[j] = SX[s + j]; tz[j] = SX[2 * s + j];
     }
     __syncthreads();
@@ -480,6 +548,14 @@ hipError_t allow_stage_lds() {
     return once;
 }
 
+// Channels per staging work-group: as many as fit in LDS, but few enough that the launch has
+// about 512 work-groups (a single cloud with wide feature maps would otherwise run on a few CUs).
+int stage_channels(int c, int b, int row) {
+    const int fit = kStageFloats / row;
+    const int want = (int)(((int64_t)c * b + 511) / 512);
+    return max(1, min(c, min(fit, want)));
+}
+
 dim3 grid_rows(int64_t per_row, int64_t rows) {
     const int64_t gx = (per_row + 255) / 256;
     return dim3((unsigned)(gx < 4096 ? (gx > 0 ? gx : 1) : 4096), (unsigned)(rows < 65535 ? rows : 65535));
@@ -517,11 +593,21 @@ int32_t ssf_pn2_knn(void* stream, int32_t b, int32_t s_q, int32_t n, int32_t k,
     if (b == 0 || s_q == 0) return SSF_PN2_OK;
     if (b > 65535) return fail(SSF_PN2_E_ARG, "knn: b > 65535");
     hipStream_t st = (hipStream_t)stream;
-    const dim3 grid((s_q + kKnnThreads - 1) / kKnnThreads, b);
-    if (k <= 4) hipLaunchKernelGGL(k_knn<4>, grid, dim3(kKnnThreads), 0, st, d_query, s_q, d_ref, n, k, d_dist, d_idx);
-    else if (k <= 8) hipLaunchKernelGGL(k_knn<8>, grid, dim3(kKnnThreads), 0, st, d_query, s_q, d_ref, n, k, d_dist, d_idx);
-    else if (k <= 16) hipLaunchKernelGGL(k_knn<16>, grid, dim3(kKnnThreads), 0, st, d_query, s_q, d_ref, n, k, d_dist, d_idx);
-    else hipLaunchKernelGGL(k_knn<32>, grid, dim3(kKnnThreads), 0, st, d_query, s_q, d_ref, n, k, d_dist, d_idx);
+    // small batches (the live node runs one cloud): the reference set is split over the waves
+    // of a work-group (8 waves, 4 for k > 16) and the partial lists merged in LDS
+    if ((int64_t)b * ((s_q + kKnnThreads - 1) / kKnnThreads) < 512) {
+        const dim3 grid((s_q + 63) / 64, b);
+        if (k <= 4) hipLaunchKernelGGL((k_knn_split<4, 8>), grid, dim3(512), 0, st, d_query, s_q, d_ref, n, k, d_dist, d_idx);
+        else if (k <= 8) hipLaunchKernelGGL((k_knn_split<8, 8>), grid, dim3(512), 0, st, d_query, s_q, d_ref, n, k, d_dist, d_idx);
+        else if (k <= 16) hipLaunchKernelGGL((k_knn_split<16, 8>), grid, dim3(512), 0, st, d_query, s_q, d_ref, n, k, d_dist, d_idx);
+        else hipLaunchKernelGGL((k_knn_split<32, 4>), grid, dim3(256), 0, st, d_query, s_q, d_ref, n, k, d_dist, d_idx);
+    } else {
+        const dim3 grid((s_q + kKnnThreads - 1) / kKnnThreads, b);
+        if (k <= 4) hipLaunchKernelGGL((k_knn<4, kKnnThreads>), grid, dim3(kKnnThreads), 0, st, d_query, s_q, d_ref, n, k, d_dist, d_idx);
+        else if (k <= 8) hipLaunchKernelGGL((k_knn<8, kKnnThreads>), grid, dim3(kKnnThreads), 0, st, d_query, s_q, d_ref, n, k, d_dist, d_idx);
+        else if (k <= 16) hipLaunchKernelGGL((k_knn<16, kKnnThreads>), grid, dim3(kKnnThreads), 0, st, d_query, s_q, d_ref, n, k, d_dist, d_idx);
+        else hipLaunchKernelGGL((k_knn<32, kKnnThreads>), grid, dim3(kKnnThreads), 0, st, d_query, s_q, d_ref, n, k, d_dist, d_idx);
+    }
     return hip_status(hipGetLastError(), "k_knn");
 }
 
@@ -538,7 +624,7 @@ int32_t ssf_pn2_gather(void* stream, int32_t b, int32_t c, int32_t n, int32_t g,
     if (total == 0) return SSF_PN2_OK;
     if (n <= kStageFloats && b <= 65535) {
         if (hipError_t e = allow_stage_lds(); e != hipSuccess) return hip_status(e, "gather: LDS limit");
-        const int ch = min(c, kStageFloats / n);
+        const int ch = stage_channels(c, b, n);
         hipLaunchKernelGGL(k_gather_lds, dim3((c + ch - 1) / ch, b), dim3(kStageThreads),
                            (size_t)ch * n * 4, (hipStream_t)stream, d_feat, c, n, d_idx, g, ch, d_out, c, 0,
                            (const float*)nullptr, 1, d_bad);
@@ -560,12 +646,12 @@ int32_t ssf_pn2_group_relative(void* stream, int32_t b, int32_t n, int32_t s, in
     if (hipError_t e = allow_stage_lds(); e != hipSuccess) return hip_status(e, "group_relative: LDS limit");
     hipStream_t st = (hipStream_t)stream;
     const int g = s * k, oc = 3 + c;
-    const int chx = min(3, kStageFloats / n);
+    const int chx = stage_channels(3, b, n);
     hipLaunchKernelGGL(k_gather_lds, dim3((3 + chx - 1) / chx, b), dim3(kStageThreads), (size_t)chx * n * 4, st,
                        d_xyz, 3, n, d_idx, g, chx, d_out, oc, 0, d_new_xyz, k, d_bad);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return hip_status(e, "k_gather_lds (xyz)");
     if (c > 0) {
-        const int ch = min(c, kStageFloats / n);
+        const int ch = stage_channels(c, b, n);
         hipLaunchKernelGGL(k_gather_lds, dim3((c + ch - 1) / ch, b), dim3(kStageThreads), (size_t)ch * n * 4, st,
                            d_feat, c, n, d_idx, g, ch, d_out, oc, 3, (const float*)nullptr, 1, d_bad);
     }
@@ -581,7 +667,7 @@ int32_t ssf_pn2_three_interpolate(void* stream, int32_t b, int32_t c, int32_t m,
     if (total == 0) return SSF_PN2_OK;
     if (m <= kStageFloats && b <= 65535) {
         if (hipError_t e = allow_stage_lds(); e != hipSuccess) return hip_status(e, "three_interpolate: LDS limit");
-        const int ch = min(c, kStageFloats / m);
+        const int ch = stage_channels(c, b, m);
         hipLaunchKernelGGL(k_three_interp_lds, dim3((c + ch - 1) / ch, b), dim3(kStageThreads),
                            (size_t)ch * m * 4, (hipStream_t)stream, d_feat, c, m, d_idx, d_weight, n, ch,
                            d_out, d_bad);
@@ -601,10 +687,17 @@ int32_t ssf_pn2_upsample_flow(void* stream, int32_t b, int32_t n, int32_t s, int
     if (b == 0 || n == 0) return SSF_PN2_OK;
     if (b > 65535) return fail(SSF_PN2_E_ARG, "upsample_flow: b > 65535");
     hipStream_t st = (hipStream_t)stream;
-    const dim3 grid((n + kUpThreads - 1) / kUpThreads, b);
-    if (k <= 4) hipLaunchKernelGGL(k_upsample<4>, grid, dim3(kUpThreads), 0, st, d_xyz, n, d_sparse_xyz, s, d_sparse_feat, c, k, d_out);
-    else if (k <= 8) hipLaunchKernelGGL(k_upsample<8>, grid, dim3(kUpThreads), 0, st, d_xyz, n, d_sparse_xyz, s, d_sparse_feat, c, k, d_out);
-    else hipLaunchKernelGGL(k_upsample<16>, grid, dim3(kUpThreads), 0, st, d_xyz, n, d_sparse_xyz, s, d_sparse_feat, c, k, d_out);
+    if ((int64_t)b * ((n + kUpThreads - 1) / kUpThreads) < 512) {
+        const dim3 grid((n + 63) / 64, b);
+        if (k <= 4) hipLaunchKernelGGL((k_upsample<4, 64>), grid, dim3(64), 0, st, d_xyz, n, d_sparse_xyz, s, d_sparse_feat, c, k, d_out);
+        else if (k <= 8) hipLaunchKernelGGL((k_upsample<8, 64>), grid, dim3(64), 0, st, d_xyz, n, d_sparse_xyz, s, d_sparse_feat, c, k, d_out);
+        else hipLaunchKernelGGL((k_upsample<16, 64>), grid, dim3(64), 0, st, d_xyz, n, d_sparse_xyz, s, d_sparse_feat, c, k, d_out);
+    } else {
+        const dim3 grid((n + kUpThreads - 1) / kUpThreads, b);
+        if (k <= 4) hipLaunchKernelGGL((k_upsample<4, kUpThreads>), grid, dim3(kUpThreads), 0, st, d_xyz, n, d_sparse_xyz, s, d_sparse_feat, c, k, d_out);
+        else if (k <= 8) hipLaunchKernelGGL((k_upsample<8, kUpThreads>), grid, dim3(kUpThreads), 0, st, d_xyz, n, d_sparse_xyz, s, d_sparse_feat, c, k, d_out);
+        else hipLaunchKernelGGL((k_upsample<16, kUpThreads>), grid, dim3(kUpThreads), 0, st, d_xyz, n, d_sparse_xyz, s, d_sparse_feat, c, k, d_out);
+    }
     return hip_status(hipGetLastError(), "k_upsample");
 }
 

@@ -179,3 +179,20 @@ def test_group_relative_vs_oracle(dev, oracle, c, n, s, k):
         want = np.concatenate([want, oracle.pn2_gather(feat, idx)], axis=1)
     assert got.shape == (2, 3 + c, s, k)
     assert np.array_equal(got, want)
+
+
+def test_large_batch_launch_paths_vs_oracle(dev, oracle):
+    """b * ceil(s / 256) >= 512: the 256-thread k-NN / UpsampleFlow launches (the small-batch
+    64-thread ones are covered above)"""
+    from ssf import pointnet2 as P
+    rng = np.random.default_rng(64)
+    ref = _cloud(rng, 64, 512)
+    q = _cloud(rng, 64, 2048)
+    d, i = P.knn(16, _t(q, dev), _t(ref, dev))
+    od, oi = oracle.pn2_knn(16, q, ref)
+    assert np.array_equal(i.cpu().numpy(), oi) and np.array_equal(d.cpu().numpy(), od)
+    xyz = _cloud(rng, 64, 2048).transpose(0, 2, 1).copy()
+    sxyz = _cloud(rng, 64, 128).transpose(0, 2, 1).copy()
+    sf = rng.standard_normal((64, 2, 128)).astype(np.float32)
+    got = P.upsample_flow(_t(xyz, dev), _t(sxyz, dev), _t(sf, dev), k=3).cpu().numpy()
+    assert np.array_equal(got, oracle.pn2_upsample_flow(xyz, sxyz, sf, k=3))

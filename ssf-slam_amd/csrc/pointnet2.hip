@@ -151,13 +151,13 @@ __global__ __launch_bounds__(kFpsThreads) void k_fps(const float* __restrict__ x
 typedef float f2v __attribute__((ext_vector_type(2)));
 constexpr int kFpsLdsMax = 8192;
 
-template <int PPT>
-__global__ __launch_bounds__(kFpsThreads) void k_fps_pk(const float* __restrict__ xyz, int n,
+template <int PPT, int TPB>
+__global__ __launch_bounds__(TPB) void k_fps_pk(const float* __restrict__ xyz, int n,
                                                         int npoint, const int32_t* __restrict__ start,
                                                         int32_t* __restrict__ out) {
-    static_assert(PPT % 2 == 0 && PPT * kFpsThreads <= kFpsLdsMax, "PPT");
+    static_assert(PPT % 2 == 0 && PPT * TPB <= kFpsLdsMax, "PPT");
     __shared__ float sx[kFpsLdsMax], sy[kFpsLdsMax], sz[kFpsLdsMax];
-    __shared__ unsigned long long slot[2][kFpsWaves];
+    __shared__ unsigned long long slot[2][TPB / 64];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const float* P = xyz + (int64_t)b * n * 3;
     int32_t* O = out + (int64_t)b * npoint;
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kFpsThreads) void k_fps_pk(const float* __restrict_
     float pd[PPT];
 #pragma unroll
     for (int j = 0; j < PPT; ++j) {
-        const int i = tid + j * kFpsThreads;
+        const int i = tid + j * TPB;
         const int ic = i < n ? i : n - 1;
         const float x = P[3 * ic], y = P[3 * ic + 1], z = P[3 * ic + 2];
         px[j / 2][j % 2] = x; py[j / 2][j % 2] = y; pz[j / 2][j % 2] = z;
@@ -198,13 +198,13 @@ __global__ __launch_bounds__(kFpsThreads) void k_fps_pk(const float* __restrict_
         // lanes holding that maximum
         const unsigned dbits = bd >= 0.0f ? __float_as_uint(bd) : 0u;
         const unsigned wmax = __ockl_wfred_max_u32(dbits);
-        const unsigned myidx = bd >= 0.0f ? (unsigned)(tid + bj * kFpsThreads) : 0x7fffffffu;
+        const unsigned myidx = bd >= 0.0f ? (unsigned)(tid + bj * TPB) : 0x7fffffffu;
         const unsigned widx = __ockl_wfred_min_u32(dbits == wmax ? myidx : 0x7fffffffu);
         if (lane == 0) slot[it & 1][w] = ((unsigned long long)wmax << 32) | (0x7fffffffu - widx);
         __syncthreads();
         unsigned long long best = slot[it & 1][0];
 #pragma unroll
-        for (int k = 1; k < kFpsWaves; ++k) {
+        for (int k = 1; k < TPB / 64; ++k) {
             const unsigned long long s2 = slot[it & 1][k];
             best = s2 > best ? s2 : best;
         }
@@ -575,9 +575,8 @@ int32_t ssf_pn2_furthest_point_sample(void* stream, int32_t b, int32_t n, int32_
     if (b == 0 || npoint == 0) return SSF_PN2_OK;
     hipStream_t s = (hipStream_t)stream;
     const int ppt = (n + kFpsThreads - 1) / kFpsThreads;
-    if (ppt <= 4) hipLaunchKernelGGL(k_fps_pk<4>, dim3(b), dim3(kFpsThreads), 0, s, d_xyz, n, npoint, d_start, d_idx);
-    else if (ppt <= 8) hipLaunchKernelGGL(k_fps_pk<8>, dim3(b), dim3(kFpsThreads), 0, s, d_xyz, n, npoint, d_start, d_idx);
-    else if (ppt <= 16) hipLaunchKernelGGL(k_fps_pk<16>, dim3(b), dim3(kFpsThreads), 0, s, d_xyz, n, npoint, d_start, d_idx);
+    if (n <= 4096) hipLaunchKernelGGL((k_fps_pk<16, 256>), dim3(b), dim3(256), 0, s, d_xyz, n, npoint, d_start, d_idx);
+    else if (n <= 8192) hipLaunchKernelGGL((k_fps_pk<32, 256>), dim3(b), dim3(256), 0, s, d_xyz, n, npoint, d_start, d_idx);
     else if (ppt <= 32) hipLaunchKernelGGL(k_fps<32>, dim3(b), dim3(kFpsThreads), 0, s, d_xyz, n, npoint, d_start, nullptr, d_idx);
     else {
         if (!d_temp) return fail(SSF_PN2_E_ARG, "fps: n > 16384 needs d_temp (b * n floats)");

@@ -10,6 +10,12 @@
 //   grouping_operation     <- index_points_group      utils/soflow.py:21-32 ([B,C,N] layout)
 //   three_interpolate      <- the weighted 3-NN sum   utils/utils.py:658-663
 //   upsample_flow (fused)  <- UpsampleFlow.forward    utils/soflow.py:1442-1470
+//   group_relative (fused) <- the grouping block of PointNetSetAbstraction.forward, utils.py:228-234
+//
+// Kernels (DESIGN.md §5 has their measured rates): k_fps_pk / k_fps (one work-group per cloud,
+// packed-f32 distances, DPP wave reductions), k_knn / k_knn_split (brute-force exact k-NN over
+// LDS tiles; the split variant spreads one cloud's reference set over 8 waves), k_gather_lds /
+// k_three_interp_lds (feature rows staged in LDS) with global fallbacks, k_upsample (fused).
 //
 // Layouts are the extension's: coordinates [B, N, 3] ("xyz_t"), features [B, C, N], indices
 // int32.  Every entry point is stateless and asynchronous on the caller's stream.
@@ -62,13 +68,14 @@ SSF_DEV void nn_insert(double (&kk)[K], double key) {
 SSF_DEV float sq3(float dx, float dy, float dz) { return (dx * dx + dy * dy) + dz * dz; }
 
 // ------------------------------------------------------------------------------------------
-// Furthest point sampling (utils.py:68-89).  One work-group per cloud; PPT points per thread
-// kept in registers (point t + j * kFpsThreads), with their running min distance.  Iteration i:
-// every thread folds the last centroid into its distances and keeps its best (distance, lowest
-// index); a wave reduction to a u64 key (distance bits : ~index) and a cross-wave pass over an
-// LDS slot (double-buffered by iteration parity, so one barrier per iteration) give the next
-// centroid, whose coordinates travel with the key.  torch.max returns the FIRST maximum, hence
-// the lowest index on ties.  PPT == 0: distances live in global scratch (N > 16384).
+// Furthest point sampling (utils.py:68-89), clouds of more than 8192 points (k_fps_pk below
+// takes the smaller ones).  One work-group per cloud; PPT points per thread kept in registers
+// (point t + j * kFpsThreads), with their running min distance.  Iteration i: every thread folds
+// the last centroid into its distances and keeps its best (distance, lowest index); a wave
+// reduction to a u64 key (distance bits : ~index) and a cross-wave pass over an LDS slot
+// (double-buffered by iteration parity, so one barrier per iteration) give the next centroid,
+// whose coordinates travel with the key.  torch.max returns the FIRST maximum, hence the lowest
+// index on ties.  PPT == 0: distances live in global scratch (N > 16384).
 constexpr int kFpsThreads = 512;
 constexpr int kFpsWaves = kFpsThreads / 64;
 

@@ -87,3 +87,15 @@ def test_pointnet2_header_symbols_exported_and_arg_checks():
     assert L.ssf_pn2_upsample_flow(None, 1, 8, 5000, 3, 3, 1, 1, 1, 1) == _abi.SSF_E_ARG  # s > 4096
     assert L.ssf_pn2_gather(None, 1, 1, 4, 4, 1, 1, 1, None) == _abi.SSF_E_ARG
     assert L.ssf_pn2_group_relative(None, 1, 40000, 4, 4, 0, 1, 1, None, 1, 1, 1) == _abi.SSF_E_ARG  # n too big
+
+
+def test_pointnet2_python_mirror_rejects_host_tensors():
+    """ssf.pointnet2 has no CPU path: host tensors are refused before any library call"""
+    import torch
+    from ssf import pointnet2 as P
+    x = torch.zeros(1, 8, 3)
+    for call in (lambda: P.furthest_point_sample(x, 4), lambda: P.knn(3, x, x),
+                 lambda: P.three_nn(x, x), lambda: P.gather_operation(torch.zeros(1, 2, 8), torch.zeros(1, 4)),
+                 lambda: P.upsample_flow(torch.zeros(1, 3, 8), torch.zeros(1, 3, 4), torch.zeros(1, 3, 4))):
+        with pytest.raises(ValueError, match="CUDA"):
+            call()

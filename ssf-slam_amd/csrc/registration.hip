@@ -988,7 +988,7 @@ SSF_DEV void evaluate_with(Get get, int n, const double q[4], const double t[3],
             for (int v = u; v < 6; ++v) ne[k++] += rho1 * J[u] * J[v];
         }
     }
-    block_sum<kNE>(ne, lds);
+    block_sum_rs<kNE>(ne, lds);
 #pragma unroll
     for (int k = 0; k < kNE; ++k) ne[k] *= 2.0;
 }

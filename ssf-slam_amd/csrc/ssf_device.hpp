@@ -50,6 +50,43 @@ SSF_DEV void block_sum(double (&v)[N], double* lds) {
     __syncthreads();
 }
 
+// Deterministic block sum of N <= 32 doubles per thread, reduce-scatter form: five butterfly
+// steps halve the values each lane carries (32 shuffled doubles instead of 6 N), lane L ends
+// with value L >> 1 summed over its 32-lane half, one more step completes the wave; lane pairs
+// write their value to LDS, thread k < N adds the waves in index order, every thread reads the
+// N totals.  lds must hold (blockDim/64) * N doubles.  Same fixed order on every run.
+template <int N>
+SSF_DEV void block_sum_rs(double (&v)[N], double* lds) {
+    static_assert(N <= 32, "block_sum_rs: N <= 32");
+    const int lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    double a[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) a[i] = i < N ? v[i] : 0.0;
+#pragma unroll
+    for (int h = 16, bit = 32; h >= 1; h >>= 1, bit >>= 1) {
+        const bool up = (lane & bit) != 0;
+#pragma unroll
+        for (int i = 0; i < h; ++i) {
+            const double keep = up ? a[h + i] : a[i];
+            const double send = up ? a[i] : a[h + i];
+            a[i] = keep + __shfl_xor(send, bit, kWave);
+        }
+    }
+    a[0] += __shfl_xor(a[0], 1, kWave);
+    const int idx = lane >> 1;
+    if ((lane & 1) == 0 && idx < N) lds[w * N + idx] = a[0];
+    __syncthreads();
+    if (threadIdx.x < N) {
+        double s = 0.0;
+        for (int i = 0; i < nw; ++i) s += lds[i * N + threadIdx.x];
+        lds[threadIdx.x] = s;                  // only this thread reads slot threadIdx.x
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = lds[k];
+    __syncthreads();
+}
+
 template <typename T>
 SSF_DEV T block_sum_scalar(T x, T* lds) {
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;

@@ -475,7 +475,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             load_x(P, Fl, i, x);
             accum_kabsch(k, x, cs, cd);
         }
-        block_sum<16>(k, red);
+        block_sum_rs<16>(k, red);
         if (tid == 0) {
             for (int i = 0; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
             for (int i = 0; i < 16; ++i) S.sums[i] = k[i];
@@ -513,7 +513,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
 #pragma unroll
                 for (int c = r; c < 6; ++c) a[6 + up(r, c)] += v[r] * v[c];
         });
-        block_sum<27>(a, red);
+        block_sum_rs<27>(a, red);
         if (tid == 0) {
             const double nn = (double)n;
             double m[6];
@@ -878,7 +878,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
                 }
             }
         }
-        block_sum<14>(acc, red);
+        block_sum_rs<14>(acc, red);
         changed = block_sum_scalar<int>(changed, ired);
         nlab = block_sum_scalar<int>(nlab, ired);
         if (tid == 0) {
@@ -956,7 +956,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
                 for (int b = a; b < 6; ++b) acc[7 + up(a, b)] += wv * v[b];
             }
         });
-        block_sum<28>(acc, red);
+        block_sum_rs<28>(acc, red);
         if (tid == 0) {
             S.passes += 1;
             for (int k = 0; k < 28; ++k) S.sums[k] = acc[k];
@@ -1014,7 +1014,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             }
         });
         acc[28] += log(prod) + (double)pexp * 0.69314718055994530942;
-        block_sum<29>(acc, red);
+        block_sum_rs<29>(acc, red);
         if (tid == 0) {
             S.passes += 1;
             S.em_iter = it;
@@ -1065,7 +1065,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
                 for (int c = 0; c < 3; ++c) k1[7 + r * 3 + c] += ws * dv[c];
             }
         });
-        block_sum<16>(k1, red);
+        block_sum_rs<16>(k1, red);
         if (tid == 0) {
             S.passes += 1;
             for (int i = 0; i < 26; ++i) out[i] = 0.0;

@@ -3,22 +3,34 @@
 One step = one new frame for each of B sequences in flight on this GPU, through the whole hot
 path (BASELINE.json north_star):
   * scene-flow dynamic-point mask: GaussianMixture(2) fit + Kabsch pose + quaternion
-    (PointCloudOdometry_noSeg.py:97-125)                       -> k_mask_pose         [stream A]
+    (PointCloudOdometry_noSeg.py:97-125)                       -> k_mask_pose         [mask streams]
   * frameFeature: ring binning, curvature, planar selection (frameFeature.cpp:45-123)
                                                                -> k_bin_* / k_curv_select / k_compact
-  * plane table of the new frame (it is the next step's last frame) + registration of the pair
-    (previous frame, new frame): association + 10 Gauss-Newton iterations + pose accumulation
-    (lidarOdometry_onlyPC.cpp:147-252, :87-90)                 -> k_plane_table / k_associate / k_solve
-                                                                                      [stream B]
+  * plane table of the new frame (it is the next step's last frame)    -> k_plane_table_sorted
+                                                                                      [feature stream]
+  * registration of the pair (previous frame, new frame): association + 10 Gauss-Newton
+    iterations + pose accumulation (lidarOdometry_onlyPC.cpp:147-252, :87-90)
+                                                               -> k_associate_* / k_solve [reg stream]
   * N > 1: one RCCL all_gather of the step's per-frame 6-DoF poses (weak scaling: every rank
     owns B sequences, no other data-path collective).
-Inputs are resident in HBM before the timed region.  Rank 0 prints ONE JSON line.
+Configs (BASELINE.json): default = configs[1]/[4] shape (B = 256 pairs in flight, 120k points);
+--n-az 4000 = configs[4] (256k-point scans); --mask-before-features --batch 32 = configs[2]
+(the features, and so the registration, see only the GMM background points).
+
+Inputs are resident in HBM before the timed region.  After the timed region a short kernel pass
+re-runs a few steps on ONE stream with per-kernel HIP events (ssf_profile_enable), so the
+roofline fractions come from kernel-only durations (the timed run overlaps streams, where an
+event pair also counts time spent queued behind other streams' work-groups).
+`python bench.py --gpus N` without WORLD_SIZE starts N ranks itself (torch.distributed.run).
+Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,187 +40,237 @@ for p in (os.path.join(REPO, "ssf-slam_amd"), REPO):
         sys.path.insert(0, p)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# HBM bytes per k_mask_pose launch measured with rocprofv3 PMC passes on this bench command
-# (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE); used when its workload config matches.
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+F64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector, spec (AMD datasheet); f64 MFMA is no faster
+# HBM bytes / f64 FLOPs per k_mask_pose launch measured with rocprofv3 PMC passes on this bench
+# command (tools/pmc_traffic.py, tools/pmc_f64.py); used when their workload config matches.
 TRAFFIC_JSON = os.path.join(REPO, "profiles", "r01_k_mask_pose_traffic.json")
+F64_JSON = os.path.join(REPO, "profiles", "r02_k_mask_pose_f64.json")
+METRIC = "LiDAR front-end frames/sec (mask+feature+GN), 64-beam 120k pts, 1/2/4/8 GPUs"
 
 
-def mask_traffic(B, N):
+def _profile_value(path, B, N, key):
     try:
-        with open(TRAFFIC_JSON) as f:
+        with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None
     cfg = t.get("config", {})
     if cfg.get("sequences_per_gpu") != B or cfg.get("points_per_frame") != N:
         return None
-    return t.get("traffic_bytes_per_launch")
+    return t.get(key)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without WORLD_SIZE in the env, bench.py starts them")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="sequences in flight per GPU")
-    ap.add_argument("--n-az", type=int, default=1875, help="azimuth steps (64 x 1875 = 120k pts)")
+    ap.add_argument("--n-az", type=int, default=1875,
+                    help="azimuth steps (64 x 1875 = 120k pts; 4000 -> 256k, BASELINE configs[4])")
     ap.add_argument("--rows", type=int, default=64)
     ap.add_argument("--solver", default="gn", choices=["gn", "ceres_lm"])
     ap.add_argument("--iters", type=int, default=None)
-    ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic sequences (tiled)")
+    ap.add_argument("--distinct", type=int, default=None,
+                    help="distinct synthetic sequences (default: every sequence distinct)")
+    ap.add_argument("--mask-before-features", action="store_true",
+                    help="BASELINE configs[2]: features and registration on the GMM background "
+                         "points only (beyond the reference, whose frameFeature sees every point)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="CPU baseline sample: run the oracle for at least this long (bounded)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="CPU baseline: seconds per leg (single thread, all cores, sklearn)")
+    ap.add_argument("--cpu-cores", type=int, default=None,
+                    help="processes of the all-cores leg (default: this job's CPU share)")
+    ap.add_argument("--kernel-pass", type=int, default=3,
+                    help="steps re-run on one stream with per-kernel events after the timed run")
     ap.add_argument("--serial", action="store_true", help="one stream (per-kernel timing without overlap)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N>1 rehearsal on a one-GPU box: every rank on cuda:0, gloo collectives "
                          "(the printed line is marked rehearsal; not a scaling measurement)")
     ap.add_argument("--feat-priority", type=int, default=-1,
-                    help="HIP stream priority of the features/registration stream (lower = higher)")
+                    help="HIP stream priority of the features/registration streams (lower = higher)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="registration on the features stream (default: its own stream and context, so "
-                         "features + plane table of step k+1 run ahead of the registration of step k; "
-                         "measured 40.7-40.9k -> 43.8-44.2k frames/s, poses bit-identical)")
+                         "features + plane table of step k+1 run ahead of the registration of step k)")
     ap.add_argument("--dump-poses", default=None,
                     help="save the accumulated poses after the timed steps (.npy; stream-order check)")
-    ap.add_argument("--mask-lag", type=int, default=0,
-                    help="mask launch k waits for the registration chain of step k-lag (0: no throttle)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="CPU-only check of the rank launch: every rank joins a gloo group, rank 0 "
+                         "prints the world it sees and exits (no GPU is touched)")
     ap.add_argument("--mask-streams", type=int, default=3,
                     help="mask launches of consecutive steps alternate over this many streams: the "
                          "GMM of a frame depends on no other frame, so a step's slow frames overlap "
                          "the next step's mask instead of idling the other CUs")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def make_data(args, dev, n_frames, rank):
-    """[n_frames] batches of B frames: pos/flow packed [B*N, 3] f32, resident in HBM."""
-    from ssf import synth
-    S = max(1, min(args.distinct, args.batch))
-    seqs = []
-    for s in range(S):
-        seq_id = rank * 1000 + s
-        sc = synth.Scene(seq_id)
-        fr = [synth.scan(seq_id, k, n_rows=args.rows, n_az=args.n_az, device=dev, scene=sc)
-              for k in range(n_frames)]
-        seqs.append(fr)
-    batches = []
-    for k in range(n_frames):
-        pos = torch.cat([seqs[b % S][k]["pos1"] for b in range(args.batch)]).contiguous()
-        flow = torch.cat([seqs[b % S][k]["flow"] for b in range(args.batch)]).contiguous()
-        batches.append((pos, flow))
-    del seqs
-    return batches
+# ---------------------------------------------------------------------------- rank launch
+def launch_ranks(args) -> int:
+    """--gpus N with no WORLD_SIZE: start N ranks of this script with torch.distributed.run as a
+    child process (nothing here has touched the GPU) and return its exit code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------------- CPU baseline
+def _cpu_share():
+    for k in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        v = os.environ.get(k)
+        if v and v.isdigit() and int(v) > 0:
+            return int(v)
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def _run_legs(specs, seconds):
+    """start every leg process at once; -> list of parsed JSON results"""
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    procs = []
+    for leg, seq, extra in specs:
+        cmd = [sys.executable, "-m", "oracle.cpu_leg", leg, "--seq", str(seq), "--seconds",
+               str(seconds), *extra]
+        e = dict(os.environ) if leg == "sklearn" else env
+        procs.append(subprocess.Popen(cmd, cwd=REPO, env=e, stdout=subprocess.PIPE,
+                                      stderr=subprocess.DEVNULL, text=True))
+    out = []
+    for p in procs:
+        try:
+            so, _ = p.communicate(timeout=seconds * 4 + 120)
+            out.append(json.loads(so.strip().splitlines()[-1]))
+        except Exception as e:  # a failed leg is reported, never silently dropped
+            p.kill()
+            out.append(dict(frames=0, seconds=0.0, error=str(e)))
+    return out
 
 
 def cpu_baseline(args):
-    """The CPU oracle (C restatement of the reference path, single thread) on a bounded sample:
-    frames of one synthetic sequence through mask + features + plane table + registration
-    (warm-started pairs, frames cycled), timed on this host until >= cpu_seconds have elapsed."""
-    from oracle import oracle as O
+    """The CPU restatement of the reference path (oracle/ssf_oracle.c), timed on this host
+    BEFORE the GPU is touched, on a bounded sample of the same workload: one leg single-threaded,
+    one with a process per core of this job's CPU share (one sequence each), and the reference's
+    own third-party mask call (sklearn GaussianMixture) for the mask stage alone."""
+    iters = args.iters or (10 if args.solver == "gn" else 8)
+    extra = ["--rows", str(args.rows), "--n-az", str(args.n_az), "--solver", args.solver,
+             "--iters", str(iters)]
+    cores = args.cpu_cores or _cpu_share()
+    T = args.cpu_seconds
+    single = _run_legs([("oracle", 0, extra)], T)[0]
+    many = _run_legs([("oracle", s, extra) for s in range(cores)], T)
+    skl = _run_legs([("sklearn", 0, ["--rows", str(args.rows), "--n-az", str(args.n_az)])], T)[0]
+    rate = lambda r: r["frames"] / r["seconds"] if r.get("seconds") else 0.0
+    agg = sum(rate(r) for r in many)
+    N = args.rows * args.n_az
+    work = f"mask+features+plane table+{args.solver} x{iters}"
+    return dict(
+        value=agg, unit="frames/s", cores=cores, kind="port",
+        sample=f"{sum(r['frames'] for r in many)} frames of {args.rows}-beam {N}-pt synthetic "
+               f"scans ({work}) through oracle/ssf_oracle.c, {cores} processes x 1 thread "
+               f"(one sequence each, {T:.0f} s each, concurrent)",
+        legs={
+            "single_thread": dict(value=rate(single), cores=1, frames=single.get("frames"),
+                                  seconds=single.get("seconds"), kind="port"),
+            "all_cores": dict(value=agg, cores=cores, frames=sum(r["frames"] for r in many),
+                              per_process=[round(rate(r), 3) for r in many], kind="port"),
+            "sklearn_mask_only": dict(value=rate(skl), cores="BLAS default",
+                                      frames=skl.get("frames"), seconds=skl.get("seconds"),
+                                      kind="third-party (sklearn GaussianMixture + numpy Kabsch)",
+                                      note=skl.get("skipped") or f"sklearn {skl.get('sklearn')}, "
+                                      "mask + pose only (no features, no registration)"),
+        })
+
+
+# ---------------------------------------------------------------------------- data
+def make_data(args, dev, n_frames, rank):
+    """[n_frames] batches of B frames: pos/flow packed [B*N, 3] f32, resident in HBM.  Sequence
+    b of rank r is synth sequence r * 100000 + (b mod distinct)."""
+    import torch
     from ssf import synth
-    O.lib()
-    sc = synth.Scene(0)
-    n_src = 4
-    fr = [synth.scan(0, k, n_rows=args.rows, n_az=args.n_az, scene=sc) for k in range(n_src)]
-    fr = [(f["pos1"].numpy(), f["flow"].numpy()) for f in fr]
-    prof = O.profile(args.rows)
-    mode = O.MODE_GN if args.solver == "gn" else O.MODE_CERES_LM
-    iters = args.iters or (10 if args.solver == "gn" else 8)
-    last = O.extract_planes(fr[0][0], args.rows)
-    q, t = np.array([0, 0, 0, 1.0]), np.zeros(3)
-    done = 0
-    t0 = time.perf_counter()
-    while True:
-        p, f = fr[1 + done % (n_src - 1)]
-        O.mask_and_pose(p, f, [0.3, 0.6, 0.9])
-        curr = O.extract_planes(p, args.rows)
-        q, t, _, _ = O.register_pair(last, curr, prof.plane_max, mode=mode, max_iter=iters, q_init=q, t_init=t)
-        last = curr
-        done += 1
-        el = time.perf_counter() - t0
-        if (el >= args.cpu_seconds and done >= 2) or el > 30.0:
-            break
-    return dict(value=done / el, unit="frames/s", cores=1, kind="port",
-                sample=f"{done} frames of {args.rows}-beam {args.rows * args.n_az}-pt synthetic scans "
-                       f"(mask+features+plane table+{args.solver} x{iters}) through oracle/ssf_oracle.c, "
-                       f"1 thread, {el:.2f} s")
+    S = max(1, min(args.distinct or args.batch, args.batch))
+    N = args.rows * args.n_az
+    pos = [torch.empty((args.batch * N, 3), dtype=torch.float32, device=dev) for _ in range(n_frames)]
+    flow = [torch.empty((args.batch * N, 3), dtype=torch.float32, device=dev) for _ in range(n_frames)]
+    for s in range(S):
+        seq_id = rank * 100000 + s
+        sc = synth.Scene(seq_id)
+        for k in range(n_frames):
+            f = synth.scan(seq_id, k, n_rows=args.rows, n_az=args.n_az, device=dev, scene=sc)
+            for b in range(s, args.batch, S):
+                pos[k][b * N:(b + 1) * N].copy_(f["pos1"])
+                flow[k][b * N:(b + 1) * N].copy_(f["flow"])
+    return list(zip(pos, flow))
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.warmup < 1:
-        args.warmup = 1  # the first frame of a sequence has no last frame to register against
-    if args.rehearse_one_gpu:
-        local = 0
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.rehearse_one_gpu:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
-        else:
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+# ---------------------------------------------------------------------------- pipeline
+class Pipeline:
+    """Per-step launches of the hot path on (mask, features, registration) streams."""
 
-    import ssf
-    from ssf import dist as sd
-    iters = args.iters or (10 if args.solver == "gn" else 8)
-    B, N = args.batch, args.rows * args.n_az
-    n_frames = args.warmup + args.steps + 1
-    batches = make_data(args, dev, n_frames, rank)
-    off, h_off = ssf.frame_offsets([N] * B, dev)
-    fe_mask = ssf.Frontend(args.rows, device=local)
-    fe_feat = ssf.Frontend(args.rows, device=local, solver=args.solver, max_iter=iters)
-    fe_mask.reserve(B, N)
-    fe_feat.reserve(B, N)
-    fe_mask.seed(20240000 + rank)
-    n_ms = 1 if args.serial else max(1, args.mask_streams)
-    s_masks = [torch.cuda.Stream(dev) for _ in range(n_ms)]
-    # the registration chain is serial across steps: its stream gets the higher priority so the
-    # mask launches (independent frames) fill the CUs it leaves free
-    s_feat = s_masks[0] if args.serial else torch.cuda.Stream(dev, priority=args.feat_priority)
-    # registration on its own stream and context: features + plane table of step k + 1 do not
-    # wait for the registration of step k (it only needs the plane table of its two frames)
-    s_reg = s_feat if args.serial or not args.pipeline else torch.cuda.Stream(dev, priority=args.feat_priority)
-    fe_reg = fe_feat if s_reg is s_feat else ssf.Frontend(args.rows, device=local, solver=args.solver,
-                                                          max_iter=iters)
-    if fe_reg is not fe_feat:
-        fe_reg.reserve(B, N)
-    # per-step outputs (double-buffered plane clouds: last <- curr)
-    pose_rel = ssf.identity_poses(B, dev)
-    pose_abs = ssf.identity_poses(B, dev)
-    mask_out = [None] * n_frames
-    gathered = []
-    ev = {k: [] for k in ("mask", "feat", "table", "reg")}
-    state = {"last": None, "last_table": None}
-    chain_done = [None] * n_frames
+    def __init__(self, args, dev, B, N, iters, world):
+        import torch
+        import ssf
+        self.args, self.dev, self.B, self.N, self.world = args, dev, B, N, world
+        self.fe_mask = ssf.Frontend(args.rows, device=dev.index)
+        self.fe_feat = ssf.Frontend(args.rows, device=dev.index, solver=args.solver, max_iter=iters)
+        self.fe_mask.reserve(B, N)
+        self.fe_feat.reserve(B, N)
+        n_ms = 1 if args.serial else max(1, args.mask_streams)
+        self.s_masks = [torch.cuda.Stream(dev) for _ in range(n_ms)]
+        # the registration chain is serial across steps: its streams get the higher priority so
+        # the mask launches (independent frames) fill the CUs it leaves free
+        self.s_feat = self.s_masks[0] if args.serial else torch.cuda.Stream(dev, priority=args.feat_priority)
+        # registration on its own stream and context: features + plane table of step k + 1 do
+        # not wait for the registration of step k (it only needs the plane table of its frames)
+        pipelined = not args.serial and args.pipeline
+        self.s_reg = torch.cuda.Stream(dev, priority=args.feat_priority) if pipelined else self.s_feat
+        self.fe_reg = self.fe_feat
+        if pipelined:
+            self.fe_reg = ssf.Frontend(args.rows, device=dev.index, solver=args.solver, max_iter=iters)
+            self.fe_reg.reserve(B, N)
+        self.pose_rel = ssf.identity_poses(B, dev)
+        self.pose_abs = ssf.identity_poses(B, dev)
+        self.last = self.last_table = None
+        self.records = []           # per step: (pose snapshot on s_reg, mask out)
+        self.gathered = []
+        self.ev = {k: [] for k in ("mask", "feat", "table", "reg")}
 
-    def step(k, timing):
+    def contexts(self):
+        return [self.fe_mask, self.fe_feat] + ([self.fe_reg] if self.fe_reg is not self.fe_feat else [])
+
+    def step(self, k, batches, off, h_off, timing, streams=None, want_stats=False):
+        import torch
+        from ssf import dist as sd
+        a = self.args
         pos, flow = batches[k]
-        s_mask = s_masks[k % n_ms]
-        # optional throttle (off by default): mask k waits for the registration chain of step
-        # k-lag.  Measured: 33.2-33.9 k frames/s with lag 1-3 against 39.5 k without -- the
-        # unthrottled masks overlap each other's straggler tails, and the chain catches up
-        if not args.serial and args.mask_lag > 0 and k - args.mask_lag >= 0:
-            s_mask.wait_event(chain_done[k - args.mask_lag])
+        s_mask, s_feat, s_reg = streams or (self.s_masks[k % len(self.s_masks)], self.s_feat, self.s_reg)
+        mk = lambda: torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(s_mask):
-            e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(s_mask)
-            out, bg = fe_mask.mask_pose(pos, flow, off, h_off, mode="gmm", want_mask=True)
-            e1.record(s_mask)
-            mask_out[k] = out
+            m0, m1 = mk(), mk()
+            m0.record(s_mask)
+            out, bg = self.fe_mask.mask_pose(pos, flow, off, h_off, mode="gmm", want_mask=True)
+            m1.record(s_mask)
+        keep = None
+        if a.mask_before_features:          # configs[2]: the features wait for the mask
+            if s_feat is not s_mask:
+                s_feat.wait_event(m1)
+                bg.record_stream(s_feat)
+            keep = bg
         with torch.cuda.stream(s_feat):
-            es = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            es = [mk() for _ in range(3)]
             es[0].record(s_feat)
-            pb = fe_feat.extract_planes_batch(pos, off, h_off, max_points=N)
+            pb = self.fe_feat.extract_planes_batch(pos, off, h_off, max_points=self.N, keep=keep)
             es[1].record(s_feat)
-            table = fe_feat.plane_table(pb)
+            table = self.fe_feat.plane_table(pb)
             es[2].record(s_feat)
         if s_reg is not s_feat:
             s_reg.wait_event(es[2])
@@ -216,104 +278,260 @@ def main():
             # the caching allocator from handing their blocks to s_feat until s_reg is done
             for t in (pb.xyzi, pb.count, *[x for x in table if isinstance(x, torch.Tensor)]):
                 t.record_stream(s_reg)
+        stats = None
         with torch.cuda.stream(s_reg):
-            if state["last"] is not None:
-                fe_reg.register(state["last"], state["last_table"], pb, pose_rel, pose_abs)
-            es[3].record(s_reg)
-            chain_done[k] = torch.cuda.Event()
-            chain_done[k].record(s_reg)
-        state["last"], state["last_table"] = pb, table
-        if world > 1:   # the one exchange step: per-frame 6-DoF poses of every rank (RCCL)
-            cur = torch.cuda.current_stream(dev)
+            r0, r1 = mk(), mk()
+            r0.record(s_reg)        # after the wait: registration time excludes queueing on s_feat
+            if self.last is not None:
+                res = self.fe_reg.register(self.last, self.last_table, pb, self.pose_rel, self.pose_abs,
+                                           want_nlog=want_stats)
+                if want_stats:
+                    stats = (res["ncorr"], res["nlog"])
+            r1.record(s_reg)
+            snap = self.pose_abs.clone() if self.world > 1 else None   # step-k poses, on s_reg
+        self.last, self.last_table = pb, table
+        if self.world > 1:   # the one exchange step: per-frame 6-DoF poses of every rank (RCCL)
+            cur = torch.cuda.current_stream(self.dev)
             cur.wait_stream(s_mask)
-            cur.wait_stream(s_feat)
             cur.wait_stream(s_reg)
-            gathered.append(sd.gather_poses(sd.pose_record(pose_abs, mask_out[k])))
+            snap.record_stream(cur)
+            rec = sd.pose_record(snap, out)
+            self.records.append(rec)
+            self.gathered.append(sd.gather_poses(rec))
         if timing:
-            ev["mask"].append((e0, e1)); ev["feat"].append((es[0], es[1]))
-            ev["table"].append((es[1], es[2])); ev["reg"].append((es[2], es[3]))
+            self.ev["mask"].append((m0, m1)); self.ev["feat"].append((es[0], es[1]))
+            self.ev["table"].append((es[1], es[2])); self.ev["reg"].append((r0, r1))
+        return dict(out=out, bg=bg, pb=pb, stats=stats)
+
+
+def kernel_pass(pipe, batches, off, h_off, ks, rows, row_start, row_end):
+    """Steps ks re-run on ONE stream with per-kernel HIP events: kernel-only durations plus the
+    algorithmic byte counts of the same launches (SURVEY §8(d) per-unit figures)."""
+    import torch
+    import ssf
+    s = torch.cuda.Stream(pipe.dev)
+    s.wait_stream(torch.cuda.current_stream(pipe.dev))
+    ctxs = pipe.contexts()
+    pipe.last = pipe.last_table = None
+    for c in ctxs:
+        c.kernel_times()          # drop anything recorded earlier
+        c.profile(True)
+    B, N = pipe.B, pipe.N
+    acc = dict(points=0, kept=0, in_range=0, plane=0, plane_reg=0, corr_evals=0, corr=0, mask_passes=[])
+    with torch.cuda.stream(s):
+        for i, k in enumerate(ks):
+            r = pipe.step(k, batches, off, h_off, False, streams=(s, s, s), want_stats=True)
+            # counts for the byte model (profiling paused: this extra launch is not timed)
+            pipe.fe_feat.profile(False)
+            keep = r["bg"] if pipe.args.mask_before_features else None
+            _, _, roff, _ = pipe.fe_feat.extract_planes_batch(batches[k][0], off, h_off, max_points=N,
+                                                              debug=True, keep=keep)
+            pipe.fe_feat.profile(True)
+            roff = roff.to(torch.int64)
+            acc["points"] += B * N
+            acc["kept"] += int(roff[:, -1].sum())
+            acc["in_range"] += int((roff[:, rows - row_end] - roff[:, row_start]).sum())
+            acc["plane"] += int(r["pb"].count.sum())
+            acc["mask_passes"].append(r["out"][:, 25])
+            if r["stats"] is not None:
+                nc, nl = r["stats"]
+                nc = nc.to(torch.int64).clamp(min=0)
+                acc["corr"] += int(nc.sum())
+                acc["corr_evals"] += int((nc * (nl.to(torch.int64) + 1)).sum())
+                acc["plane_reg"] += int(r["pb"].count.sum())
+    s.synchronize()
+    times = {}
+    for c in ctxs:
+        for name, (n, ms) in c.kernel_times().items():
+            a, b = times.get(name, (0, 0.0))
+            times[name] = (a + n, b + ms)
+        c.profile(False)
+    return times, acc
+
+
+def rooflines(times, acc, B, N):
+    """{kernel: launches, ms per launch, algorithmic bytes per launch, GB/s, fraction of HBM
+    peak}.  The byte totals cover exactly the launches the pass profiled (features, table and
+    mask: every pass step; association and solve: the steps that had a last frame)."""
+    import torch
+    passes = float(torch.cat(acc["mask_passes"]).mean()) if acc["mask_passes"] else 0.0
+    n_mask = len(acc["mask_passes"])
+    model = {   # DESIGN.md §5 / SURVEY §8(d) per-unit figures
+        "k_mask_pose": B * N * (24.0 * passes + 1.0) * n_mask,     # [flow,xyz] f32 per pass + mask
+        "k_bin_count": 13.0 * acc["points"],                        # xyz read, row id written
+        "k_bin_scatter": 13.0 * acc["points"] + 16.0 * acc["kept"], # xyz + id read, float4 written
+        "k_curv_select": 16.0 * acc["in_range"],                    # §8(d): 16 B x points of rows in range
+        "k_compact": 36.0 * acc["plane"],
+        "k_plane_table_sorted": 49.0 * acc["plane"],
+        "k_associate_lds": 64.0 * acc["plane_reg"],
+        "k_associate_sorted": 64.0 * acc["plane_reg"],
+        "k_solve": 36.0 * acc["corr_evals"],                        # §8(d): 36 B x C per evaluation
+    }
+    out = {}
+    for name, (n, ms) in sorted(times.items(), key=lambda kv: -kv[1][1]):
+        d = dict(launches=n, ms=ms / n)
+        if name in model and ms > 0:
+            bytes_per = model[name] / n
+            gbs = bytes_per / (ms / n * 1e-3) / 1e9
+            d.update(bytes=bytes_per, gbs=gbs, frac=gbs / HBM_PEAK_GBS)
+        out[name] = d
+    if "k_solve" in out:
+        n = out["k_solve"]["launches"]
+        out["k_solve"].update(corr_per_launch=acc["corr"] / n,
+                              evaluations_per_pair=acc["corr_evals"] / max(1, acc["corr"]),
+                              note="corr = valid correspondences counted on device (ncorr); "
+                                   "evaluations = 1 + logged iterations (nlog)")
+    if "k_curv_select" in out:
+        out["k_curv_select"]["in_range_points_per_launch"] = acc["in_range"] / out["k_curv_select"]["launches"]
+    return out, passes
+
+
+def main():
+    args = parse()
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(ws or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a "
+                 f"{world}-rank run as {args.gpus} GPUs")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        import torch
+        import torch.distributed as dist
+        if world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        got = [None] * world
+        if world > 1:
+            dist.all_gather_object(got, dict(rank=rank, local=local, pid=os.getpid()))
+        else:
+            got = [dict(rank=0, local=local, pid=os.getpid())]
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": args.gpus, "world": world,
+                              "ranks": got}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    if args.warmup < 1:
+        args.warmup = 1  # the first frame of a sequence has no last frame to register against
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)          # before anything touches the GPU
+
+    import torch
+    import torch.distributed as dist
+    if args.rehearse_one_gpu:
+        local = 0
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    backend = None
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "gloo" if args.rehearse_one_gpu else "nccl"
+        if backend == "gloo":
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if dist.get_world_size() != args.gpus:
+            sys.exit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+
+    import ssf
+    iters = args.iters or (10 if args.solver == "gn" else 8)
+    B, N = args.batch, args.rows * args.n_az
+    n_frames = args.warmup + args.steps + 1
+    t_data = time.perf_counter()
+    batches = make_data(args, dev, n_frames, rank)
+    t_data = time.perf_counter() - t_data
+    off, h_off = ssf.frame_offsets([N] * B, dev)
+    pipe = Pipeline(args, dev, B, N, iters, world)
+    pipe.fe_mask.seed(20240000 + rank)
 
     for k in range(args.warmup):
-        step(k, False)
+        pipe.step(k, batches, off, h_off, False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
-        step(k, True)
+        pipe.step(k, batches, off, h_off, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if args.dump_poses and rank == 0:
-        np.save(args.dump_poses, pose_abs.cpu().numpy())
+        np.save(args.dump_poses, pipe.pose_abs.cpu().numpy())
+    gather_ok = None
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.rehearse_one_gpu else dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # every gathered record of this rank must be the pose of its own step (stream order)
+        gather_ok = all(torch.equal(g[rank * B:(rank + 1) * B].cpu(), r.cpu())
+                        for g, r in zip(pipe.gathered, pipe.records))
+        flag = torch.tensor([1 if gather_ok else 0], dtype=torch.int32,
+                            device="cpu" if backend == "gloo" else dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        gather_ok = bool(flag.item())
 
-    # ---- per-kernel timing (HIP events on the launching streams) + algorithmic bytes
+    # ---- overlapped-run events (context) and the kernel pass (the roofline's durations)
     def avg_ms(pairs):
-        return float(np.mean([a.elapsed_time(b) for a, b in pairs]))
+        return float(np.mean([a.elapsed_time(b) for a, b in pairs])) if pairs else 0.0
 
-    mask_ms = avg_ms(ev["mask"])
-    feat_ms = avg_ms(ev["feat"])
-    table_ms = avg_ms(ev["table"])
-    reg_ms = avg_ms(ev["reg"])
-    passes = torch.stack([mask_out[k][:, 25] for k in range(args.warmup, args.warmup + args.steps)])
-    status = torch.stack([mask_out[k][:, 16] for k in range(args.warmup, args.warmup + args.steps)])
-    mean_passes = float(passes.mean())
-    # k_mask_pose: out[25] counts its algorithmic bytes in units of one [flow, xyz] float32
-    # stream (24 B/pt; Lloyd skip passes count their record/queue bytes); + 1 B/pt mask write
-    mask_bytes = B * N * (24.0 * mean_passes + 1.0)
-    # frameFeature chain: bin_count 12 R + 1 W, bin_scatter 13 R + 16 W, curv_select 16 R + 4 W(sel)
-    feat_bytes = B * N * (12 + 1 + 13 + 16 + 16) * 1.0
-    kernels = {
-        # gbs: per launch (launches of consecutive steps overlap on two streams, so a launch's
-        # duration includes time shared with the next one); aggregate_gbs: all mask bytes of the
-        # timed steps over the timed wall time
-        "k_mask_pose": dict(ms=mask_ms, bytes=mask_bytes, gbs=mask_bytes / mask_ms / 1e6,
-                            aggregate_gbs=mask_bytes * args.steps / elapsed / 1e9,
-                            passes_per_frame=mean_passes, streams=n_ms),
-        "features(5 kernels)": dict(ms=feat_ms, bytes=feat_bytes, gbs=feat_bytes / feat_ms / 1e6),
-        "plane_table": dict(ms=table_ms),
-        "register(assoc+solve)": dict(ms=reg_ms),
-    }
-    dom = max(kernels, key=lambda k: kernels[k]["ms"])
+    overlapped = {k: avg_ms(v) for k, v in pipe.ev.items()}
+    ks = list(range(args.warmup, min(args.warmup + args.kernel_pass, n_frames)))
+    kernels, passes = {}, 0.0
+    if args.kernel_pass > 0:
+        cfg = pipe.fe_feat.cfg
+        times, acc = kernel_pass(pipe, batches, off, h_off, ks, args.rows, cfg.row_start, cfg.row_end)
+        kernels, passes = rooflines(times, acc, B, N)
+
     total_frames = B * args.steps * world
     value = total_frames / elapsed
+    cfg_name = ("configs[2] noSeg mask-before-features" if args.mask_before_features else
+                "configs[4] 256k-pt stress" if args.n_az >= 4000 else "configs[1]/[4] 120k-pt")
     line = {
-        "metric": "LiDAR front-end frames/sec (mask+feature+GN), 64-beam 120k pts, 1/2/4/8 GPUs",
+        "metric": METRIC,
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f32 features / f64 mask+solve",
-        "data": "synthetic (seeded ray-cast 64-beam scans, ssf/synth.py)",
-        "config": {"workload": f"{B} sequences in flight per GPU x {args.rows}-beam {N}-pt scans; "
-                               f"mask(GMM+Kabsch) + features + plane table + {args.solver} x{iters}",
+        "data": f"synthetic (seeded ray-cast 64-beam scans, ssf/synth.py; "
+                f"{min(args.distinct or B, B)} distinct sequences per rank)",
+        "config": {"workload": f"{cfg_name}: {B} sequences in flight per GPU x {args.rows}-beam "
+                               f"{N}-pt scans; mask(GMM+Kabsch) + "
+                               f"{'masked ' if args.mask_before_features else ''}features + plane "
+                               f"table + {args.solver} x{iters}",
                    "sequences_per_gpu": B, "points_per_frame": N, "solver": args.solver,
-                   "iters": iters, "parallelism": f"sequence-sharded x{world}",
+                   "iters": iters, "mask_before_features": bool(args.mask_before_features),
+                   "parallelism": f"sequence-sharded x{world}",
+                   "world_size_initialised": (dist.get_world_size() if world > 1 else 1),
+                   "backend": backend or "none",
                    **({"rehearsal": "all ranks on one GPU, gloo"} if args.rehearse_one_gpu else {})},
-        "roofline": None, "cpu_baseline": None, "kernels": kernels,
-        "mask_status_nonzero": int((status != 0).sum()),
+        "roofline": None, "cpu_baseline": cpu,
+        "kernels": kernels, "overlapped_event_ms": overlapped,
+        "mask_passes_per_frame": passes, "gather_check": gather_ok,
+        "data_gen_s": round(t_data, 2),
     }
-    if "k_mask_pose" == dom:
-        achieved = mask_bytes / (mask_ms * 1e-3) / 1e9
-        line["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": achieved / HBM_PEAK_GBS, "traffic": mask_traffic(B, N),
-                            "kernel": "k_mask_pose"}
-    else:
-        k = kernels[dom]
-        b = k.get("bytes")
-        if b:
-            achieved = b / (k["ms"] * 1e-3) / 1e9
-            line["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                                "kernel": dom}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args)
+    mk = kernels.get("k_mask_pose")
+    if mk and "gbs" in mk:
+        line["roofline"] = {"bound": "hbm", "achieved": mk["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": mk["frac"], "traffic": _profile_value(TRAFFIC_JSON, B, N,
+                                                                          "traffic_bytes_per_launch"),
+                            "kernel": "k_mask_pose",
+                            "duration": "kernel-only (one-stream kernel pass, HIP events)"}
+        flops = _profile_value(F64_JSON, B, N, "f64_flops_per_launch")
+        if flops:
+            tf = flops / (mk["ms"] * 1e-3) / 1e12
+            line["roofline_f64"] = {"bound": "valu_f64", "achieved": tf, "peak": F64_PEAK_TFLOPS,
+                                    "unit": "TFLOP/s", "frac": tf / F64_PEAK_TFLOPS,
+                                    "kernel": "k_mask_pose", "flops_source": os.path.basename(F64_JSON)}
+    ns = {k: kernels[k]["frac"] for k in ("k_curv_select", "k_solve") if k in kernels and "frac" in kernels[k]}
+    if ns:
+        line["north_star_kernels_hbm_frac"] = ns
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -69,6 +69,19 @@ const char* ssf_last_error(const ssf_ctx* ctx);
 /* Pre-size device scratch so later calls never allocate (graph-capture friendly). */
 int32_t ssf_reserve(ssf_ctx* ctx, int32_t max_frames, int64_t max_points_per_frame);
 
+/* Kernel timing (no reference counterpart: the reference has no timers).  While
+ * enabled, every kernel this context launches is bracketed by HIP events on its stream; on a
+ * stream no other stream competes with, each interval is that kernel's duration.
+ * ssf_profile_read synchronises on the recorded events and returns, per kernel name, the
+ * launches and total milliseconds recorded since the previous read (then clears them). */
+typedef struct {
+    char name[48];
+    int32_t launches;
+    double total_ms;
+} ssf_kernel_time;
+int32_t ssf_profile_enable(ssf_ctx* ctx, int32_t on);
+int32_t ssf_profile_read(ssf_ctx* ctx, ssf_kernel_time* out, int32_t cap, int32_t* n_out);
+
 /* ---------------------------------------------------------------------------------------
  * frameFeature: replaces cloudHandler() (src/frameFeature.cpp:35-139) -- ring binning
  * (:45-81), 11-tap curvature (:84-107) and greedy planar selection (:110-123) -- for a batch
@@ -152,6 +165,44 @@ int32_t ssf_register_batch(ssf_ctx* ctx, void* stream, int32_t n_pairs,
                            int64_t curr_total_points, int64_t max_plane_points,
                            double* d_pose_rel, double* d_pose_abs,
                            double* d_log, int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_nn);
+
+/* Single-pair form with the SURVEY §8(b) signature: frameRegistration() on the globals
+ * lastFramePlanePtr / currFramePlanePtr / para_q / para_t (src/lidarOdometry_onlyPC.cpp:51-71,
+ * 147-252).  The plane clouds are device float4 (x, y, z, intensity) as frameFeature publishes
+ * them; the warm start h_q_init (x,y,z,w) / h_t_init is the previous pair's solution (:164,
+ * 251-252) and the solution comes back in h_q_out / h_t_out.  The last frame's plane table and
+ * search index are built inside the call (ctx scratch).  A last frame with <= 10 points adds no
+ * residual (:158): the warm start is returned unchanged, rc 0, log->n_corr = -1.  Synchronous.
+ * log (nullable): per LM/GN iteration the pose after it, the Ceres cost, a status code and the
+ * trust-region radius. */
+enum {
+    SSF_STEP_REJECTED = 0,        /* LM step computed, rho <= 1e-3, radius shrunk            */
+    SSF_STEP_ACCEPTED = 1,        /* LM step accepted                                        */
+    SSF_STEP_INVALID = 2,         /* LM/GN linear solve failed or non-positive model decrease */
+    SSF_STEP_PARAM_TOL = 3,       /* ParameterToleranceReached (|dx| <= 1e-8 (|x| + 1e-8))   */
+    SSF_STEP_FUNC_TOL = 4,        /* FunctionToleranceReached (|dcost| <= 1e-6 cost)         */
+    SSF_STEP_GRAD_TOL = 5,        /* GradientToleranceReached (max-norm <= 1e-10)            */
+    SSF_STEP_GN = 6               /* undamped Gauss-Newton step (SSF_SOLVER_GN)              */
+};
+typedef struct {
+    double q[4];       /* pose after the iteration, q x,y,z,w                          */
+    double t[3];
+    double cost;       /* Ceres cost 1/2 sum rho(r^2) over the duplicated blocks        */
+    int32_t status;    /* SSF_STEP_*                                                    */
+    int32_t pad;
+    double radius;     /* trust-region radius after the iteration (0 in GN mode)         */
+} ssf_step;
+typedef struct {
+    int32_t cap;       /* in: capacity of steps[] (cfg.max_iter holds a full log)        */
+    int32_t n_steps;   /* out: iterations logged                                        */
+    int32_t n_corr;    /* out: valid correspondences (-1: skipped, :158)                */
+    int32_t pad;
+    ssf_step* steps;   /* caller-owned host array of cap entries                        */
+} ssf_step_log;
+int32_t ssf_register_pair(ssf_ctx* ctx, void* stream, const float* d_last_xyzi, int64_t m_last,
+                          const float* d_curr_xyzi, int64_t m_curr, const double* h_q_init,
+                          const double* h_t_init, double* h_q_out, double* h_t_out,
+                          ssf_step_log* log);
 
 /* ---------------------------------------------------------------------------------------
  * PointCloudOdometry{,_noSeg}.py: replaces the dynamic-point mask + slove_RT_by_SVD + Quaternion

@@ -68,6 +68,12 @@ def lib():
     L.orc_profile_get.argtypes = [C.c_int32, C.POINTER(Profile)]
     L.orc_ring_id.argtypes = [C.c_float, C.c_float, C.c_float, C.c_int32]
     L.orc_ring_id.restype = C.c_int32
+    L.orc_ring_id_of_angle.argtypes = [C.c_float, C.c_int32]
+    L.orc_ring_id_of_angle.restype = C.c_int32
+    L.orc_xindex_build.argtypes = [C.c_void_p, C.c_int64]
+    L.orc_xindex_build.restype = C.c_void_p
+    L.orc_xindex_free.argtypes = [C.c_void_p]
+    L.orc_xindex_knn.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
     L.orc_bin.argtypes = [f32p, C.c_int64, C.c_int64, C.c_int32, f32p, i64p, i64p, i32p]
     L.orc_bin.restype = C.c_int64
     L.orc_curvature.argtypes = [f32p, i64p, C.c_int32, C.c_int32, C.c_int32, f32p]
@@ -164,6 +170,24 @@ def extract_planes(pts, n_rows):
 
 
 # --------------------------------------------------------------------------- registration
+def ring_id_of_angle(angle, n_rows):
+    return lib().orc_ring_id_of_angle(float(np.float32(angle)), n_rows)
+
+
+def xknn(cloud, q, k):
+    """k-NN through the oracle's x-sorted index (must equal knn())."""
+    cloud = np.ascontiguousarray(cloud, np.float32)
+    X = lib().orc_xindex_build(cloud.ctypes.data, cloud.shape[0])
+    try:
+        idx = np.zeros(k, np.int32)
+        d2 = np.zeros(k, np.float32)
+        qq = np.ascontiguousarray(q, np.float32)
+        lib().orc_xindex_knn(X, qq.ctypes.data, k, idx.ctypes.data, d2.ctypes.data)
+    finally:
+        lib().orc_xindex_free(X)
+    return idx, d2
+
+
 def knn(cloud, q, k):
     cloud = np.ascontiguousarray(cloud, np.float32)
     idx = np.zeros(k, np.int32)

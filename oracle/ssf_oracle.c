@@ -35,21 +35,29 @@ int orc_profile_get(int32_t n_rows, orc_profile* p) {
  * angle = atan(z / sqrt(x*x + y*y)) * 180 / M_PI: the ratio is formed in float (sqrt of a
  * float), atan / scaling in double, stored to a float.  The `||` guards at :59 and :64 are
  * always true and are therefore omitted. */
-int32_t orc_ring_id(float x, float y, float z, int32_t n_rows) {
-    float r2 = x * x + y * y;
-    float ratio = z / sqrtf(r2);
-    float angle = (float)(atan((double)ratio) * 180.0 / M_PI);
+/* The row of a float angle, with the C++ promotions of the reference's expressions:
+ *   :60  (angle + 15) / 2 + 0.5   float + int, float / int (float), then + double
+ *   :66  (2 - angle) * 3.0 + 0.5  int - float is a FLOAT subtraction, then double
+ *   :68  (-8.83 - angle) * 2.0    double - float (double) */
+int32_t orc_ring_id_of_angle(float angle, int32_t n_rows) {
     int32_t id = -1;
     if (n_rows == 16) {
         id = (int32_t)((double)((angle + 15.0f) / 2.0f) + 0.5);        /* :60 */
     } else if (n_rows == 64) {
         if ((double)angle >= -8.83)                                      /* :65 */
-            id = (int32_t)((2.0 - (double)angle) * 3.0 + 0.5);           /* :66 */
+            id = (int32_t)((double)(2.0f - angle) * 3.0 + 0.5);          /* :66 */
         else
             id = n_rows / 2 + (int32_t)((-8.83 - (double)angle) * 2.0 + 0.5); /* :68 */
     }
     if (id > -1 && id < n_rows) return id;                               /* :73 */
     return -1;
+}
+
+int32_t orc_ring_id(float x, float y, float z, int32_t n_rows) {
+    float r2 = x * x + y * y;
+    float ratio = z / sqrtf(r2);
+    float angle = (float)(atan((double)ratio) * 180.0 / M_PI);
+    return orc_ring_id_of_angle(angle, n_rows);
 }
 
 /* frameFeature.cpp:45-81 -- stable append per row, intensity = indexInRow + id/100.0 */
@@ -176,6 +184,85 @@ void orc_knn(const float* cloud, int64_t m, const float q[3], int32_t k, int32_t
     for (int32_t r = cnt; r < k; ++r) { idx[r] = -1; d2[r] = INFINITY; }
 }
 
+/* The same exact k-NN through an x-sorted index (the CPU baseline's stand-in for the kd-tree;
+ * brute force made the baseline O(M^2)).  Candidates are visited outward from the query's x
+ * and ranked by (d2, index) lexicographically, so the list is identical to orc_knn's whatever
+ * the visit order.  A walk stops once dx*dx exceeds the k-th distance: d2 >= dx*dx holds in
+ * float because each addition of a non-negative term rounds monotonically. */
+typedef struct { float x; int32_t i; } orc_xkey;
+
+static int xkey_cmp(const void* a, const void* b) {
+    const orc_xkey* u = (const orc_xkey*)a;
+    const orc_xkey* v = (const orc_xkey*)b;
+    if (u->x < v->x) return -1;
+    if (u->x > v->x) return 1;
+    return (u->i > v->i) - (u->i < v->i);
+}
+
+orc_xindex* orc_xindex_build(const float* cloud, int64_t m) {
+    orc_xindex* X = (orc_xindex*)malloc(sizeof(orc_xindex));
+    orc_xkey* k = (orc_xkey*)malloc(sizeof(orc_xkey) * (size_t)(m > 0 ? m : 1));
+    for (int64_t j = 0; j < m; ++j) { k[j].x = cloud[4 * j]; k[j].i = (int32_t)j; }
+    qsort(k, (size_t)m, sizeof(orc_xkey), xkey_cmp);
+    X->cloud = cloud;
+    X->m = m;
+    X->xs = (float*)malloc(sizeof(float) * (size_t)(m > 0 ? m : 1));
+    X->order = (int32_t*)malloc(sizeof(int32_t) * (size_t)(m > 0 ? m : 1));
+    for (int64_t j = 0; j < m; ++j) { X->xs[j] = k[j].x; X->order[j] = k[j].i; }
+    free(k);
+    return X;
+}
+
+void orc_xindex_free(orc_xindex* X) {
+    if (!X) return;
+    free(X->xs); free(X->order); free(X);
+}
+
+static int lexless(float da, int32_t ia, float db, int32_t ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+static void xknn_visit(const orc_xindex* X, int64_t c, const float q[3], int32_t k, int32_t* idx,
+                       float* d2, int32_t* cnt) {
+    const int32_t j = X->order[c];
+    const float* p = X->cloud + 4 * (int64_t)j;
+    float dx = q[0] - p[0];
+    float dy = q[1] - p[1];
+    float dz = q[2] - p[2];
+    float d = dx * dx + dy * dy;
+    d = d + dz * dz;
+    if (*cnt == k && !lexless(d, j, d2[k - 1], idx[k - 1])) return;
+    int32_t pos = *cnt < k ? *cnt : k - 1;
+    while (pos > 0 && lexless(d, j, d2[pos - 1], idx[pos - 1])) {
+        d2[pos] = d2[pos - 1];
+        idx[pos] = idx[pos - 1];
+        pos--;
+    }
+    d2[pos] = d;
+    idx[pos] = j;
+    if (*cnt < k) (*cnt)++;
+}
+
+void orc_xindex_knn(const orc_xindex* X, const float q[3], int32_t k, int32_t* idx, float* d2) {
+    int32_t cnt = 0;
+    int64_t lo = 0, hi = X->m;                       /* first sorted x >= q.x */
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (X->xs[mid] < q[0]) lo = mid + 1; else hi = mid;
+    }
+    for (int64_t c = lo; c < X->m; ++c) {
+        float dx = q[0] - X->xs[c];
+        if (cnt == k && dx * dx > d2[k - 1]) break;
+        xknn_visit(X, c, q, k, idx, d2, &cnt);
+    }
+    for (int64_t c = lo - 1; c >= 0; --c) {
+        float dx = q[0] - X->xs[c];
+        if (cnt == k && dx * dx > d2[k - 1]) break;
+        xknn_visit(X, c, q, k, idx, d2, &cnt);
+    }
+    for (int32_t r = cnt; r < k; ++r) { idx[r] = -1; d2[r] = INFINITY; }
+}
+
 /* Eigen ColPivHouseholderQR<Matrix<float,5,3>>::solve(-1) restated (Eigen 3.3
  * ColPivHouseholder.h computeInPlace / _solve_impl, Householder.h makeHouseholder /
  * applyHouseholderOnTheLeft), reductions in index order.  Eigen's SIMD reduction order is
@@ -292,9 +379,10 @@ void orc_plane_table(const float* last, int64_t m, float plane_max, float* norma
                      int32_t* pick5, int32_t* gate_rank) {
     int32_t idx[30];
     float d2[30];
+    orc_xindex* X = orc_xindex_build(last, m);
     for (int64_t a = 0; a < m; ++a) {
         float q[3] = {last[4 * a], last[4 * a + 1], last[4 * a + 2]};
-        orc_knn(last, m, q, 30, idx, d2);
+        orc_xindex_knn(X, q, 30, idx, d2);
         int32_t K = m < 30 ? (int32_t)m : 30;
         float nrm[3] = {0, 0, 0};
         int32_t ok = 0;
@@ -344,6 +432,7 @@ void orc_plane_table(const float* last, int64_t m, float plane_max, float* norma
         if (pick5) for (int j = 0; j < 5; ++j) pick5[5 * a + j] = v5[j];
         if (gate_rank) gate_rank[a] = n;
     }
+    orc_xindex_free(X);
 }
 
 /* Eigen Quaterniond * Vector3d (_transformVector): uv = 2 (qv x v); v + w uv + qv x uv. */
@@ -365,14 +454,16 @@ void orc_transform_point(const double q[4], const double t[3], const float p[3],
 /* 1-NN association, lidarOdometry_onlyPC.cpp:161-169 (unbounded distance). */
 void orc_correspond(const float* last, int64_t m_last, const float* curr, int64_t m_curr,
                     const double q[4], const double t[3], int32_t* nn) {
+    orc_xindex* X = orc_xindex_build(last, m_last);
     for (int64_t i = 0; i < m_curr; ++i) {
         float p[3] = {curr[4 * i], curr[4 * i + 1], curr[4 * i + 2]}, s[3];
         orc_transform_point(q, t, p, s);
         int32_t idx;
         float d2;
-        orc_knn(last, m_last, s, 1, &idx, &d2);
+        orc_xindex_knn(X, s, 1, &idx, &d2);
         nn[i] = idx;
     }
+    orc_xindex_free(X);
 }
 
 /* Eigen quaternion product a*b, (x,y,z,w) storage. */

@@ -43,6 +43,7 @@ int orc_profile_get(int32_t n_rows, orc_profile* out);
 
 /* ---- frameFeature (src/frameFeature.cpp:45-123) ---- */
 int32_t orc_ring_id(float x, float y, float z, int32_t n_rows);
+int32_t orc_ring_id_of_angle(float angle, int32_t n_rows);
 /* Stable per-ring partition.  pts has stride `stride` floats (xyz at 0..2).
  * rxyzi: ring-ordered kept points (x,y,z,intensity) -- capacity n*4 floats.
  * ring_off[n_rows+1]: exclusive prefix of per-ring counts.
@@ -63,6 +64,11 @@ int64_t orc_extract_planes(const float* pts, int64_t n, int64_t stride, int32_t 
 /* ---- lidarOdometry_onlyPC (src/lidarOdometry_onlyPC.cpp:74-82,147-252) ---- */
 void orc_knn(const float* cloud_xyzi, int64_t m, const float q[3], int32_t k, int32_t* idx,
              float* d2);
+/* The same k-NN lists through an x-sorted index (plane table and association use it). */
+typedef struct { const float* cloud; int64_t m; float* xs; int32_t* order; } orc_xindex;
+orc_xindex* orc_xindex_build(const float* cloud_xyzi, int64_t m);
+void orc_xindex_free(orc_xindex* X);
+void orc_xindex_knn(const orc_xindex* X, const float q[3], int32_t k, int32_t* idx, float* d2);
 void orc_plane_table(const float* last_xyzi, int64_t m, float plane_max, float* normal,
                      int32_t* valid, int32_t* pick5, int32_t* gate_rank);
 void orc_transform_point(const double q[4], const double t[3], const float p[3], float out[3]);

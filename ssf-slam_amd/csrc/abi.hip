@@ -17,6 +17,32 @@
 
 using ssf::DevBuf;
 
+// Kernel timing (ssf_profile_enable): events recorded on the launching stream right before each
+// kernel and at the end of the ABI call; consecutive events bracket one kernel.  On a stream
+// that no other stream competes with, that is the kernel's own duration.
+struct KTimer {
+    bool on = false;
+    struct Mark { hipEvent_t ev; const char* name; };   // name == nullptr closes an ABI call
+    std::vector<Mark> marks;
+    std::vector<hipEvent_t> pool;                       // events reused after every read
+    static constexpr size_t kMaxMarks = 1 << 14;
+    void mark(hipStream_t s, const char* name) {
+        if (marks.size() >= kMaxMarks) return;          // unread backlog: stop recording
+        if (marks.size() == pool.size()) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) return;
+            pool.push_back(e);
+        }
+        hipEvent_t e = pool[marks.size()];
+        if (hipEventRecord(e, s) != hipSuccess) return;
+        marks.push_back({e, name});
+    }
+    void release() {
+        for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+        pool.clear(); marks.clear();
+    }
+};
+
 struct ssf_ctx {
     int device = 0;
     ssf_config cfg{};
@@ -25,6 +51,8 @@ struct ssf_ctx {
     DevBuf rid, hist, ring_off, ring_xyzi, sel, sel_cnt, plane1, off1, cnt1;
     // registration scratch
     DevBuf corr;
+    // ssf_register_pair: offsets, counts, the last frame's plane table + search index, pose, log
+    DevBuf pair;
     // mask: k-means++ draws staged per launch through a ring of slots, so launches on different
     // streams (e.g. consecutive batches overlapping their slow frames) never share a buffer
     struct DrawSlot {
@@ -46,7 +74,30 @@ struct ssf_ctx {
     uint32_t mt[624];
     int mt_pos = 625;
     std::map<int64_t, std::vector<double>> cdf_cache;  // choice(n, p=1/n) cumulative table
+    KTimer prof;
 };
+
+namespace {
+thread_local KTimer* t_prof = nullptr;   // the timer of the ABI call running on this thread
+
+// Scope of one ABI call: its launches mark into the context's timer when timing is on.
+struct ProfScope {
+    KTimer* prev;
+    KTimer* mine;
+    hipStream_t s;
+    ProfScope(ssf_ctx* c, void* stream)
+        : prev(t_prof), mine(c && c->prof.on ? &c->prof : nullptr), s((hipStream_t)stream) {
+        if (mine) t_prof = mine;
+    }
+    ~ProfScope() {
+        if (mine) { mine->mark(s, nullptr); t_prof = prev; }
+    }
+};
+}  // namespace
+
+void ssf::kmark(hipStream_t s, const char* name) {
+    if (t_prof) t_prof->mark(s, name);
+}
 
 namespace {
 
@@ -164,7 +215,7 @@ void ssf_destroy(ssf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     DevBuf* bufs[] = {&c->rid, &c->hist, &c->ring_off, &c->ring_xyzi, &c->sel, &c->sel_cnt,
-                      &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->start1, &c->vg,
+                      &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->pair, &c->start1, &c->vg,
                       &c->icp_cur, &c->icp_key, &c->icp_st, &c->icp_guess};
     for (auto& ds : c->dslot) {
         if (ds.used) { (void)hipEventSynchronize(ds.used); (void)hipEventDestroy(ds.used); }
@@ -174,7 +225,44 @@ void ssf_destroy(ssf_ctx* c) {
         ds.rec.release();
     }
     for (DevBuf* b : bufs) b->release();
+    if (!c->prof.marks.empty()) (void)hipEventSynchronize(c->prof.marks.back().ev);
+    c->prof.release();
     delete c;
+}
+
+int32_t ssf_profile_enable(ssf_ctx* c, int32_t on) {
+    if (!c) return SSF_E_ARG;
+    c->prof.on = on != 0;
+    return SSF_OK;
+}
+
+int32_t ssf_profile_read(ssf_ctx* c, ssf_kernel_time* out, int32_t cap, int32_t* n_out) {
+    if (!c || !n_out || cap < 0 || (cap > 0 && !out)) return SSF_E_ARG;
+    *n_out = 0;
+    KTimer& P = c->prof;
+    if (P.marks.empty()) return SSF_OK;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    for (const auto& m : P.marks) SSF_TRY_HIP(c, hipEventSynchronize(m.ev), "profile sync");
+    int n = 0;
+    for (size_t i = 0; i + 1 < P.marks.size(); ++i) {
+        const char* nm = P.marks[i].name;
+        if (!nm) continue;                               // between two ABI calls: no kernel
+        float ms = 0.0f;
+        SSF_TRY_HIP(c, hipEventElapsedTime(&ms, P.marks[i].ev, P.marks[i + 1].ev), "profile elapsed");
+        int k = 0;
+        while (k < n && std::strncmp(out[k].name, nm, sizeof(out[k].name)) != 0) ++k;
+        if (k == n) {
+            if (n == cap) continue;
+            std::memset(&out[k], 0, sizeof(out[k]));
+            std::strncpy(out[k].name, nm, sizeof(out[k].name) - 1);
+            ++n;
+        }
+        out[k].launches += 1;
+        out[k].total_ms += ms;
+    }
+    P.marks.clear();
+    *n_out = n;
+    return SSF_OK;
 }
 
 const char* ssf_last_error(const ssf_ctx* c) { return c ? c->err.c_str() : "null context"; }
@@ -192,7 +280,8 @@ static int32_t ensure_features(ssf_ctx* c, int32_t n_frames, int64_t total, int6
     SSF_TRY_HIP(c, c->hist.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(n_frames * n_chunks * R, 1)), "alloc hist");
     SSF_TRY_HIP(c, c->ring_off.ensure(sizeof(int32_t) * (size_t)n_frames * (R + 1)), "alloc ring_off");
     SSF_TRY_HIP(c, c->ring_xyzi.ensure(sizeof(float4) * (size_t)std::max<int64_t>(total, 1)), "alloc ring_xyzi");
-    SSF_TRY_HIP(c, c->sel.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(total, 1)), "alloc sel");
+    // + 64 dump slots for the selection stores of lanes without a selection (k_curv_select)
+    SSF_TRY_HIP(c, c->sel.ensure(sizeof(int32_t) * (size_t)(std::max<int64_t>(total, 1) + 64)), "alloc sel");
     SSF_TRY_HIP(c, c->sel_cnt.ensure(sizeof(int32_t) * (size_t)n_frames * R), "alloc sel_cnt");
     return SSF_OK;
 }
@@ -225,12 +314,13 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
     SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
     int32_t rc = ensure_features(c, n_frames, total_points, max_frame_points);
     if (rc) return rc;
+    ProfScope prof(c, stream);
     float4* ring = d_ring_xyzi ? reinterpret_cast<float4*>(d_ring_xyzi) : c->ring_xyzi.as<float4>();
     int32_t* roff = d_ring_off ? d_ring_off : c->ring_off.as<int32_t>();
     hipError_t e = ssf::launch_extract_planes(
         (hipStream_t)stream, c->cfg, n_frames, d_pts, point_stride, d_frame_off, max_frame_points,
         d_keep, c->rid.as<int8_t>(), c->hist.as<int32_t>(), roff, ring, d_curv, c->sel.as<int32_t>(),
-        c->sel_cnt.as<int32_t>(), reinterpret_cast<float4*>(d_plane_xyzi), d_plane_count);
+        c->sel.as<int32_t>() + std::max<int64_t>(total_points, 1), c->sel_cnt.as<int32_t>(), reinterpret_cast<float4*>(d_plane_xyzi), d_plane_count);
     if (e != hipSuccess) return hip_fail(c, e, "extract_planes launch");
     return SSF_OK;
 }
@@ -297,6 +387,7 @@ int32_t ssf_plane_table_batch(ssf_ctx* c, void* stream, int32_t n_frames, const 
         return fail(c, SSF_E_ARG, "plane_table_batch: bad arguments");
     if (n_frames == 0) return SSF_OK;
     SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    ProfScope prof(c, stream);
     hipError_t e = ssf::launch_plane_table((hipStream_t)stream, c->cfg, n_frames,
                                            reinterpret_cast<const float4*>(d_plane_xyzi), d_frame_off,
                                            d_plane_count, max_plane_points, d_normal, d_valid,
@@ -321,6 +412,7 @@ int32_t ssf_register_batch(ssf_ctx* c, void* stream, int32_t n_pairs, const floa
     if (n_pairs == 0) return SSF_OK;
     SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
     SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(curr_total_points, 1)), "alloc corr");
+    ProfScope prof(c, stream);
     hipError_t e = ssf::launch_register(
         (hipStream_t)stream, c->cfg, n_pairs, reinterpret_cast<const float4*>(d_last_xyzi), d_last_off,
         d_last_count, d_last_normal, d_last_valid, reinterpret_cast<const float4*>(d_last_sorted_xyzi),
@@ -328,6 +420,89 @@ int32_t ssf_register_batch(ssf_ctx* c, void* stream, int32_t n_pairs, const floa
         d_curr_count, max_plane_points, c->corr.as<ssf::CorrRec>(), d_pose_rel, d_pose_abs, d_log,
         d_nlog, d_ncorr, d_nn);
     if (e != hipSuccess) return hip_fail(c, e, "register launch");
+    return SSF_OK;
+}
+
+int32_t ssf_register_pair(ssf_ctx* c, void* stream, const float* d_last_xyzi, int64_t m_last,
+                          const float* d_curr_xyzi, int64_t m_curr, const double* h_q_init,
+                          const double* h_t_init, double* h_q_out, double* h_t_out,
+                          ssf_step_log* log) {
+    if (!c) return SSF_E_ARG;
+    if (m_last < 0 || m_curr < 0 || m_last > INT32_MAX || m_curr > INT32_MAX || !h_q_init ||
+        !h_t_init || !h_q_out || !h_t_out || (m_last > 0 && !d_last_xyzi) ||
+        (m_curr > 0 && !d_curr_xyzi) || (log && log->cap > 0 && !log->steps))
+        return fail(c, SSF_E_ARG, "register_pair: bad arguments");
+    double pose[7] = {h_q_init[0], h_q_init[1], h_q_init[2], h_q_init[3], h_t_init[0], h_t_init[1], h_t_init[2]};
+    if (log) { log->n_steps = 0; log->n_corr = -1; }
+    if (m_last <= 10 || m_curr == 0) {             // :158 -- no residuals, the warm start stands
+        for (int k = 0; k < 4; ++k) h_q_out[k] = pose[k];
+        for (int k = 0; k < 3; ++k) h_t_out[k] = pose[4 + k];
+        if (log && m_last > 10) log->n_corr = 0;
+        return SSF_OK;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    const int max_iter = c->cfg.max_iter;
+    const int64_t mx = std::max(m_last, m_curr);
+    // scratch layout (8-byte aligned pieces): offsets, counts, pose, log doubles, nlog/ncorr,
+    // normals, valid, sorted cloud (16 B aligned), sorted index
+    auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
+    const size_t o_off = 0, o_cnt = al(o_off + 4 * sizeof(int64_t)), o_pose = al(o_cnt + 4 * sizeof(int32_t));
+    const size_t o_log = al(o_pose + 7 * sizeof(double));
+    const size_t o_nl = al(o_log + (size_t)std::max(max_iter, 1) * 10 * sizeof(double));
+    const size_t o_nrm = al(o_nl + 2 * sizeof(int32_t));
+    const size_t o_val = al(o_nrm + 3 * sizeof(float) * (size_t)m_last);
+    const size_t o_srt = al(o_val + (size_t)m_last);
+    const size_t o_sid = al(o_srt + sizeof(float4) * (size_t)m_last);
+    const size_t bytes = al(o_sid + sizeof(int32_t) * (size_t)m_last);
+    SSF_TRY_HIP(c, c->pair.ensure(bytes), "alloc pair scratch");
+    char* P = c->pair.as<char>();
+    int64_t* d_off = reinterpret_cast<int64_t*>(P + o_off);     // [0, m_last] and [0, m_curr]
+    int32_t* d_cnt = reinterpret_cast<int32_t*>(P + o_cnt);
+    double* d_pose = reinterpret_cast<double*>(P + o_pose);
+    double* d_log = reinterpret_cast<double*>(P + o_log);
+    int32_t* d_nl = reinterpret_cast<int32_t*>(P + o_nl);
+    float* d_nrm = reinterpret_cast<float*>(P + o_nrm);
+    uint8_t* d_val = reinterpret_cast<uint8_t*>(P + o_val);
+    float* d_srt = reinterpret_cast<float*>(P + o_srt);
+    int32_t* d_sid = reinterpret_cast<int32_t*>(P + o_sid);
+    struct { int64_t off[4]; int32_t cnt[4]; double pose[7]; } h;
+    h.off[0] = 0; h.off[1] = m_last; h.off[2] = 0; h.off[3] = m_curr;
+    h.cnt[0] = (int32_t)m_last; h.cnt[1] = (int32_t)m_curr; h.cnt[2] = h.cnt[3] = 0;
+    for (int k = 0; k < 7; ++k) h.pose[k] = pose[k];
+    SSF_TRY_HIP(c, hipMemcpyAsync(d_off, h.off, sizeof(h.off), hipMemcpyHostToDevice, s), "H2D off");
+    SSF_TRY_HIP(c, hipMemcpyAsync(d_cnt, h.cnt, sizeof(h.cnt), hipMemcpyHostToDevice, s), "H2D counts");
+    SSF_TRY_HIP(c, hipMemcpyAsync(d_pose, h.pose, sizeof(h.pose), hipMemcpyHostToDevice, s), "H2D pose");
+    int32_t rc = ssf_plane_table_batch(c, stream, 1, d_last_xyzi, d_off, d_cnt, mx, d_nrm, d_val, d_srt, d_sid);
+    if (rc) return rc;
+    rc = ssf_register_batch(c, stream, 1, d_last_xyzi, d_off, d_cnt, d_nrm, d_val, d_srt, d_sid,
+                            d_curr_xyzi, d_off + 2, d_cnt + 1, m_curr, mx, d_pose, nullptr,
+                            d_log, d_nl, d_nl + 1, nullptr);
+    if (rc) return rc;
+    std::vector<double> hl((size_t)std::max(max_iter, 1) * 10);
+    int32_t hn[2] = {0, 0};
+    SSF_TRY_HIP(c, hipMemcpyAsync(h.pose, d_pose, sizeof(h.pose), hipMemcpyDeviceToHost, s), "D2H pose");
+    SSF_TRY_HIP(c, hipMemcpyAsync(hn, d_nl, sizeof(hn), hipMemcpyDeviceToHost, s), "D2H nlog");
+    if (log && log->cap > 0)
+        SSF_TRY_HIP(c, hipMemcpyAsync(hl.data(), d_log, sizeof(double) * hl.size(), hipMemcpyDeviceToHost, s), "D2H log");
+    SSF_TRY_HIP(c, hipStreamSynchronize(s), "sync");
+    for (int k = 0; k < 4; ++k) h_q_out[k] = h.pose[k];
+    for (int k = 0; k < 3; ++k) h_t_out[k] = h.pose[4 + k];
+    if (log) {
+        log->n_corr = hn[1];
+        const int n = std::min(std::min(hn[0], max_iter), std::max(log->cap, 0));
+        for (int i = 0; i < n; ++i) {
+            const double* r = &hl[(size_t)i * 10];
+            ssf_step& st = log->steps[i];
+            for (int k = 0; k < 4; ++k) st.q[k] = r[k];
+            for (int k = 0; k < 3; ++k) st.t[k] = r[4 + k];
+            st.cost = r[7];
+            st.status = (int32_t)r[8];
+            st.pad = 0;
+            st.radius = r[9];
+        }
+        log->n_steps = n;
+    }
     return SSF_OK;
 }
 
@@ -384,6 +559,7 @@ int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const fl
     }
     SSF_TRY_HIP(c, hipMemcpyAsync(ds.d.p, ds.h, sizeof(double) * need, hipMemcpyHostToDevice, s), "H2D draws");
     SSF_TRY_HIP(c, hipEventRecord(ds.copied, s), "draws record");
+    ProfScope prof(c, stream);
     hipError_t e = ssf::launch_mask_pose(s, n_frames, d_pts, d_flow, d_frame_off, mode, d_mask_in,
                                          ds.d.as<double>(), ds.rec.as<uint2>(), reflection, d_bg_mask, d_out);
     if (e == hipSuccess) e = hipEventRecord(ds.used, s);
@@ -404,6 +580,7 @@ int32_t ssf_accumulate_sequence(ssf_ctx* c, void* stream, int32_t n, const doubl
         SSF_TRY_HIP(c, hipMemcpyAsync(c->start1.p, h_start, sizeof(double) * 7, hipMemcpyHostToDevice, s), "H2D start");
         d_start = c->start1.as<double>();
     }
+    ProfScope prof(c, stream);
     hipError_t e = ssf::launch_accumulate(s, n, d_rel, d_start, d_abs);
     if (e != hipSuccess) return hip_fail(c, e, "accumulate launch");
     if (h_start) SSF_TRY_HIP(c, hipStreamSynchronize(s), "sync start");

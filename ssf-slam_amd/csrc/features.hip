@@ -26,7 +26,7 @@ SSF_DEV int ring_id_exact(float ratio, int n_rows) {
         id = (int)((double)((angle + 15.0f) / 2.0f) + 0.5);
     } else if (n_rows == 64) {
         if ((double)angle >= -8.83)
-            id = (int)((2.0 - (double)angle) * 3.0 + 0.5);
+            id = (int)((double)(2.0f - angle) * 3.0 + 0.5);      // int - float: a float subtraction
         else
             id = n_rows / 2 + (int)((-8.83 - (double)angle) * 2.0 + 0.5);
     }
@@ -48,7 +48,7 @@ SSF_DEV int ring_id(float x, float y, float z, int n_rows) {
         margin = 0.5e-3f;
     } else {
         const bool upper = (double)af >= -8.83;
-        v = upper ? (2.0 - (double)af) * 3.0 + 0.5 : (-8.83 - (double)af) * 2.0 + 0.5;
+        v = upper ? (double)(2.0f - af) * 3.0 + 0.5 : (-8.83 - (double)af) * 2.0 + 0.5;
         margin = upper ? 3e-3f : 2e-3f;
         if (!(fabsf(af + 8.83f) > 1e-3f)) margin = -1.0f;   // near the switch (or NaN): exact
     }
@@ -274,7 +274,8 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
                                                      const float4* __restrict__ rxyzi,
                                                      float* __restrict__ curv,
                                                      int32_t* __restrict__ sel,
-                                                     int32_t* __restrict__ sel_cnt) {
+                                                     int32_t* __restrict__ sel_cnt,
+                                                     int32_t* __restrict__ sel_dump) {
     __shared__ float win[kCurvRowsPerWG][3][kWinPad];
     __shared__ int32_t slist[kCurvRowsPerWG][64 * (kCurvDepth / 2 + 1)];
     // the wave index through readfirstlane: the compiler then knows the row, its length and
@@ -331,10 +332,10 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
         }
         nl = __builtin_amdgcn_readfirstlane(nl);
     };
-    // a trip's selections (<= 64 kCurvDepth / plane_span + 1 <= 256) leave with unconditional stores;
-    // lanes without one write the row's last slot, which no selection list reaches (at most
-    // ceil(n_r / 2) entries for plane_span >= 2)
-    const int64_t spare = base + n_r - 1;
+    // a trip's selections (<= 64 kCurvDepth / plane_span + 1 <= 128) leave with unconditional
+    // stores; lanes without one write a 64-slot dump after the last point of the batch.  (The
+    // row's own last slot is NOT free: a one-point row selects its point 0 = its last slot.)
+    int32_t* const dump = sel_dump + lane;
     // prologue loads in buffer order (the loop's waits count on b[0] being the oldest)
     float4 b[kCurvDepth];
 #pragma unroll
@@ -348,7 +349,7 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int h = 0; h < kCurvDepth / 2 + 1; ++h)   // >= 64 kCurvDepth / plane_span + 1 entries
-            sel[lane + 64 * h < nl ? base + cnt + 64 * h + lane : spare] = sl[64 * h + lane];
+            *(lane + 64 * h < nl ? sel + base + cnt + 64 * h + lane : dump) = sl[64 * h + lane];
         __builtin_amdgcn_wave_barrier();
         cnt += nl;
         nl = 0;
@@ -378,28 +379,34 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
                                  const float* pts, int stride, const int64_t* frame_off,
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
                                  int32_t* ring_off, float4* ring_xyzi, float* curv, int32_t* sel,
-                                 int32_t* sel_cnt, float4* plane, int32_t* plane_count) {
+                                 int32_t* sel_dump, int32_t* sel_cnt, float4* plane,
+                                 int32_t* plane_count) {
     const int R = cfg.n_rows;
     const int n_chunks = (int)((max_pts + kBinChunk - 1) / kBinChunk);
     if (n_frames <= 0) return hipSuccess;
     if (n_chunks > 0) {
+        kmark(s, "k_bin_count");
         hipLaunchKernelGGL(k_bin_count, dim3(n_chunks, n_frames), dim3(256), 0, s, pts, stride,
                            frame_off, R, n_chunks, keep, rid, hist);
     }
+    kmark(s, "k_bin_scan");
     hipLaunchKernelGGL(k_bin_scan, dim3(n_frames), dim3(64), 0, s, R, n_chunks, hist, ring_off);
     if (n_chunks > 0) {
+        kmark(s, "k_bin_scatter");
         hipLaunchKernelGGL(k_bin_scatter, dim3(n_chunks, n_frames), dim3(256), 0, s, pts, stride,
                            frame_off, R, n_chunks, rid, hist, ring_off, ring_xyzi);
     }
     const dim3 cgrid((R + kCurvRowsPerWG - 1) / kCurvRowsPerWG, n_frames);
+    kmark(s, "k_curv_select");
     if (curv)
         hipLaunchKernelGGL(k_curv_select<true>, cgrid, dim3(64 * kCurvRowsPerWG), 0, s, frame_off, R,
                            cfg.row_start, cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off,
-                           ring_xyzi, curv, sel, sel_cnt);
+                           ring_xyzi, curv, sel, sel_cnt, sel_dump);
     else
         hipLaunchKernelGGL(k_curv_select<false>, cgrid, dim3(64 * kCurvRowsPerWG), 0, s, frame_off, R,
                            cfg.row_start, cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off,
-                           ring_xyzi, curv, sel, sel_cnt);
+                           ring_xyzi, curv, sel, sel_cnt, sel_dump);
+    kmark(s, "k_compact");
     hipLaunchKernelGGL(k_compact, dim3(R, n_frames), dim3(256), 0, s, frame_off, R, ring_off,
                        ring_xyzi, sel, sel_cnt, plane, plane_count);
     return hipGetLastError();

@@ -1112,6 +1112,7 @@ hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const
                             const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
                             double* out) {
     if (n_frames <= 0) return hipSuccess;
+    kmark(s, "k_mask_pose");
     hipLaunchKernelGGL(k_mask_pose, dim3(n_frames), dim3(kMaskThreads), 0, s, pts, flow, frame_off,
                        mode, mask_in, draws, lloyd_rec, reflection, bg_mask, out);
     return hipGetLastError();

@@ -1299,10 +1299,12 @@ hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames
                               int32_t* sorted_idx) {
     if (n_frames <= 0 || max_m <= 0) return hipSuccess;
     if (max_m <= kSortMax && sorted_xyzi && sorted_idx) {
+        kmark(s, "k_plane_table_sorted");
         hipLaunchKernelGGL(k_plane_table_sorted, dim3(n_frames), dim3(kTableThreads), 0, s, plane,
                            frame_off, count, cfg.plane_max, normal, valid, sorted_xyzi, sorted_idx);
     } else {
         const int bx = (int)((max_m + 255) / 256);
+        kmark(s, "k_plane_table");
         hipLaunchKernelGGL(k_plane_table, dim3(bx, n_frames), dim3(256), 0, s, plane, frame_off,
                            count, cfg.plane_max, normal, valid);
     }
@@ -1321,21 +1323,25 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
         const int bx = (int)((max_m + 255) / 256);
         if (max_m <= kAssocLdsMax && last_sorted && last_sidx) {
             const int qx = (int)((max_m + kAssocQ - 1) / kAssocQ);
+            kmark(s, "k_associate_lds");
             hipLaunchKernelGGL(k_associate_lds, dim3(qx, n_pairs), dim3(kAssocThreads),
                                (size_t)max_m * sizeof(float4) + kAssocQ * sizeof(int), s, last,
                                last_off, last_count,
                                last_normal, last_valid, last_sorted, last_sidx, curr, curr_off,
                                curr_count, pose_rel, corr, nn, (int)max_m);
         } else if (max_m <= kSortMax && last_sorted && last_sidx) {
+            kmark(s, "k_associate_sorted");
             hipLaunchKernelGGL(k_associate_sorted, dim3(bx, n_pairs), dim3(256), 0, s, last, last_off,
                                last_count, last_normal, last_valid, last_sorted, last_sidx, curr,
                                curr_off, curr_count, pose_rel, corr, nn);
         } else {
+            kmark(s, "k_associate");
             hipLaunchKernelGGL(k_associate, dim3(bx, n_pairs), dim3(256), 0, s, last, last_off,
                                last_count, last_normal, last_valid, curr, curr_off, curr_count,
                                pose_rel, corr, nn);
         }
     }
+    kmark(s, "k_solve");
     hipLaunchKernelGGL(k_solve, dim3(n_pairs), dim3(kSolveThreads), 0, s, corr, curr_off,
                        curr_count, last_count, cfg.solver, cfg.max_iter, pose_rel, pose_abs, log,
                        nlog, ncorr);
@@ -1345,6 +1351,7 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
 hipError_t launch_accumulate(hipStream_t s, int n, const double* rel, const double* start,
                              double* abs_out) {
     if (n <= 0) return hipSuccess;
+    kmark(s, "k_accumulate");
     hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(64), 0, s, n, rel, start, abs_out);
     return hipGetLastError();
 }

@@ -30,6 +30,11 @@ struct DevBuf {
     void release() { if (p) (void)hipFree(p); p = nullptr; bytes = 0; }
 };
 
+// Kernel timing (ssf_profile_enable): a launcher calls kmark(stream, "k_name") right before
+// each kernel it launches; the ABI entry that owns those launches closes the last interval.
+// With timing off (the default) kmark is one thread-local load and a branch.
+void kmark(hipStream_t s, const char* name);
+
 constexpr int kBinChunk = 4096;   // points per binning work-group
 constexpr int kMaxRows = 64;
 
@@ -45,7 +50,8 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
                                  const float* pts, int stride, const int64_t* frame_off,
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
                                  int32_t* ring_off, float4* ring_xyzi, float* curv, int32_t* sel,
-                                 int32_t* sel_cnt, float4* plane, int32_t* plane_count);
+                                 int32_t* sel_dump, int32_t* sel_cnt, float4* plane,
+                                 int32_t* plane_count);
 
 // ---- launchers (registration.hip) ----
 hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames,

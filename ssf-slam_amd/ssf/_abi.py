@@ -29,7 +29,8 @@ EXPORTS = [
     "ssf_reserve", "ssf_extract_planes_batch", "ssf_extract_planes", "ssf_plane_table_batch",
     "ssf_register_batch", "ssf_mask_pose_batch", "ssf_rng_seed", "ssf_accumulate_sequence",
     "ssf_voxel_grid_batch", "ssf_icp_params_default", "ssf_icp_batch",
-    "ssf_extract_planes_batch_masked",
+    "ssf_extract_planes_batch_masked", "ssf_register_pair", "ssf_profile_enable",
+    "ssf_profile_read",
 ]
 # Every symbol include/ssf_pointnet2.h declares (TFlow point-set operators).
 PN2_EXPORTS = [
@@ -48,6 +49,24 @@ ICP_STATES = {0: "not_converged", 1: "iterations", 2: "transform", 3: "abs_mse",
 class IcpParams(C.Structure):
     _fields_ = [("max_iter", C.c_int32), ("max_corr_dist", C.c_float), ("trans_eps", C.c_double),
                 ("fit_eps", C.c_double)]
+
+
+STEP_STATUS = {0: "rejected", 1: "accepted", 2: "invalid", 3: "param_tol", 4: "func_tol",
+               5: "grad_tol", 6: "gn"}
+
+
+class Step(C.Structure):
+    _fields_ = [("q", C.c_double * 4), ("t", C.c_double * 3), ("cost", C.c_double),
+                ("status", C.c_int32), ("pad", C.c_int32), ("radius", C.c_double)]
+
+
+class StepLog(C.Structure):
+    _fields_ = [("cap", C.c_int32), ("n_steps", C.c_int32), ("n_corr", C.c_int32),
+                ("pad", C.c_int32), ("steps", C.POINTER(Step))]
+
+
+class KernelTime(C.Structure):
+    _fields_ = [("name", C.c_char * 48), ("launches", C.c_int32), ("total_ms", C.c_double)]
 
 
 class Config(C.Structure):
@@ -96,6 +115,12 @@ def lib():
     L.ssf_register_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64,
                                      vp, vp, vp, vp, vp, vp]
     L.ssf_register_batch.restype = i32
+    L.ssf_register_pair.argtypes = [vp, vp, vp, i64, vp, i64, vp, vp, vp, vp, C.POINTER(StepLog)]
+    L.ssf_register_pair.restype = i32
+    L.ssf_profile_enable.argtypes = [vp, i32]
+    L.ssf_profile_enable.restype = i32
+    L.ssf_profile_read.argtypes = [vp, C.POINTER(KernelTime), i32, C.POINTER(i32)]
+    L.ssf_profile_read.restype = i32
     L.ssf_mask_pose_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, i32, vp, vp]
     L.ssf_mask_pose_batch.restype = i32
     L.ssf_accumulate_sequence.argtypes = [vp, vp, i32, vp, vp, vp]

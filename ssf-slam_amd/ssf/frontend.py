@@ -97,6 +97,18 @@ class Frontend:
     def reserve(self, max_frames: int, max_points_per_frame: int):
         self._check(_abi.lib().ssf_reserve(self._h, max_frames, max_points_per_frame), "ssf_reserve")
 
+    def profile(self, on: bool = True):
+        """Bracket every kernel this context launches with HIP events (kernel-only durations
+        when the stream runs alone); read them with kernel_times()."""
+        self._check(_abi.lib().ssf_profile_enable(self._h, 1 if on else 0), "ssf_profile_enable")
+
+    def kernel_times(self) -> dict:
+        """{kernel name: (launches, total ms)} recorded since the previous call (synchronises)."""
+        buf = (_abi.KernelTime * 64)()
+        n = C.c_int32(0)
+        self._check(_abi.lib().ssf_profile_read(self._h, buf, 64, C.byref(n)), "ssf_profile_read")
+        return {buf[i].name.decode(): (int(buf[i].launches), float(buf[i].total_ms)) for i in range(n.value)}
+
     def seed(self, seed: int):
         """np.random.seed(seed) for the GMM's k-means++ RandomState."""
         self._check(_abi.lib().ssf_rng_seed(self._h, seed & 0xFFFFFFFF), "ssf_rng_seed")
@@ -177,8 +189,33 @@ class Frontend:
         self._check(rc, "ssf_plane_table_batch")
         return normal, valid, sx, si
 
+    def register_pair(self, last_xyzi, curr_xyzi, q_init=(0.0, 0.0, 0.0, 1.0),
+                      t_init=(0.0, 0.0, 0.0)):
+        """frameRegistration() for one pair with the reference's globals as arguments
+        (ssf_register_pair): plane clouds [m, 4] f32 on the device, warm start para_q (x,y,z,w)
+        / para_t -> (q, t, steps, n_corr); steps = per-iteration dicts (pose, cost, status,
+        radius); n_corr = -1 when the last frame has <= 10 points (:158)."""
+        last_xyzi = self._dev(last_xyzi, torch.float32)
+        curr_xyzi = self._dev(curr_xyzi, torch.float32)
+        if last_xyzi.dim() != 2 or last_xyzi.shape[1] != 4 or curr_xyzi.dim() != 2 or curr_xyzi.shape[1] != 4:
+            raise ValueError("plane clouds must be [m, 4] (x, y, z, intensity)")
+        qi = (C.c_double * 4)(*[float(v) for v in q_init])
+        ti = (C.c_double * 3)(*[float(v) for v in t_init])
+        qo, to = (C.c_double * 4)(), (C.c_double * 3)()
+        cap = max(1, int(self.cfg.max_iter))
+        steps = (_abi.Step * cap)()
+        log = _abi.StepLog(cap, 0, 0, 0, steps)
+        rc = _abi.lib().ssf_register_pair(self._h, _stream(self.device), _ptr(last_xyzi),
+                                          last_xyzi.shape[0], _ptr(curr_xyzi), curr_xyzi.shape[0],
+                                          qi, ti, qo, to, C.byref(log))
+        self._check(rc, "ssf_register_pair")
+        out = [dict(q=list(steps[i].q), t=list(steps[i].t), cost=steps[i].cost,
+                    status=_abi.STEP_STATUS.get(steps[i].status, steps[i].status),
+                    radius=steps[i].radius) for i in range(log.n_steps)]
+        return list(qo), list(to), out, int(log.n_corr)
+
     def register(self, last: PlaneBatch, last_table, curr: PlaneBatch, pose_rel, pose_abs=None,
-                 want_log=False, want_nn=False):
+                 want_log=False, want_nn=False, want_nlog=False):
         """frameRegistration for P pairs (last[p], curr[p]).  pose_rel [P,7] f64 (q xyzw, t) is the
         warm start in and the solution out; pose_abs [P,7] is accumulated in place if given."""
         P = curr.count.numel()
@@ -190,6 +227,7 @@ class Frontend:
         ncorr = torch.empty(P, dtype=torch.int32, device=self.device)
         if want_log:
             log = torch.zeros((P, self.cfg.max_iter, 10), dtype=torch.float64, device=self.device)
+        if want_log or want_nlog:
             nlog = torch.zeros(P, dtype=torch.int32, device=self.device)
         if want_nn:
             nn = torch.full((curr.xyzi.shape[0],), -1, dtype=torch.int32, device=self.device)

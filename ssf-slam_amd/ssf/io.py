@@ -96,8 +96,10 @@ def _field_offsets(msg, names):
 
 
 def cloud_points(msg):
-    """PointCloud2 -> (host view [n, point_step/4] f32 of its data, byte offset of x).  x, y, z
-    must be consecutive FLOAT32s, which every layout the reference publishes satisfies."""
+    """PointCloud2 -> (host array [n, point_step/4] f32 of its points, byte offset of x).  x, y, z
+    must be consecutive FLOAT32s, which every layout the reference publishes satisfies.  An
+    organized cloud (height > 1) is read row by row at `row_step`, so padded rows are skipped
+    (row_step 0, as some publishers leave it, means dense rows)."""
     if msg.is_bigendian:
         raise SSFError("big-endian PointCloud2 is not supported")
     ox, oy, oz = _field_offsets(msg, ("x", "y", "z"))
@@ -107,12 +109,22 @@ def cloud_points(msg):
     n = int(msg.width) * int(msg.height)
     if step % 4 or step < ox + 12:
         raise SSFError(f"unsupported point_step {step}")
-    if n * step > len(msg.data):
-        raise SSFError("PointCloud2 data shorter than width * height * point_step")
+    w, h = int(msg.width), int(msg.height)
+    row_step = int(getattr(msg, "row_step", 0) or 0) or w * step
+    if row_step < w * step or row_step % 4:
+        raise SSFError(f"row_step {row_step} shorter than width * point_step or unaligned")
     if n == 0:
         return np.zeros((0, step // 4), np.float32), ox
-    buf = np.frombuffer(msg.data, dtype="<f4", count=n * step // 4)
-    return buf.reshape(n, step // 4), ox
+    if (h - 1) * row_step + w * step > len(msg.data):
+        raise SSFError("PointCloud2 data shorter than its rows (height * row_step)")
+    if row_step == w * step:
+        buf = np.frombuffer(msg.data, dtype="<f4", count=n * step // 4)
+        return buf.reshape(n, step // 4), ox
+    rows = np.frombuffer(msg.data, dtype=np.uint8, count=(h - 1) * row_step + w * step)
+    out = np.empty((h, w * step), np.uint8)
+    for r in range(h):
+        out[r] = rows[r * row_step:r * row_step + w * step]
+    return out.view("<f4").reshape(n, step // 4), ox
 
 
 def cloud_xyz(msg) -> np.ndarray:
@@ -261,9 +273,11 @@ def tum_line(stamp, t, q_xyzw) -> str:
 
 class TumWriter:
     """Appends one line per pose to RESULT_PATH, reopening the file in append mode for every
-    pose as the reference does (a crash loses at most the pose being written)."""
+    pose as the reference does (a crash loses at most the pose being written).  Like the
+    reference (mapOptmization.cpp:355, std::ios::app only) an existing file is never wiped
+    unless the runner asks for it explicitly (truncate=True)."""
 
-    def __init__(self, path: str, truncate: bool = True):
+    def __init__(self, path: str, truncate: bool = False):
         self.path = path
         if truncate:
             open(path, "w").close()

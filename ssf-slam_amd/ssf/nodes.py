@@ -8,10 +8,14 @@ way `launch/*.launch` wires the nodes and writes the odometry as a TUM trajector
   FrameFeatureNode         src/frameFeature.cpp:35-139
       /velodyne_points -> /plane_frame_cloud1 (PointXYZI layout, stamp copied, frame "map")
                        -> /org_frame_cloud1   (the input, frame "map")
-  LidarOdometryNode        src/lidarOdometry_onlyPC.cpp:85-124, 147-311
+  LidarOdometryNode        src/lidarOdometry_onlyPC.cpp:85-124, 147-311  (run_onlyPC.launch)
       /plane_frame_cloud1 -> /frame_odom2 (Odometry, frame "map", child "map_child")
                           -> /frame_odom_path2 (Path of every pose so far)
                           -> /plane_frame_cloud2 (the current plane cloud, frame "map")
+  LidarOdometryIngestNode  src/lidarOdometry.cpp:78-205  (run_noSeg / run_Seg launch graphs)
+      /frame_odom1 -> odometryQueue;  /plane_frame_cloud1 -> pops the queue front from the
+      second plane cloud on and accumulates it -> /frame_odom2, /frame_odom_path2,
+      /plane_frame_cloud2 (no registration: the pose is the SSF Kabsch pose)
 
 rospy, sensor_msgs and nav_msgs are not in this image: messages are the plain stand-ins of
 `ssf.io` / below, and a `Bus` delivers them in-process.  Subscribed callbacks are duck-typed
@@ -22,13 +26,14 @@ the stand-in to the real message class.
 from __future__ import annotations
 
 import copy
-from collections import defaultdict
+from collections import defaultdict, deque
 from dataclasses import dataclass, field
 
 import numpy as np
 import torch
 
 from . import io as sio
+from ._abi import SSFError
 from .frontend import Frontend, PlaneBatch, frame_offsets, identity_poses
 
 
@@ -146,26 +151,87 @@ class LidarOdometryNode:
         return odom
 
 
+class LidarOdometryIngestNode:
+    """src/lidarOdometry.cpp, the odometry node of the SSF launch graphs (run_noSeg.launch:8,
+    run_Seg.launch:8): no registration -- the relative pose comes from /frame_odom1.
+
+    odomHandler (:169-173) queues every /frame_odom1 message; cloudThread (:176-205) takes plane
+    clouds in order, the first one only sets flagStart, and every later one pops the FRONT of the
+    odometry queue (frameRegistration, :145-159: data[0:3] -> para_t, data[3:7] -> para_q x,y,z,w)
+    and accumulates it (publishResult :80-83) on the device.  With the publisher's order (cloud
+    first, then its pose) plane cloud k therefore consumes the pose published with frame k - 1.
+    The reference reads front() of an EMPTY queue when a plane cloud overtakes the poses (UB,
+    :148); here that raises SSFError."""
+
+    def __init__(self, publish, device=None, frontend: Frontend | None = None):
+        self.fe = frontend or Frontend(64, device=device)
+        self.publish = publish
+        self.queue = deque()                        # odometryQueue
+        self.flag_start = False
+        self.q_0_last = [0.0, 0.0, 0.0, 1.0]        # q_0_last / t_0_last (:68-71)
+        self.t_0_last = [0.0, 0.0, 0.0]
+        self.path = Path(sio.Header(0, 0, "map"))
+        self.num_frame = 0
+
+    def on_odom(self, msg):
+        data = [float(v) for v in msg.data]
+        if len(data) < 7:
+            raise SSFError(f"/frame_odom1 carries {len(data)} values, expected [t(3), q(4)]")
+        self.queue.append(data)
+
+    def on_plane_cloud(self, msg):
+        self.num_frame += 1
+        stamp = sio.stamp_of(msg.header)
+        if not self.flag_start:                     # :196-197
+            self.flag_start = True
+            return None
+        if not self.queue:
+            raise SSFError("plane cloud before its /frame_odom1 pose: the reference reads "
+                           "odometryQueue.front() of an empty queue here (lidarOdometry.cpp:148)")
+        d = self.queue.popleft()                    # frameRegistration (:147-155)
+        rel = torch.tensor([[d[3], d[4], d[5], d[6], d[0], d[1], d[2]]], dtype=torch.float64,
+                           device=self.fe.device)
+        start = self.q_0_last + self.t_0_last
+        ab = self.fe.accumulate_sequence(rel, start=start)[0].cpu().numpy()   # :80-83
+        self.q_0_last = [float(v) for v in ab[0:4]]
+        self.t_0_last = [float(v) for v in ab[4:7]]
+        hdr = sio.Header(stamp[0], stamp[1], "map")
+        pose = Pose(tuple(self.t_0_last), tuple(self.q_0_last))
+        odom = Odometry(hdr, "map_child", pose)
+        self.publish("/frame_odom2", odom)                                    # :96-107
+        self.path.poses.append((hdr, pose))                                   # :109-116
+        self.path.header = sio.Header(stamp[0], stamp[1], "map")
+        self.publish("/frame_odom_path2", self.path)
+        xyzi = sio.cloud_xyzi(msg)                                            # :118-122
+        self.publish("/plane_frame_cloud2", sio.xyzi_to_cloud(xyzi, stamp, "map"))
+        return odom
+
+
 class PointCloudOdometryNode:
-    """scripts/PointCloudOdometry_noSeg.py main loop body for one npz frame: publish the cloud,
-    then the GMM mask + Kabsch pose as [t, q] (or the ground-truth mask of
-    PointCloudOdometry.py:91 with mode='gt')."""
+    """The data-source node of the launch graphs, for one npz frame: publish the cloud, then
+      mode 'gmm'  -- PointCloudOdometry_noSeg.py:62-127: GMM mask + Kabsch pose as [t, q];
+      mode 'gt'   -- PointCloudOdometry.py:60-105: background = s_fg_mask == 0, Kabsch, [t, q];
+      mode 'none' -- PointCloudOdometry_onlyPC.py:37-65: the cloud only (no /frame_odom1)."""
 
     def __init__(self, publish, device=None, frontend: Frontend | None = None, mode: str = "gmm",
                  seed: int | None = None):
+        if mode not in ("gmm", "gt", "none"):
+            raise ValueError(f"mode {mode!r}")
         self.fe = frontend or Frontend(64, device=device)
         self.publish = publish
         self.mode = mode
         if seed is not None:
             self.fe.seed(seed)
 
-    def on_frame(self, pos1, flow, stamp=(0, 0), gt_mask=None):
+    def on_frame(self, pos1, flow=None, stamp=(0, 0), gt_mask=None):
         dev = self.fe.device
         pos = pos1 if isinstance(pos1, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(pos1, np.float32))
-        fl = flow if isinstance(flow, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(flow, np.float32))
         pos = pos.to(dev, torch.float32).contiguous()
-        fl = fl.to(dev, torch.float32).contiguous()
         self.publish("/velodyne_points", sio.xyz_to_cloud(pos.cpu().numpy(), stamp, "livox_frame"))   # :73-94
+        if self.mode == "none":
+            return None
+        fl = flow if isinstance(flow, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(flow, np.float32))
+        fl = fl.to(dev, torch.float32).contiguous()
         off, h_off = frame_offsets([pos.shape[0]], dev)
         m = None
         if self.mode != "gmm":
@@ -232,22 +298,45 @@ class MapOptimizationNode:
             self.publish("/map_frame_res3", sio.xyzi_to_cloud(transform_cloud(xyzi, T), tp, "map"))
 
 
+LAUNCH_GRAPHS = {
+    # launch file: (data-source mode, odometry node, npz keys)
+    "onlyPC": ("none", "registration", ("pos1",)),             # run_onlyPC.launch:7-15
+    "noSeg": ("gmm", "ingest", ("pos1", "gt")),                 # run_noSeg.launch:7-16
+    "Seg": ("gt", "ingest", ("pos1", "gt", "s_fg_mask")),       # run_Seg.launch:7-16
+}
+
+
 def run_sequence(root: str, tum_path: str | None = None, n_rows: int = 64, device=None,
                  solver: str = "ceres_lm", max_iter: int | None = None, seed: int | None = None,
-                 rate_hz: float = 10.0, keys=("pos1", "gt"), map_tum_path: str | None = None):
-    """Replay a DATASET_PATH directory through PointCloudOdometry -> frameFeature ->
-    lidarOdometry_onlyPC as the launch files wire them.  Stamps are synthetic and monotone
-    (frame k at k / rate_hz; the reference uses wall-clock ros::Time::now()).  Writes the
-    /frame_odom2 poses as TUM lines when `tum_path` is given.
-    -> dict(odom1 [F, 7] f64 [t, q], odom2 [F-1, 7] f64 [t, q], stamps)"""
+                 rate_hz: float = 10.0, launch: str = "onlyPC", map_tum_path: str | None = None,
+                 truncate_results: bool = False):
+    """Replay a DATASET_PATH directory through the node graph of launch/run_<launch>.launch:
+      onlyPC: PointCloudOdometry_onlyPC -> frameFeature -> lidarOdometry_onlyPC (registration)
+      noSeg:  PointCloudOdometry_noSeg (GMM mask + Kabsch -> /frame_odom1) -> frameFeature ->
+              lidarOdometry (pose ingest + accumulation)
+      Seg:    PointCloudOdometry (ground-truth mask s_fg_mask == 0) -> same as noSeg
+    plus mapOptmization when `map_tum_path` is given.  Stamps are synthetic and monotone (frame k
+    at k / rate_hz; the reference uses wall-clock ros::Time::now()).  The /frame_odom2 poses are
+    appended to `tum_path` as TUM lines (like the reference, an existing file is extended unless
+    truncate_results=True).
+    -> dict(odom1 [F, 7] f64 [t, q] (empty for onlyPC), odom2 [F-1, 7] f64 [t, q], stamps)"""
+    if launch not in LAUNCH_GRAPHS:
+        raise ValueError(f"launch {launch!r}: one of {sorted(LAUNCH_GRAPHS)}")
+    src_mode, odo_kind, keys = LAUNCH_GRAPHS[launch]
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     bus = Bus()
-    pco = PointCloudOdometryNode(bus.publish, device=dev, seed=seed)
+    pco = PointCloudOdometryNode(bus.publish, device=dev, seed=seed, mode=src_mode)
     ff = FrameFeatureNode(bus.publish, n_rows=n_rows, device=dev)
-    lo = LidarOdometryNode(bus.publish, n_rows=n_rows, device=dev, solver=solver, max_iter=max_iter)
+    if odo_kind == "registration":
+        lo = LidarOdometryNode(bus.publish, n_rows=n_rows, device=dev, solver=solver, max_iter=max_iter)
+    else:
+        lo = LidarOdometryIngestNode(bus.publish, device=dev)
+        bus.subscribe("/frame_odom1", lo.on_odom)
     bus.subscribe("/velodyne_points", ff.on_cloud)
     bus.subscribe("/plane_frame_cloud1", lo.on_plane_cloud)
     odom1, odom2, stamps = [], [], []
+    if tum_path and truncate_results:
+        open(tum_path, "w").close()
     writer = sio.TumWriter(tum_path) if tum_path else None
 
     def on_odom1(msg):
@@ -263,6 +352,8 @@ def run_sequence(root: str, tum_path: str | None = None, n_rows: int = 64, devic
     bus.subscribe("/frame_odom2", on_odom2)
     mo = None
     if map_tum_path is not None:                     # mapOptmization on /plane_frame_cloud2 + /frame_odom2
+        if map_tum_path and truncate_results:
+            open(map_tum_path, "w").close()
         mo = MapOptimizationNode(bus.publish, device=dev, tum_path=map_tum_path or None)
         bus.subscribe("/plane_frame_cloud2", mo.on_plane_cloud)
         bus.subscribe("/frame_odom2", mo.on_odom)
@@ -271,7 +362,8 @@ def run_sequence(root: str, tum_path: str | None = None, n_rows: int = 64, devic
         t_ns = fr["index"] * period_ns
         stamp = (t_ns // 1_000_000_000, t_ns % 1_000_000_000)
         stamps.append(stamp)
-        pco.on_frame(fr[keys[0]], fr[keys[1]], stamp)
+        pco.on_frame(fr["pos1"], fr.get("gt"), stamp,
+                     gt_mask=fr.get("s_fg_mask") if src_mode == "gt" else None)
     return dict(odom1=np.asarray(odom1, np.float64).reshape(-1, 7),
                 odom2=np.asarray(odom2, np.float64).reshape(-1, 7), stamps=stamps,
                 loops=mo.closer.constraints if mo else [])

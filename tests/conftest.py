@@ -23,7 +23,13 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def dev():
+    """cuda:0, which must be a gfx950.  A `-m gpu` run on a box where HIP does not enumerate
+    the device FAILS here instead of skipping: a green GPU suite with zero tests run would
+    claim parity it never checked (the CPU suite deselects these tests with -m "not gpu")."""
     import torch
     if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+        pytest.fail("no HIP device visible: the -m gpu suite needs an MI355X (gfx950)")
+    arch = getattr(torch.cuda.get_device_properties(0), "gcnArchName", "")
+    if not arch.startswith("gfx950"):
+        pytest.fail(f"cuda:0 is {arch!r}, not gfx950")
     return torch.device("cuda", 0)

@@ -152,3 +152,45 @@ def test_mask_before_features_equals_compacted_cloud(oracle, dev):
         ref = O.extract_planes(clouds[f][keeps[f] != 0], 64)
         got = pb.frame(f).cpu().numpy()
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), f
+
+
+def test_ring_id_upper_branch_float_subtraction(oracle, dev):
+    """frameFeature.cpp:66 `(2 - angle)` is a float subtraction: at these bin edges its
+    rounding picks the other row than a double subtraction would (known-answer cases shared with
+    tests/test_oracle_known.py); the device rows equal the oracle's."""
+    import ssf
+    from test_oracle_known import UPPER_EDGE_CASES, _f32_from_bits
+    pts = np.array([[1.0, 0.0, _f32_from_bits(zb)] for zb, _, _, _ in UPPER_EDGE_CASES], np.float32)
+    pts = np.concatenate([pts, frame(0, 0)[0]])
+    fe = ssf.Frontend(64, device=dev.index or 0)
+    out, h_off = _run(fe, [pts], dev)
+    pb, ring, roff, curv = out
+    rx, off_ref, src, rid = oracle.bin_rings(pts, 64)
+    assert rid[:3].tolist() == [c[2] for c in UPPER_EDGE_CASES]
+    assert np.array_equal(roff[0].cpu().numpy().astype(np.int64), off_ref)
+    kept = int(off_ref[-1])
+    assert np.array_equal(ring[:kept].cpu().numpy(), rx)
+
+
+def test_masked_rows_with_0_1_2_points(oracle, dev):
+    """Rows in range left with 0, 1, 2, 3 and 11 points by the keep mask (a GMM that splits a frame
+    badly does this, BASELINE configs[2]): a one-point row selects its only point, which is also its
+    last slot -- the selection stores of the other lanes must not land there.  Bit-exact vs the
+    oracle on the compacted cloud, masked and as an unmasked cloud with the same rows."""
+    import ssf
+    pts = frame(0, 0, n_az=600)[0]
+    rid = oracle.ring_ids(pts, 64)
+    keep = np.ones(len(pts), np.uint8)
+    for row, n in [(8, 0), (9, 1), (10, 2), (11, 3), (12, 11), (13, 1), (57, 1), (58, 2)]:
+        idx = np.nonzero(rid == row)[0]
+        keep[idx[n:]] = 0
+    fe = ssf.Frontend(64, device=dev.index or 0)
+    t = torch.from_numpy(np.concatenate([pts, pts])).to(dev)
+    k2 = torch.from_numpy(np.concatenate([keep, keep])).to(dev)
+    off, h_off = ssf.frame_offsets([len(pts), len(pts)], dev)
+    pb = fe.extract_planes_batch(t, off, h_off, keep=k2)
+    ref = oracle.extract_planes(pts[keep != 0], 64)
+    for f in range(2):
+        assert np.array_equal(pb.frame(f).cpu().numpy().view(np.uint32), ref.view(np.uint32)), f
+    out, h2 = _run(fe, [pts[keep != 0]], dev)
+    _check_frame(oracle, fe, out, h2, 0, pts[keep != 0], 64)

@@ -1,6 +1,7 @@
-"""End-to-end node chain: an npz DATASET_PATH directory replayed through
-PointCloudOdometry -> frameFeature -> lidarOdometry_onlyPC with the reference's topic layouts,
-/frame_odom1 and /frame_odom2 against the oracle, and the TUM file written from /frame_odom2.
+"""End-to-end node chains (SURVEY §8(b) process surface, §8(f) rows 1-2): an npz DATASET_PATH
+directory replayed through the node graphs of launch/run_onlyPC.launch, run_noSeg.launch and
+run_Seg.launch with the reference's topic layouts; /frame_odom1 and /frame_odom2 against the
+oracle, and the TUM file appended from /frame_odom2.
 
 Bars: /frame_odom1 [t, q] and /frame_odom2 accumulated poses within 1e-5 m / 1e-6 rad of the
 oracle run with the same seeded RandomState draws and the same warm-start chain."""
@@ -18,26 +19,25 @@ def _angle(q1, q2):
     return 2.0 * np.arccos(min(1.0, d))
 
 
-def test_run_sequence_matches_oracle(oracle, dev, tmp_path):
-    from ssf import io as sio
-    from ssf import nodes
-    frames = [frame(4, k, n_az=1875) for k in range(4)]
+def _dataset(tmp_path, frames, with_mask=False):
     data = tmp_path / "data"          # the reference loads every file of DATASET_PATH
     data.mkdir()
     for k, f in enumerate(frames):
-        np.savez(str(data / f"{k:06d}.npz"), pos1=f[0], gt=f[1])
+        extra = dict(s_fg_mask=f[2]) if with_mask else {}
+        np.savez(str(data / f"{k:06d}.npz"), pos1=f[0], gt=f[1], **extra)
+    return str(data)
+
+
+def test_run_onlyPC_launch_matches_oracle(oracle, dev, tmp_path):
+    """run_onlyPC.launch: PointCloudOdometry_onlyPC (cloud only, no /frame_odom1) ->
+    frameFeature -> lidarOdometry_onlyPC (Ceres-LM registration, warm start chained)."""
+    from ssf import io as sio
+    from ssf import nodes
+    frames = [frame(4, k, n_az=1875) for k in range(4)]
     tum = str(tmp_path / "traj.txt")
     with torch.cuda.device(dev):
-        res = nodes.run_sequence(str(data), tum, seed=123)
-    assert res["odom1"].shape == (4, 7) and res["odom2"].shape == (3, 7)
-
-    rs = oracle.LegacyRandomState(123)
-    for k, f in enumerate(frames):
-        ref = oracle.mask_and_pose(f[0], f[1], rs.random_sample(3))
-        assert ref["rc"] == 0
-        assert np.abs(res["odom1"][k, 0:3] - ref["t"]).max() < 1e-5
-        assert _angle(res["odom1"][k, 3:7], ref["q_xyzw"]) < 1e-6
-
+        res = nodes.run_sequence(_dataset(tmp_path, frames), tum, launch="onlyPC")
+    assert res["odom1"].shape == (0, 7) and res["odom2"].shape == (3, 7)
     planes = [oracle.extract_planes(f[0], 64) for f in frames]
     q_rel, t_rel = np.array([0.0, 0, 0, 1]), np.zeros(3)
     q_abs, t_abs = np.array([0.0, 0, 0, 1]), np.zeros(3)
@@ -48,10 +48,71 @@ def test_run_sequence_matches_oracle(oracle, dev, tmp_path):
         got = res["odom2"][k - 1]
         assert np.abs(got[0:3] - t_abs).max() < 1e-5, k
         assert _angle(got[3:7], q_abs) < 1e-6, k
-
     stamps, t, q = sio.read_tum(tum)
     assert stamps == ["0.100000000", "0.200000000", "0.300000000"]
     assert np.abs(t - res["odom2"][:, 0:3]).max() <= 5e-7 and np.abs(q - res["odom2"][:, 3:7]).max() <= 5e-7
+
+
+@pytest.mark.parametrize("launch", ["noSeg", "Seg"])
+def test_run_ssf_launch_matches_oracle(oracle, dev, tmp_path, launch):
+    """run_noSeg.launch / run_Seg.launch: PointCloudOdometry_noSeg (GMM mask, seeded) or
+    PointCloudOdometry (s_fg_mask == 0) -> Kabsch -> /frame_odom1 [t, q]; frameFeature;
+    lidarOdometry (src/lidarOdometry.cpp:145-159, 176-205): the first plane cloud pops nothing,
+    plane cloud k pops the queue front -- the pose published with frame k - 1 -- and accumulates
+    it.  /frame_odom1 against the oracle's mask + Kabsch, /frame_odom2 against the oracle's
+    accumulation of those poses in queue order, and the appended TUM file."""
+    from ssf import io as sio
+    from ssf import nodes
+    frames = [frame(6, k, n_az=1875) for k in range(5)]
+    tum = str(tmp_path / "traj.txt")
+    with open(tum, "w") as f:                      # RESULT_PATH is appended to, never wiped
+        f.write("0.000000000 0.000000 0.000000 0.000000 0.000000 0.000000 0.000000 1.000000\n")
+    with torch.cuda.device(dev):
+        res = nodes.run_sequence(_dataset(tmp_path, frames, with_mask=True), tum, seed=123,
+                                 launch=launch)
+    assert res["odom1"].shape == (5, 7) and res["odom2"].shape == (4, 7)
+    rs = oracle.LegacyRandomState(123)
+    ref_t, ref_q = [], []
+    for k, f in enumerate(frames):
+        if launch == "noSeg":
+            ref = oracle.mask_and_pose(f[0], f[1], rs.random_sample(3))
+            assert ref["rc"] == 0
+            t_k, q_k = ref["t"], ref["q_xyzw"]
+        else:
+            bg = f[2] == 0
+            rc, R, t_k = oracle.kabsch(f[0].astype(np.float64) + f[1], f[0].astype(np.float64), mask=bg)
+            assert rc == 0
+            rc, q_k = oracle.quat_from_R(R)
+            assert rc == 0
+        assert np.abs(res["odom1"][k, 0:3] - t_k).max() < 1e-5, k
+        assert _angle(res["odom1"][k, 3:7], q_k) < 1e-6, k
+        ref_t.append(np.asarray(t_k)); ref_q.append(np.asarray(q_k))
+    q_abs, t_abs = np.array([0.0, 0, 0, 1]), np.zeros(3)
+    for k in range(1, len(frames)):                 # plane cloud k <- odometryQueue.front() = pose k - 1
+        q_abs, t_abs = oracle.accumulate(q_abs, t_abs, ref_q[k - 1], ref_t[k - 1])
+        got = res["odom2"][k - 1]
+        assert np.abs(got[0:3] - t_abs).max() < 2e-5, k
+        assert _angle(got[3:7], q_abs) < 2e-6, k
+    stamps, t, q = sio.read_tum(tum)
+    assert stamps == ["0.000000000", "0.100000000", "0.200000000", "0.300000000", "0.400000000"]
+    assert np.abs(t[1:] - res["odom2"][:, 0:3]).max() <= 5e-7
+
+
+def test_ingest_node_empty_queue_raises(dev):
+    """A plane cloud that overtakes its pose: the reference reads front() of an empty queue (UB,
+    lidarOdometry.cpp:148); the node raises instead of inventing a pose."""
+    from ssf import io as sio
+    from ssf import nodes
+    bus = nodes.Bus(keep=4)
+    lo = nodes.LidarOdometryIngestNode(bus.publish, device=dev)
+    xyzi = np.zeros((20, 4), np.float32)
+    lo.on_plane_cloud(sio.xyzi_to_cloud(xyzi, (0, 0)))        # first cloud: flagStart only
+    with pytest.raises(nodes.SSFError):
+        lo.on_plane_cloud(sio.xyzi_to_cloud(xyzi, (0, 1)))
+    lo.on_odom(nodes.Float64MultiArray([1.0, 2.0, 3.0, 0.0, 0.0, 0.0, 1.0]))
+    od = lo.on_plane_cloud(sio.xyzi_to_cloud(xyzi, (0, 2)))
+    assert od.pose.position == (1.0, 2.0, 3.0) and od.pose.orientation == (0.0, 0.0, 0.0, 1.0)
+    assert len(bus.log["/plane_frame_cloud2"]) == 1
 
 
 def test_nodes_message_layouts(dev):
@@ -89,13 +150,10 @@ def test_map_optimization_node_chain(dev, tmp_path):
     from ssf import io as sio
     from ssf import nodes
     frames = [frame(5, k, n_az=900) for k in range(4)]
-    data = tmp_path / "data"
-    data.mkdir()
-    for k, f in enumerate(frames):
-        np.savez(str(data / f"{k:06d}.npz"), pos1=f[0], gt=f[1])
     tum2, tum3 = str(tmp_path / "odom2.txt"), str(tmp_path / "map.txt")
     with torch.cuda.device(dev):
-        res = nodes.run_sequence(str(data), tum2, seed=7, map_tum_path=tum3)
+        res = nodes.run_sequence(_dataset(tmp_path, frames), tum2, seed=7, map_tum_path=tum3,
+                                 launch="onlyPC")
     assert res["loops"] == []
     s2, t2, q2 = sio.read_tum(tum2)
     s3, t3, q3 = sio.read_tum(tum3)

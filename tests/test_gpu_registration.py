@@ -214,3 +214,45 @@ def test_accumulate_sequence(oracle, dev):
     for i in range(20):
         q, t = oracle.accumulate(q, t, rel[i, :4], rel[i, 4:])
         assert np.abs(out[i, 4:] - t).max() < 1e-12 and np.abs(out[i, :4] - q).max() < 1e-12
+
+
+@pytest.mark.parametrize("solver,iters,mode", [("ceres_lm", 8, 0), ("gn", 10, 1)])
+def test_ssf_register_pair_abi(oracle, dev, solver, iters, mode):
+    """ssf_register_pair: frameRegistration() on the reference's globals --
+    raw last/current plane clouds, para_q/para_t warm start in, solution + per-step log out
+    (lidarOdometry_onlyPC.cpp:147-252).  Per-iteration poses, costs and status codes against the
+    oracle; the warm start is chained over three consecutive pairs as cloudThread does
+    (:251-252, :307)."""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index, solver=solver, max_iter=iters)
+    planes = [oracle.extract_planes(frame(4, k, n_az=1875)[0], 64) for k in range(4)]
+    q, t = [0.0, 0.0, 0.0, 1.0], [0.0, 0.0, 0.0]
+    qr, tr = np.array(q), np.array(t)
+    for k in range(1, 4):
+        L = torch.from_numpy(planes[k - 1]).to(dev)
+        Cc = torch.from_numpy(planes[k]).to(dev)
+        q, t, steps, nc = fe.register_pair(L, Cc, q, t)
+        qr, tr, log, c = oracle.register_pair(planes[k - 1], planes[k], 0.05, mode=mode,
+                                              max_iter=iters, q_init=qr, t_init=tr)
+        assert nc == c and len(steps) == log.shape[0], (k, nc, c, len(steps), log.shape)
+        for i, st in enumerate(steps):
+            assert ssf._abi.STEP_STATUS[int(log[i, 8])] == st["status"], (k, i)
+            assert np.abs(np.array(st["t"]) - log[i, 4:7]).max() < TOL_T, (k, i)
+            assert _quat_angle(np.array(st["q"]), log[i, :4]) < TOL_R, (k, i)
+            assert abs(st["cost"] - log[i, 7]) <= 1e-9 * max(1.0, abs(log[i, 7]))
+        assert np.abs(np.array(t) - tr).max() < TOL_T and _quat_angle(np.array(q), qr) < TOL_R
+        qr, tr = np.array(q), np.array(t)       # chain the GPU solution (bars are per pair)
+
+
+def test_ssf_register_pair_skip_and_empty(dev):
+    """<= 10 last-frame points: no residual, the warm start is returned unchanged (:158)."""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index)
+    small = torch.zeros((10, 4), dtype=torch.float32, device=dev)
+    curr = torch.from_numpy(np.random.default_rng(0).normal(size=(50, 4)).astype(np.float32)).to(dev)
+    q0, t0 = [0.0, 0.0, 0.1, 0.99498743710662], [0.5, 0.25, -0.125]
+    q, t, steps, nc = fe.register_pair(small, curr, q0, t0)
+    assert q == q0 and t == t0 and steps == [] and nc == -1
+    empty = torch.zeros((0, 4), dtype=torch.float32, device=dev)
+    q, t, steps, nc = fe.register_pair(curr, empty, q0, t0)
+    assert q == q0 and t == t0 and nc == 0

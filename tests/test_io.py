@@ -108,3 +108,37 @@ def test_sequence_files_order_and_safe_load(tmp_path):
         sio.load_frame(str(tmp_path / "0003.npz"))
     with pytest.raises(sio.SSFError):
         sio.load_frame(files[0], keys=("pos1", "flow"))
+
+
+def test_tum_writer_appends_like_the_reference(tmp_path):
+    """mapOptmization.cpp:355 opens RESULT_PATH with std::ios::app only: an existing
+    trajectory is extended, never wiped (truncation is an explicit runner option)."""
+    p = str(tmp_path / "traj.txt")
+    with open(p, "w") as f:
+        f.write("0.000000000 0 0 0 0 0 0 1\n")
+    sio.TumWriter(p).write((1, 0), [1.0, 2.0, 3.0], [0, 0, 0, 1])
+    assert open(p).read().count("\n") == 2
+    sio.TumWriter(p, truncate=True).write((2, 0), [1.0, 2.0, 3.0], [0, 0, 0, 1])
+    assert open(p).read().count("\n") == 1
+
+
+def test_organized_cloud_with_padded_rows():
+    """height > 1 with row_step > width * point_step: each row is read at its row_step."""
+    h, w, step, pad = 3, 5, 16, 24
+    rows = np.zeros((h, w * step + pad), np.uint8)
+    pts = np.arange(h * w * 3, dtype=np.float32).reshape(h, w, 3)
+    for r in range(h):
+        rec = np.zeros((w, 4), np.float32)
+        rec[:, :3] = pts[r]
+        rows[r, : w * step] = rec.view(np.uint8).reshape(-1)
+        rows[r, w * step:] = 0xFF                      # padding garbage must not leak in
+    msg = sio.PointCloud2(sio.Header(), h, w, list(sio.VELODYNE_FIELDS), False, step,
+                          w * step + pad, rows.tobytes(), True)
+    assert np.array_equal(sio.cloud_xyz(msg), pts.reshape(-1, 3))
+    msg.row_step = w * step - 4
+    with pytest.raises(sio.SSFError):
+        sio.cloud_xyz(msg)
+    msg.row_step = w * step + pad
+    msg.data = msg.data[:-(pad + 4)]
+    with pytest.raises(sio.SSFError):
+        sio.cloud_xyz(msg)

@@ -113,3 +113,48 @@ def test_oracle_register_on_synthetic_pair(oracle):
     assert c > 100
     assert np.abs(t - np.array(tg)).max() < 0.1
     assert log.shape[0] >= 1 and np.all(np.diff(log[log[:, 8] == 1, 7]) <= 0)  # accepted steps decrease cost
+
+
+# Upper-branch bin edges where `2 - angle` (frameFeature.cpp:66, int - float: a FLOAT
+# subtraction) rounds across the edge that the double expression would not cross.  The z values
+# put a point at x = 1, y = 0 exactly on those float angles (found by ulp search).
+UPPER_EDGE_CASES = [  # (z bits, float angle, row with float '2 - angle', row with double)
+    (0x3C0EFB24, 0.5000000596046448, 5, 4),
+    (-0x3CD683DB, -1.4999998807907104, 11, 10),
+    (-0x3D32D5D0, -2.499999761581421, 14, 13),
+]
+
+
+def _f32_from_bits(b):
+    sign = b < 0
+    v = np.array([abs(b)], np.uint32).view(np.float32)[0]
+    return -v if sign else v
+
+
+def test_ring_id_upper_branch_float_subtraction(oracle):
+    """frameFeature.cpp:66 `(2 - angle) * 3.0 + 0.5`: 2 - angle is computed and rounded in
+    float, then promoted.  At these bin edges the float rounding lands on the other row."""
+    for zb, ang, row_f, row_d in UPPER_EDGE_CASES:
+        assert oracle.ring_id_of_angle(ang, 64) == row_f
+        a32 = np.float32(ang)
+        assert int(float(np.float32(2) - a32) * 3.0 + 0.5) == row_f
+        assert int((2.0 - float(a32)) * 3.0 + 0.5) == row_d != row_f
+        z = _f32_from_bits(zb)
+        assert oracle.ring_ids(np.array([[1.0, 0.0, z]], np.float32), 64).tolist() == [row_f]
+
+
+def test_xindex_knn_equals_brute_force(oracle):
+    """The oracle's x-sorted k-NN index returns the brute-force (d2, index) lists exactly,
+    including exact duplicates and equal-distance ties (quantised coordinates)."""
+    rng = np.random.default_rng(11)
+    for trial in range(4):
+        m = 700
+        c = np.zeros((m, 4), np.float32)
+        c[:, :3] = np.round(rng.normal(0, 3, (m, 3)) * (4 if trial % 2 else 64)) / (4 if trial % 2 else 64)
+        c[rng.choice(m, 50), :3] = c[rng.choice(m, 50), :3]          # exact duplicates
+        for k in (1, 5, 30):
+            for qi in rng.choice(m, 40, replace=False):
+                q = c[qi, :3] + (0 if qi % 3 else np.float32(0.125))
+                i1, d1 = oracle.knn(c, q, k)
+                i2, d2 = oracle.xknn(c, q, k)
+                assert np.array_equal(i1, i2) and np.array_equal(d1, d2), (trial, k, qi)

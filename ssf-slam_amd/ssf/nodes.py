@@ -278,7 +278,7 @@ class MapOptimizationNode:
         from scipy.spatial.transform import Rotation
         while self.planes and self.odoms:
             pm, om = self.planes[0], self.odoms[0]
-            tp, to = sio.stamp_of(pm.header), (om.header.stamp_sec, om.header.stamp_nsec)
+            tp, to = sio.stamp_of(pm.header), sio.stamp_of(om.header)
             if abs((tp[0] - to[0]) + (tp[1] - to[1]) * 1e-9) > 0.005:    # time sync (:436-439)
                 return
             self.planes.pop(0)

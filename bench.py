@@ -43,23 +43,25 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 F64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector, spec (AMD datasheet); f64 MFMA is no faster
-# HBM bytes / f64 FLOPs per k_mask_pose launch measured with rocprofv3 PMC passes on this bench
-# command (tools/pmc_traffic.py, tools/pmc_f64.py); used when their workload config matches.
-TRAFFIC_JSON = os.path.join(REPO, "profiles", "r01_k_mask_pose_traffic.json")
+# HBM bytes per launch of every kernel / f64 FLOPs per k_mask_pose launch, measured with rocprofv3
+# PMC passes on a serial run of this bench (tools/pmc_traffic.py, tools/pmc_f64.py); used when
+# their workload config matches the run's.
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "r02_traffic.json")
 F64_JSON = os.path.join(REPO, "profiles", "r02_k_mask_pose_f64.json")
 METRIC = "LiDAR front-end frames/sec (mask+feature+GN), 64-beam 120k pts, 1/2/4/8 GPUs"
 
 
-def _profile_value(path, B, N, key):
+def _load_profile(path, B, N, masked):
     try:
         with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None
     cfg = t.get("config", {})
-    if cfg.get("sequences_per_gpu") != B or cfg.get("points_per_frame") != N:
+    if (cfg.get("sequences_per_gpu") != B or cfg.get("points_per_frame") != N
+            or bool(cfg.get("mask_before_features")) != bool(masked)):
         return None
-    return t.get(key)
+    return t
 
 
 def parse(argv=None):
@@ -516,14 +518,20 @@ def main():
         "mask_passes_per_frame": passes, "gather_check": gather_ok,
         "data_gen_s": round(t_data, 2),
     }
+    traffic = _load_profile(TRAFFIC_JSON, B, N, args.mask_before_features)
+    if traffic:
+        for k, v in kernels.items():
+            t = traffic["kernels"].get(k, {}).get("traffic_bytes_per_launch")
+            if t:
+                v["traffic"] = t
     mk = kernels.get("k_mask_pose")
     if mk and "gbs" in mk:
         line["roofline"] = {"bound": "hbm", "achieved": mk["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": mk["frac"], "traffic": _profile_value(TRAFFIC_JSON, B, N,
-                                                                          "traffic_bytes_per_launch"),
+                            "frac": mk["frac"], "traffic": mk.get("traffic"),
                             "kernel": "k_mask_pose",
                             "duration": "kernel-only (one-stream kernel pass, HIP events)"}
-        flops = _profile_value(F64_JSON, B, N, "f64_flops_per_launch")
+        f64 = _load_profile(F64_JSON, B, N, args.mask_before_features)
+        flops = f64 and f64.get("f64_flops_per_launch")
         if flops:
             tf = flops / (mk["ms"] * 1e-3) / 1e12
             line["roofline_f64"] = {"bound": "valu_f64", "achieved": tf, "peak": F64_PEAK_TFLOPS,

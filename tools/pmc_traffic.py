@@ -1,68 +1,78 @@
-"""HBM traffic per launch of one kernel from two rocprofv3 counter passes (bench.py roofline.traffic).
+"""HBM traffic per launch of every kernel from two rocprofv3 counter passes (bench.py `traffic`).
 
 Collect the passes separately (FETCH_SIZE needs 3 TCC counters, WRITE_SIZE 2; one run cannot
-hold both), on the bench command whose roofline they annotate:
+hold both), on a serial bench command (one stream, so every launch is that kernel alone):
 
-    rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o f -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
-    rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o w -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o f -- python bench.py --serial ...
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o w -- python bench.py --serial ...
     python tools/pmc_traffic.py gpurun_out/pmc_fetch/f_counter_collection.csv \
         gpurun_out/pmc_write/w_counter_collection.csv --bench-log gpurun_out/pmc_fetch.log \
-        --out profiles/r01_k_mask_pose_traffic.json
+        --out profiles/r02_traffic.json
 
 Units and corrections (/opt/skills/guides/MI355X_MICROARCH.md, "HBM [CDNA4]"): FETCH_SIZE and
 WRITE_SIZE are KiB; on gfx950 FETCH_SIZE tallies wide coalesced streaming reads at half their
-bytes, so it is doubled; WRITE_SIZE is taken as is.  The first launch (cold caches, first touch)
-is reported but excluded from the per-launch mean.
+bytes, so it is doubled; WRITE_SIZE is taken as is.  The first launch of each kernel (cold
+caches, first touch) is reported but excluded from the per-launch mean.
 """
 from __future__ import annotations
 
 import argparse
 import csv
 import json
+from collections import defaultdict
+
+KERNELS = ("k_mask_pose", "k_bin_count", "k_bin_scan", "k_bin_scatter", "k_curv_select", "k_compact",
+           "k_plane_table_sorted", "k_associate_lds", "k_associate_sorted", "k_solve")
 
 
-def launches(path, kernel):
-    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+def launches(path):
+    """{kernel: [counter value per dispatch, in dispatch order]} for the front-end kernels"""
+    rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    return [float(r["Counter_Value"]) for r in rows]
+    out = defaultdict(list)
+    for r in rows:
+        name = r["Kernel_Name"]
+        for k in KERNELS:
+            if k + "(" in name or k + "<" in name or name.startswith(k) or (" " + k) in name:
+                out[k].append(float(r["Counter_Value"]))
+                break
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_csv")
     ap.add_argument("write_csv")
-    ap.add_argument("--kernel", default="k_mask_pose")
     ap.add_argument("--bench-log", help="stdout of the profiled bench run (its JSON line names the config)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
-    fetch = launches(a.fetch_csv, a.kernel)
-    write = launches(a.write_csv, a.kernel)
-    if len(fetch) < 2 or len(write) < 2:
-        raise SystemExit(f"need >= 2 launches of {a.kernel} in each pass ({len(fetch)}, {len(write)})")
-    f_mean = sum(fetch[1:]) / (len(fetch) - 1)
-    w_mean = sum(write[1:]) / (len(write) - 1)
-    out = {
-        "kernel": a.kernel,
-        "fetch_size_kib": fetch,
-        "write_size_kib": write,
-        "read_bytes_per_launch": 2.0 * f_mean * 1024.0,
-        "write_bytes_per_launch": w_mean * 1024.0,
-        "traffic_bytes_per_launch": 2.0 * f_mean * 1024.0 + w_mean * 1024.0,
-        "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half tally of wide streaming reads) + WRITE_SIZE KiB x 1024; "
-                      "first launch excluded",
-    }
+    fetch, write = launches(a.fetch_csv), launches(a.write_csv)
+    out = {"correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half tally of wide streaming reads) + "
+                         "WRITE_SIZE KiB x 1024; first launch of each kernel excluded",
+           "kernels": {}}
+    for k in KERNELS:
+            f, w = fetch.get(k, []), write.get(k, [])
+            if len(f) < 2 or len(w) < 2:
+                continue
+            fm = sum(f[1:]) / (len(f) - 1)
+            wm = sum(w[1:]) / (len(w) - 1)
+            out["kernels"][k] = dict(launches=len(f), read_bytes_per_launch=2.0 * fm * 1024.0,
+                                     write_bytes_per_launch=wm * 1024.0,
+                                     traffic_bytes_per_launch=2.0 * fm * 1024.0 + wm * 1024.0)
     if a.bench_log:
         for line in open(a.bench_log):
             if line.startswith("{"):
                 d = json.loads(line)
-                out["config"] = {k: d["config"][k] for k in ("sequences_per_gpu", "points_per_frame")}
-                k = d["kernels"].get(a.kernel)
-                if k:
-                    out["algorithmic_bytes_per_launch"] = k["bytes"]
-                    out["passes_per_frame"] = k.get("passes_per_frame")
+                out["config"] = {k: d["config"][k] for k in ("sequences_per_gpu", "points_per_frame",
+                                                              "mask_before_features")}
+                for k, v in d.get("kernels", {}).items():
+                    if k in out["kernels"] and "bytes" in v:
+                        out["kernels"][k]["algorithmic_bytes_per_launch"] = v["bytes"]
+                        out["kernels"][k]["traffic_over_algorithmic"] = (
+                            out["kernels"][k]["traffic_bytes_per_launch"] / v["bytes"])
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
-    print(json.dumps({k: v for k, v in out.items() if not isinstance(v, list)}, indent=1))
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":

@@ -102,6 +102,8 @@ def parse(argv=None):
     ap.add_argument("--launch-check", action="store_true",
                     help="CPU-only check of the rank launch: every rank joins a gloo group, rank 0 "
                          "prints the world it sees and exits (no GPU is touched)")
+    ap.add_argument("--mask-split", type=int, default=0,
+                    help="work-groups per frame of the GMM fit (0: automatic, ssf_set_mask_split)")
     ap.add_argument("--mask-streams", type=int, default=3,
                     help="mask launches of consecutive steps alternate over this many streams: the "
                          "GMM of a frame depends on no other frame, so a step's slow frames overlap "
@@ -225,6 +227,7 @@ class Pipeline:
         self.fe_mask = ssf.Frontend(args.rows, device=dev.index)
         self.fe_feat = ssf.Frontend(args.rows, device=dev.index, solver=args.solver, max_iter=iters)
         self.fe_mask.reserve(B, N)
+        self.fe_mask.mask_split(args.mask_split)
         self.fe_feat.reserve(B, N)
         n_ms = 1 if args.serial else max(1, args.mask_streams)
         self.s_masks = [torch.cuda.Stream(dev) for _ in range(n_ms)]
@@ -361,9 +364,11 @@ def rooflines(times, acc, B, N):
     model = {   # DESIGN.md §5 / SURVEY §8(d) per-unit figures
         "k_mask_pose": B * N * (24.0 * passes + 1.0) * n_mask,     # [flow,xyz] f32 per pass + mask
         "k_bin_count": 13.0 * acc["points"],                        # xyz read, row id written
-        "k_bin_scatter": 13.0 * acc["points"] + 16.0 * acc["kept"], # xyz + id read, float4 written
-        "k_curv_select": 16.0 * acc["in_range"],                    # §8(d): 16 B x points of rows in range
-        "k_compact": 36.0 * acc["plane"],
+        "k_bin_scatter": 13.0 * acc["points"] + 12.0 * acc["kept"], # xyz + id read, packed xyz written
+        # §8(d) counts 16 B per point of the rows in range (12 B xyz read + a 4-B curvature
+        # write); the product path writes no curvature, only the selected indices
+        "k_curv_select": 12.0 * acc["in_range"] + 4.0 * acc["plane"],
+        "k_compact": 20.0 * acc["plane"],                           # index + xyz read, xyzi written
         "k_plane_table_sorted": 49.0 * acc["plane"],
         "k_associate_lds": 64.0 * acc["plane_reg"],
         "k_associate_sorted": 64.0 * acc["plane_reg"],

@@ -239,12 +239,18 @@ enum {
     SSF_POSE_OUT_PASSES = 25   /* algorithmic bytes / (24 B x points): full-pass equivalents */
 };
 enum { SSF_POSE_EMPTY = -1, SSF_POSE_REFLECTION = -2, SSF_POSE_NOT_ORTHOGONAL = -3,
-       SSF_POSE_GMM_FAILED = -4 };
+       SSF_POSE_GMM_FAILED = -4, SSF_POSE_SYNC_FAILED = -5 };
 int32_t ssf_mask_pose_batch(ssf_ctx* ctx, void* stream, int32_t n_frames, const float* d_pts,
                             const float* d_flow, const int64_t* d_frame_off,
                             const int64_t* h_frame_off, int32_t mode, const uint8_t* d_mask_in,
                             const double* h_draws, int32_t reflection, uint8_t* d_bg_mask,
                             double* d_out);
+/* Work-groups per frame of the GMM fit in ssf_mask_pose_batch (no reference counterpart;
+ * results do not depend on it beyond f64 summation order): 0 = automatic (as many as keep the
+ * chip full: ~256 / frames, at most 8; 1 for 256 frames and more), 1..8 = fixed.  With more
+ * than one, a frame's points are cut into contiguous parts whose per-pass sums are exchanged
+ * in global memory; a partner that never arrives gives status SSF_POSE_SYNC_FAILED. */
+int32_t ssf_set_mask_split(ssf_ctx* ctx, int32_t parts_per_frame);
 /* Seed the context's numpy-legacy RandomState (MT19937) -- the `np.random.seed(s)` the reference
  * never calls; every GMM frame then consumes 3 doubles in frame order, as the reference's global
  * RandomState does across frames. */

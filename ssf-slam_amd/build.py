@@ -73,6 +73,21 @@ def build_diag() -> str:
     return out
 
 
+def build_variant(name: str, defines: dict) -> str:
+    """Experiment library (tools/ only, loaded through SSF_LIB): every source compiled with extra
+    -D defines into ssf/_lib/libssf_frontend_<name>.so.  Never loaded by the product path."""
+    out = os.path.join(OUT_DIR, f"libssf_frontend_{name}.so")
+    extra = [f"-D{k}={v}" for k, v in defines.items()]
+    objs = []
+    for src in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(OBJ_DIR, src.replace(".hip", f"_{name}.o"))
+        subprocess.run([HIPCC, *FLAGS, *FILE_FLAGS.get(src, []), *extra, "-c", s, "-o", o], check=True)
+        objs.append(o)
+    subprocess.run([HIPCC, *FLAGS, "-shared", *objs, "-o", out], check=True)
+    return out
+
+
 if __name__ == "__main__":
     if "--diag" in sys.argv:
         print(build_diag())

@@ -58,12 +58,15 @@ struct ssf_ctx {
     struct DrawSlot {
         DevBuf d;
         DevBuf rec;                    // Lloyd label/bound records (8 B) + relabel queue (4 B) per point
+        DevBuf sync, parts;            // frame split: ticket + arrival counters, exchange slots
         double* h = nullptr;           // pinned staging
         int64_t hcap = 0;
         hipEvent_t copied = nullptr;   // this slot's H2D finished: the staging may be rewritten
         hipEvent_t used = nullptr;     // the kernel that read this slot finished
     };
     static constexpr int kDrawSlots = 4;
+    int mask_split = 0;                // ssf_set_mask_split: 0 = automatic
+    int mask_slots = -1;               // resident k_mask_pose work-groups (queried once)
     DrawSlot dslot[kDrawSlots];
     int dnext = 0;
     DevBuf start1;
@@ -223,6 +226,8 @@ void ssf_destroy(ssf_ctx* c) {
         if (ds.h) (void)hipHostFree(ds.h);
         ds.d.release();
         ds.rec.release();
+        ds.sync.release();
+        ds.parts.release();
     }
     for (DevBuf* b : bufs) b->release();
     if (!c->prof.marks.empty()) (void)hipEventSynchronize(c->prof.marks.back().ev);
@@ -267,6 +272,12 @@ int32_t ssf_profile_read(ssf_ctx* c, ssf_kernel_time* out, int32_t cap, int32_t*
 
 const char* ssf_last_error(const ssf_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+int32_t ssf_set_mask_split(ssf_ctx* c, int32_t parts_per_frame) {
+    if (!c || parts_per_frame < 0 || parts_per_frame > 8) return SSF_E_ARG;
+    c->mask_split = parts_per_frame;
+    return SSF_OK;
+}
+
 int32_t ssf_rng_seed(ssf_ctx* c, uint32_t seed) {
     if (!c) return SSF_E_ARG;
     mt_seed(c, seed);
@@ -279,7 +290,7 @@ static int32_t ensure_features(ssf_ctx* c, int32_t n_frames, int64_t total, int6
     SSF_TRY_HIP(c, c->rid.ensure((size_t)std::max<int64_t>(total, 1)), "alloc rid");
     SSF_TRY_HIP(c, c->hist.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(n_frames * n_chunks * R, 1)), "alloc hist");
     SSF_TRY_HIP(c, c->ring_off.ensure(sizeof(int32_t) * (size_t)n_frames * (R + 1)), "alloc ring_off");
-    SSF_TRY_HIP(c, c->ring_xyzi.ensure(sizeof(float4) * (size_t)std::max<int64_t>(total, 1)), "alloc ring_xyzi");
+    SSF_TRY_HIP(c, c->ring_xyzi.ensure(3 * sizeof(float) * (size_t)std::max<int64_t>(total, 1)), "alloc ring_xyz");
     // + 64 dump slots for the selection stores of lanes without a selection (k_curv_select)
     SSF_TRY_HIP(c, c->sel.ensure(sizeof(int32_t) * (size_t)(std::max<int64_t>(total, 1) + 64)), "alloc sel");
     SSF_TRY_HIP(c, c->sel_cnt.ensure(sizeof(int32_t) * (size_t)n_frames * R), "alloc sel_cnt");
@@ -296,6 +307,8 @@ int32_t ssf_reserve(ssf_ctx* c, int32_t max_frames, int64_t max_points_per_frame
     for (auto& ds : c->dslot) {
         SSF_TRY_HIP(c, ds.d.ensure(sizeof(double) * 3 * (size_t)std::max(max_frames, 1)), "alloc draws");
         SSF_TRY_HIP(c, ds.rec.ensure(sizeof(uint2) * (size_t)(total + 2 * (int64_t)max_frames + 2) + sizeof(uint32_t) * (size_t)(total + 64 * (int64_t)max_frames)), "alloc lloyd records");
+        SSF_TRY_HIP(c, ds.sync.ensure(ssf::mask_sync_bytes(std::max(max_frames, 1)) + 16), "alloc mask sync");
+        SSF_TRY_HIP(c, ds.parts.ensure(ssf::mask_parts_bytes(std::max(max_frames, 1), 8)), "alloc mask parts");
     }
     return SSF_OK;
 }
@@ -315,11 +328,12 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
     int32_t rc = ensure_features(c, n_frames, total_points, max_frame_points);
     if (rc) return rc;
     ProfScope prof(c, stream);
-    float4* ring = d_ring_xyzi ? reinterpret_cast<float4*>(d_ring_xyzi) : c->ring_xyzi.as<float4>();
+    float4* ring4 = reinterpret_cast<float4*>(d_ring_xyzi);   // debug output only (nullable)
     int32_t* roff = d_ring_off ? d_ring_off : c->ring_off.as<int32_t>();
     hipError_t e = ssf::launch_extract_planes(
         (hipStream_t)stream, c->cfg, n_frames, d_pts, point_stride, d_frame_off, max_frame_points,
-        d_keep, c->rid.as<int8_t>(), c->hist.as<int32_t>(), roff, ring, d_curv, c->sel.as<int32_t>(),
+        d_keep, c->rid.as<int8_t>(), c->hist.as<int32_t>(), roff, c->ring_xyzi.as<float>(), ring4,
+        d_curv, c->sel.as<int32_t>(),
         c->sel.as<int32_t>() + std::max<int64_t>(total_points, 1), c->sel_cnt.as<int32_t>(), reinterpret_cast<float4*>(d_plane_xyzi), d_plane_count);
     if (e != hipSuccess) return hip_fail(c, e, "extract_planes launch");
     return SSF_OK;
@@ -532,10 +546,21 @@ int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const fl
         SSF_TRY_HIP(c, hipEventSynchronize(ds.copied), "draws event");   // staging reusable
     }
     const size_t rec_need = mode == SSF_MASK_GMM ? sizeof(uint2) * (size_t)(total + 2 * (int64_t)n_frames + 2) + sizeof(uint32_t) * (size_t)(total + 64 * (int64_t)n_frames) : 0;
-    if (ds.d.bytes < sizeof(double) * need || ds.rec.bytes < rec_need) {   // growing frees the old buffer
+    // parts per frame: fixed, or automatic -- enough to fill the resident work-group slots
+    if (c->mask_slots < 0) c->mask_slots = ssf::mask_pose_slots(c->device);
+    int G = c->mask_split;
+    if (G <= 0) G = c->mask_slots > 0 ? c->mask_slots / n_frames : 1;
+    G = std::max(1, std::min(G, 8));
+    if (mode != SSF_MASK_GMM) G = 1;
+    const size_t sync_need = G > 1 ? ssf::mask_sync_bytes(n_frames) + 16 : 0;
+    const size_t parts_need = G > 1 ? ssf::mask_parts_bytes(n_frames, G) : 0;
+    if (ds.d.bytes < sizeof(double) * need || ds.rec.bytes < rec_need || ds.sync.bytes < sync_need ||
+        ds.parts.bytes < parts_need) {                                    // growing frees the old buffer
         SSF_TRY_HIP(c, hipEventSynchronize(ds.used), "draws event");
         SSF_TRY_HIP(c, ds.d.ensure(sizeof(double) * need), "alloc draws");
         if (rec_need) SSF_TRY_HIP(c, ds.rec.ensure(rec_need), "alloc lloyd records");
+        if (sync_need) SSF_TRY_HIP(c, ds.sync.ensure(sync_need), "alloc mask sync");
+        if (parts_need) SSF_TRY_HIP(c, ds.parts.ensure(parts_need), "alloc mask parts");
     } else {
         SSF_TRY_HIP(c, hipStreamWaitEvent(s, ds.used, 0), "draws wait");   // device-side: no host stall
     }
@@ -561,7 +586,8 @@ int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const fl
     SSF_TRY_HIP(c, hipEventRecord(ds.copied, s), "draws record");
     ProfScope prof(c, stream);
     hipError_t e = ssf::launch_mask_pose(s, n_frames, d_pts, d_flow, d_frame_off, mode, d_mask_in,
-                                         ds.d.as<double>(), ds.rec.as<uint2>(), reflection, d_bg_mask, d_out);
+                                         ds.d.as<double>(), ds.rec.as<uint2>(), reflection, d_bg_mask, d_out,
+                                         G, c->mask_slots, ds.sync.as<uint32_t>(), ds.parts.as<double>());
     if (e == hipSuccess) e = hipEventRecord(ds.used, s);
     if (e != hipSuccess) return hip_fail(c, e, "mask_pose launch");
     return SSF_OK;

@@ -7,12 +7,14 @@
 //                 gives each point its rank among same-row points; waves own contiguous
 //                 quarters of the chunk and are prefixed in order -> the reference's push_back
 //                 order exactly.  The chunk is regrouped by row in LDS and stored in contiguous
-//                 per-row runs.  intensity = indexInRow + row/100.0 (:77)
+//                 per-row runs of packed xyz (12 B/pt: the ring order alone carries indexInRow,
+//                 so intensity = indexInRow + row/100.0 (:77) is recomputed where it is needed)
 //   k_curv_select one wave per (frame,row): the row streams through a circular LDS window, the
 //                 11-tap stencil (:84-107) is evaluated left to right in float, and the same
 //                 wave runs the greedy spacing rule (:110-123) with a 64-bit ballot of
 //                 candidates per 64 points (jstart is wave-uniform).
-//   k_compact     row-major concatenation of the selected points (framePlanePtr order).
+//   k_compact     row-major concatenation of the selected points (framePlanePtr order), with
+//                 their encoded intensity.
 #include "ssf_device.hpp"
 #include "ssf_internal.hpp"
 
@@ -131,13 +133,15 @@ __global__ __launch_bounds__(64) void k_bin_scan(int n_rows, int n_chunks, int32
 // one scattered store per point (a LiDAR scan interleaves the rows point by point).
 constexpr int kScatterSteps = kBinChunk / 256;   // 16 points per thread
 
+struct Xyz { float x, y, z; };                      // packed ring-ordered point (12 B)
+
 __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ pts, int stride,
                                                      const int64_t* __restrict__ frame_off,
                                                      int n_rows, int n_chunks,
                                                      const int8_t* __restrict__ rid,
                                                      const int32_t* __restrict__ chunk_base,
                                                      const int32_t* __restrict__ ring_off,
-                                                     float4* __restrict__ out) {
+                                                     Xyz* __restrict__ out, float4* __restrict__ out4) {
     __shared__ float4 tile[kBinChunk];            // 64 KiB
     __shared__ uint8_t row_of[kBinChunk];
     __shared__ int wrun[4][kMaxRows];
@@ -227,11 +231,16 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
     }
     __syncthreads();
     const int total = roff[kMaxRows];
-    for (int k = tid; k < total; k += 256) out[rbase[row_of[k]] + k] = tile[k];
+    for (int k = tid; k < total; k += 256) {
+        const float4 v = tile[k];
+        const int64_t o = rbase[row_of[k]] + k;
+        out[o] = Xyz{v.x, v.y, v.z};
+        if (out4) out4[o] = v;                      // debug ring-ordered cloud (x, y, z, intensity)
+    }
 }
 
 // One WAVE per (frame, row), four rows per work-group, no block barrier.  The wave streams its
-// row in 64-point groups (one coalesced float4 load per lane) into a 256-point circular LDS
+// row in 64-point groups (one coalesced 12-byte load per lane) into a 256-point circular LDS
 // window (point p at p & 255, see stencil11w); group g-1's 11-tap stencil (:84-107, evaluated left to
 // right in float exactly as the reference) is computed once group g has landed, and the greedy
 // spacing rule (:110-123) runs on the same wave with a 64-bit ballot of candidates per group
@@ -247,37 +256,46 @@ constexpr int kCurvDepth = SSF_CURV_DEPTH;   // 64-point groups in flight per wa
 
 // The window holds 256 points (4 groups; point p at p & 255) plus a mirror of its first 16 at
 // [256, 272), so the 11 taps of centre j are the contiguous a[b .. b + 10], b = (j - 5) & 255:
-// one base address, immediate LDS offsets.
+// one base address, immediate LDS offsets; (x, y, z) of a point in one float4.
 constexpr int kWin = 256;
 constexpr int kWinPad = kWin + 16;
 
-SSF_DEV float stencil11w(const float* a, int j) {
-    const float* t = a + ((j - 5) & (kWin - 1));
-    float s = t[0] + t[1];
-    s = s + t[2];
-    s = s + t[3];
-    s = s + t[4];
-    s = s - 10.0f * t[5];
-    s = s + t[6];
-    s = s + t[7];
-    s = s + t[8];
-    s = s + t[9];
-    s = s + t[10];
-    return s;
+// The 11 taps of centre j from a float4 (x, y, z, -) window: 11 ds_read_b128 (16-B aligned,
+// immediate offsets) serve all three coordinates; each coordinate's sum is evaluated left to
+// right in float exactly as frameFeature.cpp:86-105.
+SSF_DEV void stencil11w(const float4* a, int j, float& dx, float& dy, float& dz) {
+    const float4* t = a + ((j - 5) & (kWin - 1));
+    float4 u[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) {
+        u[k] = t[k];
+        // keep .w live: a whole-float4 read is ds_read_b128 (4 LDS cycles per wave), the
+        // x, y, z read the compiler would otherwise emit is ds_read_b96 (8 cycles)
+        asm volatile("" ::"v"(u[k].w));
+    }
+    float sx = u[0].x + u[1].x, sy = u[0].y + u[1].y, sz = u[0].z + u[1].z;
+#pragma unroll
+    for (int k = 2; k < 11; ++k) {
+        if (k == 5) { sx = sx - 10.0f * u[5].x; sy = sy - 10.0f * u[5].y; sz = sz - 10.0f * u[5].z; }
+        else { sx = sx + u[k].x; sy = sy + u[k].y; sz = sz + u[k].z; }
+    }
+    dx = sx; dy = sy; dz = sz;
 }
 
-template <bool kCurv>
+// kHalves: 64-entry selection stores per trip (a trip selects <= 64 kCurvDepth / plane_span + 1
+// points: one store for plane_span >= 4, two below)
+template <bool kCurv, int kHalves>
 __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__ frame_off,
                                                      int n_rows, int row_start, int row_end,
                                                      float plane_min, int plane_span,
                                                      const int32_t* __restrict__ ring_off,
-                                                     const float4* __restrict__ rxyzi,
+                                                     const Xyz* __restrict__ rxyz,
                                                      float* __restrict__ curv,
                                                      int32_t* __restrict__ sel,
                                                      int32_t* __restrict__ sel_cnt,
                                                      int32_t* __restrict__ sel_dump) {
-    __shared__ float win[kCurvRowsPerWG][3][kWinPad];
-    __shared__ int32_t slist[kCurvRowsPerWG][64 * (kCurvDepth / 2 + 1)];
+    __shared__ float4 win[kCurvRowsPerWG][kWinPad];
+    __shared__ int32_t slist[kCurvRowsPerWG][64 * kHalves];
     // the wave index through readfirstlane: the compiler then knows the row, its length and
     // every loop bound are wave-uniform (scalar loads, no exec-masked loops)
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -293,26 +311,26 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
         if (lane == 0) sel_cnt[(int64_t)f * n_rows + r] = 0;
         return;
     }
-    float* wx = win[w][0];
-    float* wy = win[w][1];
-    float* wz = win[w][2];
+    float4* wv = win[w];
     int32_t* sl = slist[w];
-    const float4* src = rxyzi + base;
+    const Xyz* src = rxyz + base;
     const int ng = (n_r + 63) >> 6;
     auto load = [&](int g) { return src[min(64 * g + lane, n_r - 1)]; };   // clamped
     int cnt = 0, nl = 0, jstart = 0;                           // wave-uniform
-    auto group = [&](float4& buf, int g) {
+    auto group = [&](Xyz& buf, int g) {
         {                                                      // group g into the window
             const int p = (64 * g + lane) & (kWin - 1);
-            wx[p] = buf.x; wy[p] = buf.y; wz[p] = buf.z;
-            if (p < kWinPad - kWin) { wx[p + kWin] = buf.x; wy[p + kWin] = buf.y; wz[p + kWin] = buf.z; }
+            const float4 q = make_float4(buf.x, buf.y, buf.z, 0.0f);
+            wv[p] = q;
+            if (p < kWinPad - kWin) wv[p + kWin] = q;
             buf = load(g + kCurvDepth);
         }
         if (g == 0 || g > ng) return;                          // uniform
         const int j = 64 * (g - 1) + lane;                     // group g-1: its stencil is complete
         float v = 0.0f;
         if (j >= 5 && j < n_r - 5) {
-            const float dx = stencil11w(wx, j), dy = stencil11w(wy, j), dz = stencil11w(wz, j);
+            float dx, dy, dz;
+            stencil11w(wv, j, dx, dy, dz);
             v = dx * dx + dy * dy;
             v = v + dz * dz;
         }
@@ -332,12 +350,13 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
         }
         nl = __builtin_amdgcn_readfirstlane(nl);
     };
-    // a trip's selections (<= 64 kCurvDepth / plane_span + 1 <= 128) leave with unconditional
-    // stores; lanes without one write a 64-slot dump after the last point of the batch.  (The
-    // row's own last slot is NOT free: a one-point row selects its point 0 = its last slot.)
-    int32_t* const dump = sel_dump + lane;
+    // a trip's selections (<= 64 kHalves) leave with unconditional stores; lanes without one write
+    // the row's last slot, which no selection list reaches when the row has >= 2 points (at most
+    // ceil(n_r / 2) entries for plane_span >= 2).  A ONE-point row selects its point 0, its last
+    // slot: those lanes write a 64-slot dump after the last point of the batch instead.
+    int32_t* const spare = n_r >= 2 ? sel + base + n_r - 1 : sel_dump + lane;
     // prologue loads in buffer order (the loop's waits count on b[0] being the oldest)
-    float4 b[kCurvDepth];
+    Xyz b[kCurvDepth];
 #pragma unroll
     for (int k = 0; k < kCurvDepth; ++k) {
         b[k] = load(k);
@@ -348,8 +367,8 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
         for (int k = 0; k < kCurvDepth; ++k) group(b[k], g + k);
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int h = 0; h < kCurvDepth / 2 + 1; ++h)   // >= 64 kCurvDepth / plane_span + 1 entries
-            *(lane + 64 * h < nl ? sel + base + cnt + 64 * h + lane : dump) = sl[64 * h + lane];
+        for (int h = 0; h < kHalves; ++h)
+            *(lane + 64 * h < nl ? sel + base + cnt + 64 * h + lane : spare) = sl[64 * h + lane];
         __builtin_amdgcn_wave_barrier();
         cnt += nl;
         nl = 0;
@@ -359,7 +378,7 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
 
 __global__ __launch_bounds__(256) void k_compact(const int64_t* __restrict__ frame_off, int n_rows,
                                                  const int32_t* __restrict__ ring_off,
-                                                 const float4* __restrict__ rxyzi,
+                                                 const Xyz* __restrict__ rxyz,
                                                  const int32_t* __restrict__ sel,
                                                  const int32_t* __restrict__ sel_cnt,
                                                  float4* __restrict__ plane,
@@ -372,13 +391,19 @@ __global__ __launch_bounds__(256) void k_compact(const int64_t* __restrict__ fra
     if (r == n_rows - 1 && tid == 0) plane_count[f] = pre + n;
     const int64_t fb = frame_off[f];
     const int64_t base = fb + ring_off[(int64_t)f * (n_rows + 1) + r];
-    for (int k = tid; k < n; k += blockDim.x) plane[fb + pre + k] = rxyzi[base + sel[base + k]];
+    const double rfrac = (double)r / 100.0;
+    for (int k = tid; k < n; k += blockDim.x) {
+        const int j = sel[base + k];                 // indexInRow
+        const Xyz p = rxyz[base + j];
+        plane[fb + pre + k] = make_float4(p.x, p.y, p.z, (float)((double)j + rfrac));   // :77
+    }
 }
 
 hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_frames,
                                  const float* pts, int stride, const int64_t* frame_off,
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
-                                 int32_t* ring_off, float4* ring_xyzi, float* curv, int32_t* sel,
+                                 int32_t* ring_off, float* ring_xyz, float4* ring_xyzi, float* curv,
+                                 int32_t* sel,
                                  int32_t* sel_dump, int32_t* sel_cnt, float4* plane,
                                  int32_t* plane_count) {
     const int R = cfg.n_rows;
@@ -394,21 +419,23 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
     if (n_chunks > 0) {
         kmark(s, "k_bin_scatter");
         hipLaunchKernelGGL(k_bin_scatter, dim3(n_chunks, n_frames), dim3(256), 0, s, pts, stride,
-                           frame_off, R, n_chunks, rid, hist, ring_off, ring_xyzi);
+                           frame_off, R, n_chunks, rid, hist, ring_off,
+                           reinterpret_cast<Xyz*>(ring_xyz), ring_xyzi);
     }
     const dim3 cgrid((R + kCurvRowsPerWG - 1) / kCurvRowsPerWG, n_frames);
     kmark(s, "k_curv_select");
-    if (curv)
-        hipLaunchKernelGGL(k_curv_select<true>, cgrid, dim3(64 * kCurvRowsPerWG), 0, s, frame_off, R,
-                           cfg.row_start, cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off,
-                           ring_xyzi, curv, sel, sel_cnt, sel_dump);
-    else
-        hipLaunchKernelGGL(k_curv_select<false>, cgrid, dim3(64 * kCurvRowsPerWG), 0, s, frame_off, R,
-                           cfg.row_start, cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off,
-                           ring_xyzi, curv, sel, sel_cnt, sel_dump);
+    const Xyz* rx = reinterpret_cast<const Xyz*>(ring_xyz);
+    const bool two = cfg.plane_span < 4;
+#define SSF_CURV_LAUNCH(C, H)                                                                     \
+    hipLaunchKernelGGL((k_curv_select<C, H>), cgrid, dim3(64 * kCurvRowsPerWG), 0, s, frame_off, R, \
+                       cfg.row_start, cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off, rx, curv, \
+                       sel, sel_cnt, sel_dump)
+    if (curv) { if (two) SSF_CURV_LAUNCH(true, 2); else SSF_CURV_LAUNCH(true, 1); }
+    else { if (two) SSF_CURV_LAUNCH(false, 2); else SSF_CURV_LAUNCH(false, 1); }
+#undef SSF_CURV_LAUNCH
     kmark(s, "k_compact");
     hipLaunchKernelGGL(k_compact, dim3(R, n_frames), dim3(256), 0, s, frame_off, R, ring_off,
-                       ring_xyzi, sel, sel_cnt, plane, plane_count);
+                       rx, sel, sel_cnt, plane, plane_count);
     return hipGetLastError();
 }
 

@@ -252,18 +252,19 @@ SSF_DEV void load_raw(const float* __restrict__ P, const float* __restrict__ Fl,
     r[3] = P[3 * i];  r[4] = P[3 * i + 1];  r[5] = P[3 * i + 2];
 }
 
+// Points [r0, r1) of the frame (the work-group's part, see Split).
 template <class Fn>
-SSF_DEV void for_points(const float* __restrict__ P, const float* __restrict__ Fl, int64_t n, Fn&& fn) {
+SSF_DEV void for_points(const float* __restrict__ P, const float* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
     const int64_t T = blockDim.x;
-    int64_t i = threadIdx.x;
-    if (i >= n) return;
+    int64_t i = r0 + threadIdx.x;
+    if (i >= r1) return;
     float rn[6];
     load_raw(P, Fl, i, rn);
-    for (; i < n; i += T) {
+    for (; i < r1; i += T) {
         double x[6];
 #pragma unroll
         for (int d = 0; d < 6; ++d) x[d] = (double)rn[d];
-        load_raw(P, Fl, min(i + T, n - 1), rn);     // unconditional (clamped): a counted wait
+        load_raw(P, Fl, min(i + T, r1 - 1), rn);    // unconditional (clamped): a counted wait
         fn(i, x);
     }
 }
@@ -278,23 +279,24 @@ SSF_DEV double uni(double v) {
 // Lloyd only: D points in flight per thread (a rolling register buffer of raw floats).  Each
 // thread visits its points in the same order as for_points, so every sum is bit-identical.
 template <int D, class Fn>
-SSF_DEV void for_points_deep(const float* __restrict__ P, const float* __restrict__ Fl, int64_t n, Fn&& fn) {
+SSF_DEV void for_points_deep(const float* __restrict__ P, const float* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
     const int64_t T = blockDim.x;
-    const int64_t i0 = threadIdx.x;
+    const int64_t i0 = r0 + threadIdx.x;
+    if (r1 <= r0) return;                                  // uniform (an empty part)
     // loads are unconditional (indices clamped to the last point): the compiler can then count
     // them and wait with vmcnt(N) instead of draining every prefetch at a conditional join
     float buf[D][6];
 #pragma unroll
-    for (int d = 0; d < D; ++d) load_raw(P, Fl, min(i0 + d * T, n - 1), buf[d]);
-    for (int64_t base = i0; base < n; base += D * T) {
+    for (int d = 0; d < D; ++d) load_raw(P, Fl, min(i0 + d * T, r1 - 1), buf[d]);
+    for (int64_t base = i0; base < r1; base += D * T) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             const int64_t i = base + d * T;
             double x[6];
 #pragma unroll
             for (int k = 0; k < 6; ++k) x[k] = (double)buf[d][k];
-            load_raw(P, Fl, min(i + D * T, n - 1), buf[d]);
-            if (i < n) fn(i, x);
+            load_raw(P, Fl, min(i + D * T, r1 - 1), buf[d]);
+            if (i < r1) fn(i, x);
         }
     }
 }
@@ -304,20 +306,20 @@ SSF_DEV void for_points_deep(const float* __restrict__ P, const float* __restric
 // last step may not exist (w1 = 0: computed on a duplicate, weighted out).  Loads clamped and
 // unconditional, as in for_points.
 template <class Fn>
-SSF_DEV void for_point_pairs(const float* __restrict__ P, const float* __restrict__ Fl, int64_t n, Fn&& fn) {
+SSF_DEV void for_point_pairs(const float* __restrict__ P, const float* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
     const int64_t T = blockDim.x;
-    int64_t i = threadIdx.x;
-    if (i >= n) return;
+    int64_t i = r0 + threadIdx.x;
+    if (i >= r1) return;
     float ra[6], rb[6];
     load_raw(P, Fl, i, ra);
-    load_raw(P, Fl, min(i + T, n - 1), rb);
-    for (; i < n; i += 2 * T) {
+    load_raw(P, Fl, min(i + T, r1 - 1), rb);
+    for (; i < r1; i += 2 * T) {
         double xa[6], xb[6];
 #pragma unroll
         for (int d = 0; d < 6; ++d) { xa[d] = (double)ra[d]; xb[d] = (double)rb[d]; }
-        const double wb = (i + T < n) ? 1.0 : 0.0;
-        load_raw(P, Fl, min(i + 2 * T, n - 1), ra);
-        load_raw(P, Fl, min(i + 3 * T, n - 1), rb);
+        const double wb = (i + T < r1) ? 1.0 : 0.0;
+        load_raw(P, Fl, min(i + 2 * T, r1 - 1), ra);
+        load_raw(P, Fl, min(i + 3 * T, r1 - 1), rb);
         fn(xa, xb, wb);
     }
 }
@@ -419,6 +421,79 @@ __device__ __noinline__ int kabsch_finish(const double* k, const double cs[3], c
     return status;
 }
 
+// ---- one frame over G work-groups --------------------------------------------------------
+// With G > 1 (small batches: G x frames fills the chip; see launch_mask_pose) every frame is
+// cut into G contiguous parts of its points, one work-group each.  Each pass then sums over
+// the work-group's part and the G partial sums are exchanged through global memory: every part
+// stores its block totals write-through (sc1, relaxed agent-scope atomic stores) into its slot,
+// drains them (s_waitcnt vmcnt(0)) and adds 1 to the frame's arrival counter; lane 0 polls the
+// counter (relaxed agent loads, s_sleep) until all G parts of this exchange have arrived, and
+// the totals are read back with sc1 loads and added in part order -- so every work-group of the
+// frame holds the same bits and runs the same lane-0 algebra to the same decisions
+// (cdna_hip_programming.md Guideline 16, MI355X_MICROARCH.md "Valid forms", row 1: one
+// storing wave, one atomic-add signal, sc1 polls and sc1 loads, one work-group per CU).
+// Slots are double-buffered by exchange parity: a part can run at most one exchange ahead of a
+// reader of the previous one.  Work-groups take (frame, part) tickets in order from a counter,
+// so every partly started frame has its parts on resident work-groups and the ones it waits for
+// are taken by the next work-group that becomes free (no wait on a work-group that cannot be
+// dispatched).  A bounded spin turns a lost partner into status SSF_POSE_SYNC_FAILED, never a hang.
+constexpr int kSlot = 32;                         // doubles per part and exchange
+constexpr int kMaxSplit = 8;                      // parts per frame at most
+constexpr uint32_t kSpinLimit = 1u << 24;         // x s_sleep 2 (~128 cycles): ~1 s
+
+struct Split {
+    int G, g;                  // parts per frame, this work-group's part
+    int64_t r0, r1;            // its points [r0, r1) of the frame
+    double* part;              // the frame's slots [2][G][kSlot]
+    uint32_t* arrive;          // the frame's arrival counter (monotonic over its exchanges)
+    uint32_t seq;              // exchanges done (uniform)
+};
+
+template <int N, bool kMin = false>
+SSF_DEV bool exchange(Split& X, double (&v)[N], double* tmp, int* okflag) {
+    static_assert(N <= kSlot, "exchange: N <= kSlot");
+    if (X.G == 1) return true;
+    double* slot = X.part + (size_t)(X.seq & 1u) * (size_t)X.G * kSlot;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        if (threadIdx.x == (unsigned)k)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(slot + X.g * kSlot + k),
+                               (unsigned long long)__double_as_longlong(v[k]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    X.seq += 1u;
+    if (threadIdx.x < 64) {                        // wave 0 stored every value
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) {
+            __hip_atomic_fetch_add(X.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t target = (uint32_t)X.G * X.seq;
+            uint32_t spins = 0;
+            int ok = 1;
+            while (__hip_atomic_load(X.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > kSpinLimit) { ok = 0; break; }
+            }
+            *okflag = ok;
+        }
+    }
+    __syncthreads();
+    if (!*okflag) return false;                    // uniform
+    if (threadIdx.x < (unsigned)N) {
+        double acc = kMin ? __builtin_inf() : 0.0;
+        for (int gg = 0; gg < X.G; ++gg) {
+            const double x = __longlong_as_double((long long)__hip_atomic_load(
+                reinterpret_cast<unsigned long long*>(slot + gg * kSlot + threadIdx.x), __ATOMIC_RELAXED,
+                __HIP_MEMORY_SCOPE_AGENT));
+            acc = kMin ? (x < acc ? x : acc) : acc + x;
+        }
+        tmp[threadIdx.x] = acc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = tmp[k];
+    __syncthreads();
+    return true;
+}
+
 SSF_DEV void accum_kabsch(double (&k)[16], const double* x, const double cs[3], const double cd[3]) {
     double s[3], d[3];
     for (int i = 0; i < 3; ++i) { d[i] = x[3 + i] - cd[i]; s[i] = (x[3 + i] + x[i]) - cs[i]; }
@@ -435,21 +510,56 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     const float* __restrict__ pts, const float* __restrict__ flow,
     const int64_t* __restrict__ frame_off, int mode, const uint8_t* __restrict__ mask_in,
     const double* __restrict__ draws, uint2* __restrict__ lloyd_rec, int reflection,
-    uint8_t* __restrict__ bg_mask, double* __restrict__ out_all) {
+    uint8_t* __restrict__ bg_mask, double* __restrict__ out_all, int n_frames, int G,
+    uint32_t* __restrict__ sync, double* __restrict__ parts) {
     __shared__ MaskShared S;
     __shared__ double red[kNW * 32];
     __shared__ int ired[kNW];
     __shared__ unsigned long long cand_lds[2];
     __shared__ double bsum[kKppBlocks];   // k-means++ per-64-point-block distance totals
     __shared__ uint32_t lq[kNW * kLQ];     // Lloyd skip passes: per-wave relabel entries of a trip
-    const int f = blockIdx.x, tid = threadIdx.x;
+    __shared__ double xtmp[kSlot];          // exchange totals
+    __shared__ int tk, okflag;
+    const int tid = threadIdx.x;
+    // G == 1: work-group = frame.  G > 1: (frame, part) tickets in order (see Split).
+    for (int iter = 0;; ++iter) {
+    int f, g = 0;
+    if (G == 1) {
+        if (iter > 0) break;
+        f = blockIdx.x;
+    } else {
+        __syncthreads();                       // the previous frame's readers of S / tk are done
+        if (tid == 0) tk = (int)atomicAdd(sync, 1u);
+        __syncthreads();
+        f = tk / G;
+        g = tk - f * G;
+        if (f >= n_frames) break;              // uniform: every wave leaves
+    }
+    [&]() {                                    // one frame part; `return` ends it
     const int64_t fb = frame_off[f], n = frame_off[f + 1] - fb;
     const float* P = pts + 3 * fb;
     const float* Fl = flow + 3 * fb;
     double* out = out_all + (int64_t)f * SSF_POSE_OUT_STRIDE;
+    Split X;
+    X.G = G; X.g = g;
+    {
+        const int64_t chunk = ((n + G - 1) / G + 127) / 128 * 128;   // parts start at even records
+        X.r0 = min(n, (int64_t)g * chunk);
+        X.r1 = min(n, X.r0 + chunk);
+    }
+    X.part = parts + (size_t)f * 2 * (size_t)G * kSlot;
+    X.arrive = sync + 4 + f;
+    X.seq = 0;
+    const int64_t r0 = X.r0, r1 = X.r1;
+    auto sync_failed = [&]() {                 // a partner never arrived: report, never hang
+        if (tid == 0 && g == 0) {
+            for (int i = 0; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
+            out[SSF_POSE_OUT_STATUS] = SSF_POSE_SYNC_FAILED;
+        }
+    };
     if (tid == 0) {
         S.passes = 0; S.status = 0; S.km_iter = 0; S.em_iter = 0; S.converged = 0;
-        for (int i = 26; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
+        if (g == 0) for (int i = 26; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
     }
 #ifdef SSF_MASK_STAMPS
     const unsigned long long stamp0 = __builtin_amdgcn_s_memtime();
@@ -488,7 +598,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     }
 
     if (n < 2) {
-        if (tid == 0) {
+        if (tid == 0 && g == 0) {
             for (int i = 0; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
             out[SSF_POSE_OUT_STATUS] = SSF_POSE_GMM_FAILED;
         }
@@ -504,7 +614,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         double a[27];
 #pragma unroll
         for (int i = 0; i < 27; ++i) a[i] = 0.0;
-        for_points(P, Fl, n, [&](int64_t i, const double* x) {
+        for_points(P, Fl, r0, r1, [&](int64_t i, const double* x) {
             double v[6];
 #pragma unroll
             for (int d = 0; d < 6; ++d) { v[d] = x[d] - x0[d]; a[d] += v[d]; }
@@ -514,6 +624,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
                 for (int c = r; c < 6; ++c) a[6 + up(r, c)] += v[r] * v[c];
         });
         block_sum_rs<27>(a, red);
+        if (!exchange<27>(X, a, xtmp, &okflag)) { sync_failed(); return; }
         if (tid == 0) {
             const double nn = (double)n;
             double m[6];
@@ -560,8 +671,9 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         // distances to the first centre; each wave owns a contiguous segment so the
         // in-order cumulative sum needs only one block-level exchange of wave totals
         const int nw = blockDim.x >> 6, w = tid >> 6, lane = lane_id();
-        const int64_t seg = (((n + nw - 1) / nw) + 63) / 64 * 64;
-        const int64_t ws = (int64_t)w * seg, we = ws + seg < n ? ws + seg : n;
+        const int64_t nloc = r1 - r0;
+        const int64_t seg = (((nloc + nw - 1) / nw) + 63) / 64 * 64;
+        const int64_t ws = r0 + (int64_t)w * seg, we = ws + seg < r1 ? ws + seg : r1;
         // D(i) = squared distance to the first centre; recomputed (same expression, same bits)
         // wherever it is needed instead of being stored
         auto dist0 = [&](int64_t i) {
@@ -598,6 +710,19 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         __syncthreads();
         double pot = 0.0, carry = 0.0;
         for (int k = 0; k < nw; ++k) { if (k == w) carry = pot; pot += red[k]; }
+        if (G > 1) {
+            // the in-order cumulative sum runs over the parts in order: part g starts after the
+            // potentials of parts 0..g-1 (part totals exchanged as a G-vector)
+            double tv[kMaxSplit];
+#pragma unroll
+            for (int k = 0; k < kMaxSplit; ++k) tv[k] = k == g ? pot : 0.0;
+            if (!exchange<kMaxSplit>(X, tv, xtmp, &okflag)) { sync_failed(); return; }
+            double before = 0.0, total = 0.0;
+#pragma unroll
+            for (int k = 0; k < kMaxSplit; ++k) { if (k < g) before += tv[k]; total += tv[k]; }
+            carry += before;
+            pot = total;
+        }
         if (tid == 0) {
             S.rand1 = draws[3 * f + 1] * pot;
             S.rand2 = draws[3 * f + 2] * pot;
@@ -660,8 +785,10 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             carry += __shfl(v, 63, 64);
         }
         __syncthreads();
-        const int64_t cand[2] = {cand_lds[0] < (unsigned long long)n ? (int64_t)cand_lds[0] : n - 1,
-                                 cand_lds[1] < (unsigned long long)n ? (int64_t)cand_lds[1] : n - 1};
+        double cmin[2] = {(double)cand_lds[0], (double)cand_lds[1]};   // < 2^53: exact
+        if (!exchange<2, true>(X, cmin, xtmp, &okflag)) { sync_failed(); return; }
+        const int64_t cand[2] = {cmin[0] < (double)n ? (int64_t)cmin[0] : n - 1,
+                                 cmin[1] < (double)n ? (int64_t)cmin[1] : n - 1};
         double cc[2][6], ccn[2] = {0.0, 0.0};
         for (int j = 0; j < 2; ++j) {
             double x[6];
@@ -689,6 +816,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             }
         }
         block_sum<2>(cp, red);
+        if (!exchange<2>(X, cp, xtmp, &okflag)) { sync_failed(); return; }
         if (tid == 0) {
             const int best = cp[1] < cp[0] ? 1 : 0;
             S.c1 = cand[best];
@@ -720,7 +848,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     uint2* __restrict__ LR = lloyd_rec + ((fb + 2 * (int64_t)f + 1) & ~(int64_t)1);
     // the relabel queues follow the records: frame f's at fb + 64 f, n entries + 64 spare slots
     uint32_t* __restrict__ LQ =
-        reinterpret_cast<uint32_t*>(lloyd_rec + frame_off[gridDim.x] + 2 * (int64_t)gridDim.x + 2) + fb +
+        reinterpret_cast<uint32_t*>(lloyd_rec + frame_off[n_frames] + 2 * (int64_t)n_frames + 2) + fb +
         64 * (int64_t)f;
     for (int it = 0; it < kLloydMax; ++it) {
         if (tid == 0) {
@@ -788,7 +916,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             // from the previous centres (the pass that wrote it used the same expression)
             const double cpn0 = uni(S.csnp[0]), cpn1 = uni(S.csnp[1]);
             auto full_pass = [&](auto wrec_c) {
-                for_points_deep<kLloydDeep>(P, Fl, n, [&](int64_t i, const double* x) {
+                for_points_deep<kLloydDeep>(P, Fl, r0, r1, [&](int64_t i, const double* x) {
                     const LdsDouble* cenp = lds_laundered(S.cenp);
                     double dp0 = 0.0, dp1 = 0.0;
 #pragma unroll
@@ -802,7 +930,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             };
             if (wrec) full_pass(std::true_type{});    // two loop bodies: no branch per point
             else full_pass(std::false_type{});
-            nlab = (int)((n - tid + blockDim.x - 1) / blockDim.x);
+            nlab = (int)((r1 - r0 - tid + blockDim.x - 1) / blockDim.x);
         } else {
             // skip pass, two streams per wave over its own segment.  (1) the records, 16 bytes
             // (two records) per lane per load, 8 loads in flight: the points whose sign could
@@ -810,8 +938,8 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             // global memory.  (2) the queue, 512 entries at a time: every entry load, then every
             // point gather, then the relabelling -- two round trips per 512 queued points.
             const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = lane_id();
-            const int64_t seg = ((n + kNW - 1) / kNW + 127) / 128 * 128;
-            const int64_t ws = (int64_t)w * seg, we = ws + seg < n ? ws + seg : n;
+            const int64_t seg = ((r1 - r0 + kNW - 1) / kNW + 127) / 128 * 128;
+            const int64_t ws = r0 + (int64_t)w * seg, we = ws + seg < r1 ? ws + seg : r1;
             uint32_t* __restrict__ WQ = LQ + ws;        // capacity seg >= the wave's points
             const int64_t qspare = n - ws;               // LQ[n, n + 64): spare slots
             const uint4* __restrict__ LR4 = reinterpret_cast<const uint4*>(LR);
@@ -881,6 +1009,16 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         block_sum_rs<14>(acc, red);
         changed = block_sum_scalar<int>(changed, ired);
         nlab = block_sum_scalar<int>(nlab, ired);
+        if (G > 1) {
+            double v[16];
+#pragma unroll
+            for (int k = 0; k < 14; ++k) v[k] = acc[k];
+            v[14] = (double)changed; v[15] = (double)nlab;
+            if (!exchange<16>(X, v, xtmp, &okflag)) { sync_failed(); return; }
+#pragma unroll
+            for (int k = 0; k < 14; ++k) acc[k] = v[k];
+            changed = (int)v[14]; nlab = (int)v[15];
+        }
         if (tid == 0) {
             // traffic accounting in 24-byte-per-point units: a full pass reads [flow, xyz] (+8 B
             // of records written when wrec); a skip pass reads 8 B of records per point and
@@ -941,7 +1079,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         double acc[28];
 #pragma unroll
         for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-        for_points(P, Fl, n, [&](int64_t, const double* x) {
+        for_points(P, Fl, r0, r1, [&](int64_t, const double* x) {
             double v[6], dt0 = 0.0, dt1 = 0.0;
 #pragma unroll
             for (int d = 0; d < 6; ++d) { v[d] = x[d] - mean[d]; dt0 += v[d] * cen[d]; dt1 += v[d] * cen[6 + d]; }
@@ -957,6 +1095,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             }
         });
         block_sum_rs<28>(acc, red);
+        if (!exchange<28>(X, acc, xtmp, &okflag)) { sync_failed(); return; }
         if (tid == 0) {
             S.passes += 1;
             for (int k = 0; k < 28; ++k) S.sums[k] = acc[k];
@@ -982,7 +1121,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         // mantissa * 2^pexp (frexp per point: the product never overflows, one log per thread)
         double prod = 1.0;
         int pexp = 0;
-        for_point_pairs(P, Fl, n, [&](const double* xa, const double* xb, double wb) {
+        for_point_pairs(P, Fl, r0, r1, [&](const double* xa, const double* xb, double wb) {
             // Aq / bq are re-read from LDS once per PAIR of points (lds_laundered)
             const LdsDouble* Aq = lds_laundered(S.Aq);
             const LdsDouble* bq = lds_laundered(S.bq);
@@ -1015,6 +1154,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         });
         acc[28] += log(prod) + (double)pexp * 0.69314718055994530942;
         block_sum_rs<29>(acc, red);
+        if (!exchange<29>(X, acc, xtmp, &okflag)) { sync_failed(); return; }
         if (tid == 0) {
             S.passes += 1;
             S.em_iter = it;
@@ -1041,7 +1181,9 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         double k1[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) k1[i] = 0.0;
-        for_points(P, Fl, n, [&](int64_t i, const double* x) {
+        if (tid == 0) S.label0 = 0;
+        __syncthreads();
+        for_points(P, Fl, r0, r1, [&](int64_t i, const double* x) {
             // Aq / bq are re-read from LDS (broadcast ds_reads) for every point (lds_laundered)
             const LdsDouble* Aq = lds_laundered(S.Aq);
             const LdsDouble* bq = lds_laundered(S.bq);
@@ -1066,9 +1208,19 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             }
         });
         block_sum_rs<16>(k1, red);
+        if (G > 1) {                             // + the label of point 0 (part 0 has it)
+            double v[17];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = k1[k];
+            v[16] = g == 0 ? (double)S.label0 : 0.0;
+            if (!exchange<17>(X, v, xtmp, &okflag)) { sync_failed(); return; }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) k1[k] = v[k];
+            if (tid == 0) S.label0 = (int)v[16];
+            __syncthreads();
+        }
         if (tid == 0) {
             S.passes += 1;
-            for (int i = 0; i < 26; ++i) out[i] = 0.0;
             const double n1 = k1[0];
             int bg;
             if (n1 * 2.0 > (double)n) bg = 1;
@@ -1076,45 +1228,72 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             else bg = S.label0;                     // Counter.most_common tie -> first seen
             S.bg = bg;
             S.bg_pred = pred;
-            double* kb = S.sums;
-            for (int i = 0; i < 16; ++i) kb[i] = bg ? k1[i] : S.ktot[i] - k1[i];
-            const double cs[3] = {S.x0[3] + S.x0[0], S.x0[4] + S.x0[1], S.x0[5] + S.x0[2]};
-            const double cd[3] = {S.x0[3], S.x0[4], S.x0[5]};
-            int st = S.status;
-            if (st == 0) st = kabsch_finish(kb, cs, cd, reflection, out);
-            out[SSF_POSE_OUT_STATUS] = st;
-            out[SSF_POSE_OUT_BGLABEL] = bg;
-            out[SSF_POSE_OUT_NBG] = kb[0];
-            out[SSF_POSE_OUT_KM_ITER] = S.km_iter;
-            out[SSF_POSE_OUT_EM_ITER] = S.em_iter;
-            out[SSF_POSE_OUT_CONVERGED] = S.converged;
-            out[SSF_POSE_OUT_CENTER0] = (double)S.c0;
-            out[SSF_POSE_OUT_CENTER1] = (double)S.c1;
+            if (g == 0) {                           // part 0 publishes the frame's pose
+                for (int i = 0; i < 26; ++i) out[i] = 0.0;
+                double* kb = S.sums;
+                for (int i = 0; i < 16; ++i) kb[i] = bg ? k1[i] : S.ktot[i] - k1[i];
+                const double cs[3] = {S.x0[3] + S.x0[0], S.x0[4] + S.x0[1], S.x0[5] + S.x0[2]};
+                const double cd[3] = {S.x0[3], S.x0[4], S.x0[5]};
+                int st = S.status;
+                if (st == 0) st = kabsch_finish(kb, cs, cd, reflection, out);
+                out[SSF_POSE_OUT_STATUS] = st;
+                out[SSF_POSE_OUT_BGLABEL] = bg;
+                out[SSF_POSE_OUT_NBG] = kb[0];
+                out[SSF_POSE_OUT_KM_ITER] = S.km_iter;
+                out[SSF_POSE_OUT_EM_ITER] = S.em_iter;
+                out[SSF_POSE_OUT_CONVERGED] = S.converged;
+                out[SSF_POSE_OUT_CENTER0] = (double)S.c0;
+                out[SSF_POSE_OUT_CENTER1] = (double)S.c1;
 #ifdef SSF_MASK_STAMPS
-            out[SSF_POSE_OUT_CENTER0] = S.dg_n > 0.0 ? S.dg_cyc / S.dg_n : 0.0;
-            out[SSF_POSE_OUT_CENTER1] = S.dg_n > 0.0 ? S.dg_lab / (S.dg_n * (double)n) : 0.0;
-            out[SSF_POSE_OUT_CONVERGED] = S.dg_wfull;
-            out[SSF_POSE_OUT_NBG] = S.dg_full1;
+                out[SSF_POSE_OUT_CENTER0] = S.dg_n > 0.0 ? S.dg_cyc / S.dg_n : 0.0;
+                out[SSF_POSE_OUT_CENTER1] = S.dg_n > 0.0 ? S.dg_lab / (S.dg_n * (double)n) : 0.0;
+                out[SSF_POSE_OUT_CONVERGED] = S.dg_wfull;
+                out[SSF_POSE_OUT_NBG] = S.dg_full1;
 #endif
-            out[SSF_POSE_OUT_LOWER_BOUND] = S.lb;
-            out[SSF_POSE_OUT_PASSES] = S.passes;
+                out[SSF_POSE_OUT_LOWER_BOUND] = S.lb;
+                out[SSF_POSE_OUT_PASSES] = S.passes;
+            }
         }
         __syncthreads();
     }
     if (bg_mask && S.bg != S.bg_pred) {
-        for (int64_t i = tid; i < n; i += blockDim.x) bg_mask[fb + i] ^= 1;
+        for (int64_t i = r0 + tid; i < r1; i += blockDim.x) bg_mask[fb + i] ^= 1;
     }
     SSF_STAMP(5);
+    }();                                       // the frame part
+    }                                          // tickets
 }
+
+int mask_pose_slots(int device) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mask_pose, kMaskThreads, 0) != hipSuccess) return 0;
+    return cus * per;
+}
+
+size_t mask_sync_bytes(int n_frames) { return (size_t)(4 + n_frames) * sizeof(uint32_t); }
+size_t mask_parts_bytes(int n_frames, int G) { return (size_t)n_frames * 2 * G * kSlot * sizeof(double); }
 
 hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,
                             const int64_t* frame_off, int mode, const uint8_t* mask_in,
                             const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
-                            double* out) {
+                            double* out, int G, int slots, uint32_t* sync, double* parts) {
     if (n_frames <= 0) return hipSuccess;
+    if (mode != SSF_MASK_GMM || G < 1 || !sync || !parts) G = 1;
+    if (G > kMaxSplit) G = kMaxSplit;
+    int grid = n_frames;
+    if (G > 1) {
+        // zero the ticket and arrival counters (16-byte multiple, from the allocation start)
+        const size_t zb = (mask_sync_bytes(n_frames) + 15) & ~(size_t)15;
+        hipError_t e = hipMemsetAsync(sync, 0, zb, s);
+        if (e != hipSuccess) return e;
+        const int64_t want = (int64_t)n_frames * G;
+        grid = (int)(slots > 0 && want > slots ? slots : want);
+    }
     kmark(s, "k_mask_pose");
-    hipLaunchKernelGGL(k_mask_pose, dim3(n_frames), dim3(kMaskThreads), 0, s, pts, flow, frame_off,
-                       mode, mask_in, draws, lloyd_rec, reflection, bg_mask, out);
+    hipLaunchKernelGGL(k_mask_pose, dim3(grid), dim3(kMaskThreads), 0, s, pts, flow, frame_off,
+                       mode, mask_in, draws, lloyd_rec, reflection, bg_mask, out, n_frames, G, sync,
+                       parts);
     return hipGetLastError();
 }
 

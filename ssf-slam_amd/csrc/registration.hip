@@ -913,34 +913,6 @@ __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
 }
 
 // ------------------------------------------------------------------------------------------
-// Residual + local Jacobian of PlaneFeatureCost (:25-43) composed with the
-// EigenQuaternionParameterization 4x3 Jacobian (same algebra as the oracle's residual_jac).
-SSF_DEV double residual_jac(const double q[4], const double t[3], const double po[3],
-                            const double pa[3], const double n[3], double J[6]) {
-    double f[3];
-    quat_rotate(q, po, f);
-    const double d0 = (f[0] + t[0]) - pa[0], d1 = (f[1] + t[1]) - pa[1], d2 = (f[2] + t[2]) - pa[2];
-    double r = d0 * n[0] + d1 * n[1];
-    r = r + d2 * n[2];
-    const double x = q[0], y = q[1], z = q[2], w = q[3];
-    const double u0 = y * po[2] - z * po[1], u1 = z * po[0] - x * po[2], u2 = x * po[1] - y * po[0];
-    const double pxn0 = po[1] * n[2] - po[2] * n[1], pxn1 = po[2] * n[0] - po[0] * n[2],
-                 pxn2 = po[0] * n[1] - po[1] * n[0];
-    const double uxn0 = u1 * n[2] - u2 * n[1], uxn1 = u2 * n[0] - u0 * n[2], uxn2 = u0 * n[1] - u1 * n[0];
-    const double nxq0 = n[1] * z - n[2] * y, nxq1 = n[2] * x - n[0] * z, nxq2 = n[0] * y - n[1] * x;
-    const double pnq0 = po[1] * nxq2 - po[2] * nxq1, pnq1 = po[2] * nxq0 - po[0] * nxq2,
-                 pnq2 = po[0] * nxq1 - po[1] * nxq0;
-    const double g0 = 2.0 * w * pxn0 + 2.0 * uxn0 + 2.0 * pnq0;
-    const double g1 = 2.0 * w * pxn1 + 2.0 * uxn1 + 2.0 * pnq1;
-    const double g2 = 2.0 * w * pxn2 + 2.0 * uxn2 + 2.0 * pnq2;
-    const double g3 = 2.0 * (n[0] * u0 + n[1] * u1 + n[2] * u2);
-    J[0] = g0 * w - g1 * z + g2 * y - g3 * x;
-    J[1] = g0 * z + g1 * w - g2 * x - g3 * y;
-    J[2] = -g0 * y + g1 * x + g2 * w - g3 * z;
-    J[3] = n[0]; J[4] = n[1]; J[5] = n[2];
-    return r;
-}
-
 constexpr int kSolveThreads = 512;
 constexpr int kNE = 28;  // 21 (packed upper JtWJ) + 6 (JtWr) + cost
 
@@ -958,60 +930,107 @@ struct CorrLds {
     float po[3][kSolveLdsCap], pa[3][kSolveLdsCap], n[3][kSolveLdsCap];
 };
 
-template <class Get>
-SSF_DEV void evaluate_with(Get get, int n, const double q[4], const double t[3],
-                           double (&ne)[kNE], double* lds) {
+// Eigen Quaterniond::toRotationMatrix (x, y, z, w storage).
+SSF_DEV void quat_to_R(const double q[4], double R[9]) {
+    const double tx = 2.0 * q[0], ty = 2.0 * q[1], tz = 2.0 * q[2];
+    const double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+    const double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+    const double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+    R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz;         R[2] = txz + twy;
+    R[3] = txy + twz;         R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;         R[7] = tyz + twx;         R[8] = 1.0 - (txx + tyy);
+}
+
+// Per-correspondence residual r = (R po + t - pa) . n (PlaneFeatureCost, :25-43) and its local
+// Jacobian [2 (R po x n), n]: the EigenQuaternionParameterization's 4x3 Jacobian composed with
+// the autodiff gradient (what the oracle's residual_jac spells out) reduces to that for a unit
+// quaternion, so an evaluation costs ~65 f64 operations per correspondence instead of ~140 (same
+// values to rounding, explicit FMAs; the per-step poses keep the 1e-5 m / 1e-6 rad bar against
+// the oracle).  R is built once per evaluation (wave-uniform).  Huber(0.1) corrector as Ceres:
+// rho'(s) = 0.1 / sqrt(s) above s = 0.01 (sqrt(r^2) taken as |r|), rho(s) = 0.2 sqrt(s) - 0.01.
+// One correspondence's Huber-weighted contribution (x wgt: 0 for a padding slot) to the
+// normal equations ne (21 packed upper J^T W J, 6 J^T W r, cost).
+SSF_DEV void accum_corr(const double R[9], const double t[3], const double po[3], const double pa[3],
+                        const double nn[3], double wgt, double (&ne)[kNE]) {
+    const double a = 0.1, b = 0.1 * 0.1;
+    double u[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) u[k] = __builtin_fma(R[3 * k + 2], po[2], __builtin_fma(R[3 * k + 1], po[1], R[3 * k] * po[0]));
+    const double d0 = (u[0] + t[0]) - pa[0], d1 = (u[1] + t[1]) - pa[1], d2 = (u[2] + t[2]) - pa[2];
+    const double r = __builtin_fma(d2, nn[2], __builtin_fma(d1, nn[1], d0 * nn[0]));
+    double J[6];
+    J[0] = 2.0 * __builtin_fma(u[1], nn[2], -u[2] * nn[1]);
+    J[1] = 2.0 * __builtin_fma(u[2], nn[0], -u[0] * nn[2]);
+    J[2] = 2.0 * __builtin_fma(u[0], nn[1], -u[1] * nn[0]);
+    J[3] = nn[0]; J[4] = nn[1]; J[5] = nn[2];
+    const double s = r * r;
+    double rho0, rho1;
+    if (s > b) {
+        const double rr = fabs(r);
+        rho0 = 2.0 * a * rr - b;
+        rho1 = a / rr;
+        if (rho1 < DBL_MIN) rho1 = DBL_MIN;
+    } else {
+        rho0 = s; rho1 = 1.0;
+    }
+    ne[27] = __builtin_fma(0.5 * wgt, rho0, ne[27]);
+    rho1 *= wgt;
+    int k = 0;
+#pragma unroll
+    for (int uu = 0; uu < 6; ++uu) {             // explicit FMAs: the file is built without
+        const double wj = rho1 * J[uu];          // contraction (bit-exact float stages)
+        ne[21 + uu] = __builtin_fma(wj, r, ne[21 + uu]);
+#pragma unroll
+        for (int v = uu; v < 6; ++v) { ne[k] = __builtin_fma(wj, J[v], ne[k]); ++k; }
+    }
+}
+
+SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4], const double t[3],
+                      double (&ne)[kNE], double* lds) {
 #pragma unroll
     for (int k = 0; k < kNE; ++k) ne[k] = 0.0;
-    const double a = 0.1, b = 0.1 * 0.1;
+    double R[9];
+    quat_to_R(q, R);
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        double po[3], pa[3], nn[3];
-        if (!get(i, po, pa, nn)) continue;
-        double J[6];
-        const double r = residual_jac(q, t, po, pa, nn, J);
-        const double s = r * r;
-        double rho0, rho1;
-        if (s > b) {
-            const double rr = sqrt(s);
-            rho0 = 2.0 * a * rr - b;
-            rho1 = a / rr;
-            if (rho1 < DBL_MIN) rho1 = DBL_MIN;
-        } else {
-            rho0 = s; rho1 = 1.0;
-        }
-        ne[27] += 0.5 * rho0;
-        int k = 0;
-#pragma unroll
-        for (int u = 0; u < 6; ++u) {
-            ne[21 + u] += rho1 * J[u] * r;
-#pragma unroll
-            for (int v = u; v < 6; ++v) ne[k++] += rho1 * J[u] * J[v];
-        }
+        const CorrRec c = rec[i];
+        if (c.valid == 0.0f) continue;
+        const double po[3] = {c.po[0], c.po[1], c.po[2]}, pa[3] = {c.pa[0], c.pa[1], c.pa[2]},
+                     nn[3] = {c.n[0], c.n[1], c.n[2]};
+        accum_corr(R, t, po, pa, nn, 1.0, ne);
     }
     block_sum_rs<kNE>(ne, lds);
 #pragma unroll
     for (int k = 0; k < kNE; ++k) ne[k] *= 2.0;
 }
 
-SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4], const double t[3],
-                      double (&ne)[kNE], double* lds) {
-    evaluate_with([&](int i, double* po, double* pa, double* nn) {
-        const CorrRec c = rec[i];
-        if (c.valid == 0.0f) return false;
-        po[0] = c.po[0]; po[1] = c.po[1]; po[2] = c.po[2];
-        pa[0] = c.pa[0]; pa[1] = c.pa[1]; pa[2] = c.pa[2];
-        nn[0] = c.n[0]; nn[1] = c.n[1]; nn[2] = c.n[2];
-        return true;
-    }, n, q, t, ne, lds);
-}
-
+// LDS-resident correspondences, two per step (i, i + T; a missing second one is a clamped
+// duplicate weighted 0): both loads are in flight before either is used.
 SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double t[3],
                       double (&ne)[kNE], double* lds) {
-    evaluate_with([&](int i, double* po, double* pa, double* nn) {
 #pragma unroll
-        for (int d = 0; d < 3; ++d) { po[d] = C.po[d][i]; pa[d] = C.pa[d][i]; nn[d] = C.n[d][i]; }
-        return true;
-    }, nv, q, t, ne, lds);
+    for (int k = 0; k < kNE; ++k) ne[k] = 0.0;
+    double R[9];
+    quat_to_R(q, R);
+    const int T = blockDim.x;
+    for (int i = threadIdx.x; i < nv; i += 2 * T) {
+        const int i2 = min(i + T, nv - 1);
+        const double w2 = i + T < nv ? 1.0 : 0.0;
+        float f[2][9];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            f[0][d] = C.po[d][i]; f[0][3 + d] = C.pa[d][i]; f[0][6 + d] = C.n[d][i];
+            f[1][d] = C.po[d][i2]; f[1][3 + d] = C.pa[d][i2]; f[1][6 + d] = C.n[d][i2];
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const double po[3] = {f[h][0], f[h][1], f[h][2]}, pa[3] = {f[h][3], f[h][4], f[h][5]},
+                         nn[3] = {f[h][6], f[h][7], f[h][8]};
+            accum_corr(R, t, po, pa, nn, h ? w2 : 1.0, ne);
+        }
+    }
+    block_sum_rs<kNE>(ne, lds);
+#pragma unroll
+    for (int k = 0; k < kNE; ++k) ne[k] *= 2.0;
 }
 
 SSF_DEV int chol_solve6(double M[6][6], const double b[6], double y[6]) {
@@ -1038,6 +1057,47 @@ SSF_DEV int chol_solve6(double M[6][6], const double b[6], double y[6]) {
         double v = z[i];
         for (int k = i + 1; k < 6; ++k) v -= L[k][i] * y[k];
         y[i] = v / L[i][i];
+    }
+    return 0;
+}
+
+// Cholesky solve of the packed symmetric normal equations A y = -g (A = ne[0..20] upper packed,
+// g = ne[21..26]): 21 + 21 doubles of state, one reciprocal per diagonal instead of a division
+// per element (the GN path runs it redundantly on every thread).
+SSF_DEV int chol_solve_packed(const double (&ne)[kNE], double y[6]) {
+    double L[21];                         // L(i, j), j <= i, at pk(j, i)
+    double inv[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        double s = ne[pk(j, j)];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s -= L[pk(k, j)] * L[pk(k, j)];
+        if (!(s > 0.0)) return -1;
+        const double d = sqrt(s);
+        inv[j] = 1.0 / d;
+        L[pk(j, j)] = d;
+#pragma unroll
+        for (int i = j + 1; i < 6; ++i) {
+            double v = ne[pk(i, j)];
+#pragma unroll
+            for (int k = 0; k < j; ++k) v -= L[pk(k, i)] * L[pk(k, j)];
+            L[pk(j, i)] = v * inv[j];
+        }
+    }
+    double z[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        double v = -ne[21 + i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) v -= L[pk(k, i)] * z[k];
+        z[i] = v * inv[i];
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+        double v = z[i];
+#pragma unroll
+        for (int k = i + 1; k < 6; ++k) v -= L[pk(i, k)] * y[k];
+        y[i] = v * inv[i];
     }
     return 0;
 }
@@ -1076,6 +1136,11 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
     const int p = blockIdx.x, tid = threadIdx.x;
     const int n = curr_count[p];
     const CorrRec* rec = corr + curr_off[p];
+#ifdef SSF_SOLVE_STAMPS
+    // diagnostic build only: s_memtime phase stamps into the last log row (cost/status/radius)
+    const unsigned long long st0 = __builtin_amdgcn_s_memtime();
+    unsigned long long st1 = st0, st2 = st0;
+#endif
     if (tid == 0) {
         for (int k = 0; k < 4; ++k) S.q[k] = pose_rel[7 * p + k];
         for (int k = 0; k < 3; ++k) S.t[k] = pose_rel[7 * p + 4 + k];
@@ -1084,35 +1149,39 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
     __syncthreads();
     const bool skip = last_count[p] <= 10;                              // :158
     if (!skip) {
-        // order-preserving compaction of the valid records: thread tid owns a contiguous chunk,
-        // an exclusive scan of the chunk counts gives its first output slot
-        const int per = (n + blockDim.x - 1) / blockDim.x;
-        const int r0 = min(n, tid * per), r1 = min(n, r0 + per);
-        int mine = 0;
-        for (int i = r0; i < r1; ++i) mine += rec[i].valid != 0.0f;
+        // order-preserving compaction of the valid records into LDS, coalesced: record i goes
+        // to thread i % T in trip i / T; per trip a ballot + the wave counts give every valid
+        // record its rank.  kPre trips' records are loaded before the first is used (one load
+        // latency per kPre trips).
+        constexpr int kPre = 2;
         const int lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
-        int incl = mine;
+        const int T = blockDim.x;
+        int nv = 0;                                                     // uniform
+        for (int i0 = 0; i0 < n; i0 += kPre * T) {
+            CorrRec c[kPre];
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        if (lane == 63) wtot[w] = incl;
-        __syncthreads();
-        int before = 0, nv = 0;
-        for (int k = 0; k < nw; ++k) { const int v = wtot[k]; if (k < w) before += v; nv += v; }
-        const bool in_lds = nv <= kSolveLdsCap;                        // uniform
-        if (in_lds) {
-            int pos = before + incl - mine;
-            for (int i = r0; i < r1; ++i) {
-                const CorrRec c = rec[i];
-                if (c.valid == 0.0f) continue;
+            for (int k = 0; k < kPre; ++k) c[k] = rec[min(i0 + k * T + tid, n - 1)];   // clamped
 #pragma unroll
-                for (int d = 0; d < 3; ++d) { C.po[d][pos] = c.po[d]; C.pa[d][pos] = c.pa[d]; C.n[d][pos] = c.n[d]; }
-                ++pos;
+            for (int k = 0; k < kPre; ++k) {
+                const bool v = i0 + k * T + tid < n && c[k].valid != 0.0f;
+                const uint64_t m = __ballot(v);
+                if (lane == 0) wtot[w] = __popcll(m);
+                __syncthreads();
+                int before = nv, tot = 0;
+                for (int j = 0; j < nw; ++j) { const int x = wtot[j]; if (j < w) before += x; tot += x; }
+                const int pos = before + __popcll(m & lanemask_lt());
+                if (v && pos < kSolveLdsCap) {
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) { C.po[d][pos] = c[k].po[d]; C.pa[d][pos] = c[k].pa[d]; C.n[d][pos] = c[k].n[d]; }
+                }
+                nv += tot;
+                __syncthreads();                                        // wtot is rewritten next trip
             }
         }
-        __syncthreads();
+        const bool in_lds = nv <= kSolveLdsCap;                        // uniform
+#ifdef SSF_SOLVE_STAMPS
+        st1 = __builtin_amdgcn_s_memtime();
+#endif
         if (tid == 0 && ncorr_out) ncorr_out[p] = nv;
         auto eval_at = [&](const double* qq, const double* tt, double (&ne_)[kNE]) {
             if (in_lds) evaluate(C, nv, qq, tt, ne_, red);
@@ -1123,6 +1192,9 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
         for (int k = 0; k < 4; ++k) q[k] = S.q[k];
         for (int k = 0; k < 3; ++k) t[k] = S.t[k];
         eval_at(q, t, ne);
+#ifdef SSF_SOLVE_STAMPS
+        st2 = __builtin_amdgcn_s_memtime();
+#endif
         if (tid == 0) {
             for (int k = 0; k < kNE; ++k) S.ne[k] = ne[k];
             for (int u = 0; u < 6; ++u) S.s[u] = 1.0 / (1.0 + sqrt(ne[pk(u, u)]));
@@ -1130,34 +1202,31 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
         }
         __syncthreads();
         if (mode == SSF_SOLVER_GN) {
+            // every thread holds the same sums after the block reduction, so every thread runs
+            // the same 6x6 solve on the same bits and carries the same pose: no lane-0 step, no
+            // LDS broadcast, no extra barrier per iteration (thread 0 alone writes the log)
+            int nl = 0;
             for (int it = 0; it < max_iter; ++it) {
-                if (tid == 0) {
-                    double M[6][6], b[6], y[6];
-                    for (int u = 0; u < 6; ++u) {
-                        b[u] = -S.ne[21 + u];
-                        for (int v = 0; v < 6; ++v) M[u][v] = S.ne[pk(u, v)];
-                    }
-                    if (chol_solve6(M, b, y) != 0) {
-                        write_log(log, max_iter, p, S.nlog++, S.q, S.t, S.ne[27], 2, 0);
-                        S.done = 1;
-                    } else {
-                        double qn[4];
-                        quat_plus(S.q, y, qn);
-                        for (int k = 0; k < 4; ++k) S.q[k] = qn[k];
-                        S.t[0] += y[3]; S.t[1] += y[4]; S.t[2] += y[5];
-                    }
+                double y[6];
+                if (chol_solve_packed(ne, y) != 0) {                         // uniform
+                    if (tid == 0) write_log(log, max_iter, p, nl, q, t, ne[27], 2, 0);
+                    ++nl;
+                    break;
                 }
-                __syncthreads();
-                if (S.done) break;
-                for (int k = 0; k < 4; ++k) q[k] = S.q[k];
-                for (int k = 0; k < 3; ++k) t[k] = S.t[k];
+                double qn[4];
+                quat_plus(q, y, qn);
+                for (int k = 0; k < 4; ++k) q[k] = qn[k];
+                t[0] += y[3]; t[1] += y[4]; t[2] += y[5];
                 eval_at(q, t, ne);
-                if (tid == 0) {
-                    for (int k = 0; k < kNE; ++k) S.ne[k] = ne[k];
-                    write_log(log, max_iter, p, S.nlog++, S.q, S.t, ne[27], 6, 0);
-                }
-                __syncthreads();
+                if (tid == 0) write_log(log, max_iter, p, nl, q, t, ne[27], 6, 0);
+                ++nl;
             }
+            if (tid == 0) {
+                for (int k = 0; k < 4; ++k) S.q[k] = q[k];
+                for (int k = 0; k < 3; ++k) S.t[k] = t[k];
+                S.nlog = nl;
+            }
+            __syncthreads();
         } else {
             for (int it = 1; it <= max_iter; ++it) {
                 if (tid == 0) {
@@ -1258,6 +1327,13 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
         ncorr_out[p] = -1;
     }
     if (tid == 0) {
+#ifdef SSF_SOLVE_STAMPS
+        if (log) {
+            double* r = log + ((int64_t)p * max_iter + max_iter - 1) * 10;
+            r[7] = (double)(st1 - st0); r[8] = (double)(st2 - st1);
+            r[9] = (double)(__builtin_amdgcn_s_memtime() - st2);
+        }
+#endif
         for (int k = 0; k < 4; ++k) pose_rel[7 * p + k] = S.q[k];
         for (int k = 0; k < 3; ++k) pose_rel[7 * p + 4 + k] = S.t[k];
         if (nlog_out) nlog_out[p] = S.nlog;

@@ -49,8 +49,9 @@ struct alignas(16) CorrRec {
 hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_frames,
                                  const float* pts, int stride, const int64_t* frame_off,
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
-                                 int32_t* ring_off, float4* ring_xyzi, float* curv, int32_t* sel,
-                                 int32_t* sel_dump, int32_t* sel_cnt, float4* plane,
+                                 int32_t* ring_off, float* ring_xyz, float4* ring_xyzi,
+                                 float* curv, int32_t* sel, int32_t* sel_dump, int32_t* sel_cnt,
+                                 float4* plane,
                                  int32_t* plane_count);
 
 // ---- launchers (registration.hip) ----
@@ -69,10 +70,16 @@ hipError_t launch_accumulate(hipStream_t s, int n, const double* rel, const doub
                              double* abs_out);
 
 // ---- launchers (mask_pose.hip) ----
+// G > 1 cuts every frame into G parts on G work-groups (sync: ticket + per-frame arrival
+// counters, mask_sync_bytes; parts: exchange slots, mask_parts_bytes); slots = resident
+// work-groups of k_mask_pose on the device (mask_pose_slots).
 hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,
                             const int64_t* frame_off, int mode, const uint8_t* mask_in,
                             const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
-                            double* out);
+                            double* out, int G, int slots, uint32_t* sync, double* parts);
+int mask_pose_slots(int device);
+size_t mask_sync_bytes(int n_frames);
+size_t mask_parts_bytes(int n_frames, int G);
 
 // ---- launchers (loop.hip) ----
 struct IcpState {             // one per ICP problem, device-resident across iterations

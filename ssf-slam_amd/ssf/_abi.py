@@ -21,7 +21,7 @@ MASK_GMM, MASK_GT, MASK_GIVEN = 0, 1, 2
 POSE_OUT_STRIDE = 32
 POSE_OUT = dict(T=0, Q=3, R=7, STATUS=16, NBG=17, BGLABEL=18, KM_ITER=19, EM_ITER=20,
                 CONVERGED=21, CENTER0=22, CENTER1=23, LOWER_BOUND=24, PASSES=25)
-POSE_EMPTY, POSE_REFLECTION, POSE_NOT_ORTHOGONAL, POSE_GMM_FAILED = -1, -2, -3, -4
+POSE_EMPTY, POSE_REFLECTION, POSE_NOT_ORTHOGONAL, POSE_GMM_FAILED, POSE_SYNC_FAILED = -1, -2, -3, -4, -5
 
 # Every symbol include/ssf_frontend.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -30,7 +30,7 @@ EXPORTS = [
     "ssf_register_batch", "ssf_mask_pose_batch", "ssf_rng_seed", "ssf_accumulate_sequence",
     "ssf_voxel_grid_batch", "ssf_icp_params_default", "ssf_icp_batch",
     "ssf_extract_planes_batch_masked", "ssf_register_pair", "ssf_profile_enable",
-    "ssf_profile_read",
+    "ssf_profile_read", "ssf_set_mask_split",
 ]
 # Every symbol include/ssf_pointnet2.h declares (TFlow point-set operators).
 PN2_EXPORTS = [
@@ -117,6 +117,8 @@ def lib():
     L.ssf_register_batch.restype = i32
     L.ssf_register_pair.argtypes = [vp, vp, vp, i64, vp, i64, vp, vp, vp, vp, C.POINTER(StepLog)]
     L.ssf_register_pair.restype = i32
+    L.ssf_set_mask_split.argtypes = [vp, i32]
+    L.ssf_set_mask_split.restype = i32
     L.ssf_profile_enable.argtypes = [vp, i32]
     L.ssf_profile_enable.restype = i32
     L.ssf_profile_read.argtypes = [vp, C.POINTER(KernelTime), i32, C.POINTER(i32)]

@@ -109,6 +109,10 @@ class Frontend:
         self._check(_abi.lib().ssf_profile_read(self._h, buf, 64, C.byref(n)), "ssf_profile_read")
         return {buf[i].name.decode(): (int(buf[i].launches), float(buf[i].total_ms)) for i in range(n.value)}
 
+    def mask_split(self, parts_per_frame: int = 0):
+        """Work-groups per frame of the GMM fit (0 = automatic, 1..8 fixed)."""
+        self._check(_abi.lib().ssf_set_mask_split(self._h, int(parts_per_frame)), "ssf_set_mask_split")
+
     def seed(self, seed: int):
         """np.random.seed(seed) for the GMM's k-means++ RandomState."""
         self._check(_abi.lib().ssf_rng_seed(self._h, seed & 0xFFFFFFFF), "ssf_rng_seed")

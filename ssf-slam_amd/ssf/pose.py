@@ -49,6 +49,8 @@ def _raise_status(st):
         raise ValueError("Matrix must be orthogonal, i.e. its transpose should be its inverse")
     if st == _abi.POSE_EMPTY:
         raise ValueError("no background points")
+    if st == _abi.POSE_SYNC_FAILED:
+        raise RuntimeError("mask kernel: a frame part never arrived at an exchange (sync timeout)")
     if st == _abi.POSE_GMM_FAILED:
         raise ValueError("Fitting the mixture model failed (ill-defined empirical covariance)")
 

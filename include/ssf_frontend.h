@@ -245,6 +245,15 @@ int32_t ssf_mask_pose_batch(ssf_ctx* ctx, void* stream, int32_t n_frames, const 
                             const int64_t* h_frame_off, int32_t mode, const uint8_t* d_mask_in,
                             const double* h_draws, int32_t reflection, uint8_t* d_bg_mask,
                             double* d_out);
+/* The same block on float64 pos / flow (the reference's own dtype when the npz arrays or the
+ * ASF network output arrive as float64, PointCloudOdometry_noSeg.py:97-118): every load is exact,
+ * so R / t carry no float32 rounding of the inputs.  Otherwise identical to ssf_mask_pose_batch
+ * (same modes, draws, outputs and status codes); 48 B per point per pass instead of 24. */
+int32_t ssf_mask_pose_batch_f64(ssf_ctx* ctx, void* stream, int32_t n_frames, const double* d_pts,
+                                const double* d_flow, const int64_t* d_frame_off,
+                                const int64_t* h_frame_off, int32_t mode, const uint8_t* d_mask_in,
+                                const double* h_draws, int32_t reflection, uint8_t* d_bg_mask,
+                                double* d_out);
 /* Work-groups per frame of the GMM fit in ssf_mask_pose_batch (no reference counterpart;
  * results do not depend on it beyond f64 summation order): 0 = automatic (as many as keep the
  * chip full: ~256 / frames, at most 8; 1 for 256 frames and more), 1..8 = fixed.  With more

@@ -12,7 +12,10 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "ssf", "_lib")
 OBJ_DIR = os.path.join(HERE, "build")
 LIB = os.path.join(OUT_DIR, "libssf_frontend.so")
-SOURCES = ["abi.hip", "features.hip", "registration.hip", "mask_pose.hip", "loop.hip", "pointnet2.hip"]
+SOURCES = ["abi.hip", "features.hip", "registration.hip", "mask_pose.hip", "mask_pose_f64.hip", "loop.hip",
+           "pointnet2.hip"]
+# sources that include another source file
+SRC_DEPS = {"mask_pose_f64.hip": ["mask_pose.hip"]}
 HEADERS = ["ssf_device.hpp", "ssf_internal.hpp", "svd3.hpp", os.path.join("..", "..", "include", "ssf_frontend.h"),
            os.path.join("..", "..", "include", "ssf_pointnet2.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -21,7 +24,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-Wall"]
 # The f64 GMM/Kabsch kernel is compared with tolerances (labels, iteration counts, 1e-5 m), not
 # bit for bit, so it may contract multiply-adds into FMAs (half the f64 instructions).
-FILE_FLAGS = {"mask_pose.hip": ["-ffp-contract=fast"]}
+FILE_FLAGS = {"mask_pose.hip": ["-ffp-contract=fast"], "mask_pose_f64.hip": ["-ffp-contract=fast"]}
 
 
 def _stale(target, deps):
@@ -40,7 +43,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         s = os.path.join(CSRC, src)
         o = os.path.join(OBJ_DIR, src.replace(".hip", ".o"))
         objs.append(o)
-        if force or _stale(o, [s] + hdrs):
+        if force or _stale(o, [s] + hdrs + [os.path.join(CSRC, d) for d in SRC_DEPS.get(src, [])]):
             jobs.append([HIPCC, *FLAGS, *FILE_FLAGS.get(src, []), "-c", s, "-o", o])
 
     def run(cmd):
@@ -66,7 +69,8 @@ def build_diag() -> str:
     for src in SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(OBJ_DIR, src.replace(".hip", "_diag.o"))
-        extra = {"mask_pose.hip": ["-DSSF_MASK_STAMPS"], "registration.hip": ["-DSSF_TABLE_STAMPS", "-DSSF_ASSOC_STAMPS"]}.get(src, [])
+        extra = {"mask_pose.hip": ["-DSSF_MASK_STAMPS"], "mask_pose_f64.hip": ["-DSSF_MASK_STAMPS"],
+                 "registration.hip": ["-DSSF_TABLE_STAMPS", "-DSSF_ASSOC_STAMPS"]}.get(src, [])
         subprocess.run([HIPCC, *FLAGS, *FILE_FLAGS.get(src, []), *extra, "-c", s, "-o", o], check=True)
         objs.append(o)
     subprocess.run([HIPCC, *FLAGS, "-shared", *objs, "-o", out], check=True)

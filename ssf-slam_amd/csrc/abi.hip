@@ -520,8 +520,11 @@ int32_t ssf_register_pair(ssf_ctx* c, void* stream, const float* d_last_xyzi, in
     return SSF_OK;
 }
 
-int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_pts,
-                            const float* d_flow, const int64_t* d_frame_off,
+}  // extern "C"
+
+template <class T>
+static int32_t mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const T* d_pts,
+                            const T* d_flow, const int64_t* d_frame_off,
                             const int64_t* h_frame_off, int32_t mode, const uint8_t* d_mask_in,
                             const double* h_draws, int32_t reflection, uint8_t* d_bg_mask,
                             double* d_out) {
@@ -591,6 +594,26 @@ int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const fl
     if (e == hipSuccess) e = hipEventRecord(ds.used, s);
     if (e != hipSuccess) return hip_fail(c, e, "mask_pose launch");
     return SSF_OK;
+}
+
+extern "C" {
+
+int32_t ssf_mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_pts,
+                            const float* d_flow, const int64_t* d_frame_off,
+                            const int64_t* h_frame_off, int32_t mode, const uint8_t* d_mask_in,
+                            const double* h_draws, int32_t reflection, uint8_t* d_bg_mask,
+                            double* d_out) {
+    return mask_pose_batch(c, stream, n_frames, d_pts, d_flow, d_frame_off, h_frame_off, mode,
+                           d_mask_in, h_draws, reflection, d_bg_mask, d_out);
+}
+
+int32_t ssf_mask_pose_batch_f64(ssf_ctx* c, void* stream, int32_t n_frames, const double* d_pts,
+                                const double* d_flow, const int64_t* d_frame_off,
+                                const int64_t* h_frame_off, int32_t mode, const uint8_t* d_mask_in,
+                                const double* h_draws, int32_t reflection, uint8_t* d_bg_mask,
+                                double* d_out) {
+    return mask_pose_batch(c, stream, n_frames, d_pts, d_flow, d_frame_off, h_frame_off, mode,
+                           d_mask_in, h_draws, reflection, d_bg_mask, d_out);
 }
 
 int32_t ssf_accumulate_sequence(ssf_ctx* c, void* stream, int32_t n, const double* d_rel,

@@ -87,7 +87,9 @@ struct MaskShared {
     int km_iter, em_iter, strict, converged, done, status, label0, bg, bg_pred, lfull;
 };
 
-SSF_DEV void load_x(const float* __restrict__ P, const float* __restrict__ Fl, int64_t i, double x[6]) {
+// T: the storage type of pos / flow (float: LiDAR data; double: the f64 Python boundary).
+template <class T>
+SSF_DEV void load_x(const T* __restrict__ P, const T* __restrict__ Fl, int64_t i, double x[6]) {
     x[0] = (double)Fl[3 * i]; x[1] = (double)Fl[3 * i + 1]; x[2] = (double)Fl[3 * i + 2];
     x[3] = (double)P[3 * i];  x[4] = (double)P[3 * i + 1];  x[5] = (double)P[3 * i + 2];
 }
@@ -247,18 +249,19 @@ SSF_DEV double em_delta1(const double v[6], Ptr Aq, Ptr bq, double cq) {
 
 // Streams the frame's points through f(i, x): every thread keeps the NEXT point's loads in
 // flight (as the raw six floats, converted when used) while it computes the current one.
-SSF_DEV void load_raw(const float* __restrict__ P, const float* __restrict__ Fl, int64_t i, float r[6]) {
+template <class T>
+SSF_DEV void load_raw(const T* __restrict__ P, const T* __restrict__ Fl, int64_t i, T r[6]) {
     r[0] = Fl[3 * i]; r[1] = Fl[3 * i + 1]; r[2] = Fl[3 * i + 2];
     r[3] = P[3 * i];  r[4] = P[3 * i + 1];  r[5] = P[3 * i + 2];
 }
 
 // Points [r0, r1) of the frame (the work-group's part, see Split).
-template <class Fn>
-SSF_DEV void for_points(const float* __restrict__ P, const float* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
+template <class Ts, class Fn>
+SSF_DEV void for_points(const Ts* __restrict__ P, const Ts* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
     const int64_t T = blockDim.x;
     int64_t i = r0 + threadIdx.x;
     if (i >= r1) return;
-    float rn[6];
+    Ts rn[6];
     load_raw(P, Fl, i, rn);
     for (; i < r1; i += T) {
         double x[6];
@@ -278,14 +281,14 @@ SSF_DEV double uni(double v) {
 
 // Lloyd only: D points in flight per thread (a rolling register buffer of raw floats).  Each
 // thread visits its points in the same order as for_points, so every sum is bit-identical.
-template <int D, class Fn>
-SSF_DEV void for_points_deep(const float* __restrict__ P, const float* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
+template <int D, class Ts, class Fn>
+SSF_DEV void for_points_deep(const Ts* __restrict__ P, const Ts* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
     const int64_t T = blockDim.x;
     const int64_t i0 = r0 + threadIdx.x;
     if (r1 <= r0) return;                                  // uniform (an empty part)
     // loads are unconditional (indices clamped to the last point): the compiler can then count
     // them and wait with vmcnt(N) instead of draining every prefetch at a conditional join
-    float buf[D][6];
+    Ts buf[D][6];
 #pragma unroll
     for (int d = 0; d < D; ++d) load_raw(P, Fl, min(i0 + d * T, r1 - 1), buf[d]);
     for (int64_t base = i0; base < r1; base += D * T) {
@@ -305,12 +308,12 @@ SSF_DEV void for_points_deep(const float* __restrict__ P, const float* __restric
 // LDS re-read of the parameter doubles is what bounds the EM pass).  The second point of the
 // last step may not exist (w1 = 0: computed on a duplicate, weighted out).  Loads clamped and
 // unconditional, as in for_points.
-template <class Fn>
-SSF_DEV void for_point_pairs(const float* __restrict__ P, const float* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
+template <class Ts, class Fn>
+SSF_DEV void for_point_pairs(const Ts* __restrict__ P, const Ts* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
     const int64_t T = blockDim.x;
     int64_t i = r0 + threadIdx.x;
     if (i >= r1) return;
-    float ra[6], rb[6];
+    Ts ra[6], rb[6];
     load_raw(P, Fl, i, ra);
     load_raw(P, Fl, min(i + T, r1 - 1), rb);
     for (; i < r1; i += 2 * T) {
@@ -506,8 +509,9 @@ SSF_DEV void accum_kabsch(double (&k)[16], const double* x, const double cs[3], 
         for (int c = 0; c < 3; ++c) k[7 + r * 3 + c] += s[r] * d[c];
 }
 
+template <class T>
 __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
-    const float* __restrict__ pts, const float* __restrict__ flow,
+    const T* __restrict__ pts, const T* __restrict__ flow,
     const int64_t* __restrict__ frame_off, int mode, const uint8_t* __restrict__ mask_in,
     const double* __restrict__ draws, uint2* __restrict__ lloyd_rec, int reflection,
     uint8_t* __restrict__ bg_mask, double* __restrict__ out_all, int n_frames, int G,
@@ -537,8 +541,8 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     }
     [&]() {                                    // one frame part; `return` ends it
     const int64_t fb = frame_off[f], n = frame_off[f + 1] - fb;
-    const float* P = pts + 3 * fb;
-    const float* Fl = flow + 3 * fb;
+    const T* P = pts + 3 * fb;
+    const T* Fl = flow + 3 * fb;
     double* out = out_all + (int64_t)f * SSF_POSE_OUT_STRIDE;
     Split X;
     X.G = G; X.g = g;
@@ -992,7 +996,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
                 uint32_t e[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) e[k] = WQ[min(j0 + k * 64 + lane, qc - 1)];
-                float px[8][6];
+                T px[8][6];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) load_raw(P, Fl, (int64_t)(e[k] & 0x7FFFFFFFu), px[k]);
 #pragma unroll
@@ -1264,20 +1268,12 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     }                                          // tickets
 }
 
-int mask_pose_slots(int device) {
-    int cus = 0, per = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mask_pose, kMaskThreads, 0) != hipSuccess) return 0;
-    return cus * per;
-}
-
-size_t mask_sync_bytes(int n_frames) { return (size_t)(4 + n_frames) * sizeof(uint32_t); }
-size_t mask_parts_bytes(int n_frames, int G) { return (size_t)n_frames * 2 * G * kSlot * sizeof(double); }
-
-hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,
-                            const int64_t* frame_off, int mode, const uint8_t* mask_in,
-                            const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
-                            double* out, int G, int slots, uint32_t* sync, double* parts) {
+template <class T>
+static hipError_t launch_mask_pose_t(hipStream_t s, int n_frames, const T* pts, const T* flow,
+                                     const int64_t* frame_off, int mode, const uint8_t* mask_in,
+                                     const double* draws, uint2* lloyd_rec, int reflection,
+                                     uint8_t* bg_mask, double* out, int G, int slots,
+                                     uint32_t* sync, double* parts) {
     if (n_frames <= 0) return hipSuccess;
     if (mode != SSF_MASK_GMM || G < 1 || !sync || !parts) G = 1;
     if (G > kMaxSplit) G = kMaxSplit;
@@ -1290,11 +1286,43 @@ hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const
         const int64_t want = (int64_t)n_frames * G;
         grid = (int)(slots > 0 && want > slots ? slots : want);
     }
-    kmark(s, "k_mask_pose");
-    hipLaunchKernelGGL(k_mask_pose, dim3(grid), dim3(kMaskThreads), 0, s, pts, flow, frame_off,
+    kmark(s, sizeof(T) == 8 ? "k_mask_pose_f64" : "k_mask_pose");
+    hipLaunchKernelGGL(k_mask_pose<T>, dim3(grid), dim3(kMaskThreads), 0, s, pts, flow, frame_off,
                        mode, mask_in, draws, lloyd_rec, reflection, bg_mask, out, n_frames, G, sync,
                        parts);
     return hipGetLastError();
 }
+
+// One storage type per translation unit (mask_pose_f64.hip compiles this file again with
+// SSF_MASK_F64_TU), so the float kernel's code generation does not depend on the f64 variant.
+#ifndef SSF_MASK_F64_TU
+int mask_pose_slots(int device) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_mask_pose<float>, kMaskThreads, 0) != hipSuccess) return 0;
+    return cus * per;
+}
+
+size_t mask_sync_bytes(int n_frames) { return (size_t)(4 + n_frames) * sizeof(uint32_t); }
+size_t mask_parts_bytes(int n_frames, int G) { return (size_t)n_frames * 2 * G * kSlot * sizeof(double); }
+
+hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,
+                            const int64_t* frame_off, int mode, const uint8_t* mask_in,
+                            const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
+                            double* out, int G, int slots, uint32_t* sync, double* parts) {
+    return launch_mask_pose_t(s, n_frames, pts, flow, frame_off, mode, mask_in, draws, lloyd_rec,
+                              reflection, bg_mask, out, G, slots, sync, parts);
+}
+
+#else
+hipError_t launch_mask_pose(hipStream_t s, int n_frames, const double* pts, const double* flow,
+                            const int64_t* frame_off, int mode, const uint8_t* mask_in,
+                            const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
+                            double* out, int G, int slots, uint32_t* sync, double* parts) {
+    return launch_mask_pose_t(s, n_frames, pts, flow, frame_off, mode, mask_in, draws, lloyd_rec,
+                              reflection, bg_mask, out, G, slots, sync, parts);
+}
+
+#endif
 
 }  // namespace ssf

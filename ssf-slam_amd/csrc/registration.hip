@@ -322,6 +322,8 @@ constexpr int kTableThreads = 1024;
 
 constexpr int kLdsWalkMax = 6144;         // after the sort, frames up to this size walk in LDS
 // (16 m bytes of points + the deferred-query grid (16.6 KiB + 2 m) fit below the permutation)
+constexpr int kLdsSoaMax = 9088;          // ... and up to this size as 14-B SoA points: 16 m + 16.6 KiB
+// of points, permutation and grid leave >= 1 KiB of deferred queue in the 160 KiB image
 
 // Diagnostic build only (-DSSF_TABLE_STAMPS): lane 0 writes s_memtime deltas after the sort,
 // the bounded walks and the deferred walks into sorted_idx[m .. m+3] (frame padding, read by
@@ -335,27 +337,51 @@ constexpr int kLdsWalkMax = 6144;         // after the sort, frames up to this s
 // Outward x-walk from sorted rank r.  bounded: the list is seeded with the sentinel distance 1,
 // so only points with d2 < 1 enter it, and the walk stops once dx^2 >= 1 (only those points are
 // needed to decide most queries, see bounded_decides).
-template <bool kLds>
-SSF_DEV void knn_walk(const float4* __restrict__ SPg, const float4* __restrict__ SPl,
-                      const int* __restrict__ idx, int m, int r, const float4& q, bool bounded,
-                      double (&kk)[kK]) {
+// Sorted-point views the walks read through (all inlined; the address space of each pointer --
+// LDS or global -- is inferred at the call site):
+//   PtsF4  16-B points (x, y, z, -) + a separate int permutation (sorted rank -> original index)
+//   PtsSoA x / y / z float arrays + a u16 permutation: 14 B per point, so ~9k-point frames fit in
+//          LDS next to the deferred-query grid
+struct PtsF4 {
+    const float4* S;
+    const int* I;
+    SSF_DEV float4 pt(int c) const { return S[c]; }
+    SSF_DEV int id(int c) const { return I[c]; }
+};
+struct PtsSoA {
+    const float* X;
+    const float* Y;
+    const float* Z;
+    const uint16_t* I;
+    SSF_DEV float4 pt(int c) const { return make_float4(X[c], Y[c], Z[c], 0.f); }
+    SSF_DEV int id(int c) const { return (int)I[c]; }
+};
+
+struct PtsF4W {                     // 16-B points with the original index in .w
+    const float4* S;
+    SSF_DEV float4 pt(int c) const { return S[c]; }
+    SSF_DEV int id(int c) const { return __float_as_int(S[c].w); }
+};
+
+template <class V>
+SSF_DEV void knn_walk(const V& v, int m, int r, const float4& q, bool bounded, double (&kk)[kK]) {
     const float lim = bounded ? 1.0f : __builtin_inff();
 #pragma unroll
     for (int k = 0; k < kK; ++k) kk[k] = knn_key(lim, 0x7fffffff);
     for (int c = r; c < m; ++c) {                         // rightwards (x non-decreasing)
-        const float4 p = kLds ? SPl[c] : SPg[c];
+        const float4 p = v.pt(c);
         const float dx = q.x - p.x;
         const float dx2 = dx * dx;
         if (dx2 > key_dist(kk[kK - 1]) || dx2 >= lim) break;
-        const double key = knn_key(l2_simple(q, p), idx[c]);
+        const double key = knn_key(l2_simple(q, p), v.id(c));
         key_insert<kK>(kk, key);              // branch-free: a key >= kk[K-1] passes through
     }
     for (int c = r - 1; c >= 0; --c) {                    // leftwards
-        const float4 p = kLds ? SPl[c] : SPg[c];
+        const float4 p = v.pt(c);
         const float dx = q.x - p.x;
         const float dx2 = dx * dx;
         if (dx2 > key_dist(kk[kK - 1]) || dx2 >= lim) break;
-        const double key = knn_key(l2_simple(q, p), idx[c]);
+        const double key = knn_key(l2_simple(q, p), v.id(c));
         key_insert<kK>(kk, key);              // branch-free: a key >= kk[K-1] passes through
     }
 }
@@ -390,7 +416,6 @@ SSF_DEV int bounded_decides(const float4* __restrict__ P, int m, const double (&
     return nq >= 2 ? 1 : 0;
 }
 
-template <bool kLds>
 SSF_DEV void table_finish(const float4* __restrict__ P, int m, float plane_max, int64_t o,
                           const double (&kk)[kK], float* __restrict__ normal,
                           uint8_t* __restrict__ valid) {
@@ -411,8 +436,9 @@ SSF_DEV void table_finish(const float4* __restrict__ P, int m, float plane_max, 
 constexpr int kGridG = 64;
 constexpr int kGridBytes = 4 * kGridG * kGridG + 256;      // + 2 m bytes of list
 
-SSF_DEV void table_deferred_grid(const float4* __restrict__ P, const float4* __restrict__ SPl,
-                                 const int* __restrict__ idx, int m, float plane_max, int64_t base,
+template <class V>
+SSF_DEV void table_deferred_grid(const float4* __restrict__ P, const V& v, int m, float plane_max,
+                                 int64_t base,
                                  float* __restrict__ normal, uint8_t* __restrict__ valid,
                                  const int* queue, int nq, char* gridmem,
                                  int32_t* stamp_out, unsigned long long stamp0) {
@@ -422,7 +448,7 @@ SSF_DEV void table_deferred_grid(const float4* __restrict__ P, const float4* __r
     uint16_t* list = reinterpret_cast<uint16_t*>(gridmem + kGridBytes);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
     float ymn = __builtin_inff(), ymx = -__builtin_inff();
-    for (int r = tid; r < m; r += blockDim.x) { const float y = SPl[r].y; ymn = fminf(ymn, y); ymx = fmaxf(ymx, y); }
+    for (int r = tid; r < m; r += blockDim.x) { const float y = v.pt(r).y; ymn = fminf(ymn, y); ymx = fmaxf(ymx, y); }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         ymn = fminf(ymn, __shfl_xor(ymn, o, 64));
@@ -433,7 +459,7 @@ SSF_DEV void table_deferred_grid(const float4* __restrict__ P, const float4* __r
     __syncthreads();
     float y0 = __builtin_inff(), y1 = -__builtin_inff();
     for (int k = 0; k < nw; ++k) { y0 = fminf(y0, scr[2 * k]); y1 = fmaxf(y1, scr[2 * k + 1]); }
-    const float x0 = SPl[0].x, x1 = SPl[m - 1].x;
+    const float x0 = v.pt(0).x, x1 = v.pt(m - 1).x;
     float h = fmaxf(x1 - x0, y1 - y0) / (float)G;
     if (!(h > 0.0f)) h = 1.0f;
     const float invh = 1.0f / h;
@@ -443,7 +469,7 @@ SSF_DEV void table_deferred_grid(const float4* __restrict__ P, const float4* __r
     };
     for (int r = tid; r < m; r += blockDim.x) {
         int cx, cy;
-        cell(SPl[r], cx, cy);
+        cell(v.pt(r), cx, cy);
         atomicAdd(&cend[cy * G + cx], 1u);
     }
     __syncthreads();
@@ -467,7 +493,7 @@ SSF_DEV void table_deferred_grid(const float4* __restrict__ P, const float4* __r
     __syncthreads();
     for (int r = tid; r < m; r += blockDim.x) {               // cend[c]: start -> end of cell c
         int cx, cy;
-        cell(SPl[r], cx, cy);
+        cell(v.pt(r), cx, cy);
         list[atomicAdd(&cend[cy * G + cx], 1u)] = (uint16_t)r;
     }
     __syncthreads();
@@ -475,7 +501,7 @@ SSF_DEV void table_deferred_grid(const float4* __restrict__ P, const float4* __r
     const int t2 = (tid & 63) * nw + w;                        // entry k -> wave k % nw
     for (int k = t2; k < nq; k += blockDim.x) {
         const int r = queue[k];
-        const float4 q = SPl[r];
+        const float4 q = v.pt(r);
         int cx, cy;
         cell(q, cx, cy);
         double kk[kK];
@@ -516,30 +542,28 @@ SSF_DEV void table_deferred_grid(const float4* __restrict__ P, const float4* __r
             }
             if (done) break;
             const int rj = list[j++];
-            const double key = knn_key(l2_simple(q, SPl[rj]), idx[rj]);
+            const double key = knn_key(l2_simple(q, v.pt(rj)), v.id(rj));
             if (key < kk[kK - 1]) key_insert<kK>(kk, key);
         }
-        table_finish<true>(P, m, plane_max, base + idx[r], kk, normal, valid);
+        table_finish(P, m, plane_max, base + v.id(r), kk, normal, valid);
     }
 }
 
 // Queries in sorted order (adjacent lanes ~ adjacent x): 1-m-bounded walk for everyone; the
 // undecided few go to an LDS queue and are re-walked in full afterwards, one per lane, so a
 // handful of long walks no longer stalls whole waves.  queue == nullptr: walk in full at once.
-template <bool kLds>
-SSF_DEV void table_walks(const float4* __restrict__ P, const float4* __restrict__ SPg,
-                         const float4* __restrict__ SPl, const int* __restrict__ idx, int m,
-                         float plane_max, int64_t base, float* __restrict__ normal,
-                         uint8_t* __restrict__ valid, int* queue, int qcap, int* qlen,
-                         char* gridmem = nullptr, int32_t* stamp_out = nullptr,
-                         unsigned long long stamp0 = 0) {
+template <class V>
+SSF_DEV void table_walks(const float4* __restrict__ P, const V& v, int m, float plane_max,
+                         int64_t base, float* __restrict__ normal, uint8_t* __restrict__ valid,
+                         int* queue, int qcap, int* qlen, char* gridmem = nullptr,
+                         int32_t* stamp_out = nullptr, unsigned long long stamp0 = 0) {
     for (int r = threadIdx.x; r < m; r += blockDim.x) {
-        const float4 q = kLds ? SPl[r] : SPg[r];
+        const float4 q = v.pt(r);
         double kk[kK];
         bool bounded = true;
         int dec;
         for (;;) {                                        // one walk call site: one live list
-            knn_walk<kLds>(SPg, SPl, idx, m, r, q, bounded, kk);
+            knn_walk(v, m, r, q, bounded, kk);
             if (!bounded) { dec = 1; break; }
             dec = bounded_decides(P, m, kk);
             if (dec != 0) break;
@@ -548,11 +572,11 @@ SSF_DEV void table_walks(const float4* __restrict__ P, const float4* __restrict_
             bounded = false;
         }
         if (dec == 2) {                                   // gate d2[n] < 1 fails for any n >= 5
-            const int64_t o = base + idx[r];
+            const int64_t o = base + v.id(r);
             normal[3 * o] = 0.f; normal[3 * o + 1] = 0.f; normal[3 * o + 2] = 0.f;
             valid[o] = 0;
         } else if (dec == 1) {
-            table_finish<kLds>(P, m, plane_max, base + idx[r], kk, normal, valid);
+            table_finish(P, m, plane_max, base + v.id(r), kk, normal, valid);
         }
     }
     if (!queue) return;
@@ -562,17 +586,17 @@ SSF_DEV void table_walks(const float4* __restrict__ P, const float4* __restrict_
     if (threadIdx.x == 0 && stamp_out) stamp_out[1] = *qlen;
 #endif
     const int nq = min(*qlen, qcap);
-    if (kLds && gridmem && nq > 0) {                          // uniform
-        table_deferred_grid(P, SPl, idx, m, plane_max, base, normal, valid, queue, nq, gridmem,
+    if (gridmem && nq > 0) {                                  // uniform
+        table_deferred_grid(P, v, m, plane_max, base, normal, valid, queue, nq, gridmem,
                             stamp_out, stamp0);
         return;
     }
     for (int k = threadIdx.x; k < nq; k += blockDim.x) {
         const int r = queue[k];
-        const float4 q = kLds ? SPl[r] : SPg[r];
+        const float4 q = v.pt(r);
         double kk[kK];
-        knn_walk<kLds>(SPg, SPl, idx, m, r, q, false, kk);
-        table_finish<kLds>(P, m, plane_max, base + idx[r], kk, normal, valid);
+        knn_walk(v, m, r, q, false, kk);
+        table_finish(P, m, plane_max, base + v.id(r), kk, normal, valid);
     }
 }
 
@@ -639,18 +663,57 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
         __syncthreads();
         // spare LDS between the sorted points and the permutation holds the deferred-query grid
         char* gridmem = lds + ((16 * m + 15) & ~15);
+        const PtsF4 v{SPl, idx2};
 #ifdef SSF_TABLE_STAMPS
-        table_walks<true>(P, SP, SPl, idx2, m, plane_max, base, normal, valid, queue, qcap, qlen,
-                          gridmem, SI + m + 1, tstamp0);
+        table_walks(P, v, m, plane_max, base, normal, valid, queue, qcap, qlen, gridmem, SI + m + 1,
+                    tstamp0);
 #else
-        table_walks<true>(P, SP, SPl, idx2, m, plane_max, base, normal, valid, queue, qcap, qlen,
-                          gridmem);
+        table_walks(P, v, m, plane_max, base, normal, valid, queue, qcap, qlen, gridmem);
+#endif
+        SSF_TSTAMP(3);
+    } else if (m <= kLdsSoaMax) {
+        // x | y | z float arrays and a u16 permutation over the sort image (14 m bytes), then the
+        // deferred-query grid and queue.  The permutation is read into registers first: the new
+        // arrays overwrite it.
+        constexpr int kPer = (kLdsSoaMax + kTableThreads - 1) / kTableThreads;
+        int own[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int r = tid + k * kTableThreads;
+            own[k] = r < m ? idx[r] : 0;
+        }
+        __syncthreads();
+        float* X = reinterpret_cast<float*>(lds);
+        float* Y = X + m;
+        float* Z = Y + m;
+        uint16_t* I16 = reinterpret_cast<uint16_t*>(Z + m);
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int r = tid + k * kTableThreads;
+            if (r < m) {
+                const float4 p = P[own[k]];
+                X[r] = p.x; Y[r] = p.y; Z[r] = p.z; I16[r] = (uint16_t)own[k];
+            }
+        }
+        const int goff = (14 * m + 15) & ~15;
+        char* gridmem = lds + goff;
+        const int qoff = (goff + kGridBytes + 2 * m + 15) & ~15;
+        int* queue = reinterpret_cast<int*>(lds + qoff);
+        const int qcap = ((int)sizeof(lds) - 4 - qoff) / 4;
+        __syncthreads();
+        const PtsSoA v{X, Y, Z, I16};
+#ifdef SSF_TABLE_STAMPS
+        table_walks(P, v, m, plane_max, base, normal, valid, queue, qcap, qlen, gridmem, SI + m + 1,
+                    tstamp0);
+#else
+        table_walks(P, v, m, plane_max, base, normal, valid, queue, qcap, qlen, gridmem);
 #endif
         SSF_TSTAMP(3);
     } else {
-        // queue in the (now unused) key region
+        // points from global memory, the permutation in LDS; queue in the (now unused) key region
         int* queue = reinterpret_cast<int*>(lds);
-        table_walks<false>(P, SP, SPl, idx, m, plane_max, base, normal, valid, queue, kSortMax, qlen);
+        const PtsF4 v{SP, idx};
+        table_walks(P, v, m, plane_max, base, normal, valid, queue, kSortMax, qlen);
     }
 }
 
@@ -729,6 +792,7 @@ __global__ __launch_bounds__(256) void k_associate_sorted(
 constexpr int kAssocThreads = 1024;
 constexpr int kAssocQ = 2048;              // queries per work-group (2 per thread)
 constexpr int kAssocLdsMax = 6144;         // last-frame plane points staged in LDS (96 KiB)
+constexpr int kAssocSoaMax = 12032;        // ... as 12-B SoA points: 141 KiB + queue + reductions
 #ifndef SSF_ASSOC_BAND2
 #define SSF_ASSOC_BAND2 1.0f
 #endif
@@ -743,30 +807,35 @@ SSF_DEV float4 assoc_query_point(const float4& pc, const double q[4], const doub
     return qs;
 }
 
-template <class Ld>
-SSF_DEV void assoc_walk(Ld ld, int ml, const float4& qs, float lim, float& best, int& bi) {
+// Candidates are kept as a sorted rank bc; the original index (the tie-break key) is read only
+// on an exact distance tie, and once at the end.
+template <class V>
+SSF_DEV bool assoc_better(const V& v, int c, float d, float best, int bc) {
+    return d < best || (d == best && (bc < 0 || v.id(c) < v.id(bc)));
+}
+
+template <class V>
+SSF_DEV void assoc_walk(const V& v, int ml, const float4& qs, float lim, float& best, int& bc) {
     int lo_i = 0, hi_i = ml;                                            // first x >= qs.x
     while (lo_i < hi_i) {
         const int mid = (lo_i + hi_i) >> 1;
-        if (ld(mid).x < qs.x) lo_i = mid + 1; else hi_i = mid;
+        if (v.pt(mid).x < qs.x) lo_i = mid + 1; else hi_i = mid;
     }
     for (int c = lo_i; c < ml; ++c) {
-        const float4 pl = ld(c);
+        const float4 pl = v.pt(c);
         const float dx = qs.x - pl.x;
         const float dx2 = dx * dx;
         if (dx2 > best || dx2 >= lim) break;
         const float d = l2_simple(qs, pl);
-        const int id = __float_as_int(pl.w);
-        if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+        if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
     }
     for (int c = lo_i - 1; c >= 0; --c) {
-        const float4 pl = ld(c);
+        const float4 pl = v.pt(c);
         const float dx = qs.x - pl.x;
         const float dx2 = dx * dx;
         if (dx2 > best || dx2 >= lim) break;
         const float d = l2_simple(qs, pl);
-        const int id = __float_as_int(pl.w);
-        if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+        if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
     }
 }
 
@@ -784,9 +853,9 @@ SSF_DEV void assoc_finish(const float4* __restrict__ L, int64_t lo, const float*
     if (nn_out) nn_out[ci] = bi;
 }
 
-// phases 1 and 2 for one work-group; Ld reads sorted point c as (x, y, z, original index)
-template <class Ld>
-SSF_DEV void assoc_phases(Ld ld, int ml, int mc, int i0, int64_t lo, int64_t co,
+// phases 1 and 2 for one work-group over the sorted last frame v
+template <class V>
+SSF_DEV void assoc_phases(const V& v, int ml, int mc, int i0, int64_t lo, int64_t co,
                           const double* __restrict__ pose_rel, int p, const float4* __restrict__ curr,
                           const float4* __restrict__ L, const float* __restrict__ last_normal,
                           const uint8_t* __restrict__ last_valid, CorrRec* __restrict__ corr,
@@ -799,9 +868,9 @@ SSF_DEV void assoc_phases(Ld ld, int ml, int mc, int i0, int64_t lo, int64_t co,
         const float4 pc = curr[co + i];
         const float4 qs = assoc_query_point(pc, q, t);
         float best = __builtin_inff();
-        int bi = 0x7fffffff;
-        assoc_walk(ld, ml, qs, kAssocBand2, best, bi);
-        if (best < kAssocBand2) assoc_finish(L, lo, last_normal, last_valid, pc, bi, corr, nn_out, co + i);
+        int bc = -1;
+        assoc_walk(v, ml, qs, kAssocBand2, best, bc);
+        if (best < kAssocBand2) assoc_finish(L, lo, last_normal, last_valid, pc, v.id(bc), corr, nn_out, co + i);
         else queue[atomicAdd(qlen, 1)] = i;                             // <= kAssocQ entries
     }
     __syncthreads();
@@ -810,7 +879,7 @@ SSF_DEV void assoc_phases(Ld ld, int ml, int mc, int i0, int64_t lo, int64_t co,
 #endif
     // phase 2: the queued queries in groups of 64 (one per lane); for each group all waves scan
     // disjoint slices of the last frame (broadcast LDS reads, 8 in flight, no divergence) and the
-    // per-slice (distance, index) bests are merged in LDS -- lexicographic, so exact
+    // per-slice (distance, rank) bests are merged in LDS -- ties by original index, so exact
     const int nq = *qlen;
     const int nw = blockDim.x >> 6, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int chunk = (ml + nw - 1) / nw;
@@ -822,40 +891,41 @@ SSF_DEV void assoc_phases(Ld ld, int ml, int mc, int i0, int64_t lo, int64_t co,
         const float4 pc = curr[co + i];
         const float4 qs = assoc_query_point(pc, q, t);
         float best = __builtin_inff();
-        int bi = 0x7fffffff;
+        int bc = -1;
         int c = c0;
         for (; c + 8 <= c1; c += 8) {
             float4 pl[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) pl[u] = ld(c + u);
+            for (int u = 0; u < 8; ++u) pl[u] = v.pt(c + u);
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const float d = l2_simple(qs, pl[u]);
-                const int id = __float_as_int(pl[u].w);
-                if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+                if (assoc_better(v, c + u, d, best, bc)) { best = d; bc = c + u; }
             }
         }
         for (; c < c1; ++c) {
-            const float4 pl = ld(c);
-            const float d = l2_simple(qs, pl);
-            const int id = __float_as_int(pl.w);
-            if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+            const float d = l2_simple(qs, v.pt(c));
+            if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
         }
         red_d[w * 64 + lane] = best;
-        red_i[w * 64 + lane] = bi;
+        red_i[w * 64 + lane] = bc;
         __syncthreads();
         if (w == 0 && act) {
-            for (int v = 1; v < nw; ++v) {
-                const float d = red_d[v * 64 + lane];
-                const int id = red_i[v * 64 + lane];
-                if (lex_less(d, id, best, bi)) { best = d; bi = id; }
+            for (int u = 1; u < nw; ++u) {
+                const float d = red_d[u * 64 + lane];
+                const int cu = red_i[u * 64 + lane];
+                if (cu >= 0 && assoc_better(v, cu, d, best, bc)) { best = d; bc = cu; }
             }
-            assoc_finish(L, lo, last_normal, last_valid, pc, bi, corr, nn_out, co + i);
+            assoc_finish(L, lo, last_normal, last_valid, pc, v.id(max(bc, 0)), corr, nn_out, co + i);
         }
         __syncthreads();
     }
 }
 
+// kSoa = false: the last frame staged as 16-B points (index in .w), up to kAssocLdsMax;
+// kSoa = true:  as x | y | z float arrays (12 B per point, up to kAssocSoaMax), the original index
+//               read from the global permutation on distance ties and for the answer.
+template <bool kSoa>
 __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
     const float4* __restrict__ last, const int64_t* __restrict__ last_off,
     const int32_t* __restrict__ last_count, const float* __restrict__ last_normal,
@@ -865,7 +935,8 @@ __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
     const double* __restrict__ pose_rel, CorrRec* __restrict__ corr, int32_t* __restrict__ nn_out,
     int lds_cap) {
     extern __shared__ float4 SLl[];                 // [lds_cap] points, then the queue
-    int* queue = reinterpret_cast<int*>(SLl + lds_cap);
+    float* SX = reinterpret_cast<float*>(SLl);
+    int* queue = kSoa ? reinterpret_cast<int*>(SX + 3 * lds_cap) : reinterpret_cast<int*>(SLl + lds_cap);
     __shared__ int qlen;
     __shared__ float red_d[kAssocThreads];          // phase-2 per-slice bests
     __shared__ int red_i[kAssocThreads];
@@ -882,21 +953,35 @@ __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
     if (threadIdx.x == 0) qlen = 0;
     const float4* L = last + lo;
     if (ml <= lds_cap) {
-        for (int r = threadIdx.x; r < ml; r += blockDim.x) {
-            float4 v = last_sorted[lo + r];
-            v.w = __int_as_float(last_sidx[lo + r]);
-            SLl[r] = v;
+        if (kSoa) {
+            for (int r = threadIdx.x; r < ml; r += blockDim.x) {
+                const float4 v = last_sorted[lo + r];
+                SX[r] = v.x; SX[ml + r] = v.y; SX[2 * ml + r] = v.z;
+            }
+            __syncthreads();
+            const PtsSoA v{SX, SX + ml, SX + 2 * ml, nullptr};
+            struct View {
+                PtsSoA s;
+                const int32_t* I;
+                SSF_DEV float4 pt(int c) const { return s.pt(c); }
+                SSF_DEV int id(int c) const { return I[c]; }
+            };
+            assoc_phases(View{v, last_sidx + lo}, ml, mc, i0, lo, co, pose_rel, p, curr, L,
+                         last_normal, last_valid, corr, nn_out, queue, &qlen, red_d, red_i, &st1);
+        } else {
+            for (int r = threadIdx.x; r < ml; r += blockDim.x) {
+                float4 v = last_sorted[lo + r];
+                v.w = __int_as_float(last_sidx[lo + r]);
+                SLl[r] = v;
+            }
+            __syncthreads();
+            assoc_phases(PtsF4W{SLl}, ml, mc, i0, lo, co, pose_rel, p, curr, L, last_normal,
+                         last_valid, corr, nn_out, queue, &qlen, red_d, red_i, &st1);
         }
-        __syncthreads();
-        assoc_phases([&](int c) { return SLl[c]; }, ml, mc, i0, lo, co, pose_rel, p, curr, L,
-                     last_normal, last_valid, corr, nn_out, queue, &qlen, red_d, red_i, &st1);
     } else {  // a last frame above the caller's plane-point bound (the LDS size): global memory
         __syncthreads();
-        const float4* SG = last_sorted + lo;
-        const int32_t* SI = last_sidx + lo;
-        assoc_phases([&](int c) { float4 v = SG[c]; v.w = __int_as_float(SI[c]); return v; },
-                     ml, mc, i0, lo, co, pose_rel, p, curr, L, last_normal, last_valid, corr, nn_out,
-                     queue, &qlen, red_d, red_i, &st1);
+        assoc_phases(PtsF4{last_sorted + lo, last_sidx + lo}, ml, mc, i0, lo, co, pose_rel, p, curr,
+                     L, last_normal, last_valid, corr, nn_out, queue, &qlen, red_d, red_i, &st1);
     }
 #ifdef SSF_ASSOC_STAMPS
     __syncthreads();
@@ -1397,14 +1482,15 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
     if (n_pairs <= 0) return hipSuccess;
     if (max_m > 0) {
         const int bx = (int)((max_m + 255) / 256);
-        if (max_m <= kAssocLdsMax && last_sorted && last_sidx) {
+        if (max_m <= kAssocSoaMax && last_sorted && last_sidx) {
             const int qx = (int)((max_m + kAssocQ - 1) / kAssocQ);
-            kmark(s, "k_associate_lds");
-            hipLaunchKernelGGL(k_associate_lds, dim3(qx, n_pairs), dim3(kAssocThreads),
-                               (size_t)max_m * sizeof(float4) + kAssocQ * sizeof(int), s, last,
-                               last_off, last_count,
-                               last_normal, last_valid, last_sorted, last_sidx, curr, curr_off,
-                               curr_count, pose_rel, corr, nn, (int)max_m);
+            const bool soa = max_m > kAssocLdsMax;
+            kmark(s, soa ? "k_associate_lds_soa" : "k_associate_lds");
+            const size_t lds = (size_t)max_m * (soa ? 12 : sizeof(float4)) + kAssocQ * sizeof(int);
+            hipLaunchKernelGGL(soa ? k_associate_lds<true> : k_associate_lds<false>,
+                               dim3(qx, n_pairs), dim3(kAssocThreads), lds, s, last, last_off,
+                               last_count, last_normal, last_valid, last_sorted, last_sidx, curr,
+                               curr_off, curr_count, pose_rel, corr, nn, (int)max_m);
         } else if (max_m <= kSortMax && last_sorted && last_sidx) {
             kmark(s, "k_associate_sorted");
             hipLaunchKernelGGL(k_associate_sorted, dim3(bx, n_pairs), dim3(256), 0, s, last, last_off,

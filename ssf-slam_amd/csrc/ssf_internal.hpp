@@ -77,6 +77,10 @@ hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const
                             const int64_t* frame_off, int mode, const uint8_t* mask_in,
                             const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
                             double* out, int G, int slots, uint32_t* sync, double* parts);
+hipError_t launch_mask_pose(hipStream_t s, int n_frames, const double* pts, const double* flow,
+                            const int64_t* frame_off, int mode, const uint8_t* mask_in,
+                            const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
+                            double* out, int G, int slots, uint32_t* sync, double* parts);
 int mask_pose_slots(int device);
 size_t mask_sync_bytes(int n_frames);
 size_t mask_parts_bytes(int n_frames, int G);

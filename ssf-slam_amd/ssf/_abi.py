@@ -30,7 +30,7 @@ EXPORTS = [
     "ssf_register_batch", "ssf_mask_pose_batch", "ssf_rng_seed", "ssf_accumulate_sequence",
     "ssf_voxel_grid_batch", "ssf_icp_params_default", "ssf_icp_batch",
     "ssf_extract_planes_batch_masked", "ssf_register_pair", "ssf_profile_enable",
-    "ssf_profile_read", "ssf_set_mask_split",
+    "ssf_profile_read", "ssf_set_mask_split", "ssf_mask_pose_batch_f64",
 ]
 # Every symbol include/ssf_pointnet2.h declares (TFlow point-set operators).
 PN2_EXPORTS = [
@@ -125,6 +125,8 @@ def lib():
     L.ssf_profile_read.restype = i32
     L.ssf_mask_pose_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, i32, vp, vp]
     L.ssf_mask_pose_batch.restype = i32
+    L.ssf_mask_pose_batch_f64.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, i32, vp, vp]
+    L.ssf_mask_pose_batch_f64.restype = i32
     L.ssf_accumulate_sequence.argtypes = [vp, vp, i32, vp, vp, vp]
     L.ssf_accumulate_sequence.restype = i32
     L.ssf_voxel_grid_batch.argtypes = [vp, vp, i32, vp, vp, vp, C.c_float, vp, vp]

@@ -248,9 +248,12 @@ class Frontend:
     # ------------------------------------------------------------------ PointCloudOdometry*.py
     def mask_pose(self, pts, flow, off, h_off, mode="gmm", mask_in=None, draws=None,
                   reflection=0, want_mask=True):
-        """Mask + Kabsch for F frames -> (out [F,32] f64, bg_mask [total] u8 or None)."""
-        pts = self._dev(pts, torch.float32)
-        flow = self._dev(flow, torch.float32)
+        """Mask + Kabsch for F frames -> (out [F,32] f64, bg_mask [total] u8 or None).
+        pts / flow both float32 (ssf_mask_pose_batch) or both float64 (ssf_mask_pose_batch_f64:
+        no rounding of f64 inputs)."""
+        dt = torch.float64 if pts.dtype == torch.float64 else torch.float32
+        pts = self._dev(pts, dt)
+        flow = self._dev(flow, dt)
         F = h_off.numel() - 1
         total = int(h_off[-1])
         out = torch.empty((max(F, 1), _abi.POSE_OUT_STRIDE), dtype=torch.float64, device=self.device)
@@ -263,11 +266,12 @@ class Frontend:
                 raise SSFError("draws must hold 3 doubles per frame")
         if mask_in is not None:
             mask_in = self._dev(mask_in, torch.uint8)
-        rc = _abi.lib().ssf_mask_pose_batch(
+        name = "ssf_mask_pose_batch_f64" if dt == torch.float64 else "ssf_mask_pose_batch"
+        rc = getattr(_abi.lib(), name)(
             self._h, _stream(self.device), F, _ptr(pts), _ptr(flow), _ptr(off),
             C.c_void_p(h_off64.data_ptr()), MASK_MODES[mode], _ptr(mask_in),
             None if hd is None else C.c_void_p(hd.data_ptr()), int(reflection), _ptr(bg), _ptr(out))
-        self._check(rc, "ssf_mask_pose_batch")
+        self._check(rc, name)
         return out[:F], (bg[:total] if bg is not None else None)
 
     def accumulate_sequence(self, rel, start=None):

@@ -35,10 +35,21 @@ def _frontend(device) -> Frontend:
     return fe
 
 
-def _as_f32_dev(a, dev):
+def _is_f64(a) -> bool:
+    return (a.dtype == torch.float64) if isinstance(a, torch.Tensor) else (np.asarray(a).dtype == np.float64)
+
+
+def _as_dev(a, dev, dtype):
     if isinstance(a, torch.Tensor):
-        return a.to(dev, torch.float32).contiguous()
-    return torch.from_numpy(np.ascontiguousarray(np.asarray(a), dtype=np.float32)).to(dev)
+        return a.to(dev, dtype).contiguous()
+    npd = np.float64 if dtype == torch.float64 else np.float32
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(a), dtype=npd)).to(dev)
+
+
+def _storage(*arrays):
+    """float64 when any input is float64 (the reference then computes in f64 throughout; the
+    f64 kernel loads those values exactly), else float32 (LiDAR data)."""
+    return torch.float64 if any(_is_f64(a) for a in arrays) else torch.float32
 
 
 def _raise_status(st):
@@ -57,10 +68,13 @@ def _raise_status(st):
 
 def slove_RT_by_SVD(src, dst, reflection: str = "raise", device=None):
     """R (3,3), t (3,1) minimising |R src + t - dst| (reference signature, float64 results).
-    Inputs are LiDAR float32 coordinates on the device (float64 inputs are rounded to float32)."""
+    float64 inputs run the f64-storage kernel (no input rounding); float32 inputs the f32 one.
+    The kernel takes (pos, flow) = (dst, src - dst) and forms src = pos + flow in f64: exact
+    for f32 inputs, and within an ulp of src for f64 inputs."""
     fe = _frontend(device)
-    dst_t = _as_f32_dev(dst, fe.device)
-    src_t = _as_f32_dev(src, fe.device)
+    dt = _storage(src, dst)
+    dst_t = _as_dev(dst, fe.device, dt)
+    src_t = _as_dev(src, fe.device, dt)
     flow = (src_t - dst_t).contiguous()
     off, h_off = frame_offsets([dst_t.shape[0]], fe.device)
     ones = torch.ones(dst_t.shape[0], dtype=torch.uint8, device=fe.device)
@@ -81,8 +95,9 @@ def mask_and_pose(points, flow, mode: str = "gmm", gt_mask=None, seed: int | Non
     (background = s_fg_mask == 0, PointCloudOdometry.py:91) or 'given' (background = mask != 0).
     -> dict(R [F,3,3], t [F,3], q_xyzw [F,4], para_t_q [F,7], bg_mask (device u8), info)."""
     fe = _frontend(device)
-    pts = _as_f32_dev(points, fe.device)
-    fl = _as_f32_dev(flow, fe.device)
+    dt = _storage(points, flow)
+    pts = _as_dev(points, fe.device, dt)
+    fl = _as_dev(flow, fe.device, dt)
     sizes = [pts.shape[0]] if frame_sizes is None else list(frame_sizes)
     off, h_off = frame_offsets(sizes, fe.device)
     if seed is not None:

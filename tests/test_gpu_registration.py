@@ -66,15 +66,20 @@ def test_plane_table_bitexact(oracle, dev, brute):
 
 
 def test_plane_table_duplicates_and_sizes(oracle, dev):
-    """Exact duplicate points (zero-distance ties broken by index), a frame above the LDS-walk
-    limit (6144: the walk reads the sorted copy in global memory) and one above the LDS sort
-    limit (16384: brute-force k-NN) -- all bit-exact against the oracle."""
+    """Exact duplicate points (zero-distance ties broken by index) and every walk tier of the
+    sorted table: points staged in LDS as 16-B records (<= 6144), as 14-B SoA arrays (<= 9088,
+    with and without duplicates), read from the sorted copy in global memory (<= 16384), and
+    above the LDS sort limit (brute-force k-NN) -- all bit-exact against the oracle."""
     import ssf
     rng = np.random.default_rng(7)
     base = [oracle.extract_planes(frame(s, 0, n_az=1875)[0], 64) for s in range(5)]
     dup = np.concatenate([base[0], base[0][rng.choice(len(base[0]), 600, replace=False)]])
-    clouds = [dup[rng.permutation(len(dup))], np.concatenate(base[:2]), np.concatenate(base)]
-    assert len(clouds[1]) > 6144 and len(clouds[2]) > 16384
+    two = np.concatenate(base[:2])
+    dup2 = np.concatenate([two, two[rng.choice(len(two), 900, replace=False)]])
+    clouds = [dup[rng.permutation(len(dup))], two, dup2[rng.permutation(len(dup2))],
+              np.concatenate(base[:3]), np.concatenate(base)]
+    sizes = [len(c) for c in clouds]
+    assert sizes[0] <= 6144 < sizes[1] < sizes[2] <= 9088 < sizes[3] <= 16384 < sizes[4], sizes
     fe = ssf.Frontend(64, device=dev.index)
     for f, P in enumerate(clouds):          # one launch each: the kernel choice is per launch
         off, h_off = ssf.frame_offsets([len(P)], dev)
@@ -148,13 +153,20 @@ def test_16_row_profile_table_and_registration(oracle, dev):
     assert np.abs(got[4:] - t).max() < TOL_T and _quat_angle(got[:4], q) < TOL_R
 
 
-def test_associate_large_frames(oracle, dev):
-    """1-NN indices exact when the frames exceed the LDS staging size (6144 plane points): the
-    association walks the sorted last frame in global memory."""
+@pytest.mark.parametrize("k", [2, 3, 4])
+def test_associate_large_frames(oracle, dev, k):
+    """1-NN indices exact above the 16-B LDS staging size (6144 plane points): k = 2, 3 stage the
+    last frame as 12-B SoA arrays (<= 12032, ties resolved through the global permutation), k = 4
+    walks the sorted last frame in global memory.  The last frame holds exact duplicates, so
+    distance ties occur and must resolve to the lower original index."""
     import ssf
-    base = [oracle.extract_planes(frame(s, 0, n_az=1875)[0], 64) for s in range(3)]
-    L, Cc = np.concatenate(base[:2]), np.concatenate(base[1:])
-    assert len(L) > 6144 and len(Cc) > 6144
+    rng = np.random.default_rng(11 + k)
+    base = [oracle.extract_planes(frame(s, 0, n_az=1875)[0], 64) for s in range(k + 1)]
+    L = np.concatenate(base[:k])
+    L = np.concatenate([L, L[rng.choice(len(L), 300, replace=False)]])
+    L = L[rng.permutation(len(L))]
+    Cc = np.concatenate(base[1:])
+    assert 6144 < len(L) and (len(L) <= 12032) == (k < 4) and len(L) <= 16384
     fe = ssf.Frontend(64, device=dev.index)
     sizes = [len(L), len(Cc)]
     off, h_off = ssf.frame_offsets(sizes, dev)

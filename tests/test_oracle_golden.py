@@ -41,3 +41,25 @@ def test_gmm_mask_and_pose(oracle, path):
     assert abs(info["lower_bound"] - float(g["gmm_lower_bound"])) < 1e-9
     assert np.abs(res["R"] - g["R"]).max() < 1e-12
     assert np.abs(np.r_[res["t"], res["q_xyzw"]] - g["para_t_q"]).max() < 1e-12
+
+
+# ASF block on float32 network output (main_sju_occ_ros.py:256-284): the reference
+# fits sklearn in float32 and runs slove_RT_by_SVD on float32 arrays; this build computes the same
+# block in float64 on the float32 values (a documented deviation).  Bars measured on
+# the fixture (tests/golden/make_golden_asf.py): background agreement >= 99.9 % (observed
+# 99.98-100 %), R within 1e-5, t within 1e-4 m (the reference's own float32 rounding: observed
+# 1e-7..3e-6 and 2e-6..4e-5).  EM iteration counts may differ (f32 convergence; case 0: 18 vs 8).
+ASF_BARS = dict(agree=0.999, R=1e-5, t=1e-4)
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_asf_f32_block_deviation_bounded(oracle, case):
+    g = np.load(os.path.join(GOLDEN, "gmm_asf_f32.npz"))
+    assert g[f"pos1_{case}"].dtype == np.float32 and bool(g[f"means_dtype_f32_{case}"])
+    res = oracle.mask_and_pose(g[f"pos1_{case}"], g[f"flow_{case}"], g[f"draws_{case}"])
+    assert res["rc"] == 0
+    bg_ref = (g[f"labels_{case}"] == int(g[f"bg_label_{case}"])).astype(np.uint8)
+    assert (res["bg_mask"] == bg_ref).mean() >= ASF_BARS["agree"]
+    assert np.abs(res["R"] - g[f"R_{case}"]).max() < ASF_BARS["R"]
+    assert np.abs(res["t"] - g[f"t_{case}"]).max() < ASF_BARS["t"]
+    assert not bool(g[f"quat_would_raise_{case}"])

@@ -61,6 +61,28 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+EXAMPLES = os.path.join(HERE, "..", "examples")
+
+
+def build_examples() -> list:
+    """The INTEGRATION.md host bindings as compiled programs (examples/*.cpp -> examples/_bin/),
+    plain g++ against include/ and the in-tree library -- the way a reference node links it."""
+    out_dir = os.path.join(EXAMPLES, "_bin")
+    os.makedirs(out_dir, exist_ok=True)
+    built = []
+    for src in sorted(f for f in os.listdir(EXAMPLES) if f.endswith(".cpp")):
+        s = os.path.join(EXAMPLES, src)
+        exe = os.path.join(out_dir, src[:-4])
+        if _stale(exe, [s, LIB, os.path.join(HERE, "..", "include", "ssf_frontend.h")]):
+            subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(HERE, "..", "include"),
+                            "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", s, "-L", OUT_DIR,
+                            "-lssf_frontend", "-L", "/opt/rocm/lib", "-lamdhip64",
+                            "-Wl,-rpath,$ORIGIN/../../ssf-slam_amd/ssf/_lib", "-Wl,-rpath,/opt/rocm/lib",
+                            "-o", exe], check=True)
+        built.append(exe)
+    return built
+
+
 def build_diag() -> str:
     """Diagnostic library (phase stamps in k_mask_pose, -DSSF_MASK_STAMPS) for
     tools/diag_mask_phases.py; never loaded by the product path unless SSF_LIB points at it."""

@@ -78,6 +78,44 @@ def test_full_size_batch_vs_oracle(oracle, dev):
         assert np.abs(o[7:16].reshape(3, 3) - ref["R"]).max() < 1e-6
 
 
+@pytest.mark.parametrize("G", [1, 2, 3, 5, 8])
+def test_frame_split_golden(dev, G):
+    """ssf_set_mask_split: the GMM fit of one frame on G work-groups exchanging per-pass sums
+    (G = 1: the B >= 256 bench path; the automatic choice for a 1-frame launch is 8).  Labels,
+    k-means++ indices, iteration counts and the lower bound stay those of sklearn."""
+    import ssf
+    g = np.load(os.path.join(GOLDEN, "gmm_noseg_case2.npz"))
+    fe = ssf.Frontend(64, device=dev.index)
+    fe.mask_split(G)
+    out, bg, _ = _run(fe, dev, [g["pos1"]], [g["flow"]], draws=g["draws"][None, :])
+    o = out[0]
+    assert o[16] == 0
+    assert [int(o[22]), int(o[23])] == [int(v) for v in g["kmeans_pp_idx"]]
+    assert int(o[19]) == int(g["kmeans_n_iter"]) and int(o[20]) == int(g["gmm_n_iter"])
+    assert np.array_equal(bg, (g["labels"] == int(g["bg_label"])).astype(np.uint8))
+    assert abs(o[24] - float(g["gmm_lower_bound"])) < 1e-9
+    assert np.abs(o[0:3] - g["t"]).max() < 1e-5
+
+
+@pytest.mark.parametrize("G", [1, 4])
+def test_frame_split_full_size_vs_oracle(oracle, dev, G):
+    """120k-point frames with the split fixed at 1 and 4 parts per frame vs the oracle."""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index)
+    fe.mask_split(G)
+    fr = [frame(7, 2, n_az=1875), frame(8, 4, n_az=1875)]
+    draws = np.array([[0.31, 0.62, 0.13], [0.9, 0.05, 0.45]])
+    out, bg, h_off = _run(fe, dev, [f[0] for f in fr], [f[1] for f in fr], draws=draws)
+    for k, f in enumerate(fr):
+        ref = oracle.mask_and_pose(f[0], f[1], draws[k])
+        o = out[k]
+        assert o[16] == ref["rc"] == 0
+        assert int(o[19]) == int(ref["info"]["kmeans_iter"]) and int(o[20]) == int(ref["info"]["em_iter"])
+        a, b = int(h_off[k]), int(h_off[k + 1])
+        assert (bg[a:b] == ref["bg_mask"]).mean() >= 0.999
+        assert np.abs(o[0:3] - ref["t"]).max() < 1e-5
+
+
 def test_concurrent_streams_one_context(dev):
     """ssf_mask_pose_batch from one context on two streams back to back (the bench overlaps
     consecutive batches this way): every launch stages its draws in its own slot, so each result

@@ -205,6 +205,60 @@ int32_t ssf_register_pair(ssf_ctx* ctx, void* stream, const float* d_last_xyzi, 
                           ssf_step_log* log);
 
 /* ---------------------------------------------------------------------------------------
+ * Edge features + point-to-line residuals: BEYOND THE REFERENCE.  SSF-SLAM's frameFeature is
+ * planar only (src/frameFeature.cpp:110-123) and its registration point-to-plane only
+ * (src/lidarOdometry_onlyPC.cpp:25-43); the north_star asks for edge extraction and
+ * point-to-line terms, so these entry points are the build's own extension, off unless called,
+ * with parity unpinned (definitions restated in oracle/edge_oracle.c):
+ *   selection   per row in [row_start, n_rows - row_end), greedy in index order: curvature (the
+ *               :84-107 value) > edge_min and j >= jstart -> select, jstart = j + edge_span
+ *   line table  per LAST-frame edge point: exact 5-NN among that frame's edges, centroid and
+ *               covariance (double), Jacobi eigen-decomposition; valid iff the 5th squared
+ *               distance < max_nn_d2 and lambda1 > line_ratio * lambda2; direction u = the
+ *               principal eigenvector (largest-|.| component positive)
+ *   residual    e = (I - u u^T)(R p + t - c) for the 1-NN last edge of the transformed current
+ *               edge point, one Huber(0.1) block on |e|^2, doubled like every :160 block
+ */
+typedef struct {
+    float edge_min;       /* curvature threshold, m^2 (1.0)                                     */
+    int32_t edge_span;    /* greedy spacing in a row (10 for 64 rows, 3 for 16)                 */
+    float line_ratio;     /* lambda1 > line_ratio * lambda2 (3.0)                               */
+    float max_nn_d2;      /* 5th-NN squared distance gate (1.0)                                 */
+} ssf_edge_config;
+int32_t ssf_edge_config_default(int32_t n_rows, ssf_edge_config* out);
+int32_t ssf_set_edge_config(ssf_ctx* ctx, const ssf_edge_config* cfg);
+/* ssf_extract_planes_batch(_masked) plus the edge cloud: d_edge_xyzi (x,y,z,intensity, frame
+ * offsets, capacity = the points) and d_edge_count [F].  d_keep nullable. */
+int32_t ssf_extract_features_batch(ssf_ctx* ctx, void* stream, int32_t n_frames,
+                                   const float* d_pts, int32_t point_stride,
+                                   const int64_t* d_frame_off, int64_t total_points,
+                                   int64_t max_frame_points, const uint8_t* d_keep,
+                                   float* d_plane_xyzi, int32_t* d_plane_count,
+                                   float* d_edge_xyzi, int32_t* d_edge_count);
+/* Line table of frames that will be LAST frames: d_line 6 floats per edge point (centroid x,y,z,
+ * direction x,y,z) and d_line_valid u8, at the frame offsets. */
+int32_t ssf_edge_table_batch(ssf_ctx* ctx, void* stream, int32_t n_frames,
+                             const float* d_edge_xyzi, const int64_t* d_frame_off,
+                             const int32_t* d_edge_count, int64_t max_edge_points,
+                             float* d_line, uint8_t* d_line_valid);
+/* ssf_register_batch with point-to-line blocks added to every pair's problem (same LM/GN loop,
+ * same pose / log outputs).  Edge clouds at their own offsets; d_ncorr_edge nullable [P]. */
+int32_t ssf_register_batch_edges(ssf_ctx* ctx, void* stream, int32_t n_pairs,
+                                 const float* d_last_xyzi, const int64_t* d_last_off,
+                                 const int32_t* d_last_count, const float* d_last_normal,
+                                 const uint8_t* d_last_valid, const float* d_last_sorted_xyzi,
+                                 const int32_t* d_last_sorted_idx, const float* d_curr_xyzi,
+                                 const int64_t* d_curr_off, const int32_t* d_curr_count,
+                                 int64_t curr_total_points, int64_t max_plane_points,
+                                 const float* d_last_edge_xyzi, const int64_t* d_last_edge_off,
+                                 const int32_t* d_last_edge_count, const float* d_last_line,
+                                 const uint8_t* d_last_line_valid, const float* d_curr_edge_xyzi,
+                                 const int64_t* d_curr_edge_off, const int32_t* d_curr_edge_count,
+                                 int64_t curr_edge_total, int64_t max_edge_points,
+                                 double* d_pose_rel, double* d_pose_abs, double* d_log,
+                                 int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_ncorr_edge);
+
+/* ---------------------------------------------------------------------------------------
  * PointCloudOdometry{,_noSeg}.py: replaces the dynamic-point mask + slove_RT_by_SVD + Quaternion
  * block (scripts/PointCloudOdometry_noSeg.py:97-125, scripts/PointCloudOdometry.py:91-101 and the
  * identical ASF block main_sju_occ_ros.py:256-284) for F frames.

@@ -93,6 +93,19 @@ def lib():
                                     C.c_int32, f64p, f64p, f64p, f64p, f64p, C.POINTER(C.c_int32)]
     L.orc_register_pair.restype = C.c_int64
     L.orc_accumulate.argtypes = [f64p, f64p, f64p, f64p, f64p, f64p]
+    L.orc_select_edges.argtypes = [f32p, f32p, i64p, C.c_int32, C.c_int32, C.c_int32, C.c_float,
+                                   C.c_int32, f32p]
+    L.orc_select_edges.restype = C.c_int64
+    L.orc_extract_features.argtypes = [f32p, C.c_int64, C.c_int64, C.c_int32, C.c_float, C.c_int32,
+                                       f32p, f32p, C.POINTER(C.c_int64)]
+    L.orc_extract_features.restype = C.c_int64
+    L.orc_sym3_eig.argtypes = [f64p, f64p]
+    L.orc_edge_table.argtypes = [f32p, C.c_int64, C.c_float, C.c_float, f32p, i32p]
+    L.orc_register_pair_edges.argtypes = [f32p, C.c_int64, f32p, C.c_int64, f32p, C.c_int64, f32p,
+                                          C.c_int64, C.c_float, C.c_float, C.c_float, C.c_int32,
+                                          C.c_int32, f64p, f64p, f64p, f64p, f64p,
+                                          C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
+    L.orc_register_pair_edges.restype = C.c_int64
     L.orc_gmm_labels.argtypes = [f64p, C.c_int64, f64p, u8p, f64p, f64p]
     L.orc_gmm_labels.restype = C.c_int32
     L.orc_kabsch.argtypes = [f64p, f64p, C.c_int64, C.c_void_p, C.c_int32, f64p, f64p]
@@ -255,6 +268,87 @@ def register_pair(last, curr, plane_max, mode=MODE_CERES_LM, max_iter=8, q_init=
                                 np.asarray(q_init, np.float64), np.asarray(t_init, np.float64),
                                 q, t, log, C.byref(nl))
     return q, t, log[:LOG_STRIDE * nl.value].reshape(-1, LOG_STRIDE), c
+
+
+# --------------------------------------------------------------------------- edges (beyond the
+# reference; edge_oracle.c states the definitions -- parity unpinned)
+EDGE_DEFAULTS = dict(edge_min=1.0, edge_span={64: 10, 16: 3}, line_ratio=3.0, max_nn_d2=1.0)
+
+
+def _f32_or_dummy(a, width):
+    a = np.ascontiguousarray(a, np.float32)
+    return (a.reshape(-1) if a.size else np.zeros(width, np.float32)), (a.shape[0] if a.ndim else 0)
+
+
+def select_edges(rxyzi, curv, ring_off, n_rows, edge_min=None, edge_span=None):
+    p = profile(n_rows)
+    edge_min = EDGE_DEFAULTS["edge_min"] if edge_min is None else edge_min
+    edge_span = EDGE_DEFAULTS["edge_span"][n_rows] if edge_span is None else edge_span
+    rx = np.ascontiguousarray(rxyzi, np.float32)
+    n = rx.shape[0]
+    out = np.zeros((max(n, 1), 4), np.float32)
+    m = lib().orc_select_edges(rx.reshape(-1) if n else np.zeros(4, np.float32),
+                               np.ascontiguousarray(curv, np.float32) if n else np.zeros(1, np.float32),
+                               ring_off, n_rows, p.row_start, p.row_end, edge_min, edge_span,
+                               out.reshape(-1))
+    return out[:m]
+
+
+def extract_features(pts, n_rows, edge_min=None, edge_span=None):
+    """frameFeature with edges: -> (plane cloud (m,4), edge cloud (e,4))"""
+    edge_min = EDGE_DEFAULTS["edge_min"] if edge_min is None else edge_min
+    edge_span = EDGE_DEFAULTS["edge_span"][n_rows] if edge_span is None else edge_span
+    pts = np.ascontiguousarray(pts, np.float32)
+    n = pts.shape[0]
+    planes = np.zeros((max(n, 1), 4), np.float32)
+    edges = np.zeros((max(n, 1), 4), np.float32)
+    me = C.c_int64(0)
+    m = lib().orc_extract_features(pts.reshape(-1) if n else np.zeros(3, np.float32), n,
+                                   pts.shape[1] if n else 3, n_rows, edge_min, edge_span,
+                                   planes.reshape(-1), edges.reshape(-1), C.byref(me))
+    if m < 0:
+        raise ValueError("bad profile")
+    return planes[:m], edges[:me.value]
+
+
+def sym3_eig(A):
+    A = np.array(A, np.float64).reshape(9).copy()
+    V = np.zeros(9)
+    lib().orc_sym3_eig(A, V)
+    return A.reshape(3, 3).diagonal().copy(), V.reshape(3, 3)
+
+
+def edge_table(edges, max_nn_d2=None, line_ratio=None):
+    """-> (line [m,6] f32: centroid, direction; valid [m] i32)"""
+    max_nn_d2 = EDGE_DEFAULTS["max_nn_d2"] if max_nn_d2 is None else max_nn_d2
+    line_ratio = EDGE_DEFAULTS["line_ratio"] if line_ratio is None else line_ratio
+    e, m = _f32_or_dummy(edges, 4)
+    line = np.zeros((max(m, 1), 6), np.float32)
+    valid = np.zeros(max(m, 1), np.int32)
+    if m:
+        lib().orc_edge_table(e, m, max_nn_d2, line_ratio, line.reshape(-1), valid)
+    return line[:m], valid[:m]
+
+
+def register_pair_edges(last, curr, last_e, curr_e, plane_max, mode=MODE_CERES_LM, max_iter=8,
+                        q_init=(0, 0, 0, 1), t_init=(0, 0, 0), max_nn_d2=None, line_ratio=None):
+    """frameRegistration with point-to-plane AND point-to-line blocks:
+    -> (q_xyzw, t, log [iters,10], n_plane_corr, n_edge_corr)"""
+    max_nn_d2 = EDGE_DEFAULTS["max_nn_d2"] if max_nn_d2 is None else max_nn_d2
+    line_ratio = EDGE_DEFAULTS["line_ratio"] if line_ratio is None else line_ratio
+    L, ml = _f32_or_dummy(last, 4)
+    Cc, mc = _f32_or_dummy(curr, 4)
+    Le, mle = _f32_or_dummy(last_e, 4)
+    Ce, mce = _f32_or_dummy(curr_e, 4)
+    q = np.zeros(4); t = np.zeros(3)
+    log = np.zeros(LOG_STRIDE * (max_iter + 2))
+    nl = C.c_int32(0)
+    ne = C.c_int64(0)
+    c = lib().orc_register_pair_edges(L, ml, Cc, mc, Le, mle, Ce, mce, plane_max, max_nn_d2,
+                                      line_ratio, mode, max_iter, np.asarray(q_init, np.float64),
+                                      np.asarray(t_init, np.float64), q, t, log, C.byref(nl),
+                                      C.byref(ne))
+    return q, t, log[:LOG_STRIDE * nl.value].reshape(-1, LOG_STRIDE), c, ne.value
 
 
 def accumulate(q0l, t0l, qlc, tlc):

@@ -521,33 +521,66 @@ static double residual_jac(const double q[4], const double t[3], const double po
 
 typedef struct { double A[21]; double g[6]; double cost; } ne_t; /* packed upper, row-major */
 
-/* Evaluate Huber(0.1)-corrected cost / normal equations at (q, t).  Every residual block is
- * inserted twice by the reference (the i_opt loop, lidarOdometry_onlyPC.cpp:160), hence dup=2. */
-static void evaluate(const float* po, const float* pa, const float* nrm, int64_t c, const double q[4],
-                     const double t[3], int need_jac, ne_t* out) {
-    memset(out, 0, sizeof(*out));
+/* Huber(0.1) (lidarOdometry_onlyPC.cpp:239): rho(s) and rho'(s), Ceres HuberLoss. */
+static void huber(double s, double* rho0, double* rho1) {
     const double a = 0.1, b = 0.1 * 0.1;
+    if (s > b) {
+        double rr = sqrt(s);
+        *rho0 = 2.0 * a * rr - b;
+        *rho1 = a / rr;
+        if (*rho1 < DBL_MIN) *rho1 = DBL_MIN;
+    } else {
+        *rho0 = s; *rho1 = 1.0;
+    }
+}
+
+/* Evaluate Huber(0.1)-corrected cost / normal equations at (q, t).  Every residual block is
+ * inserted twice by the reference (the i_opt loop, lidarOdometry_onlyPC.cpp:160), hence dup=2.
+ * Edge blocks (beyond the reference, see orc_edge_table): the 3-vector point-to-line residual
+ * e = P (R po + t - c), P = I - u u^T, one Huber block on s = |e|^2; row k is the plane
+ * residual with "normal" P row k, so residual_jac gives its value and local Jacobian. */
+static void evaluate(const float* po, const float* pa, const float* nrm, int64_t c,
+                     const float* epo, const float* ec, const float* eu, int64_t ce,
+                     const double q[4], const double t[3], int need_jac, ne_t* out) {
+    memset(out, 0, sizeof(*out));
     for (int64_t i = 0; i < c; ++i) {
         double p0[3] = {po[3 * i], po[3 * i + 1], po[3 * i + 2]};
         double p1[3] = {pa[3 * i], pa[3 * i + 1], pa[3 * i + 2]};
         double nn[3] = {nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]};
         double J[6];
         double r = residual_jac(q, t, p0, p1, nn, need_jac ? J : NULL);
-        double s = r * r, rho0, rho1;
-        if (s > b) {
-            double rr = sqrt(s);
-            rho0 = 2.0 * a * rr - b;
-            rho1 = a / rr;
-            if (rho1 < DBL_MIN) rho1 = DBL_MIN;
-        } else {
-            rho0 = s; rho1 = 1.0;
-        }
+        double rho0, rho1;
+        huber(r * r, &rho0, &rho1);
         out->cost += 0.5 * rho0;
         if (need_jac) {
             int k = 0;
             for (int u = 0; u < 6; ++u) {
                 out->g[u] += rho1 * J[u] * r;
                 for (int v = u; v < 6; ++v) out->A[k++] += rho1 * J[u] * J[v];
+            }
+        }
+    }
+    for (int64_t i = 0; i < ce; ++i) {
+        double p0[3] = {epo[3 * i], epo[3 * i + 1], epo[3 * i + 2]};
+        double cc[3] = {ec[3 * i], ec[3 * i + 1], ec[3 * i + 2]};
+        double uu[3] = {eu[3 * i], eu[3 * i + 1], eu[3 * i + 2]};
+        double r[3], J[3][6], s = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            double nk[3];
+            for (int j = 0; j < 3; ++j) nk[j] = (j == k ? 1.0 : 0.0) - uu[k] * uu[j];
+            r[k] = residual_jac(q, t, p0, cc, nk, need_jac ? J[k] : NULL);
+            s += r[k] * r[k];
+        }
+        double rho0, rho1;
+        huber(s, &rho0, &rho1);
+        out->cost += 0.5 * rho0;
+        if (need_jac) {
+            for (int k = 0; k < 3; ++k) {
+                int m = 0;
+                for (int u = 0; u < 6; ++u) {
+                    out->g[u] += rho1 * J[k][u] * r[k];
+                    for (int v = u; v < 6; ++v) out->A[m++] += rho1 * J[k][u] * J[k][v];
+                }
             }
         }
     }
@@ -605,14 +638,15 @@ static void log_rec(double* log, int32_t* n_log, const double q[4], const double
  * DENSE_QR replaced by Cholesky of the damped normal equations), lidarOdometry_onlyPC.cpp:244-252.
  * Log status: 1 accepted, 0 rejected, 2 invalid step, 3 parameter tol, 4 function tol,
  * 5 gradient tol, 6 GN step. */
-int32_t orc_solve(const float* po, const float* pa, const float* nrm, int64_t c, int32_t mode,
-                  int32_t max_iter, const double q_init[4], const double t_init[3], double q_out[4],
-                  double t_out[3], double* log, int32_t* n_log) {
+int32_t orc_solve2(const float* po, const float* pa, const float* nrm, int64_t c,
+                   const float* epo, const float* ec, const float* eu, int64_t ce, int32_t mode,
+                   int32_t max_iter, const double q_init[4], const double t_init[3], double q_out[4],
+                   double t_out[3], double* log, int32_t* n_log) {
     double q[4], t[3];
     memcpy(q, q_init, sizeof(q)); memcpy(t, t_init, sizeof(t));
     int32_t nl = 0;
     ne_t ne, cand;
-    evaluate(po, pa, nrm, c, q, t, 1, &ne);
+    evaluate(po, pa, nrm, c, epo, ec, eu, ce, q, t, 1, &ne);
     if (mode == ORC_MODE_GN) {
         for (int32_t it = 0; it < max_iter; ++it) {
             double M[6][6], b[6], y[6];
@@ -625,7 +659,7 @@ int32_t orc_solve(const float* po, const float* pa, const float* nrm, int64_t c,
             quat_plus(q, y, qn);
             memcpy(q, qn, sizeof(q));
             t[0] += y[3]; t[1] += y[4]; t[2] += y[5];
-            evaluate(po, pa, nrm, c, q, t, 1, &ne);
+            evaluate(po, pa, nrm, c, epo, ec, eu, ce, q, t, 1, &ne);
             log_rec(log, &nl, q, t, ne.cost, 6, 0);
         }
     } else {
@@ -672,7 +706,7 @@ int32_t orc_solve(const float* po, const float* pa, const float* nrm, int64_t c,
             double qc[4], tc[3];
             quat_plus(q, delta, qc);
             tc[0] = t[0] + delta[3]; tc[1] = t[1] + delta[4]; tc[2] = t[2] + delta[5];
-            evaluate(po, pa, nrm, c, qc, tc, 1, &cand);
+            evaluate(po, pa, nrm, c, epo, ec, eu, ce, qc, tc, 1, &cand);
             double xn = 0.0, sn = 0.0;
             for (int u = 0; u < 4; ++u) { xn += q[u] * q[u]; sn += (q[u] - qc[u]) * (q[u] - qc[u]); }
             for (int u = 0; u < 3; ++u) { xn += t[u] * t[u]; sn += (t[u] - tc[u]) * (t[u] - tc[u]); }
@@ -706,6 +740,13 @@ int32_t orc_solve(const float* po, const float* pa, const float* nrm, int64_t c,
     memcpy(q_out, q, sizeof(q)); memcpy(t_out, t, sizeof(t));
     if (n_log) *n_log = nl;
     return 0;
+}
+
+int32_t orc_solve(const float* po, const float* pa, const float* nrm, int64_t c, int32_t mode,
+                  int32_t max_iter, const double q_init[4], const double t_init[3], double q_out[4],
+                  double t_out[3], double* log, int32_t* n_log) {
+    return orc_solve2(po, pa, nrm, c, NULL, NULL, NULL, 0, mode, max_iter, q_init, t_init, q_out,
+                      t_out, log, n_log);
 }
 
 int64_t orc_register_pair(const float* last, int64_t m_last, const float* curr, int64_t m_curr,

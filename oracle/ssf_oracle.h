@@ -87,6 +87,27 @@ int64_t orc_register_pair(const float* last_xyzi, int64_t m_last, const float* c
                           int64_t m_curr, float plane_max, int32_t mode, int32_t max_iter,
                           const double q_init[4], const double t_init[3], double q_out[4],
                           double t_out[3], double* log, int32_t* n_log);
+int32_t orc_solve2(const float* po, const float* pa, const float* nrm, int64_t c,
+                   const float* epo, const float* ec, const float* eu, int64_t ce, int32_t mode,
+                   int32_t max_iter, const double q_init[4], const double t_init[3], double q_out[4],
+                   double t_out[3], double* log, int32_t* n_log);
+/* edge_oracle.c: edge features + point-to-line residuals (beyond the reference, parity unpinned) */
+int64_t orc_select_edges(const float* rxyzi, const float* curv, const int64_t* ring_off,
+                         int32_t n_rows, int32_t row_start, int32_t row_end, float edge_min,
+                         int32_t edge_span, float* edge_xyzi);
+int64_t orc_extract_features(const float* pts, int64_t n, int64_t stride, int32_t n_rows,
+                             float edge_min, int32_t edge_span, float* plane_xyzi,
+                             float* edge_xyzi, int64_t* m_edge);
+void orc_sym3_eig(double A[9], double V[9]);
+void orc_edge_table(const float* edges, int64_t m, float max_nn_d2, float line_ratio,
+                    float* line, int32_t* valid);
+int64_t orc_register_pair_edges(const float* last, int64_t m_last, const float* curr,
+                                int64_t m_curr, const float* last_e, int64_t me_last,
+                                const float* curr_e, int64_t me_curr, float plane_max,
+                                float max_nn_d2, float line_ratio, int32_t mode, int32_t max_iter,
+                                const double q_init[4], const double t_init[3], double q_out[4],
+                                double t_out[3], double* log, int32_t* n_log,
+                                int64_t* n_edge_corr);
 void orc_accumulate(const double q0l[4], const double t0l[3], const double qlc[4],
                     const double tlc[3], double q0c[4], double t0c[3]);
 

@@ -65,6 +65,9 @@ struct ssf_ctx {
         hipEvent_t used = nullptr;     // the kernel that read this slot finished
     };
     static constexpr int kDrawSlots = 4;
+    // edge features (beyond the reference): selection scratch, correspondence records
+    ssf_edge_config ecfg{};
+    DevBuf esel, esel_cnt, ecorr;
     int mask_split = 0;                // ssf_set_mask_split: 0 = automatic
     int mask_slots = -1;               // resident k_mask_pose work-groups (queried once)
     DrawSlot dslot[kDrawSlots];
@@ -210,6 +213,7 @@ int32_t ssf_create(int32_t device, const ssf_config* cfg, ssf_ctx** out) {
     if (!c) return SSF_E_NOMEM;
     c->device = device;
     c->cfg = *cfg;
+    ssf_edge_config_default(cfg->n_rows, &c->ecfg);
     *out = c;
     return SSF_OK;
 }
@@ -219,7 +223,8 @@ void ssf_destroy(ssf_ctx* c) {
     (void)hipSetDevice(c->device);
     DevBuf* bufs[] = {&c->rid, &c->hist, &c->ring_off, &c->ring_xyzi, &c->sel, &c->sel_cnt,
                       &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->pair, &c->start1, &c->vg,
-                      &c->icp_cur, &c->icp_key, &c->icp_st, &c->icp_guess};
+                      &c->icp_cur, &c->icp_key, &c->icp_st, &c->icp_guess, &c->esel,
+                      &c->esel_cnt, &c->ecorr};
     for (auto& ds : c->dslot) {
         if (ds.used) { (void)hipEventSynchronize(ds.used); (void)hipEventDestroy(ds.used); }
         if (ds.copied) { (void)hipEventSynchronize(ds.copied); (void)hipEventDestroy(ds.copied); }
@@ -278,6 +283,22 @@ int32_t ssf_set_mask_split(ssf_ctx* c, int32_t parts_per_frame) {
     return SSF_OK;
 }
 
+int32_t ssf_edge_config_default(int32_t n_rows, ssf_edge_config* out) {
+    if (!out || (n_rows != 16 && n_rows != 64)) return SSF_E_ARG;
+    out->edge_min = 1.0f;
+    out->edge_span = n_rows == 64 ? 10 : 3;
+    out->line_ratio = 3.0f;
+    out->max_nn_d2 = 1.0f;
+    return SSF_OK;
+}
+
+int32_t ssf_set_edge_config(ssf_ctx* c, const ssf_edge_config* ec) {
+    if (!c || !ec || ec->edge_span < 1 || !(ec->line_ratio >= 1.0f) || !(ec->max_nn_d2 > 0.0f))
+        return c ? fail(c, SSF_E_ARG, "set_edge_config: bad arguments") : SSF_E_ARG;
+    c->ecfg = *ec;
+    return SSF_OK;
+}
+
 int32_t ssf_rng_seed(ssf_ctx* c, uint32_t seed) {
     if (!c) return SSF_E_ARG;
     mt_seed(c, seed);
@@ -318,7 +339,8 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
                                    int64_t total_points, int64_t max_frame_points,
                                    const uint8_t* d_keep, float* d_plane_xyzi,
                                    int32_t* d_plane_count, float* d_ring_xyzi, int32_t* d_ring_off,
-                                   float* d_curv) {
+                                   float* d_curv, float* d_edge_xyzi = nullptr,
+                                   int32_t* d_edge_count = nullptr) {
     if (!c) return SSF_E_ARG;
     if (n_frames < 0 || point_stride < 3 || total_points < 0 || max_frame_points < 0 ||
         (n_frames > 0 && (!d_pts || !d_frame_off || !d_plane_xyzi || !d_plane_count)))
@@ -327,6 +349,14 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
     SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
     int32_t rc = ensure_features(c, n_frames, total_points, max_frame_points);
     if (rc) return rc;
+    ssf::EdgeSel es{};
+    const bool edges = d_edge_xyzi != nullptr;
+    if (edges) {
+        SSF_TRY_HIP(c, c->esel.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(total_points, 1)), "alloc esel");
+        SSF_TRY_HIP(c, c->esel_cnt.ensure(sizeof(int32_t) * (size_t)n_frames * c->cfg.n_rows), "alloc esel_cnt");
+        es = ssf::EdgeSel{c->ecfg.edge_min, c->ecfg.edge_span, c->esel.as<int32_t>(),
+                          c->esel_cnt.as<int32_t>(), reinterpret_cast<float4*>(d_edge_xyzi), d_edge_count};
+    }
     ProfScope prof(c, stream);
     float4* ring4 = reinterpret_cast<float4*>(d_ring_xyzi);   // debug output only (nullable)
     int32_t* roff = d_ring_off ? d_ring_off : c->ring_off.as<int32_t>();
@@ -334,7 +364,8 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
         (hipStream_t)stream, c->cfg, n_frames, d_pts, point_stride, d_frame_off, max_frame_points,
         d_keep, c->rid.as<int8_t>(), c->hist.as<int32_t>(), roff, c->ring_xyzi.as<float>(), ring4,
         d_curv, c->sel.as<int32_t>(),
-        c->sel.as<int32_t>() + std::max<int64_t>(total_points, 1), c->sel_cnt.as<int32_t>(), reinterpret_cast<float4*>(d_plane_xyzi), d_plane_count);
+        c->sel.as<int32_t>() + std::max<int64_t>(total_points, 1), c->sel_cnt.as<int32_t>(),
+        reinterpret_cast<float4*>(d_plane_xyzi), d_plane_count, edges ? &es : nullptr);
     if (e != hipSuccess) return hip_fail(c, e, "extract_planes launch");
     return SSF_OK;
 }
@@ -359,6 +390,36 @@ int32_t ssf_extract_planes_batch_masked(ssf_ctx* c, void* stream, int32_t n_fram
     return extract_planes_impl(c, stream, n_frames, d_pts, point_stride, d_frame_off, total_points,
                                max_frame_points, d_keep, d_plane_xyzi, d_plane_count, d_ring_xyzi,
                                d_ring_off, d_curv);
+}
+
+int32_t ssf_extract_features_batch(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_pts,
+                                   int32_t point_stride, const int64_t* d_frame_off,
+                                   int64_t total_points, int64_t max_frame_points,
+                                   const uint8_t* d_keep, float* d_plane_xyzi,
+                                   int32_t* d_plane_count, float* d_edge_xyzi,
+                                   int32_t* d_edge_count) {
+    if (c && n_frames > 0 && (!d_edge_xyzi || !d_edge_count))
+        return fail(c, SSF_E_ARG, "extract_features_batch: null edge outputs");
+    return extract_planes_impl(c, stream, n_frames, d_pts, point_stride, d_frame_off, total_points,
+                               max_frame_points, d_keep, d_plane_xyzi, d_plane_count, nullptr,
+                               nullptr, nullptr, d_edge_xyzi, d_edge_count);
+}
+
+int32_t ssf_edge_table_batch(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_edge_xyzi,
+                             const int64_t* d_frame_off, const int32_t* d_edge_count,
+                             int64_t max_edge_points, float* d_line, uint8_t* d_line_valid) {
+    if (!c) return SSF_E_ARG;
+    if (n_frames < 0 || max_edge_points < 0 ||
+        (n_frames > 0 && (!d_edge_xyzi || !d_frame_off || !d_edge_count || !d_line || !d_line_valid)))
+        return fail(c, SSF_E_ARG, "edge_table_batch: bad arguments");
+    if (n_frames == 0) return SSF_OK;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    ProfScope prof(c, stream);
+    hipError_t e = ssf::launch_edge_table((hipStream_t)stream, c->ecfg, n_frames,
+                                         reinterpret_cast<const float4*>(d_edge_xyzi), d_frame_off,
+                                         d_edge_count, max_edge_points, d_line, d_line_valid);
+    if (e != hipSuccess) return hip_fail(c, e, "edge_table launch");
+    return SSF_OK;
 }
 
 int32_t ssf_extract_planes(ssf_ctx* c, void* stream, const float* d_pts, int64_t n,
@@ -434,6 +495,51 @@ int32_t ssf_register_batch(ssf_ctx* c, void* stream, int32_t n_pairs, const floa
         d_curr_count, max_plane_points, c->corr.as<ssf::CorrRec>(), d_pose_rel, d_pose_abs, d_log,
         d_nlog, d_ncorr, d_nn);
     if (e != hipSuccess) return hip_fail(c, e, "register launch");
+    return SSF_OK;
+}
+
+int32_t ssf_register_batch_edges(ssf_ctx* c, void* stream, int32_t n_pairs,
+                                 const float* d_last_xyzi, const int64_t* d_last_off,
+                                 const int32_t* d_last_count, const float* d_last_normal,
+                                 const uint8_t* d_last_valid, const float* d_last_sorted_xyzi,
+                                 const int32_t* d_last_sorted_idx, const float* d_curr_xyzi,
+                                 const int64_t* d_curr_off, const int32_t* d_curr_count,
+                                 int64_t curr_total_points, int64_t max_plane_points,
+                                 const float* d_last_edge_xyzi, const int64_t* d_last_edge_off,
+                                 const int32_t* d_last_edge_count, const float* d_last_line,
+                                 const uint8_t* d_last_line_valid, const float* d_curr_edge_xyzi,
+                                 const int64_t* d_curr_edge_off, const int32_t* d_curr_edge_count,
+                                 int64_t curr_edge_total, int64_t max_edge_points,
+                                 double* d_pose_rel, double* d_pose_abs, double* d_log,
+                                 int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_ncorr_edge) {
+    if (!c) return SSF_E_ARG;
+    if (n_pairs < 0 || curr_total_points < 0 || max_plane_points < 0 || curr_edge_total < 0 ||
+        max_edge_points < 0 ||
+        (n_pairs > 0 && (!d_last_xyzi || !d_last_off || !d_last_count || !d_last_normal ||
+                         !d_last_valid || !d_curr_xyzi || !d_curr_off || !d_curr_count || !d_pose_rel ||
+                         !d_last_edge_xyzi || !d_last_edge_off || !d_last_edge_count || !d_last_line ||
+                         !d_last_line_valid || !d_curr_edge_xyzi || !d_curr_edge_off || !d_curr_edge_count)))
+        return fail(c, SSF_E_ARG, "register_batch_edges: bad arguments");
+    if (n_pairs == 0) return SSF_OK;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(curr_total_points, 1)), "alloc corr");
+    SSF_TRY_HIP(c, c->ecorr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(curr_edge_total, 1)), "alloc edge corr");
+    if (max_edge_points == 0) {
+        // no edge point anywhere: the edge records are never read, but their counts are
+        SSF_TRY_HIP(c, hipMemsetAsync(c->ecorr.p, 0, sizeof(ssf::CorrRec), (hipStream_t)stream), "zero ecorr");
+    }
+    ProfScope prof(c, stream);
+    const ssf::EdgeReg er{reinterpret_cast<const float4*>(d_last_edge_xyzi), d_last_edge_off,
+                          d_last_edge_count, d_last_line, d_last_line_valid,
+                          reinterpret_cast<const float4*>(d_curr_edge_xyzi), d_curr_edge_off,
+                          d_curr_edge_count, max_edge_points, c->ecorr.as<ssf::CorrRec>(), d_ncorr_edge};
+    hipError_t e = ssf::launch_register(
+        (hipStream_t)stream, c->cfg, n_pairs, reinterpret_cast<const float4*>(d_last_xyzi), d_last_off,
+        d_last_count, d_last_normal, d_last_valid, reinterpret_cast<const float4*>(d_last_sorted_xyzi),
+        d_last_sorted_idx, reinterpret_cast<const float4*>(d_curr_xyzi), d_curr_off,
+        d_curr_count, max_plane_points, c->corr.as<ssf::CorrRec>(), d_pose_rel, d_pose_abs, d_log,
+        d_nlog, d_ncorr, nullptr, &er);
+    if (e != hipSuccess) return hip_fail(c, e, "register_edges launch");
     return SSF_OK;
 }
 

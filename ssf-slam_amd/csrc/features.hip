@@ -282,9 +282,12 @@ SSF_DEV void stencil11w(const float4* a, int j, float& dx, float& dy, float& dz)
     dx = sx; dy = sy; dz = sz;
 }
 
-// kHalves: 64-entry selection stores per trip (a trip selects <= 64 kCurvDepth / plane_span + 1
-// points: one store for plane_span >= 4, two below)
-template <bool kCurv, int kHalves>
+// kHalves: 64-entry selection stores per trip (a trip selects <= 64 kCurvDepth / span + 1
+// points: one store for span >= 4, two below)
+// kEdge (beyond the reference, off by default): the same wave also runs the edge rule --
+// greedy in index order, curvature > edge_min, spacing edge_span (the mirror image of :110-123;
+// oracle/edge_oracle.c) -- into esel / esel_cnt.
+template <bool kCurv, int kHalves, bool kEdge>
 __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__ frame_off,
                                                      int n_rows, int row_start, int row_end,
                                                      float plane_min, int plane_span,
@@ -293,9 +296,13 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
                                                      float* __restrict__ curv,
                                                      int32_t* __restrict__ sel,
                                                      int32_t* __restrict__ sel_cnt,
-                                                     int32_t* __restrict__ sel_dump) {
+                                                     int32_t* __restrict__ sel_dump,
+                                                     float edge_min, int edge_span,
+                                                     int32_t* __restrict__ esel,
+                                                     int32_t* __restrict__ esel_cnt) {
     __shared__ float4 win[kCurvRowsPerWG][kWinPad];
     __shared__ int32_t slist[kCurvRowsPerWG][64 * kHalves];
+    __shared__ int32_t elist[kEdge ? kCurvRowsPerWG : 1][kEdge ? 64 * kHalves : 1];
     // the wave index through readfirstlane: the compiler then knows the row, its length and
     // every loop bound are wave-uniform (scalar loads, no exec-masked loops)
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -309,6 +316,7 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
         if (kCurv)
             for (int j = lane; j < n_r; j += 64) curv[base + j] = 0.0f;
         if (lane == 0) sel_cnt[(int64_t)f * n_rows + r] = 0;
+        if (kEdge && lane == 0) esel_cnt[(int64_t)f * n_rows + r] = 0;
         return;
     }
     float4* wv = win[w];
@@ -317,6 +325,8 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
     const int ng = (n_r + 63) >> 6;
     auto load = [&](int g) { return src[min(64 * g + lane, n_r - 1)]; };   // clamped
     int cnt = 0, nl = 0, jstart = 0;                           // wave-uniform
+    int ecnt = 0, enl = 0, ejstart = 0;                        // wave-uniform (kEdge)
+    int32_t* el = elist[kEdge ? w : 0];
     auto group = [&](Xyz& buf, int g) {
         {                                                      // group g into the window
             const int p = (64 * g + lane) & (kWin - 1);
@@ -349,12 +359,29 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
             jstart = jj + plane_span;
         }
         nl = __builtin_amdgcn_readfirstlane(nl);
+        if (kEdge) {
+            uint64_t me = __ballot(j >= 5 && j < n_r - 5 && v > edge_min);
+            while (true) {
+                const int lo = ejstart - j0;
+                if (lo >= 64) break;
+                if (lo > 0) me &= ~((1ull << lo) - 1ull);
+                if (!me) break;
+                const int l = __ffsll((unsigned long long)me) - 1;
+                const int jj = __builtin_amdgcn_readfirstlane(j0 + l);
+                if (lane == 0) el[enl] = jj;
+                enl++;
+                ejstart = jj + edge_span;
+            }
+            enl = __builtin_amdgcn_readfirstlane(enl);
+        }
     };
     // a trip's selections (<= 64 kHalves) leave with unconditional stores; lanes without one write
     // the row's last slot, which no selection list reaches when the row has >= 2 points (at most
     // ceil(n_r / 2) entries for plane_span >= 2).  A ONE-point row selects its point 0, its last
     // slot: those lanes write a 64-slot dump after the last point of the batch instead.
     int32_t* const spare = n_r >= 2 ? sel + base + n_r - 1 : sel_dump + lane;
+    // edges never select the row's last point (j < n_r - 5), so its slot is a safe spare too
+    int32_t* const espare = kEdge ? (n_r >= 2 ? esel + base + n_r - 1 : sel_dump + lane) : nullptr;
     // prologue loads in buffer order (the loop's waits count on b[0] being the oldest)
     Xyz b[kCurvDepth];
 #pragma unroll
@@ -369,11 +396,19 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
 #pragma unroll
         for (int h = 0; h < kHalves; ++h)
             *(lane + 64 * h < nl ? sel + base + cnt + 64 * h + lane : spare) = sl[64 * h + lane];
+        if (kEdge) {
+#pragma unroll
+            for (int h = 0; h < kHalves; ++h)
+                *(lane + 64 * h < enl ? esel + base + ecnt + 64 * h + lane : espare) = el[64 * h + lane];
+        }
         __builtin_amdgcn_wave_barrier();
         cnt += nl;
         nl = 0;
+        ecnt += enl;
+        enl = 0;
     }
     if (lane == 0) sel_cnt[(int64_t)f * n_rows + r] = cnt;
+    if (kEdge && lane == 0) esel_cnt[(int64_t)f * n_rows + r] = ecnt;
 }
 
 __global__ __launch_bounds__(256) void k_compact(const int64_t* __restrict__ frame_off, int n_rows,
@@ -405,7 +440,7 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
                                  int32_t* ring_off, float* ring_xyz, float4* ring_xyzi, float* curv,
                                  int32_t* sel,
                                  int32_t* sel_dump, int32_t* sel_cnt, float4* plane,
-                                 int32_t* plane_count) {
+                                 int32_t* plane_count, const EdgeSel* edge) {
     const int R = cfg.n_rows;
     const int n_chunks = (int)((max_pts + kBinChunk - 1) / kBinChunk);
     if (n_frames <= 0) return hipSuccess;
@@ -425,17 +460,31 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
     const dim3 cgrid((R + kCurvRowsPerWG - 1) / kCurvRowsPerWG, n_frames);
     kmark(s, "k_curv_select");
     const Xyz* rx = reinterpret_cast<const Xyz*>(ring_xyz);
-    const bool two = cfg.plane_span < 4;
-#define SSF_CURV_LAUNCH(C, H)                                                                     \
-    hipLaunchKernelGGL((k_curv_select<C, H>), cgrid, dim3(64 * kCurvRowsPerWG), 0, s, frame_off, R, \
-                       cfg.row_start, cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off, rx, curv, \
-                       sel, sel_cnt, sel_dump)
-    if (curv) { if (two) SSF_CURV_LAUNCH(true, 2); else SSF_CURV_LAUNCH(true, 1); }
-    else { if (two) SSF_CURV_LAUNCH(false, 2); else SSF_CURV_LAUNCH(false, 1); }
+    const bool two = cfg.plane_span < 4 || (edge && edge->span < 4);
+    const float emin = edge ? edge->min_curv : 0.f;
+    const int espan = edge ? edge->span : 1;
+    int32_t* esel = edge ? edge->sel : nullptr;
+    int32_t* ecnt = edge ? edge->sel_cnt : nullptr;
+#define SSF_CURV_LAUNCH(C, H, E)                                                                  \
+    hipLaunchKernelGGL((k_curv_select<C, H, E>), cgrid, dim3(64 * kCurvRowsPerWG), 0, s, frame_off, \
+                       R, cfg.row_start, cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off, rx,  \
+                       curv, sel, sel_cnt, sel_dump, emin, espan, esel, ecnt)
+    if (edge) {
+        if (curv) { if (two) SSF_CURV_LAUNCH(true, 2, true); else SSF_CURV_LAUNCH(true, 1, true); }
+        else { if (two) SSF_CURV_LAUNCH(false, 2, true); else SSF_CURV_LAUNCH(false, 1, true); }
+    } else {
+        if (curv) { if (two) SSF_CURV_LAUNCH(true, 2, false); else SSF_CURV_LAUNCH(true, 1, false); }
+        else { if (two) SSF_CURV_LAUNCH(false, 2, false); else SSF_CURV_LAUNCH(false, 1, false); }
+    }
 #undef SSF_CURV_LAUNCH
     kmark(s, "k_compact");
     hipLaunchKernelGGL(k_compact, dim3(R, n_frames), dim3(256), 0, s, frame_off, R, ring_off,
                        rx, sel, sel_cnt, plane, plane_count);
+    if (edge) {
+        kmark(s, "k_compact_edges");
+        hipLaunchKernelGGL(k_compact, dim3(R, n_frames), dim3(256), 0, s, frame_off, R, ring_off,
+                           rx, edge->sel, edge->sel_cnt, edge->out, edge->count);
+    }
     return hipGetLastError();
 }
 

@@ -998,6 +998,159 @@ __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
 }
 
 // ------------------------------------------------------------------------------------------
+// Edge features (beyond the reference; oracle/edge_oracle.c states the definitions).
+// k_edge_table: one work-group per LAST frame, its edge cloud staged in LDS; per edge point the
+// exact 5-NN (packed (distance, index) keys, brute force over the frame's few hundred edges),
+// centroid + covariance in double in rank order, cyclic Jacobi, line test.
+constexpr int kEdgeK = 5;
+constexpr int kEdgeThreads = 512;
+constexpr int kEdgeLdsMax = 8192;          // edges per frame staged in LDS (128 KiB)
+
+SSF_DEV void sym3_eig(double A[9], double V[9]) {       // = orc_sym3_eig, operation for operation
+#pragma unroll
+    for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 32; ++sweep) {
+        const double off = A[1] * A[1] + A[2] * A[2] + A[5] * A[5];
+        const double dia = A[0] * A[0] + A[4] * A[4] + A[8] * A[8];
+        if (!(off > 1e-30 * dia)) break;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int p = k == 2 ? 1 : 0, q = k == 0 ? 1 : 2;
+            const double apq = A[3 * p + q];
+            if (apq == 0.0) continue;
+            const double theta = (A[3 * q + q] - A[3 * p + p]) / (2.0 * apq);
+            const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+            const double c = 1.0 / sqrt(t * t + 1.0), sn = t * c;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const double aip = A[3 * i + p], aiq = A[3 * i + q];
+                A[3 * i + p] = c * aip - sn * aiq;
+                A[3 * i + q] = sn * aip + c * aiq;
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const double api = A[3 * p + i], aqi = A[3 * q + i];
+                A[3 * p + i] = c * api - sn * aqi;
+                A[3 * q + i] = sn * api + c * aqi;
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const double vip = V[3 * i + p], viq = V[3 * i + q];
+                V[3 * i + p] = c * vip - sn * viq;
+                V[3 * i + q] = sn * vip + c * viq;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kEdgeThreads) void k_edge_table(
+    const float4* __restrict__ edges, const int64_t* __restrict__ frame_off,
+    const int32_t* __restrict__ count, float max_nn_d2, float line_ratio, float* __restrict__ line,
+    uint8_t* __restrict__ valid, int lds_cap) {
+    extern __shared__ float4 EL[];
+    const int f = blockIdx.x;
+    const int m = count[f];
+    const int64_t base = frame_off[f];
+    const float4* E = edges + base;
+    const bool in_lds = m <= lds_cap;                                   // uniform
+    if (in_lds)
+        for (int r = threadIdx.x; r < m; r += blockDim.x) EL[r] = E[r];
+    __syncthreads();
+    const float4* P = in_lds ? EL : E;
+    for (int a = threadIdx.x; a < m; a += blockDim.x) {
+        float* L = line + 6 * (base + a);
+        float out[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        uint8_t ok = 0;
+        if (m >= kEdgeK) {
+            const float4 q = P[a];
+            double kk[kEdgeK];
+#pragma unroll
+            for (int k = 0; k < kEdgeK; ++k) kk[k] = knn_key(__builtin_inff(), 0x7fffffff);
+            for (int c = 0; c < m; ++c) key_insert<kEdgeK>(kk, knn_key(l2_simple(q, P[c]), c));
+            double cen[3] = {0.0, 0.0, 0.0};
+            float4 nb[kEdgeK];
+#pragma unroll
+            for (int k = 0; k < kEdgeK; ++k) {
+                nb[k] = P[key_index(kk[k])];
+                cen[0] += (double)nb[k].x; cen[1] += (double)nb[k].y; cen[2] += (double)nb[k].z;
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j) cen[j] = cen[j] / 5.0;
+            double A[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, V[9];
+#pragma unroll
+            for (int k = 0; k < kEdgeK; ++k) {
+                const double v[3] = {(double)nb[k].x - cen[0], (double)nb[k].y - cen[1], (double)nb[k].z - cen[2]};
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) A[3 * r + c] += v[r] * v[c];
+            }
+#pragma unroll
+            for (int j = 0; j < 9; ++j) A[j] = A[j] / 5.0;
+            sym3_eig(A, V);
+            const double w[3] = {A[0], A[4], A[8]};
+            int i1 = 0;
+            if (w[1] > w[i1]) i1 = 1;
+            if (w[2] > w[i1]) i1 = 2;
+            double l2 = -__builtin_inf();
+#pragma unroll
+            for (int i = 0; i < 3; ++i) if (i != i1 && w[i] > l2) l2 = w[i];
+            double u[3] = {V[i1], V[3 + i1], V[6 + i1]};
+            int big = 0;
+            if (fabs(u[1]) > fabs(u[big])) big = 1;
+            if (fabs(u[2]) > fabs(u[big])) big = 2;
+            if (u[big] < 0.0) { u[0] = -u[0]; u[1] = -u[1]; u[2] = -u[2]; }
+#pragma unroll
+            for (int j = 0; j < 3; ++j) { out[j] = (float)cen[j]; out[3 + j] = (float)u[j]; }
+            ok = (key_dist(kk[kEdgeK - 1]) < max_nn_d2) && (w[i1] > (double)line_ratio * l2) ? 1 : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < 6; ++j) L[j] = out[j];
+        valid[base + a] = ok;
+    }
+}
+
+// k_edge_associate: per current edge point, transformToLast (:74-82) and the exact 1-NN among
+// the last frame's edges (brute force from LDS, (distance, index) order); the correspondence
+// record carries the line (centroid in pa, direction in n) and its validity.
+__global__ __launch_bounds__(256) void k_edge_associate(
+    const float4* __restrict__ last, const int64_t* __restrict__ last_off,
+    const int32_t* __restrict__ last_count, const float* __restrict__ line,
+    const uint8_t* __restrict__ line_valid, const float4* __restrict__ curr,
+    const int64_t* __restrict__ curr_off, const int32_t* __restrict__ curr_count,
+    const double* __restrict__ pose_rel, CorrRec* __restrict__ corr, int lds_cap) {
+    extern __shared__ float4 LL[];
+    const int p = blockIdx.y;
+    const int mc = curr_count[p], ml = last_count[p];
+    if ((int)(blockIdx.x * blockDim.x) >= mc) return;                   // uniform
+    const int64_t lo = last_off[p], co = curr_off[p];
+    const bool in_lds = ml <= lds_cap;                                  // uniform
+    if (in_lds)
+        for (int r = threadIdx.x; r < ml; r += blockDim.x) LL[r] = last[lo + r];
+    __syncthreads();
+    const float4* P = in_lds ? LL : last + lo;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= mc) return;
+    const double q[4] = {pose_rel[7 * p], pose_rel[7 * p + 1], pose_rel[7 * p + 2], pose_rel[7 * p + 3]};
+    const double t[3] = {pose_rel[7 * p + 4], pose_rel[7 * p + 5], pose_rel[7 * p + 6]};
+    const float4 pc = curr[co + i];
+    const float4 qs = assoc_query_point(pc, q, t);
+    float best = __builtin_inff();
+    int bi = -1;
+    for (int c = 0; c < ml; ++c) {
+        const float d = l2_simple(qs, P[c]);
+        if (d < best) { best = d; bi = c; }                             // ascending c: ties keep the lower index
+    }
+    CorrRec rec;
+    rec.po[0] = pc.x; rec.po[1] = pc.y; rec.po[2] = pc.z;
+    rec.valid = (bi >= 0 && line_valid[lo + bi]) ? 1.0f : 0.0f;
+    const float* L = line + 6 * (lo + (bi >= 0 ? bi : 0));
+    rec.pa[0] = L[0]; rec.pa[1] = L[1]; rec.pa[2] = L[2]; rec.pad0 = 0.f;
+    rec.n[0] = L[3]; rec.n[1] = L[4]; rec.n[2] = L[5]; rec.pad1 = 0.f;
+    corr[co + i] = rec;
+}
+
+// ------------------------------------------------------------------------------------------
 constexpr int kSolveThreads = 512;
 constexpr int kNE = 28;  // 21 (packed upper JtWJ) + 6 (JtWr) + cost
 
@@ -1070,8 +1223,56 @@ SSF_DEV void accum_corr(const double R[9], const double t[3], const double po[3]
     }
 }
 
+// Point-to-line block (beyond the reference): e = P (R po + t - c), P = I - u u^T; row k is the
+// plane residual with "normal" P row k, so its local Jacobian is [2 (R po x P_k), P_k]; one
+// Huber(0.1) block on s = |e|^2 (rho'(s) = 0.1 / sqrt(s) above s = 0.01).
+SSF_DEV void accum_edge(const double R[9], const double t[3], const double po[3], const double c[3],
+                        const double uu[3], double wgt, double (&ne)[kNE]) {
+    const double a = 0.1, b = 0.1 * 0.1;
+    double g[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g[k] = __builtin_fma(R[3 * k + 2], po[2], __builtin_fma(R[3 * k + 1], po[1], R[3 * k] * po[0]));
+    const double d[3] = {(g[0] + t[0]) - c[0], (g[1] + t[1]) - c[1], (g[2] + t[2]) - c[2]};
+    double r[3], J[3][6], s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        double nk[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) nk[j] = (j == k ? 1.0 : 0.0) - uu[k] * uu[j];
+        r[k] = __builtin_fma(d[2], nk[2], __builtin_fma(d[1], nk[1], d[0] * nk[0]));
+        J[k][0] = 2.0 * __builtin_fma(g[1], nk[2], -g[2] * nk[1]);
+        J[k][1] = 2.0 * __builtin_fma(g[2], nk[0], -g[0] * nk[2]);
+        J[k][2] = 2.0 * __builtin_fma(g[0], nk[1], -g[1] * nk[0]);
+        J[k][3] = nk[0]; J[k][4] = nk[1]; J[k][5] = nk[2];
+        s = __builtin_fma(r[k], r[k], s);
+    }
+    double rho0, rho1;
+    if (s > b) {
+        const double rr = sqrt(s);
+        rho0 = 2.0 * a * rr - b;
+        rho1 = a / rr;
+        if (rho1 < DBL_MIN) rho1 = DBL_MIN;
+    } else {
+        rho0 = s; rho1 = 1.0;
+    }
+    ne[27] = __builtin_fma(0.5 * wgt, rho0, ne[27]);
+    rho1 *= wgt;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        int m = 0;
+#pragma unroll
+        for (int uu2 = 0; uu2 < 6; ++uu2) {
+            const double wj = rho1 * J[k][uu2];
+            ne[21 + uu2] = __builtin_fma(wj, r[k], ne[21 + uu2]);
+#pragma unroll
+            for (int v = uu2; v < 6; ++v) { ne[m] = __builtin_fma(wj, J[k][v], ne[m]); ++m; }
+        }
+    }
+}
+
 SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4], const double t[3],
-                      double (&ne)[kNE], double* lds) {
+                      double (&ne)[kNE], double* lds, const CorrRec* __restrict__ erec = nullptr,
+                      int en = 0) {
 #pragma unroll
     for (int k = 0; k < kNE; ++k) ne[k] = 0.0;
     double R[9];
@@ -1083,6 +1284,13 @@ SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4],
                      nn[3] = {c.n[0], c.n[1], c.n[2]};
         accum_corr(R, t, po, pa, nn, 1.0, ne);
     }
+    for (int i = threadIdx.x; i < en; i += blockDim.x) {          // edge blocks (en = 0: none)
+        const CorrRec c = erec[i];
+        if (c.valid == 0.0f) continue;
+        const double po[3] = {c.po[0], c.po[1], c.po[2]}, pa[3] = {c.pa[0], c.pa[1], c.pa[2]},
+                     uu[3] = {c.n[0], c.n[1], c.n[2]};
+        accum_edge(R, t, po, pa, uu, 1.0, ne);
+    }
     block_sum_rs<kNE>(ne, lds);
 #pragma unroll
     for (int k = 0; k < kNE; ++k) ne[k] *= 2.0;
@@ -1091,7 +1299,7 @@ SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4],
 // LDS-resident correspondences, two per step (i, i + T; a missing second one is a clamped
 // duplicate weighted 0): both loads are in flight before either is used.
 SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double t[3],
-                      double (&ne)[kNE], double* lds) {
+                      double (&ne)[kNE], double* lds, int nve = 0) {
 #pragma unroll
     for (int k = 0; k < kNE; ++k) ne[k] = 0.0;
     double R[9];
@@ -1112,6 +1320,11 @@ SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double 
                          nn[3] = {f[h][6], f[h][7], f[h][8]};
             accum_corr(R, t, po, pa, nn, h ? w2 : 1.0, ne);
         }
+    }
+    for (int i = nv + threadIdx.x; i < nv + nve; i += T) {        // edge blocks after the planes
+        const double po[3] = {C.po[0][i], C.po[1][i], C.po[2][i]}, pa[3] = {C.pa[0][i], C.pa[1][i], C.pa[2][i]},
+                     uu[3] = {C.n[0][i], C.n[1][i], C.n[2][i]};
+        accum_edge(R, t, po, pa, uu, 1.0, ne);
     }
     block_sum_rs<kNE>(ne, lds);
 #pragma unroll
@@ -1204,6 +1417,9 @@ SSF_DEV void write_log(double* log, int max_iter, int p, int idx, const double q
     r[7] = cost; r[8] = status; r[9] = radius;
 }
 
+// kEdges: point-to-line blocks (ecorr at ecurr_off / ecurr_count) join every evaluation; they
+// are compacted into the same LDS arrays after the planes.
+template <bool kEdges>
 __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restrict__ corr,
                                                          const int64_t* __restrict__ curr_off,
                                                          const int32_t* __restrict__ curr_count,
@@ -1213,7 +1429,11 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
                                                          double* __restrict__ pose_abs,
                                                          double* __restrict__ log,
                                                          int32_t* __restrict__ nlog_out,
-                                                         int32_t* __restrict__ ncorr_out) {
+                                                         int32_t* __restrict__ ncorr_out,
+                                                         const CorrRec* __restrict__ ecorr,
+                                                         const int64_t* __restrict__ ecurr_off,
+                                                         const int32_t* __restrict__ ecurr_count,
+                                                         int32_t* __restrict__ ncorr_edge_out) {
     __shared__ SolveShared S;
     __shared__ double red[(kSolveThreads / 64) * kNE];
     __shared__ CorrLds C;
@@ -1221,6 +1441,8 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
     const int p = blockIdx.x, tid = threadIdx.x;
     const int n = curr_count[p];
     const CorrRec* rec = corr + curr_off[p];
+    const int en = kEdges ? ecurr_count[p] : 0;
+    const CorrRec* erec = kEdges ? ecorr + ecurr_off[p] : nullptr;
 #ifdef SSF_SOLVE_STAMPS
     // diagnostic build only: s_memtime phase stamps into the last log row (cost/status/radius)
     const unsigned long long st0 = __builtin_amdgcn_s_memtime();
@@ -1241,36 +1463,43 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
         constexpr int kPre = 2;
         const int lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
         const int T = blockDim.x;
-        int nv = 0;                                                     // uniform
-        for (int i0 = 0; i0 < n; i0 += kPre * T) {
-            CorrRec c[kPre];
+        // records [0, cnt) of src appended at LDS position `start`; returns the valid count
+        auto compact = [&](const CorrRec* __restrict__ src, int cnt, int start) {
+            int nv = 0;                                                 // uniform
+            for (int i0 = 0; i0 < cnt; i0 += kPre * T) {
+                CorrRec c[kPre];
 #pragma unroll
-            for (int k = 0; k < kPre; ++k) c[k] = rec[min(i0 + k * T + tid, n - 1)];   // clamped
+                for (int k = 0; k < kPre; ++k) c[k] = src[min(i0 + k * T + tid, cnt - 1)];   // clamped
 #pragma unroll
-            for (int k = 0; k < kPre; ++k) {
-                const bool v = i0 + k * T + tid < n && c[k].valid != 0.0f;
-                const uint64_t m = __ballot(v);
-                if (lane == 0) wtot[w] = __popcll(m);
-                __syncthreads();
-                int before = nv, tot = 0;
-                for (int j = 0; j < nw; ++j) { const int x = wtot[j]; if (j < w) before += x; tot += x; }
-                const int pos = before + __popcll(m & lanemask_lt());
-                if (v && pos < kSolveLdsCap) {
+                for (int k = 0; k < kPre; ++k) {
+                    const bool v = i0 + k * T + tid < cnt && c[k].valid != 0.0f;
+                    const uint64_t m = __ballot(v);
+                    if (lane == 0) wtot[w] = __popcll(m);
+                    __syncthreads();
+                    int before = start + nv, tot = 0;
+                    for (int j = 0; j < nw; ++j) { const int x = wtot[j]; if (j < w) before += x; tot += x; }
+                    const int pos = before + __popcll(m & lanemask_lt());
+                    if (v && pos < kSolveLdsCap) {
 #pragma unroll
-                    for (int d = 0; d < 3; ++d) { C.po[d][pos] = c[k].po[d]; C.pa[d][pos] = c[k].pa[d]; C.n[d][pos] = c[k].n[d]; }
+                        for (int d = 0; d < 3; ++d) { C.po[d][pos] = c[k].po[d]; C.pa[d][pos] = c[k].pa[d]; C.n[d][pos] = c[k].n[d]; }
+                    }
+                    nv += tot;
+                    __syncthreads();                                    // wtot is rewritten next trip
                 }
-                nv += tot;
-                __syncthreads();                                        // wtot is rewritten next trip
             }
-        }
-        const bool in_lds = nv <= kSolveLdsCap;                        // uniform
+            return nv;
+        };
+        const int nv = compact(rec, n, 0);
+        const int nve = kEdges ? compact(erec, en, nv) : 0;
+        const bool in_lds = nv + nve <= kSolveLdsCap;                  // uniform
 #ifdef SSF_SOLVE_STAMPS
         st1 = __builtin_amdgcn_s_memtime();
 #endif
         if (tid == 0 && ncorr_out) ncorr_out[p] = nv;
+        if (kEdges && tid == 0 && ncorr_edge_out) ncorr_edge_out[p] = nve;
         auto eval_at = [&](const double* qq, const double* tt, double (&ne_)[kNE]) {
-            if (in_lds) evaluate(C, nv, qq, tt, ne_, red);
-            else evaluate(rec, n, qq, tt, ne_, red);
+            if (in_lds) evaluate(C, nv, qq, tt, ne_, red, nve);
+            else evaluate(rec, n, qq, tt, ne_, red, erec, en);
         };
         double ne[kNE];
         double q[4], t[3];
@@ -1408,8 +1637,9 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
                 if (S.done) break;
             }
         }
-    } else if (tid == 0 && ncorr_out) {
-        ncorr_out[p] = -1;
+    } else if (tid == 0) {
+        if (ncorr_out) ncorr_out[p] = -1;
+        if (kEdges && ncorr_edge_out) ncorr_edge_out[p] = -1;
     }
     if (tid == 0) {
 #ifdef SSF_SOLVE_STAMPS
@@ -1478,7 +1708,7 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
                            const float4* last_sorted, const int32_t* last_sidx, const float4* curr,
                            const int64_t* curr_off, const int32_t* curr_count, int64_t max_m,
                            CorrRec* corr, double* pose_rel, double* pose_abs, double* log,
-                           int32_t* nlog, int32_t* ncorr, int32_t* nn) {
+                           int32_t* nlog, int32_t* ncorr, int32_t* nn, const EdgeReg* edge) {
     if (n_pairs <= 0) return hipSuccess;
     if (max_m > 0) {
         const int bx = (int)((max_m + 255) / 256);
@@ -1503,10 +1733,36 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
                                pose_rel, corr, nn);
         }
     }
+    if (edge && edge->max_m > 0) {
+        const int ex = (int)((edge->max_m + 255) / 256);
+        const int cap = (int)std::min<int64_t>(edge->max_m, kEdgeLdsMax);
+        kmark(s, "k_edge_associate");
+        hipLaunchKernelGGL(k_edge_associate, dim3(ex, n_pairs), dim3(256), (size_t)cap * sizeof(float4),
+                           s, edge->last, edge->last_off, edge->last_count, edge->line,
+                           edge->line_valid, edge->curr, edge->curr_off, edge->curr_count, pose_rel,
+                           edge->corr, cap);
+    }
     kmark(s, "k_solve");
-    hipLaunchKernelGGL(k_solve, dim3(n_pairs), dim3(kSolveThreads), 0, s, corr, curr_off,
-                       curr_count, last_count, cfg.solver, cfg.max_iter, pose_rel, pose_abs, log,
-                       nlog, ncorr);
+    if (edge)
+        hipLaunchKernelGGL(k_solve<true>, dim3(n_pairs), dim3(kSolveThreads), 0, s, corr, curr_off,
+                           curr_count, last_count, cfg.solver, cfg.max_iter, pose_rel, pose_abs, log,
+                           nlog, ncorr, edge->corr, edge->curr_off, edge->curr_count, edge->ncorr);
+    else
+        hipLaunchKernelGGL(k_solve<false>, dim3(n_pairs), dim3(kSolveThreads), 0, s, corr, curr_off,
+                           curr_count, last_count, cfg.solver, cfg.max_iter, pose_rel, pose_abs, log,
+                           nlog, ncorr, (const CorrRec*)nullptr, (const int64_t*)nullptr,
+                           (const int32_t*)nullptr, (int32_t*)nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_edge_table(hipStream_t s, const ssf_edge_config& ec, int n_frames,
+                             const float4* edges, const int64_t* frame_off, const int32_t* count,
+                             int64_t max_m, float* line, uint8_t* valid) {
+    if (n_frames <= 0 || max_m <= 0) return hipSuccess;
+    const int cap = (int)std::min<int64_t>(max_m, kEdgeLdsMax);
+    kmark(s, "k_edge_table");
+    hipLaunchKernelGGL(k_edge_table, dim3(n_frames), dim3(kEdgeThreads), (size_t)cap * sizeof(float4),
+                       s, edges, frame_off, count, ec.max_nn_d2, ec.line_ratio, line, valid, cap);
     return hipGetLastError();
 }
 

@@ -46,26 +46,57 @@ struct alignas(16) CorrRec {
 };
 
 // ---- launchers (features.hip) ----
+// Edge selection of launch_extract_planes (beyond the reference; nullptr = planes only):
+// selection indices / per-row counts in ctx scratch, the compacted edge cloud (float4 x, y, z,
+// intensity at the frame offsets) and per-frame counts out.
+struct EdgeSel {
+    float min_curv;
+    int span;
+    int32_t* sel;
+    int32_t* sel_cnt;
+    float4* out;
+    int32_t* count;
+};
 hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_frames,
                                  const float* pts, int stride, const int64_t* frame_off,
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
                                  int32_t* ring_off, float* ring_xyz, float4* ring_xyzi,
                                  float* curv, int32_t* sel, int32_t* sel_dump, int32_t* sel_cnt,
                                  float4* plane,
-                                 int32_t* plane_count);
+                                 int32_t* plane_count, const EdgeSel* edge = nullptr);
 
 // ---- launchers (registration.hip) ----
 hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames,
                               const float4* plane, const int64_t* frame_off, const int32_t* count,
                               int64_t max_m, float* normal, uint8_t* valid, float4* sorted_xyzi,
                               int32_t* sorted_idx);
+// Point-to-line blocks of launch_register (beyond the reference; nullptr = planes only): the
+// edge clouds, the last frames' line table (6 floats per edge: centroid, direction) and the
+// correspondence scratch / per-pair counts.
+struct EdgeReg {
+    const float4* last;
+    const int64_t* last_off;
+    const int32_t* last_count;
+    const float* line;
+    const uint8_t* line_valid;
+    const float4* curr;
+    const int64_t* curr_off;
+    const int32_t* curr_count;
+    int64_t max_m;
+    CorrRec* corr;
+    int32_t* ncorr;
+};
 hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, const float4* last,
                            const int64_t* last_off, const int32_t* last_count,
                            const float* last_normal, const uint8_t* last_valid,
                            const float4* last_sorted, const int32_t* last_sidx, const float4* curr,
                            const int64_t* curr_off, const int32_t* curr_count, int64_t max_m,
                            CorrRec* corr, double* pose_rel, double* pose_abs, double* log,
-                           int32_t* nlog, int32_t* ncorr, int32_t* nn);
+                           int32_t* nlog, int32_t* ncorr, int32_t* nn,
+                           const EdgeReg* edge = nullptr);
+hipError_t launch_edge_table(hipStream_t s, const ssf_edge_config& ec, int n_frames,
+                             const float4* edges, const int64_t* frame_off, const int32_t* count,
+                             int64_t max_m, float* line, uint8_t* valid);
 hipError_t launch_accumulate(hipStream_t s, int n, const double* rel, const double* start,
                              double* abs_out);
 

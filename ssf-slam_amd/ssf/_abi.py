@@ -31,6 +31,8 @@ EXPORTS = [
     "ssf_voxel_grid_batch", "ssf_icp_params_default", "ssf_icp_batch",
     "ssf_extract_planes_batch_masked", "ssf_register_pair", "ssf_profile_enable",
     "ssf_profile_read", "ssf_set_mask_split", "ssf_mask_pose_batch_f64",
+    "ssf_edge_config_default", "ssf_set_edge_config", "ssf_extract_features_batch",
+    "ssf_edge_table_batch", "ssf_register_batch_edges",
 ]
 # Every symbol include/ssf_pointnet2.h declares (TFlow point-set operators).
 PN2_EXPORTS = [
@@ -73,6 +75,12 @@ class Config(C.Structure):
     _fields_ = [("n_rows", C.c_int32), ("plane_min", C.c_float), ("plane_span", C.c_int32),
                 ("row_start", C.c_int32), ("row_end", C.c_int32), ("plane_max", C.c_float),
                 ("solver", C.c_int32), ("max_iter", C.c_int32)]
+
+
+class EdgeConfig(C.Structure):
+    """ssf_edge_config (beyond the reference: edge features + point-to-line residuals)."""
+    _fields_ = [("edge_min", C.c_float), ("edge_span", C.c_int32), ("line_ratio", C.c_float),
+                ("max_nn_d2", C.c_float)]
 
 
 _lib = None
@@ -127,6 +135,17 @@ def lib():
     L.ssf_mask_pose_batch.restype = i32
     L.ssf_mask_pose_batch_f64.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, i32, vp, vp]
     L.ssf_mask_pose_batch_f64.restype = i32
+    L.ssf_edge_config_default.argtypes = [i32, C.POINTER(EdgeConfig)]
+    L.ssf_edge_config_default.restype = i32
+    L.ssf_set_edge_config.argtypes = [vp, C.POINTER(EdgeConfig)]
+    L.ssf_set_edge_config.restype = i32
+    L.ssf_extract_features_batch.argtypes = [vp, vp, i32, vp, i32, vp, i64, i64, vp, vp, vp, vp, vp]
+    L.ssf_extract_features_batch.restype = i32
+    L.ssf_edge_table_batch.argtypes = [vp, vp, i32, vp, vp, vp, i64, vp, vp]
+    L.ssf_edge_table_batch.restype = i32
+    L.ssf_register_batch_edges.argtypes = ([vp, vp, i32] + [vp] * 10 + [i64, i64] + [vp] * 8 +
+                                           [i64, i64] + [vp] * 6)
+    L.ssf_register_batch_edges.restype = i32
     L.ssf_accumulate_sequence.argtypes = [vp, vp, i32, vp, vp, vp]
     L.ssf_accumulate_sequence.restype = i32
     L.ssf_voxel_grid_batch.argtypes = [vp, vp, i32, vp, vp, vp, C.c_float, vp, vp]

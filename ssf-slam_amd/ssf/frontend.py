@@ -113,6 +113,19 @@ class Frontend:
         """Work-groups per frame of the GMM fit (0 = automatic, 1..8 fixed)."""
         self._check(_abi.lib().ssf_set_mask_split(self._h, int(parts_per_frame)), "ssf_set_mask_split")
 
+    def edge_config(self, **kw):
+        """Edge-feature parameters (beyond the reference; ssf_set_edge_config): edge_min,
+        edge_span, line_ratio, max_nn_d2.  No arguments: the current defaults."""
+        ec = _abi.EdgeConfig()
+        self._check(_abi.lib().ssf_edge_config_default(self.n_rows, C.byref(ec)), "ssf_edge_config_default")
+        for k, v in kw.items():
+            if not hasattr(ec, k):
+                raise ValueError(f"unknown edge parameter {k!r}")
+            setattr(ec, k, v)
+        self._check(_abi.lib().ssf_set_edge_config(self._h, C.byref(ec)), "ssf_set_edge_config")
+        self._edge_span = int(ec.edge_span)
+        return {k: getattr(ec, k) for k, _ in ec._fields_}
+
     def seed(self, seed: int):
         """np.random.seed(seed) for the GMM's k-means++ RandomState."""
         self._check(_abi.lib().ssf_rng_seed(self._h, seed & 0xFFFFFFFF), "ssf_rng_seed")
@@ -161,6 +174,44 @@ class Frontend:
         if debug:
             return pb, ring, roff.view(max(F, 1), self.n_rows + 1)[:F], curv
         return pb
+
+    def extract_features_batch(self, pts, off, h_off, max_points=None, keep=None):
+        """extract_planes_batch plus the edge cloud (beyond the reference: edge features,
+        ssf_extract_features_batch) -> (planes PlaneBatch, edges PlaneBatch)."""
+        pts = self._dev(pts, torch.float32)
+        F = h_off.numel() - 1
+        total = int(h_off[-1])
+        sizes = (h_off[1:] - h_off[:-1])
+        mx = int(sizes.max()) if max_points is None and F > 0 else int(max_points or 0)
+        plane = torch.empty((max(total, 1), 4), dtype=torch.float32, device=self.device)
+        count = torch.empty(max(F, 1), dtype=torch.int32, device=self.device)
+        edge = torch.empty((max(total, 1), 4), dtype=torch.float32, device=self.device)
+        ecount = torch.empty(max(F, 1), dtype=torch.int32, device=self.device)
+        if keep is not None:
+            keep = self._dev(keep, torch.uint8)
+            if keep.numel() != total:
+                raise ValueError(f"keep has {keep.numel()} entries for {total} points")
+        rc = _abi.lib().ssf_extract_features_batch(
+            self._h, _stream(self.device), F, _ptr(pts), pts.shape[1], _ptr(off), total, mx,
+            _ptr(keep), _ptr(plane), _ptr(count), _ptr(edge), _ptr(ecount))
+        self._check(rc, "ssf_extract_features_batch")
+        span = getattr(self, "_edge_span", None) or (10 if self.n_rows == 64 else 3)
+        pb = PlaneBatch(plane, count[:F], off, h_off,
+                        min(mx, mx // max(1, self.cfg.plane_span) + self.n_rows + 1))
+        eb = PlaneBatch(edge, ecount[:F], off, h_off, min(mx, mx // max(1, span) + self.n_rows + 1))
+        return pb, eb
+
+    def edge_table(self, eb: PlaneBatch):
+        """Line table of frames that will be LAST frames (beyond the reference):
+        -> (line [total, 6] f32: centroid, direction; valid [total] u8)."""
+        total = eb.xyzi.shape[0]
+        line = torch.empty((total, 6), dtype=torch.float32, device=self.device)
+        valid = torch.empty(total, dtype=torch.uint8, device=self.device)
+        rc = _abi.lib().ssf_edge_table_batch(self._h, _stream(self.device), eb.count.numel(),
+                                             _ptr(eb.xyzi), _ptr(eb.off), _ptr(eb.count),
+                                             eb.max_points, _ptr(line), _ptr(valid))
+        self._check(rc, "ssf_edge_table_batch")
+        return line, valid
 
     def extract_planes(self, pts, xyz_offset: int = 0):
         """Single frame, PointCloud2-style points [n, k] f32 (point_step = 4k bytes, x/y/z at
@@ -219,9 +270,11 @@ class Frontend:
         return list(qo), list(to), out, int(log.n_corr)
 
     def register(self, last: PlaneBatch, last_table, curr: PlaneBatch, pose_rel, pose_abs=None,
-                 want_log=False, want_nn=False, want_nlog=False):
+                 want_log=False, want_nn=False, want_nlog=False, edges=None):
         """frameRegistration for P pairs (last[p], curr[p]).  pose_rel [P,7] f64 (q xyzw, t) is the
-        warm start in and the solution out; pose_abs [P,7] is accumulated in place if given."""
+        warm start in and the solution out; pose_abs [P,7] is accumulated in place if given.
+        edges = (last edges PlaneBatch, edge_table(last edges), curr edges PlaneBatch) adds the
+        point-to-line blocks (beyond the reference, ssf_register_batch_edges)."""
         P = curr.count.numel()
         pose_rel = self._dev(pose_rel, torch.float64)
         if pose_abs is not None:
@@ -236,14 +289,30 @@ class Frontend:
         if want_nn:
             nn = torch.full((curr.xyzi.shape[0],), -1, dtype=torch.int32, device=self.device)
         mx = max(last.max_points, curr.max_points)
-        rc = _abi.lib().ssf_register_batch(
+        if edges is None:
+            rc = _abi.lib().ssf_register_batch(
+                self._h, _stream(self.device), P, _ptr(last.xyzi), _ptr(last.off), _ptr(last.count),
+                _ptr(normal), _ptr(valid), _ptr(sx), _ptr(si), _ptr(curr.xyzi), _ptr(curr.off),
+                _ptr(curr.count),
+                int(curr.h_off[-1]), mx, _ptr(pose_rel), _ptr(pose_abs), _ptr(log), _ptr(nlog),
+                _ptr(ncorr), _ptr(nn))
+            self._check(rc, "ssf_register_batch")
+            return dict(pose_rel=pose_rel, pose_abs=pose_abs, ncorr=ncorr, log=log, nlog=nlog, nn=nn)
+        last_e, (line, lvalid), curr_e = edges
+        if want_nn:
+            raise ValueError("want_nn is not available with edges")
+        ncorr_e = torch.empty(P, dtype=torch.int32, device=self.device)
+        mxe = max(last_e.max_points, curr_e.max_points)
+        rc = _abi.lib().ssf_register_batch_edges(
             self._h, _stream(self.device), P, _ptr(last.xyzi), _ptr(last.off), _ptr(last.count),
             _ptr(normal), _ptr(valid), _ptr(sx), _ptr(si), _ptr(curr.xyzi), _ptr(curr.off),
-            _ptr(curr.count),
-            int(curr.h_off[-1]), mx, _ptr(pose_rel), _ptr(pose_abs), _ptr(log), _ptr(nlog),
-            _ptr(ncorr), _ptr(nn))
-        self._check(rc, "ssf_register_batch")
-        return dict(pose_rel=pose_rel, pose_abs=pose_abs, ncorr=ncorr, log=log, nlog=nlog, nn=nn)
+            _ptr(curr.count), int(curr.h_off[-1]), mx,
+            _ptr(last_e.xyzi), _ptr(last_e.off), _ptr(last_e.count), _ptr(line), _ptr(lvalid),
+            _ptr(curr_e.xyzi), _ptr(curr_e.off), _ptr(curr_e.count), int(curr_e.h_off[-1]), mxe,
+            _ptr(pose_rel), _ptr(pose_abs), _ptr(log), _ptr(nlog), _ptr(ncorr), _ptr(ncorr_e))
+        self._check(rc, "ssf_register_batch_edges")
+        return dict(pose_rel=pose_rel, pose_abs=pose_abs, ncorr=ncorr, ncorr_edge=ncorr_e, log=log,
+                    nlog=nlog, nn=None)
 
     # ------------------------------------------------------------------ PointCloudOdometry*.py
     def mask_pose(self, pts, flow, off, h_off, mode="gmm", mask_in=None, draws=None,

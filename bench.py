@@ -81,6 +81,9 @@ def parse(argv=None):
     ap.add_argument("--mask-before-features", action="store_true",
                     help="BASELINE configs[2]: features and registration on the GMM background "
                          "points only (beyond the reference, whose frameFeature sees every point)")
+    ap.add_argument("--edges", action="store_true",
+                    help="beyond the reference (off by default): edge features + point-to-line "
+                         "blocks in the registration (north_star wording; the reference is planar)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="CPU baseline: seconds per leg (single thread, all cores, sklearn)")
@@ -245,6 +248,7 @@ class Pipeline:
         self.pose_rel = ssf.identity_poses(B, dev)
         self.pose_abs = ssf.identity_poses(B, dev)
         self.last = self.last_table = None
+        self.last_e = self.last_etable = None
         self.records = []           # per step: (pose snapshot on s_reg, mask out)
         self.gathered = []
         self.ev = {k: [] for k in ("mask", "feat", "table", "reg")}
@@ -270,31 +274,40 @@ class Pipeline:
                 s_feat.wait_event(m1)
                 bg.record_stream(s_feat)
             keep = bg
+        eb = etable = None
         with torch.cuda.stream(s_feat):
             es = [mk() for _ in range(3)]
             es[0].record(s_feat)
-            pb = self.fe_feat.extract_planes_batch(pos, off, h_off, max_points=self.N, keep=keep)
+            if a.edges:                     # beyond the reference: edge features as well
+                pb, eb = self.fe_feat.extract_features_batch(pos, off, h_off, max_points=self.N, keep=keep)
+            else:
+                pb = self.fe_feat.extract_planes_batch(pos, off, h_off, max_points=self.N, keep=keep)
             es[1].record(s_feat)
             table = self.fe_feat.plane_table(pb)
+            if a.edges:
+                etable = self.fe_feat.edge_table(eb)
             es[2].record(s_feat)
         if s_reg is not s_feat:
             s_reg.wait_event(es[2])
             # the plane batch and its table are read on s_reg in this step and the next: keep
             # the caching allocator from handing their blocks to s_feat until s_reg is done
-            for t in (pb.xyzi, pb.count, *[x for x in table if isinstance(x, torch.Tensor)]):
+            extra = (eb.xyzi, eb.count, *etable) if a.edges else ()
+            for t in (pb.xyzi, pb.count, *[x for x in table if isinstance(x, torch.Tensor)], *extra):
                 t.record_stream(s_reg)
         stats = None
         with torch.cuda.stream(s_reg):
             r0, r1 = mk(), mk()
             r0.record(s_reg)        # after the wait: registration time excludes queueing on s_feat
             if self.last is not None:
+                edges = (self.last_e, self.last_etable, eb) if a.edges else None
                 res = self.fe_reg.register(self.last, self.last_table, pb, self.pose_rel, self.pose_abs,
-                                           want_nlog=want_stats)
+                                           want_nlog=want_stats, edges=edges)
                 if want_stats:
                     stats = (res["ncorr"], res["nlog"])
             r1.record(s_reg)
             snap = self.pose_abs.clone() if self.world > 1 else None   # step-k poses, on s_reg
         self.last, self.last_table = pb, table
+        self.last_e, self.last_etable = eb, etable
         if self.world > 1:   # the one exchange step: per-frame 6-DoF poses of every rank (RCCL)
             cur = torch.cuda.current_stream(self.dev)
             cur.wait_stream(s_mask)
@@ -318,6 +331,7 @@ def kernel_pass(pipe, batches, off, h_off, ks, rows, row_start, row_end):
     s.wait_stream(torch.cuda.current_stream(pipe.dev))
     ctxs = pipe.contexts()
     pipe.last = pipe.last_table = None
+    pipe.last_e = pipe.last_etable = None
     for c in ctxs:
         c.kernel_times()          # drop anything recorded earlier
         c.profile(True)
@@ -512,9 +526,11 @@ def main():
         "config": {"workload": f"{cfg_name}: {B} sequences in flight per GPU x {args.rows}-beam "
                                f"{N}-pt scans; mask(GMM+Kabsch) + "
                                f"{'masked ' if args.mask_before_features else ''}features + plane "
-                               f"table + {args.solver} x{iters}",
+                               f"table + {'edge table + point-to-line + ' if args.edges else ''}"
+                               f"{args.solver} x{iters}",
                    "sequences_per_gpu": B, "points_per_frame": N, "solver": args.solver,
                    "iters": iters, "mask_before_features": bool(args.mask_before_features),
+                   "edges": bool(args.edges),
                    "parallelism": f"sequence-sharded x{world}",
                    "world_size_initialised": (dist.get_world_size() if world > 1 else 1),
                    "backend": backend or "none",
@@ -524,7 +540,7 @@ def main():
         "mask_passes_per_frame": passes, "gather_check": gather_ok,
         "data_gen_s": round(t_data, 2),
     }
-    traffic = _load_profile(TRAFFIC_JSON, B, N, args.mask_before_features)
+    traffic = None if args.edges else _load_profile(TRAFFIC_JSON, B, N, args.mask_before_features)
     if traffic:
         for k, v in kernels.items():
             t = traffic["kernels"].get(k, {}).get("traffic_bytes_per_launch")
@@ -536,7 +552,7 @@ def main():
                             "frac": mk["frac"], "traffic": mk.get("traffic"),
                             "kernel": "k_mask_pose",
                             "duration": "kernel-only (one-stream kernel pass, HIP events)"}
-        f64 = _load_profile(F64_JSON, B, N, args.mask_before_features)
+        f64 = None if args.edges else _load_profile(F64_JSON, B, N, args.mask_before_features)
         flops = f64 and f64.get("f64_flops_per_launch")
         if flops:
             tf = flops / (mk["ms"] * 1e-3) / 1e12

@@ -1003,7 +1003,7 @@ __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
 // exact 5-NN (packed (distance, index) keys, brute force over the frame's few hundred edges),
 // centroid + covariance in double in rank order, cyclic Jacobi, line test.
 constexpr int kEdgeK = 5;
-constexpr int kEdgeThreads = 512;
+constexpr int kEdgeThreads = 1024;
 constexpr int kEdgeLdsMax = 8192;          // edges per frame staged in LDS (128 KiB)
 
 SSF_DEV void sym3_eig(double A[9], double V[9]) {       // = orc_sym3_eig, operation for operation
@@ -1066,7 +1066,12 @@ __global__ __launch_bounds__(kEdgeThreads) void k_edge_table(
             double kk[kEdgeK];
 #pragma unroll
             for (int k = 0; k < kEdgeK; ++k) kk[k] = knn_key(__builtin_inff(), 0x7fffffff);
-            for (int c = 0; c < m; ++c) key_insert<kEdgeK>(kk, knn_key(l2_simple(q, P[c]), c));
+            for (int c = 0; c < m; ++c) {
+                // most candidates of a brute-force scan are far: the insertion runs only when
+                // some lane's candidate beats its 5th key (keys are exact, so order is kept)
+                const double key = knn_key(l2_simple(q, P[c]), c);
+                if (key < kk[kEdgeK - 1]) key_insert<kEdgeK>(kk, key);
+            }
             double cen[3] = {0.0, 0.0, 0.0};
             float4 nb[kEdgeK];
 #pragma unroll
@@ -1110,29 +1115,31 @@ __global__ __launch_bounds__(kEdgeThreads) void k_edge_table(
     }
 }
 
-// k_edge_associate: per current edge point, transformToLast (:74-82) and the exact 1-NN among
-// the last frame's edges (brute force from LDS, (distance, index) order); the correspondence
-// record carries the line (centroid in pa, direction in n) and its validity.
-__global__ __launch_bounds__(256) void k_edge_associate(
+// k_edge_associate: one work-group per pair.  Per current edge point, transformToLast (:74-82)
+// and the exact 1-NN among the last frame's edges (brute force from LDS, (distance, index)
+// order); the correspondence record carries the line (centroid in pa, direction in n) and its
+// validity.  (A grid sized by the host's edge bound would launch ~50 mostly empty work-groups
+// per pair, each holding the LDS staging size.)
+constexpr int kEdgeAssocThreads = 1024;
+__global__ __launch_bounds__(kEdgeAssocThreads) void k_edge_associate(
     const float4* __restrict__ last, const int64_t* __restrict__ last_off,
     const int32_t* __restrict__ last_count, const float* __restrict__ line,
     const uint8_t* __restrict__ line_valid, const float4* __restrict__ curr,
     const int64_t* __restrict__ curr_off, const int32_t* __restrict__ curr_count,
     const double* __restrict__ pose_rel, CorrRec* __restrict__ corr, int lds_cap) {
     extern __shared__ float4 LL[];
-    const int p = blockIdx.y;
+    const int p = blockIdx.x;
     const int mc = curr_count[p], ml = last_count[p];
-    if ((int)(blockIdx.x * blockDim.x) >= mc) return;                   // uniform
+    if (mc <= 0) return;                                                // uniform
     const int64_t lo = last_off[p], co = curr_off[p];
     const bool in_lds = ml <= lds_cap;                                  // uniform
     if (in_lds)
         for (int r = threadIdx.x; r < ml; r += blockDim.x) LL[r] = last[lo + r];
     __syncthreads();
     const float4* P = in_lds ? LL : last + lo;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= mc) return;
     const double q[4] = {pose_rel[7 * p], pose_rel[7 * p + 1], pose_rel[7 * p + 2], pose_rel[7 * p + 3]};
     const double t[3] = {pose_rel[7 * p + 4], pose_rel[7 * p + 5], pose_rel[7 * p + 6]};
+    for (int i = threadIdx.x; i < mc; i += blockDim.x) {
     const float4 pc = curr[co + i];
     const float4 qs = assoc_query_point(pc, q, t);
     float best = __builtin_inff();
@@ -1148,6 +1155,7 @@ __global__ __launch_bounds__(256) void k_edge_associate(
     rec.pa[0] = L[0]; rec.pa[1] = L[1]; rec.pa[2] = L[2]; rec.pad0 = 0.f;
     rec.n[0] = L[3]; rec.n[1] = L[4]; rec.n[2] = L[5]; rec.pad1 = 0.f;
     corr[co + i] = rec;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1734,10 +1742,9 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
         }
     }
     if (edge && edge->max_m > 0) {
-        const int ex = (int)((edge->max_m + 255) / 256);
         const int cap = (int)std::min<int64_t>(edge->max_m, kEdgeLdsMax);
         kmark(s, "k_edge_associate");
-        hipLaunchKernelGGL(k_edge_associate, dim3(ex, n_pairs), dim3(256), (size_t)cap * sizeof(float4),
+        hipLaunchKernelGGL(k_edge_associate, dim3(n_pairs), dim3(kEdgeAssocThreads), (size_t)cap * sizeof(float4),
                            s, edge->last, edge->last_off, edge->last_count, edge->line,
                            edge->line_valid, edge->curr, edge->curr_off, edge->curr_count, pose_rel,
                            edge->corr, cap);

@@ -386,6 +386,8 @@ def rooflines(times, acc, B, N):
         "k_plane_table_sorted": 49.0 * acc["plane"],
         "k_associate_lds": 64.0 * acc["plane_reg"],
         "k_associate_lds_soa": 64.0 * acc["plane_reg"],
+        "k_associate_strips": 64.0 * acc["plane_reg"],
+        "k_associate_strips_soa": 64.0 * acc["plane_reg"],
         "k_associate_sorted": 64.0 * acc["plane_reg"],
         "k_solve": 36.0 * acc["corr_evals"],                        # §8(d): 36 B x C per evaluation
     }

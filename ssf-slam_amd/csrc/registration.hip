@@ -815,13 +815,15 @@ SSF_DEV bool assoc_better(const V& v, int c, float d, float best, int bc) {
 }
 
 template <class V>
-SSF_DEV void assoc_walk(const V& v, int ml, const float4& qs, float lim, float& best, int& bc) {
+SSF_DEV void assoc_walk(const V& v, int ml, const float4& qs, float lim, float& best, int& bc,
+                        int* visited = nullptr) {
     int lo_i = 0, hi_i = ml;                                            // first x >= qs.x
     while (lo_i < hi_i) {
         const int mid = (lo_i + hi_i) >> 1;
         if (v.pt(mid).x < qs.x) lo_i = mid + 1; else hi_i = mid;
     }
-    for (int c = lo_i; c < ml; ++c) {
+    int c = lo_i;
+    for (; c < ml; ++c) {
         const float4 pl = v.pt(c);
         const float dx = qs.x - pl.x;
         const float dx2 = dx * dx;
@@ -829,14 +831,16 @@ SSF_DEV void assoc_walk(const V& v, int ml, const float4& qs, float lim, float& 
         const float d = l2_simple(qs, pl);
         if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
     }
-    for (int c = lo_i - 1; c >= 0; --c) {
-        const float4 pl = v.pt(c);
+    int c2 = lo_i - 1;
+    for (; c2 >= 0; --c2) {
+        const float4 pl = v.pt(c2);
         const float dx = qs.x - pl.x;
         const float dx2 = dx * dx;
         if (dx2 > best || dx2 >= lim) break;
         const float d = l2_simple(qs, pl);
-        if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
+        if (assoc_better(v, c2, d, best, bc)) { best = d; bc = c2; }
     }
+    if (visited) *visited = (c - lo_i) + (lo_i - 1 - c2);
 }
 
 SSF_DEV void assoc_finish(const float4* __restrict__ L, int64_t lo, const float* __restrict__ last_normal,
@@ -869,9 +873,19 @@ SSF_DEV void assoc_phases(const V& v, int ml, int mc, int i0, int64_t lo, int64_
         const float4 qs = assoc_query_point(pc, q, t);
         float best = __builtin_inff();
         int bc = -1;
+#ifdef SSF_ASSOC_COUNT
+        // diagnostic build only: candidates visited by the phase-1 walk into nn_out
+        // (negative: the query went on to phase 2)
+        int vis = 0;
+        assoc_walk(v, ml, qs, kAssocBand2, best, bc, &vis);
+#else
         assoc_walk(v, ml, qs, kAssocBand2, best, bc);
+#endif
         if (best < kAssocBand2) assoc_finish(L, lo, last_normal, last_valid, pc, v.id(bc), corr, nn_out, co + i);
         else queue[atomicAdd(qlen, 1)] = i;                             // <= kAssocQ entries
+#ifdef SSF_ASSOC_COUNT
+        if (nn_out) nn_out[co + i] = best < kAssocBand2 ? vis : -1 - vis;
+#endif
     }
     __syncthreads();
 #ifdef SSF_ASSOC_STAMPS
@@ -916,7 +930,11 @@ SSF_DEV void assoc_phases(const V& v, int ml, int mc, int i0, int64_t lo, int64_
                 const int cu = red_i[u * 64 + lane];
                 if (cu >= 0 && assoc_better(v, cu, d, best, bc)) { best = d; bc = cu; }
             }
+#ifdef SSF_ASSOC_COUNT
+            assoc_finish(L, lo, last_normal, last_valid, pc, v.id(max(bc, 0)), corr, nullptr, co + i);
+#else
             assoc_finish(L, lo, last_normal, last_valid, pc, v.id(max(bc, 0)), corr, nn_out, co + i);
+#endif
         }
         __syncthreads();
     }
@@ -995,6 +1013,226 @@ __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
 #else
     (void)st1;
 #endif
+}
+
+// ------------------------------------------------------------------------------------------
+// Association over y-strips.  An x band around a query crosses every LiDAR ring: the 1-m walk
+// visits ~60 candidates per query (the ~54 points inside |dx| < the final NN distance are
+// unavoidable in x order), and the slowest lane of a wave ~217.  One work-group per pair stages
+// the last frame (x-sorted) into LDS partitioned into strips of width W >= 1 m in y, x order
+// kept inside each strip (stable partition: per-wave match masks on the strip id + per-wave
+// strip counts, chunk by chunk in x order).  A query searches its own strip (binary search in
+// x, outward walk while dx^2 + dymin^2 <= best), then the strips above and below, ring by
+// ring, while a lower bound of their |dy| can still beat the best: ~8 candidates per query,
+// every query exact (no 1-m band, no exhaustive phase).  Lower bounds: inside a searched strip,
+// dymin from the strip's actual y extent (fl(qy - yhi) <= fl(qy - py) by monotone rounding, so
+// fl(fl(dx^2) + fl(dymin^2)) <= the float distance); for the ring stop, the nominal strip edge
+// minus 1 mm (float strip assignment).  Candidates compare as (distance, original index).
+constexpr int kStripThreads = 1024;
+constexpr int kStripMax = 256;             // strips per frame (W widened beyond 255 m of y)
+constexpr int kStripWaves = kStripThreads / 64;
+constexpr int kAssocStripF4Max = 6144;     // 16-B points (x, y, z, index) staged: 96 KiB
+constexpr int kAssocStripSoaMax = 10752;   // x | y | z + u16 index (14 B): 147 KiB
+
+struct StripLds {
+    int start[kStripMax + 1];
+    int cursor[kStripMax];
+    float ylo[kStripMax], yhi[kStripMax];
+    uint16_t wc[kStripWaves][kStripMax];
+    float red[2 * kStripWaves];
+};
+
+// kSoa: the strip-major points as x | y | z float arrays and a u16 original index (configs[4]
+// frames); otherwise float4 with the index in .w.  A last frame above the launch's staging
+// capacity walks the x-sorted copy in global memory, unbounded (exact, slow, not expected).
+template <bool kSoa>
+__global__ __launch_bounds__(kStripThreads) void k_associate_strips(
+    const float4* __restrict__ last, const int64_t* __restrict__ last_off,
+    const int32_t* __restrict__ last_count, const float* __restrict__ last_normal,
+    const uint8_t* __restrict__ last_valid, const float4* __restrict__ last_sorted,
+    const int32_t* __restrict__ last_sidx, const float4* __restrict__ curr,
+    const int64_t* __restrict__ curr_off, const int32_t* __restrict__ curr_count,
+    const double* __restrict__ pose_rel, CorrRec* __restrict__ corr, int32_t* __restrict__ nn_out,
+    int lds_cap) {
+    extern __shared__ float4 SL[];                  // [ml] strip-major, x-sorted in each strip
+    __shared__ StripLds T;
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int mc = curr_count[p], ml = last_count[p];
+    if (mc <= 0 || ml <= 10) return;                                    // uniform (:158)
+    const int64_t lo = last_off[p], co = curr_off[p];
+    const float4* SP = last_sorted + lo;
+    const int32_t* SI = last_sidx + lo;
+    const double q[4] = {pose_rel[7 * p], pose_rel[7 * p + 1], pose_rel[7 * p + 2], pose_rel[7 * p + 3]};
+    const double t[3] = {pose_rel[7 * p + 4], pose_rel[7 * p + 5], pose_rel[7 * p + 6]};
+    const float4* L = last + lo;
+    if (ml > lds_cap) {                                                 // uniform
+        const PtsF4 g{SP, SI};
+        for (int i = tid; i < mc; i += kStripThreads) {
+            const float4 pc = curr[co + i];
+            const float4 qs = assoc_query_point(pc, q, t);
+            float best = __builtin_inff();
+            int bc = -1;
+            assoc_walk(g, ml, qs, __builtin_inff(), best, bc);
+            assoc_finish(L, lo, last_normal, last_valid, pc, g.id(max(bc, 0)), corr, nn_out, co + i);
+        }
+        return;
+    }
+    float* SX = reinterpret_cast<float*>(SL);
+    uint16_t* SI16 = reinterpret_cast<uint16_t*>(SX + 3 * ml);
+    // y extent
+    float y0 = __builtin_inff(), y1 = -__builtin_inff();
+    for (int r = tid; r < ml; r += kStripThreads) { const float y = SP[r].y; y0 = fminf(y0, y); y1 = fmaxf(y1, y); }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { y0 = fminf(y0, __shfl_xor(y0, o, 64)); y1 = fmaxf(y1, __shfl_xor(y1, o, 64)); }
+    if (lane == 0) { T.red[2 * w] = y0; T.red[2 * w + 1] = y1; }
+    for (int k = tid; k < kStripWaves * kStripMax; k += kStripThreads) (&T.wc[0][0])[k] = 0;
+    for (int k = tid; k < kStripMax; k += kStripThreads) T.cursor[k] = 0;
+    __syncthreads();
+    y0 = __builtin_inff(); y1 = -__builtin_inff();
+    for (int k = 0; k < kStripWaves; ++k) { y0 = fminf(y0, T.red[2 * k]); y1 = fmaxf(y1, T.red[2 * k + 1]); }
+    const float W = fmaxf(1.0f, (y1 - y0) / (float)(kStripMax - 1));
+    const float invW = 1.0f / W;
+    const int ns = min(kStripMax, (int)((y1 - y0) * invW) + 1);
+    auto strip_of = [&](float y) { return min(ns - 1, max(0, (int)((y - y0) * invW))); };
+    // histogram (cursor holds the counts), exclusive scan into start
+    for (int r = tid; r < ml; r += kStripThreads) atomicAdd(&T.cursor[strip_of(SP[r].y)], 1);
+    __syncthreads();
+    if (w == 0) {
+        const int per = (kStripMax + 63) / 64;                          // 4 strips per lane
+        int run = 0;
+        for (int k = 0; k < per; ++k) run += T.cursor[lane * per + k];
+        int incl = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(incl, o, 64); if (lane >= o) incl += y; }
+        int pre = incl - run;
+        for (int k = 0; k < per; ++k) {
+            const int sidx = lane * per + k;
+            T.start[sidx] = pre;
+            pre += T.cursor[sidx];
+            T.cursor[sidx] = T.start[sidx];
+        }
+        if (lane == 63) T.start[kStripMax] = incl;
+    }
+    __syncthreads();
+    // stable scatter, one chunk of kStripThreads points (in x order) at a time
+    for (int c0 = 0; c0 < ml; c0 += kStripThreads) {
+        const int r = c0 + tid;
+        const bool v = r < ml;
+        float4 pt = make_float4(0.f, 0.f, 0.f, 0.f);
+        int sidx = 0;
+        if (v) { pt = SP[r]; pt.w = __int_as_float(SI[r]); sidx = strip_of(pt.y); }
+        uint64_t eq = __ballot(v);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const uint64_t bb = __ballot((sidx >> b) & 1);
+            eq &= ((sidx >> b) & 1) ? bb : ~bb;
+        }
+        const int rank = __popcll(eq & lanemask_lt());
+        if (v && rank == 0) T.wc[w][sidx] = (uint16_t)__popcll(eq);
+        __syncthreads();
+        if (v) {
+            int before = T.cursor[sidx];
+            for (int k = 0; k < w; ++k) before += T.wc[k][sidx];
+            const int dst = before + rank;
+            if (kSoa) {
+                SX[dst] = pt.x; SX[ml + dst] = pt.y; SX[2 * ml + dst] = pt.z;
+                SI16[dst] = (uint16_t)__float_as_int(pt.w);
+            } else {
+                SL[dst] = pt;
+            }
+        }
+        __syncthreads();
+        for (int k = tid; k < kStripMax; k += kStripThreads) {
+            int add = 0;
+            for (int j = 0; j < kStripWaves; ++j) { add += T.wc[j][k]; T.wc[j][k] = 0; }
+            T.cursor[k] += add;
+        }
+        __syncthreads();
+    }
+    struct View {                                  // the strip-major points, either layout
+        const float4* F;
+        const float* X;
+        const uint16_t* I;
+        int m;
+        SSF_DEV float4 pt(int c) const {
+            return kSoa ? make_float4(X[c], X[m + c], X[2 * m + c], 0.f) : F[c];
+        }
+        SSF_DEV float x(int c) const { return kSoa ? X[c] : F[c].x; }
+        SSF_DEV float y(int c) const { return kSoa ? X[m + c] : F[c].y; }
+        SSF_DEV int id(int c) const { return kSoa ? (int)I[c] : __float_as_int(F[c].w); }
+    };
+    const View v{SL, SX, SI16, ml};
+    // actual y extent of every strip (the in-strip lower bound of |dy|)
+    for (int k = tid; k < ns; k += kStripThreads) {
+        float a = __builtin_inff(), b = -__builtin_inff();
+        for (int j = T.start[k]; j < T.start[k + 1]; ++j) { const float y = v.y(j); a = fminf(a, y); b = fmaxf(b, y); }
+        T.ylo[k] = a; T.yhi[k] = b;
+    }
+    __syncthreads();
+    for (int i = tid; i < mc; i += kStripThreads) {
+        const float4 pc = curr[co + i];
+        const float4 qs = assoc_query_point(pc, q, t);
+        float best = __builtin_inff();
+        int bc = -1;
+#ifdef SSF_ASSOC_COUNT
+        int vis = 0;
+#endif
+        auto search = [&](int sidx) {
+            const int a = T.start[sidx], b = T.start[sidx + 1];
+            if (a >= b) return;
+            const float yl = T.ylo[sidx], yh = T.yhi[sidx];
+            const float dyl = qs.y < yl ? yl - qs.y : (qs.y > yh ? qs.y - yh : 0.0f);
+            const float dy2 = dyl * dyl;
+            if (dy2 > best) return;
+            int l = a, h = b;                                            // first x >= qs.x
+            while (l < h) {
+                const int mid = (l + h) >> 1;
+                if (v.x(mid) < qs.x) l = mid + 1; else h = mid;
+            }
+            for (int c = l; c < b; ++c) {
+                const float4 pl = v.pt(c);
+                const float dx = qs.x - pl.x;
+                if (dx * dx + dy2 > best) break;
+                const float d = l2_simple(qs, pl);
+                if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
+#ifdef SSF_ASSOC_COUNT
+                ++vis;
+#endif
+            }
+            for (int c = l - 1; c >= a; --c) {
+                const float4 pl = v.pt(c);
+                const float dx = qs.x - pl.x;
+                if (dx * dx + dy2 > best) break;
+                const float d = l2_simple(qs, pl);
+                if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
+#ifdef SSF_ASSOC_COUNT
+                ++vis;
+#endif
+            }
+        };
+        const int s0 = strip_of(qs.y);
+        search(s0);
+        bool up = true, dn = true;
+        for (int rr = 1; up || dn; ++rr) {
+            if (up) {
+                const int su = s0 + rr;
+                // every point of strips >= su has y >= y0 + su W (less float slack)
+                const float gap = (y0 + (float)su * W) - qs.y - 1e-3f;
+                if (su >= ns || (gap > 0.0f && gap * gap > best)) up = false;
+                else search(su);
+            }
+            if (dn) {
+                const int sd = s0 - rr;
+                const float gap = qs.y - (y0 + (float)(sd + 1) * W) - 1e-3f;
+                if (sd < 0 || (gap > 0.0f && gap * gap > best)) dn = false;
+                else search(sd);
+            }
+        }
+        assoc_finish(L, lo, last_normal, last_valid, pc, v.id(max(bc, 0)), corr, nn_out, co + i);
+#ifdef SSF_ASSOC_COUNT
+        if (nn_out) nn_out[co + i] = vis;
+#endif
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1720,6 +1958,18 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
     if (n_pairs <= 0) return hipSuccess;
     if (max_m > 0) {
         const int bx = (int)((max_m + 255) / 256);
+#ifndef SSF_ASSOC_XBAND
+        if (max_m <= kSortMax && last_sorted && last_sidx) {
+            const bool soa = max_m > kAssocStripF4Max;
+            const int cap = (int)std::min<int64_t>(max_m, soa ? kAssocStripSoaMax : kAssocStripF4Max);
+            const size_t lds = soa ? (size_t)cap * 14 + 16 : (size_t)cap * sizeof(float4);
+            kmark(s, soa ? "k_associate_strips_soa" : "k_associate_strips");
+            hipLaunchKernelGGL(soa ? k_associate_strips<true> : k_associate_strips<false>,
+                               dim3(n_pairs), dim3(kStripThreads), lds, s, last, last_off, last_count,
+                               last_normal, last_valid, last_sorted, last_sidx, curr, curr_off,
+                               curr_count, pose_rel, corr, nn, cap);
+        } else
+#endif
         if (max_m <= kAssocSoaMax && last_sorted && last_sidx) {
             const int qx = (int)((max_m + kAssocQ - 1) / kAssocQ);
             const bool soa = max_m > kAssocLdsMax;

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_registration.py tests/test_gpu_configs.py tests/test_gpu_nodes.py tests/test_examples.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r2z_tests.log 2>&1 && echo TESTS_OK && \
+SSF_LIB=$PWD/ssf-slam_amd/ssf/_lib/libssf_frontend_acount.so timeout -k 10 200 python -u tools/diag_assoc_count.py 64 > gpurun_out/r2z_count.log 2>&1 && echo COUNT_OK && \
+timeout -k 10 200 python -u tools/bench_features.py --tag strips --reps 5 --chain > gpurun_out/r2z_feat.log 2>&1 && echo FEAT_OK && \
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/r2z_bench.log 2>&1 && echo BENCH_OK

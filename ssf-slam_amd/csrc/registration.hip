@@ -320,10 +320,9 @@ __global__ __launch_bounds__(256) void k_associate(const float4* __restrict__ la
 constexpr int kSortMax = 16384;           // plane points per frame sorted in LDS (128 KiB)
 constexpr int kTableThreads = 1024;
 
-constexpr int kLdsWalkMax = 6144;         // after the sort, frames up to this size walk in LDS
-// (16 m bytes of points + the deferred-query grid (16.6 KiB + 2 m) fit below the permutation)
-constexpr int kLdsSoaMax = 9088;          // ... and up to this size as 14-B SoA points: 16 m + 16.6 KiB
-// of points, permutation and grid leave >= 1 KiB of deferred queue in the 160 KiB image
+constexpr int kTableStripF4Max = 9216;    // after the sort, frames up to this size search strips of
+// 16-B points in LDS (16 m + the 12 KiB strip table + >= 2 KiB of deferred queue) ...
+constexpr int kTableStripSoaMax = 10624;  // ... and up to this size strips of 14-B SoA points
 
 // Diagnostic build only (-DSSF_TABLE_STAMPS): lane 0 writes s_memtime deltas after the sort,
 // the bounded walks and the deferred walks into sorted_idx[m .. m+3] (frame padding, read by
@@ -426,137 +425,14 @@ SSF_DEV void table_finish(const float4* __restrict__ P, int m, float plane_max, 
     valid[o] = ok;
 }
 
-// Deferred queries (no decision inside 1 m: sparse, far regions) on a 2-D (x, y) grid built in
-// spare LDS: an x band around a far point crosses every LiDAR ring and holds thousands of
-// candidates, the grid cells around it a few hundred at most.  G x G cells over the frame's
-// bounding box, u32 cell ends (count, exclusive scan, atomic scatter) and a u16 list of sorted
-// ranks.  Each query searches rings of cells outward and stops once the squared distance to
-// the unvisited region (minus a 1 mm slack for float cell assignment) exceeds its 30th key's
-// distance; keys are (distance, index), so the list is the exact 30-NN in any visit order.
-constexpr int kGridG = 64;
-constexpr int kGridBytes = 4 * kGridG * kGridG + 256;      // + 2 m bytes of list
-
-template <class V>
-SSF_DEV void table_deferred_grid(const float4* __restrict__ P, const V& v, int m, float plane_max,
-                                 int64_t base,
-                                 float* __restrict__ normal, uint8_t* __restrict__ valid,
-                                 const int* queue, int nq, char* gridmem,
-                                 int32_t* stamp_out, unsigned long long stamp0) {
-    constexpr int G = kGridG;
-    uint32_t* cend = reinterpret_cast<uint32_t*>(gridmem);
-    float* scr = reinterpret_cast<float*>(gridmem + 4 * G * G);          // 2 floats per wave
-    uint16_t* list = reinterpret_cast<uint16_t*>(gridmem + kGridBytes);
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
-    float ymn = __builtin_inff(), ymx = -__builtin_inff();
-    for (int r = tid; r < m; r += blockDim.x) { const float y = v.pt(r).y; ymn = fminf(ymn, y); ymx = fmaxf(ymx, y); }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        ymn = fminf(ymn, __shfl_xor(ymn, o, 64));
-        ymx = fmaxf(ymx, __shfl_xor(ymx, o, 64));
-    }
-    if (lane == 0) { scr[2 * w] = ymn; scr[2 * w + 1] = ymx; }
-    for (int c = tid; c < G * G; c += blockDim.x) cend[c] = 0u;
-    __syncthreads();
-    float y0 = __builtin_inff(), y1 = -__builtin_inff();
-    for (int k = 0; k < nw; ++k) { y0 = fminf(y0, scr[2 * k]); y1 = fmaxf(y1, scr[2 * k + 1]); }
-    const float x0 = v.pt(0).x, x1 = v.pt(m - 1).x;
-    float h = fmaxf(x1 - x0, y1 - y0) / (float)G;
-    if (!(h > 0.0f)) h = 1.0f;
-    const float invh = 1.0f / h;
-    auto cell = [&](const float4& p, int& cx, int& cy) {
-        cx = min(G - 1, max(0, (int)((p.x - x0) * invh)));
-        cy = min(G - 1, max(0, (int)((p.y - y0) * invh)));
-    };
-    for (int r = tid; r < m; r += blockDim.x) {
-        int cx, cy;
-        cell(v.pt(r), cx, cy);
-        atomicAdd(&cend[cy * G + cx], 1u);
-    }
-    __syncthreads();
-    {   // exclusive scan of the G*G counts: a contiguous run per thread, then the block
-        const int per = (G * G + blockDim.x - 1) / blockDim.x;
-        const int c0 = min(G * G, tid * per), c1 = min(G * G, c0 + per);
-        uint32_t run = 0;
-        for (int c = c0; c < c1; ++c) run += cend[c];
-        uint32_t incl = run;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        if (lane == 63) reinterpret_cast<uint32_t*>(scr)[2 * nw + w] = incl;
-        __syncthreads();
-        uint32_t pre = incl - run;
-        for (int k = 0; k < w; ++k) pre += reinterpret_cast<uint32_t*>(scr)[2 * nw + k];
-        for (int c = c0; c < c1; ++c) { const uint32_t v = cend[c]; cend[c] = pre; pre += v; }
-    }
-    __syncthreads();
-    for (int r = tid; r < m; r += blockDim.x) {               // cend[c]: start -> end of cell c
-        int cx, cy;
-        cell(v.pt(r), cx, cy);
-        list[atomicAdd(&cend[cy * G + cx], 1u)] = (uint16_t)r;
-    }
-    __syncthreads();
-    if (tid == 0 && stamp_out) stamp_out[3] = (int32_t)((__builtin_amdgcn_s_memtime() - stamp0) >> 4);
-    const int t2 = (tid & 63) * nw + w;                        // entry k -> wave k % nw
-    for (int k = t2; k < nq; k += blockDim.x) {
-        const int r = queue[k];
-        const float4 q = v.pt(r);
-        int cx, cy;
-        cell(q, cx, cy);
-        double kk[kK];
-#pragma unroll
-        for (int j = 0; j < kK; ++j) kk[j] = knn_key(__builtin_inff(), 0x7fffffff);
-        // one candidate per loop trip (lanes hold different queries: nested ring/cell/point loops
-        // would cost the wave the per-cell maximum over lanes at every step)
-        int rr = 0, dy = 0, dx = 0, j = 0, e = 0;
-        {
-            const int c = cy * G + cx;
-            j = c ? (int)cend[c - 1] : 0;
-            e = (int)cend[c];
-        }
-        for (;;) {
-            bool done = false;
-            while (j >= e) {                                   // next non-empty cell of the ring walk
-                const bool edge = dy == -rr || dy == rr;
-                if (edge && dx < rr) ++dx;
-                else if (!edge && dx == -rr) dx = rr;
-                else { ++dy; dx = -rr; }
-                if (dy > rr) {                                 // ring rr complete: stop test
-                    if (cx - rr <= 0 && cy - rr <= 0 && cx + rr >= G - 1 && cy + rr >= G - 1) { done = true; break; }
-                    float dmin = __builtin_inff();
-                    if (cx - rr > 0) dmin = fminf(dmin, q.x - (x0 + (float)(cx - rr) * h));
-                    if (cx + rr < G - 1) dmin = fminf(dmin, (x0 + (float)(cx + rr + 1) * h) - q.x);
-                    if (cy - rr > 0) dmin = fminf(dmin, q.y - (y0 + (float)(cy - rr) * h));
-                    if (cy + rr < G - 1) dmin = fminf(dmin, (y0 + (float)(cy + rr + 1) * h) - q.y);
-                    dmin -= 1e-3f;
-                    if (dmin > 0.0f && dmin * dmin > key_dist(kk[kK - 1])) { done = true; break; }
-                    ++rr; dy = -rr; dx = -rr;
-                }
-                const int xx = cx + dx, yy = cy + dy;
-                if (xx >= 0 && xx < G && yy >= 0 && yy < G) {
-                    const int c = yy * G + xx;
-                    j = c ? (int)cend[c - 1] : 0;
-                    e = (int)cend[c];
-                }
-            }
-            if (done) break;
-            const int rj = list[j++];
-            const double key = knn_key(l2_simple(q, v.pt(rj)), v.id(rj));
-            if (key < kk[kK - 1]) key_insert<kK>(kk, key);
-        }
-        table_finish(P, m, plane_max, base + v.id(r), kk, normal, valid);
-    }
-}
-
 // Queries in sorted order (adjacent lanes ~ adjacent x): 1-m-bounded walk for everyone; the
 // undecided few go to an LDS queue and are re-walked in full afterwards, one per lane, so a
 // handful of long walks no longer stalls whole waves.  queue == nullptr: walk in full at once.
 template <class V>
 SSF_DEV void table_walks(const float4* __restrict__ P, const V& v, int m, float plane_max,
                          int64_t base, float* __restrict__ normal, uint8_t* __restrict__ valid,
-                         int* queue, int qcap, int* qlen, char* gridmem = nullptr,
-                         int32_t* stamp_out = nullptr, unsigned long long stamp0 = 0) {
+                         int* queue, int qcap, int* qlen, int32_t* stamp_out = nullptr,
+                         unsigned long long stamp0 = 0) {
     for (int r = threadIdx.x; r < m; r += blockDim.x) {
         const float4 q = v.pt(r);
         double kk[kK];
@@ -586,11 +462,6 @@ SSF_DEV void table_walks(const float4* __restrict__ P, const V& v, int m, float 
     if (threadIdx.x == 0 && stamp_out) stamp_out[1] = *qlen;
 #endif
     const int nq = min(*qlen, qcap);
-    if (gridmem && nq > 0) {                                  // uniform
-        table_deferred_grid(P, v, m, plane_max, base, normal, valid, queue, nq, gridmem,
-                            stamp_out, stamp0);
-        return;
-    }
     for (int k = threadIdx.x; k < nq; k += blockDim.x) {
         const int r = queue[k];
         const float4 q = v.pt(r);
@@ -600,17 +471,281 @@ SSF_DEV void table_walks(const float4* __restrict__ P, const V& v, int m, float 
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// y-strips (shared by the plane table and the association; see k_associate_strips for the
+// search and its exactness argument)
+constexpr int kStripThreads = 1024;
+constexpr int kStripMax = 256;             // strips per frame (W widened beyond 255 m of y)
+constexpr int kStripWaves = kStripThreads / 64;
+constexpr int kAssocStripF4Max = 6144;     // 16-B points (x, y, z, index) staged: 96 KiB
+constexpr int kAssocStripSoaMax = 10752;   // x | y | z + u16 index (14 B): 147 KiB
+
+struct StripLds {
+    int start[kStripMax + 1];
+    int cursor[kStripMax];
+    float ylo[kStripMax], yhi[kStripMax];
+    uint16_t wc[kStripWaves][kStripMax];
+    float red[2 * kStripWaves];
+};
+
+struct StripGeo {
+    float y0, W, invW;
+    int ns;
+    SSF_DEV int strip_of(float y) const { return min(ns - 1, max(0, (int)((y - y0) * invW))); }
+};
+
+// The strip-major points, either layout: float4 (x, y, z, original index in .w) or x | y | z
+// float arrays + a u16 original index.
+template <bool kSoa>
+struct StripView {
+    const float4* F;
+    const float* X;
+    const uint16_t* I;
+    int m;
+    SSF_DEV float4 pt(int c) const { return kSoa ? make_float4(X[c], X[m + c], X[2 * m + c], 0.f) : F[c]; }
+    SSF_DEV float x(int c) const { return kSoa ? X[c] : F[c].x; }
+    SSF_DEV float y(int c) const { return kSoa ? X[m + c] : F[c].y; }
+    SSF_DEV int id(int c) const { return kSoa ? (int)I[c] : __float_as_int(F[c].w); }
+};
+
+constexpr int kStripPerMax = kSortMax / kStripThreads;   // x-order points per thread (16)
+
+// Whole work-group (kStripThreads): partition m x-sorted points into y-strips, x order kept in
+// each strip (stable: per-wave match masks on the strip id, per-wave strip counts, one chunk of
+// kStripThreads points in x order at a time).  get(k, r) returns the point of x-sorted rank
+// r = k kStripThreads + tid with its original index in .w.  Writes the strip-major points (F,
+// or X | Y | Z + I16), T.start / T.ylo / T.yhi; returns the strip geometry.
+template <bool kSoa, int kPer, class Get>
+SSF_DEV StripGeo strips_build(Get get, int m, StripLds& T, float4* F, float* X, uint16_t* I16) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float y0 = __builtin_inff(), y1 = -__builtin_inff();
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int r = k * kStripThreads + tid;
+        if (r < m) { const float y = get(k, r).y; y0 = fminf(y0, y); y1 = fmaxf(y1, y); }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { y0 = fminf(y0, __shfl_xor(y0, o, 64)); y1 = fmaxf(y1, __shfl_xor(y1, o, 64)); }
+    if (lane == 0) { T.red[2 * w] = y0; T.red[2 * w + 1] = y1; }
+    for (int k = tid; k < kStripWaves * kStripMax; k += kStripThreads) (&T.wc[0][0])[k] = 0;
+    for (int k = tid; k < kStripMax; k += kStripThreads) T.cursor[k] = 0;
+    __syncthreads();
+    StripGeo g;
+    y0 = __builtin_inff(); y1 = -__builtin_inff();
+    for (int k = 0; k < kStripWaves; ++k) { y0 = fminf(y0, T.red[2 * k]); y1 = fmaxf(y1, T.red[2 * k + 1]); }
+    g.y0 = y0;
+    // W > 1 m by a margin far above the float error of the strip assignment: a point two strips
+    // away from the query's is then always more than 1 m away (the bounded 30-NN searches the
+    // query's strip and its two neighbours only)
+    g.W = fmaxf(1.001f, (y1 - y0) / (float)(kStripMax - 1));
+    g.invW = 1.0f / g.W;
+    g.ns = min(kStripMax, (int)((y1 - y0) * g.invW) + 1);
+    // histogram (cursor holds the counts), exclusive scan into start
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int r = k * kStripThreads + tid;
+        if (r < m) atomicAdd(&T.cursor[g.strip_of(get(k, r).y)], 1);
+    }
+    __syncthreads();
+    if (w == 0) {
+        constexpr int per = (kStripMax + 63) / 64;                      // 4 strips per lane
+        int run = 0;
+        for (int k = 0; k < per; ++k) run += T.cursor[lane * per + k];
+        int incl = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(incl, o, 64); if (lane >= o) incl += y; }
+        int pre = incl - run;
+        for (int k = 0; k < per; ++k) {
+            const int sidx = lane * per + k;
+            T.start[sidx] = pre;
+            pre += T.cursor[sidx];
+            T.cursor[sidx] = T.start[sidx];
+        }
+        if (lane == 63) T.start[kStripMax] = incl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {                                    // stable scatter by chunk
+        if (k * kStripThreads >= m) break;                              // uniform
+        const int r = k * kStripThreads + tid;
+        const bool v = r < m;
+        float4 pt = make_float4(0.f, 0.f, 0.f, 0.f);
+        int sidx = 0;
+        if (v) { pt = get(k, r); sidx = g.strip_of(pt.y); }
+        uint64_t eq = __ballot(v);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const uint64_t bb = __ballot((sidx >> b) & 1);
+            eq &= ((sidx >> b) & 1) ? bb : ~bb;
+        }
+        const int rank = __popcll(eq & lanemask_lt());
+        if (v && rank == 0) T.wc[w][sidx] = (uint16_t)__popcll(eq);
+        __syncthreads();
+        if (v) {
+            int before = T.cursor[sidx];
+            for (int j = 0; j < w; ++j) before += T.wc[j][sidx];
+            const int dst = before + rank;
+            if (kSoa) {
+                X[dst] = pt.x; X[m + dst] = pt.y; X[2 * m + dst] = pt.z;
+                I16[dst] = (uint16_t)__float_as_int(pt.w);
+            } else {
+                F[dst] = pt;
+            }
+        }
+        __syncthreads();
+        for (int j = tid; j < kStripMax; j += kStripThreads) {
+            int add = 0;
+            for (int u = 0; u < kStripWaves; ++u) { add += T.wc[u][j]; T.wc[u][j] = 0; }
+            T.cursor[j] += add;
+        }
+        __syncthreads();
+    }
+    // actual y extent of every strip (the in-strip lower bound of |dy|)
+    const StripView<kSoa> v{F, X, I16, m};
+    for (int j = tid; j < g.ns; j += kStripThreads) {
+        float a = __builtin_inff(), b = -__builtin_inff();
+        for (int c = T.start[j]; c < T.start[j + 1]; ++c) { const float y = v.y(c); a = fminf(a, y); b = fmaxf(b, y); }
+        T.ylo[j] = a; T.yhi[j] = b;
+    }
+    __syncthreads();
+    return g;
+}
+
+// One strip of the k-NN search: binary search of q.x (or the query's own position `start`),
+// outward walks while fl(dx^2) + fl(dymin^2) can still beat the 30th key and stays below lim.
+template <bool kSoa>
+SSF_DEV void strip_search(const StripView<kSoa>& v, const StripLds& T, int sidx, int start,
+                          const float4& q, float lim, double (&kk)[kK]) {
+    const int a = T.start[sidx], b = T.start[sidx + 1];
+    if (a >= b) return;
+    const float yl = T.ylo[sidx], yh = T.yhi[sidx];
+    const float dyl = q.y < yl ? yl - q.y : (q.y > yh ? q.y - yh : 0.0f);
+    const float dy2 = dyl * dyl;
+    if (dy2 > key_dist(kk[kK - 1]) || dy2 >= lim) return;
+    int l = start;
+    if (l < 0) {
+        l = a;
+        int h = b;                                                       // first x >= q.x
+        while (l < h) {
+            const int mid = (l + h) >> 1;
+            if (v.x(mid) < q.x) l = mid + 1; else h = mid;
+        }
+    }
+    for (int c = l; c < b; ++c) {                                        // rightwards
+        const float4 p = v.pt(c);
+        const float dx = q.x - p.x;
+        const float t = dx * dx + dy2;
+        if (t > key_dist(kk[kK - 1]) || t >= lim) break;
+        key_insert<kK>(kk, knn_key(l2_simple(q, p), v.id(c)));
+    }
+    for (int c = l - 1; c >= a; --c) {                                   // leftwards
+        const float4 p = v.pt(c);
+        const float dx = q.x - p.x;
+        const float t = dx * dx + dy2;
+        if (t > key_dist(kk[kK - 1]) || t >= lim) break;
+        key_insert<kK>(kk, knn_key(l2_simple(q, p), v.id(c)));
+    }
+}
+
+// k-NN within radius R = kRings m (keys seeded (R^2, INT_MAX), walks stop at R^2): with
+// W > 1 m only the query's strip (searched from its own position) and kRings strips on either
+// side can hold points within R.  Keys are (distance, original index), so the list equals the
+// x-walk's for every point closer than R; kRings = 1 is knn_walk's 1-m bounded mode.  The
+// strips are unrolled (no loop nest around the walks: that spilled the 30 keys).
+template <int kRings, bool kSoa>
+SSF_DEV void strip_knn_radius(const StripView<kSoa>& v, const StripLds& T, const StripGeo& g,
+                              int self, const float4& q, double (&kk)[kK]) {
+    constexpr float R2 = (float)(kRings * kRings);
+#pragma unroll
+    for (int k = 0; k < kK; ++k) kk[k] = knn_key(R2, 0x7fffffff);
+    const int s0 = g.strip_of(q.y);
+    strip_search(v, T, s0, self, q, R2, kk);
+#pragma unroll
+    for (int rr = 1; rr <= kRings; ++rr) {
+        if (s0 + rr < g.ns) strip_search(v, T, s0 + rr, -1, q, R2, kk);
+        if (s0 - rr >= 0) strip_search(v, T, s0 - rr, -1, q, R2, kk);
+    }
+}
+
+// The table's walks over the strips, queries in strip-major order (adjacent lanes: the same
+// strip, adjacent x).  1-m bounded search for everyone; the undecided few are queued and
+// searched in full afterwards (as table_walks).
+#ifndef SSF_DEFER_RINGS
+#define SSF_DEFER_RINGS 6
+#endif
+constexpr int kDeferRings = SSF_DEFER_RINGS;     // deferred queries: strips within this many metres
+
+SSF_DEV void table_deferred_walk(const float4* __restrict__ P, const float4* __restrict__ SP,
+                                 const int32_t* __restrict__ SI, int m, int qi, const float4& q,
+                                 double (&kk)[kK]) {
+    int l = 0, h = m;                                  // x rank of (q.x, qi) in the sorted copy
+    while (l < h) {
+        const int mid = (l + h) >> 1;
+        if (lex_less(SP[mid].x, SI[mid], q.x, qi)) l = mid + 1; else h = mid;
+    }
+    knn_walk(PtsF4{SP, SI}, m, l, q, false, kk);
+}
+
+// The deferred few (no decision inside 1 m: sparse, far regions) walk the x-sorted copy the
+// sort left in global memory (SP / SI, L2-resident), unbounded, from their x rank (binary
+// search on (x, index)): a strip ring search there would need a loop nest whose register
+// pressure spills the bounded walks that share the kernel.
+template <bool kSoa>
+SSF_DEV void table_strip_walks(const float4* __restrict__ P, const StripView<kSoa>& v,
+                               const StripLds& T, const StripGeo& g, int m, float plane_max,
+                               int64_t base, float* __restrict__ normal, uint8_t* __restrict__ valid,
+                               int* queue, int qcap, int* qlen, const float4* __restrict__ SP,
+                               const int32_t* __restrict__ SI, int32_t* stamp_out,
+                               unsigned long long stamp0) {
+    for (int j = threadIdx.x; j < m; j += blockDim.x) {
+        const float4 q = v.pt(j);
+        double kk[kK];
+        int dec;
+        strip_knn_radius<1>(v, T, g, j, q, kk);
+        dec = bounded_decides(P, m, kk);
+        if (dec == 0) {
+            const int slot = atomicAdd(qlen, 1);
+            if (slot < qcap) queue[slot] = j;
+            else { table_deferred_walk(P, SP, SI, m, v.id(j), q, kk); dec = 1; }   // queue full
+        }
+        if (dec == 2) {
+            const int64_t o = base + v.id(j);
+            normal[3 * o] = 0.f; normal[3 * o + 1] = 0.f; normal[3 * o + 2] = 0.f;
+            valid[o] = 0;
+        } else if (dec == 1) {
+            table_finish(P, m, plane_max, base + v.id(j), kk, normal, valid);
+        }
+    }
+    __syncthreads();
+#ifdef SSF_TABLE_STAMPS
+    if (threadIdx.x == 0 && stamp_out) { stamp_out[0] = (int32_t)((__builtin_amdgcn_s_memtime() - stamp0) >> 4); stamp_out[1] = *qlen; }
+#endif
+    const int nq = min(*qlen, qcap);
+    // spread the deferred queries over the waves (entry k -> wave k % nw)
+    const int nw = blockDim.x >> 6, t2 = (threadIdx.x & 63) * nw + (threadIdx.x >> 6);
+    for (int k = t2; k < nq; k += blockDim.x) {
+        const int j = queue[k];
+        const float4 q = v.pt(j);
+        double kk[kK];
+        // within 4 m from the strips (exact when the 30th key is closer than 4 m), else the
+        // x-sorted global copy, unbounded
+        strip_knn_radius<kDeferRings>(v, T, g, j, q, kk);
+        if (!(key_dist(kk[kK - 1]) < (float)(kDeferRings * kDeferRings)))
+            table_deferred_walk(P, SP, SI, m, v.id(j), q, kk);
+        table_finish(P, m, plane_max, base + v.id(j), kk, normal, valid);
+    }
+}
+
 __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
     const float4* __restrict__ plane, const int64_t* __restrict__ frame_off,
     const int32_t* __restrict__ count, float plane_max, float* __restrict__ normal,
     uint8_t* __restrict__ valid, float4* __restrict__ sorted_xyzi, int32_t* __restrict__ sorted_idx) {
     // 160 KiB of LDS: [0, 64K) keys, [64K, 128K) permutation, [128K, 160K) spare.  After the
-    // sort, frames <= kLdsWalkMax move the permutation to the spare region and put the sorted
-    // points (<= 96 KiB) over the keys and the old permutation.
+    // sort, frames <= kTableStripSoaMax rebuild the whole image as y-strips of the sorted points
+    // + the strip table + the deferred queue; larger frames walk the sorted copy in global memory.
     __shared__ __attribute__((aligned(16))) char lds[kSortMax * 8 + 32768];
     float* key = reinterpret_cast<float*>(lds);
     int* idx = reinterpret_cast<int*>(lds + kSortMax * 4);
-    float4* SPl = reinterpret_cast<float4*>(lds);
     const int f = blockIdx.x, tid = threadIdx.x;
     const int m = count[f];
     const int64_t base = frame_off[f];
@@ -652,62 +787,53 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
     SSF_TSTAMP(0);
     int* qlen = reinterpret_cast<int*>(lds + sizeof(lds) - 4);   // last word of the LDS image
     if (tid == 0) *qlen = 0;
-    if (m <= kLdsWalkMax) {
-        // spare region: [128K, 128K + 4m) permutation, the rest (>= 8 KiB) the deferred queue
-        int* idx2 = reinterpret_cast<int*>(lds + kSortMax * 8);
-        int* queue = idx2 + m;
-        const int qcap = (32768 - 4 * m - 4) / 4;
-        for (int r = tid; r < m; r += blockDim.x) idx2[r] = idx[r];
-        __syncthreads();
-        for (int r = tid; r < m; r += blockDim.x) SPl[r] = P[idx2[r]];
-        __syncthreads();
-        // spare LDS between the sorted points and the permutation holds the deferred-query grid
-        char* gridmem = lds + ((16 * m + 15) & ~15);
-        const PtsF4 v{SPl, idx2};
-#ifdef SSF_TABLE_STAMPS
-        table_walks(P, v, m, plane_max, base, normal, valid, queue, qcap, qlen, gridmem, SI + m + 1,
-                    tstamp0);
-#else
-        table_walks(P, v, m, plane_max, base, normal, valid, queue, qcap, qlen, gridmem);
-#endif
-        SSF_TSTAMP(3);
-    } else if (m <= kLdsSoaMax) {
-        // x | y | z float arrays and a u16 permutation over the sort image (14 m bytes), then the
-        // deferred-query grid and queue.  The permutation is read into registers first: the new
-        // arrays overwrite it.
-        constexpr int kPer = (kLdsSoaMax + kTableThreads - 1) / kTableThreads;
-        int own[kPer];
+    if (m <= kTableStripSoaMax) {
+        // the sorted permutation into registers (the strip layout overwrites the sort image),
+        // then the strip-major points, the strip table and the deferred queue in the 160 KiB
+        const bool soa = m > kTableStripF4Max;                          // uniform
+        int own[kStripPerMax];
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int r = tid + k * kTableThreads;
+        for (int k = 0; k < kStripPerMax; ++k) {
+            const int r = k * kTableThreads + tid;
             own[k] = r < m ? idx[r] : 0;
         }
         __syncthreads();
+        float4* F = reinterpret_cast<float4*>(lds);
         float* X = reinterpret_cast<float*>(lds);
-        float* Y = X + m;
-        float* Z = Y + m;
-        uint16_t* I16 = reinterpret_cast<uint16_t*>(Z + m);
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int r = tid + k * kTableThreads;
-            if (r < m) {
-                const float4 p = P[own[k]];
-                X[r] = p.x; Y[r] = p.y; Z[r] = p.z; I16[r] = (uint16_t)own[k];
-            }
-        }
-        const int goff = (14 * m + 15) & ~15;
-        char* gridmem = lds + goff;
-        const int qoff = (goff + kGridBytes + 2 * m + 15) & ~15;
+        uint16_t* I16 = reinterpret_cast<uint16_t*>(X + 3 * m);
+        const int toff = ((soa ? 14 * m : 16 * m) + 15) & ~15;
+        StripLds& T = *reinterpret_cast<StripLds*>(lds + toff);
+        const int qoff = (toff + (int)sizeof(StripLds) + 15) & ~15;
         int* queue = reinterpret_cast<int*>(lds + qoff);
         const int qcap = ((int)sizeof(lds) - 4 - qoff) / 4;
-        __syncthreads();
-        const PtsSoA v{X, Y, Z, I16};
+        auto get = [&](int k, int) {
+            float4 p = P[own[k]];
+            p.w = __int_as_float(own[k]);
+            return p;
+        };
 #ifdef SSF_TABLE_STAMPS
-        table_walks(P, v, m, plane_max, base, normal, valid, queue, qcap, qlen, gridmem, SI + m + 1,
-                    tstamp0);
+        int32_t* stamp_out = SI + m + 1;
+        const unsigned long long st0 = tstamp0;
 #else
-        table_walks(P, v, m, plane_max, base, normal, valid, queue, qcap, qlen, gridmem);
+        int32_t* stamp_out = nullptr;
+        const unsigned long long st0 = 0;
 #endif
+#ifdef SSF_TABLE_STAMPS
+#define SSF_TSTAMP_BUILD() do { if (tid == 0) stamp_out[3] = (int32_t)((__builtin_amdgcn_s_memtime() - st0) >> 4); } while (0)
+#else
+#define SSF_TSTAMP_BUILD() do { } while (0)
+#endif
+        if (soa) {
+            const StripGeo g = strips_build<true, kStripPerMax>(get, m, T, F, X, I16);
+            SSF_TSTAMP_BUILD();
+            table_strip_walks(P, StripView<true>{F, X, I16, m}, T, g, m, plane_max, base, normal,
+                              valid, queue, qcap, qlen, SP, SI, stamp_out, st0);
+        } else {
+            const StripGeo g = strips_build<false, kStripPerMax>(get, m, T, F, X, I16);
+            SSF_TSTAMP_BUILD();
+            table_strip_walks(P, StripView<false>{F, X, I16, m}, T, g, m, plane_max, base, normal,
+                              valid, queue, qcap, qlen, SP, SI, stamp_out, st0);
+        }
         SSF_TSTAMP(3);
     } else {
         // points from global memory, the permutation in LDS; queue in the (now unused) key region
@@ -1028,20 +1154,6 @@ __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
 // dymin from the strip's actual y extent (fl(qy - yhi) <= fl(qy - py) by monotone rounding, so
 // fl(fl(dx^2) + fl(dymin^2)) <= the float distance); for the ring stop, the nominal strip edge
 // minus 1 mm (float strip assignment).  Candidates compare as (distance, original index).
-constexpr int kStripThreads = 1024;
-constexpr int kStripMax = 256;             // strips per frame (W widened beyond 255 m of y)
-constexpr int kStripWaves = kStripThreads / 64;
-constexpr int kAssocStripF4Max = 6144;     // 16-B points (x, y, z, index) staged: 96 KiB
-constexpr int kAssocStripSoaMax = 10752;   // x | y | z + u16 index (14 B): 147 KiB
-
-struct StripLds {
-    int start[kStripMax + 1];
-    int cursor[kStripMax];
-    float ylo[kStripMax], yhi[kStripMax];
-    uint16_t wc[kStripWaves][kStripMax];
-    float red[2 * kStripWaves];
-};
-
 // kSoa: the strip-major points as x | y | z float arrays and a u16 original index (configs[4]
 // frames); otherwise float4 with the index in .w.  A last frame above the launch's staging
 // capacity walks the x-sorted copy in global memory, unbounded (exact, slow, not expected).
@@ -1056,7 +1168,7 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     int lds_cap) {
     extern __shared__ float4 SL[];                  // [ml] strip-major, x-sorted in each strip
     __shared__ StripLds T;
-    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int p = blockIdx.x, tid = threadIdx.x;
     const int mc = curr_count[p], ml = last_count[p];
     if (mc <= 0 || ml <= 10) return;                                    // uniform (:158)
     const int64_t lo = last_off[p], co = curr_off[p];
@@ -1079,96 +1191,12 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     }
     float* SX = reinterpret_cast<float*>(SL);
     uint16_t* SI16 = reinterpret_cast<uint16_t*>(SX + 3 * ml);
-    // y extent
-    float y0 = __builtin_inff(), y1 = -__builtin_inff();
-    for (int r = tid; r < ml; r += kStripThreads) { const float y = SP[r].y; y0 = fminf(y0, y); y1 = fmaxf(y1, y); }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { y0 = fminf(y0, __shfl_xor(y0, o, 64)); y1 = fmaxf(y1, __shfl_xor(y1, o, 64)); }
-    if (lane == 0) { T.red[2 * w] = y0; T.red[2 * w + 1] = y1; }
-    for (int k = tid; k < kStripWaves * kStripMax; k += kStripThreads) (&T.wc[0][0])[k] = 0;
-    for (int k = tid; k < kStripMax; k += kStripThreads) T.cursor[k] = 0;
-    __syncthreads();
-    y0 = __builtin_inff(); y1 = -__builtin_inff();
-    for (int k = 0; k < kStripWaves; ++k) { y0 = fminf(y0, T.red[2 * k]); y1 = fmaxf(y1, T.red[2 * k + 1]); }
-    const float W = fmaxf(1.0f, (y1 - y0) / (float)(kStripMax - 1));
-    const float invW = 1.0f / W;
-    const int ns = min(kStripMax, (int)((y1 - y0) * invW) + 1);
-    auto strip_of = [&](float y) { return min(ns - 1, max(0, (int)((y - y0) * invW))); };
-    // histogram (cursor holds the counts), exclusive scan into start
-    for (int r = tid; r < ml; r += kStripThreads) atomicAdd(&T.cursor[strip_of(SP[r].y)], 1);
-    __syncthreads();
-    if (w == 0) {
-        const int per = (kStripMax + 63) / 64;                          // 4 strips per lane
-        int run = 0;
-        for (int k = 0; k < per; ++k) run += T.cursor[lane * per + k];
-        int incl = run;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(incl, o, 64); if (lane >= o) incl += y; }
-        int pre = incl - run;
-        for (int k = 0; k < per; ++k) {
-            const int sidx = lane * per + k;
-            T.start[sidx] = pre;
-            pre += T.cursor[sidx];
-            T.cursor[sidx] = T.start[sidx];
-        }
-        if (lane == 63) T.start[kStripMax] = incl;
-    }
-    __syncthreads();
-    // stable scatter, one chunk of kStripThreads points (in x order) at a time
-    for (int c0 = 0; c0 < ml; c0 += kStripThreads) {
-        const int r = c0 + tid;
-        const bool v = r < ml;
-        float4 pt = make_float4(0.f, 0.f, 0.f, 0.f);
-        int sidx = 0;
-        if (v) { pt = SP[r]; pt.w = __int_as_float(SI[r]); sidx = strip_of(pt.y); }
-        uint64_t eq = __ballot(v);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const uint64_t bb = __ballot((sidx >> b) & 1);
-            eq &= ((sidx >> b) & 1) ? bb : ~bb;
-        }
-        const int rank = __popcll(eq & lanemask_lt());
-        if (v && rank == 0) T.wc[w][sidx] = (uint16_t)__popcll(eq);
-        __syncthreads();
-        if (v) {
-            int before = T.cursor[sidx];
-            for (int k = 0; k < w; ++k) before += T.wc[k][sidx];
-            const int dst = before + rank;
-            if (kSoa) {
-                SX[dst] = pt.x; SX[ml + dst] = pt.y; SX[2 * ml + dst] = pt.z;
-                SI16[dst] = (uint16_t)__float_as_int(pt.w);
-            } else {
-                SL[dst] = pt;
-            }
-        }
-        __syncthreads();
-        for (int k = tid; k < kStripMax; k += kStripThreads) {
-            int add = 0;
-            for (int j = 0; j < kStripWaves; ++j) { add += T.wc[j][k]; T.wc[j][k] = 0; }
-            T.cursor[k] += add;
-        }
-        __syncthreads();
-    }
-    struct View {                                  // the strip-major points, either layout
-        const float4* F;
-        const float* X;
-        const uint16_t* I;
-        int m;
-        SSF_DEV float4 pt(int c) const {
-            return kSoa ? make_float4(X[c], X[m + c], X[2 * m + c], 0.f) : F[c];
-        }
-        SSF_DEV float x(int c) const { return kSoa ? X[c] : F[c].x; }
-        SSF_DEV float y(int c) const { return kSoa ? X[m + c] : F[c].y; }
-        SSF_DEV int id(int c) const { return kSoa ? (int)I[c] : __float_as_int(F[c].w); }
-    };
-    const View v{SL, SX, SI16, ml};
-    // actual y extent of every strip (the in-strip lower bound of |dy|)
-    for (int k = tid; k < ns; k += kStripThreads) {
-        float a = __builtin_inff(), b = -__builtin_inff();
-        for (int j = T.start[k]; j < T.start[k + 1]; ++j) { const float y = v.y(j); a = fminf(a, y); b = fmaxf(b, y); }
-        T.ylo[k] = a; T.yhi[k] = b;
-    }
-    __syncthreads();
+    const StripGeo geo = strips_build<kSoa, kStripPerMax>(
+        [&](int, int r) { float4 pt = SP[r]; pt.w = __int_as_float(SI[r]); return pt; }, ml, T, SL, SX, SI16);
+    const float y0 = geo.y0, W = geo.W;
+    const int ns = geo.ns;
+    auto strip_of = [&](float y) { return geo.strip_of(y); };
+    const StripView<kSoa> v{SL, SX, SI16, ml};
     for (int i = tid; i < mc; i += kStripThreads) {
         const float4 pc = curr[co + i];
         const float4 qs = assoc_query_point(pc, q, t);
@@ -1177,7 +1205,7 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
 #ifdef SSF_ASSOC_COUNT
         int vis = 0;
 #endif
-        auto search = [&](int sidx) {
+        auto search = [&](int sidx) __attribute__((always_inline)) {
             const int a = T.start[sidx], b = T.start[sidx + 1];
             if (a >= b) return;
             const float yl = T.ylo[sidx], yh = T.yhi[sidx];

@@ -28,7 +28,7 @@ def main():
     st[:, [0, 1, 3, 4]] *= 16
     for name, red in (("mean", np.mean), ("p90", lambda a: np.percentile(a, 90)), ("max", np.max)):
         print(f"B={B} {name}: m {red(cnt):.0f}; cycles: sort {red(st[:,0]):.3e}  bounded-walks-end "
-              f"{red(st[:,1]):.3e} (queue {red(st[:,2]):.0f})  grid-built {red(st[:,4]):.3e}  end {red(st[:,3]):.3e}")
+              f"{red(st[:,1]):.3e} (queue {red(st[:,2]):.0f})  strips-built {red(st[:,4]):.3e}  end {red(st[:,3]):.3e}")
     f = int(np.argmax(st[:, 3]))
     print(f"slowest frame {f}: m {cnt[f]} sort {st[f,0]:.3e} bounded {st[f,1]:.3e} queue {st[f,2]:.0f} end {st[f,3]:.3e}")
 

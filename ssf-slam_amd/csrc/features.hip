@@ -248,7 +248,10 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
 // groups; loads clamped and unconditional) keep three groups in flight: a rotation by register
 // moves, or a load or store under a branch, makes the compiler wait for every load at each
 // group.  The selected indices collect in LDS and leave once per trip.
-constexpr int kCurvRowsPerWG = 4;
+#ifndef SSF_CURV_ROWS_PER_WG
+#define SSF_CURV_ROWS_PER_WG 4
+#endif
+constexpr int kCurvRowsPerWG = SSF_CURV_ROWS_PER_WG;
 #ifndef SSF_CURV_DEPTH
 #define SSF_CURV_DEPTH 3
 #endif
@@ -288,7 +291,7 @@ SSF_DEV void stencil11w(const float4* a, int j, float& dx, float& dy, float& dz)
 // greedy in index order, curvature > edge_min, spacing edge_span (the mirror image of :110-123;
 // oracle/edge_oracle.c) -- into esel / esel_cnt.
 template <bool kCurv, int kHalves, bool kEdge>
-__global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__ frame_off,
+__global__ __launch_bounds__(64 * kCurvRowsPerWG) void k_curv_select(const int64_t* __restrict__ frame_off,
                                                      int n_rows, int row_start, int row_end,
                                                      float plane_min, int plane_span,
                                                      const int32_t* __restrict__ ring_off,

@@ -329,7 +329,11 @@ int32_t ssf_reserve(ssf_ctx* c, int32_t max_frames, int64_t max_points_per_frame
         SSF_TRY_HIP(c, ds.d.ensure(sizeof(double) * 3 * (size_t)std::max(max_frames, 1)), "alloc draws");
         SSF_TRY_HIP(c, ds.rec.ensure(sizeof(uint2) * (size_t)(total + 2 * (int64_t)max_frames + 2) + sizeof(uint32_t) * (size_t)(total + 64 * (int64_t)max_frames)), "alloc lloyd records");
         SSF_TRY_HIP(c, ds.sync.ensure(ssf::mask_sync_bytes(std::max(max_frames, 1)) + 16), "alloc mask sync");
-        SSF_TRY_HIP(c, ds.parts.ensure(ssf::mask_parts_bytes(std::max(max_frames, 1), 8)), "alloc mask parts");
+        // exchange slots of the automatic split for max_frames (a fixed split grows them on demand)
+        if (c->mask_slots < 0) c->mask_slots = ssf::mask_pose_slots(c->device);
+        const int g_auto = std::max(1, std::min(8, c->mask_slots > 0 ? c->mask_slots / std::max(max_frames, 1) : 1));
+        const size_t pb = ssf::mask_parts_bytes(std::max(max_frames, 1), g_auto);
+        if (pb) SSF_TRY_HIP(c, ds.parts.ensure(pb), "alloc mask parts");
     }
     return SSF_OK;
 }

@@ -435,19 +435,27 @@ __device__ __noinline__ int kabsch_finish(const double* k, const double cs[3], c
 // frame holds the same bits and runs the same lane-0 algebra to the same decisions
 // (cdna_hip_programming.md Guideline 16, MI355X_MICROARCH.md "Valid forms", row 1: one
 // storing wave, one atomic-add signal, sc1 polls and sc1 loads, one work-group per CU).
-// Slots are double-buffered by exchange parity: a part can run at most one exchange ahead of a
-// reader of the previous one.  Work-groups take (frame, part) tickets in order from a counter,
-// so every partly started frame has its parts on resident work-groups and the ones it waits for
-// are taken by the next work-group that becomes free (no wait on a work-group that cannot be
-// dispatched).  A bounded spin turns a lost partner into status SSF_POSE_SYNC_FAILED, never a hang.
+// Every exchange of a launch has its OWN slot lines (slot = exchange index), never a line
+// rewritten in the launch: an sc1 load bypasses the CU's L1 but is served by the reader XCD's
+// L2 when that L2 already holds the line, and another XCD's sc1 store does not reach that copy.
+// Measured on MI355X with a work-sharing variant of this kernel that re-read rewritten
+// parameter lines across XCDs: 375-810 stale reads per 256-frame launch.  A
+// line read here for the first time cannot be cached stale.
+// Work-groups take (frame, part) tickets in order from a counter, so every partly started frame
+// has its parts on resident work-groups and the ones it waits for are taken by the next
+// work-group that becomes free (no wait on a work-group that cannot be dispatched).  A bounded
+// spin turns a lost partner into status SSF_POSE_SYNC_FAILED, never a hang.
 constexpr int kSlot = 32;                         // doubles per part and exchange
 constexpr int kMaxSplit = 8;                      // parts per frame at most
 constexpr uint32_t kSpinLimit = 1u << 24;         // x s_sleep 2 (~128 cycles): ~1 s
+// exchanges per frame at most: pass 0, 3 in k-means++, one per Lloyd iteration (<= 300), the
+// GMM init, one per EM iteration (<= 100), the final pass
+constexpr int kMaxExchanges = 1 + 3 + 300 + 1 + 100 + 1;
 
 struct Split {
     int G, g;                  // parts per frame, this work-group's part
     int64_t r0, r1;            // its points [r0, r1) of the frame
-    double* part;              // the frame's slots [2][G][kSlot]
+    double* part;              // the frame's slots [kMaxExchanges][G][kSlot]
     uint32_t* arrive;          // the frame's arrival counter (monotonic over its exchanges)
     uint32_t seq;              // exchanges done (uniform)
 };
@@ -456,7 +464,8 @@ template <int N, bool kMin = false>
 SSF_DEV bool exchange(Split& X, double (&v)[N], double* tmp, int* okflag) {
     static_assert(N <= kSlot, "exchange: N <= kSlot");
     if (X.G == 1) return true;
-    double* slot = X.part + (size_t)(X.seq & 1u) * (size_t)X.G * kSlot;
+    if (X.seq >= (uint32_t)kMaxExchanges) return false;   // cannot happen (iteration caps); never reuse a line
+    double* slot = X.part + (size_t)X.seq * (size_t)X.G * kSlot;
 #pragma unroll
     for (int k = 0; k < N; ++k)
         if (threadIdx.x == (unsigned)k)
@@ -551,7 +560,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         X.r0 = min(n, (int64_t)g * chunk);
         X.r1 = min(n, X.r0 + chunk);
     }
-    X.part = parts + (size_t)f * 2 * (size_t)G * kSlot;
+    X.part = parts + (size_t)f * kMaxExchanges * (size_t)G * kSlot;
     X.arrive = sync + 4 + f;
     X.seq = 0;
     const int64_t r0 = X.r0, r1 = X.r1;
@@ -1304,7 +1313,9 @@ int mask_pose_slots(int device) {
 }
 
 size_t mask_sync_bytes(int n_frames) { return (size_t)(4 + n_frames) * sizeof(uint32_t); }
-size_t mask_parts_bytes(int n_frames, int G) { return (size_t)n_frames * 2 * G * kSlot * sizeof(double); }
+size_t mask_parts_bytes(int n_frames, int G) {
+    return G > 1 ? (size_t)n_frames * kMaxExchanges * G * kSlot * sizeof(double) : 0;
+}
 
 hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,
                             const int64_t* frame_off, int mode, const uint8_t* mask_in,

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--splits", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--distinct", type=int, default=32)
+    ap.add_argument("--dump", default=None, help="write the first split's outputs (out, mask) to this .npz")
     a = ap.parse_args()
     import ssf
     from ssf import synth
@@ -57,6 +58,9 @@ def main():
                    km_iter=float(o[:, 19].mean()), em_iter=float(o[:, 20].mean()))
         if ref is None:
             ref = (o.clone(), bg.cpu().clone())
+            if a.dump:
+                import numpy as np
+                np.savez(a.dump, out=o.numpy(), bg=bg.cpu().numpy())
         else:
             row["labels_equal_split1"] = float((bg.cpu() == ref[1]).float().mean())
             row["iters_equal_split1"] = bool(torch.equal(o[:, 19:21], ref[0][:, 19:21]))

@@ -330,6 +330,9 @@ SSF_DEV double uni(double v) {
 
 // Lloyd only: D points in flight per thread (a rolling register buffer of raw floats).  Each
 // thread visits its points in the same order as for_points, so every sum is bit-identical.
+// fn(i, x, val) runs for every slot of the last trip too (val = false past r1, x = the clamped
+// last point): a store under a branch in a streaming loop made the compiler drain the prefetches
+// at the join (the record-writing full pass took 411 k cycles against 264 k without records).
 template <int D, class Ts, class Fn>
 SSF_DEV void for_points_deep(const Ts* __restrict__ P, const Ts* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
     const int64_t T = blockDim.x;
@@ -348,7 +351,7 @@ SSF_DEV void for_points_deep(const Ts* __restrict__ P, const Ts* __restrict__ Fl
 #pragma unroll
             for (int k = 0; k < 6; ++k) x[k] = (double)buf[d][k];
             load_raw(P, Fl, min(i + D * T, r1 - 1), buf[d]);
-            if (i < r1) fn(i, x);
+            fn(i, x, i < r1);   // every slot (no branch around the body's stores); val = 0 is weighted out
         }
     }
 }
@@ -978,7 +981,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             // from the previous centres (the pass that wrote it used the same expression)
             const double cpn0 = uni(S.csnp[0]), cpn1 = uni(S.csnp[1]);
             auto full_pass = [&](auto wrec_c) {
-                for_points_deep<kLloydDeep>(P, Fl, r0, r1, [&](int64_t i, const double* x) {
+                for_points_deep<kLloydDeep>(P, Fl, r0, r1, [&](int64_t i, const double* x, bool val) {
                     const LdsDouble* cenp = lds_laundered(S.cenp);
                     double dp0 = 0.0, dp1 = 0.0;
 #pragma unroll
@@ -987,7 +990,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
                         dp0 += v * cenp[d]; dp1 += v * cenp[6 + d];
                     }
                     const int lp = (-2.0 * dp1 + cpn1) < (-2.0 * dp0 + cpn0) ? 1 : 0;
-                    label(wrec_c, i, x, lp, true);
+                    label(wrec_c, i, x, lp, val);
                 });
             };
             if (wrec) full_pass(std::true_type{});    // two loop bodies: no branch per point

@@ -3,7 +3,7 @@ on the bench's workload: B distinct synthetic sequences (ssf/synth.py), frame k 
 an npz with the per-frame stamps and iteration counts, used to size the straggler work (how long
 the slowest frames run against the mean, and in which phase).
 
-    SSF_LIB=ssf-slam_amd/ssf/_lib/libssf_frontend_diag.so python tools/diag_mask_frames.py OUT.npz [B [help mode]]
+    SSF_LIB=ssf-slam_amd/ssf/_lib/libssf_frontend_diag.so python tools/diag_mask_frames.py OUT.npz [B]
 """
 import os
 import sys
@@ -28,9 +28,6 @@ def main():
     flow = torch.cat([f["flow"] for f in fr]).contiguous()
     off, h_off = ssf.frame_offsets([f["pos1"].shape[0] for f in fr], dev)
     fe = ssf.Frontend(64, device=0)
-    if len(sys.argv) > 3:
-        fe.mask_split(1)
-        fe.mask_help(int(sys.argv[3]))
     fe.seed(1)
     fe.mask_pose(pts, flow, off, h_off)
     torch.cuda.synchronize()

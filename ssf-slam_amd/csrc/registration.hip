@@ -415,6 +415,28 @@ SSF_DEV int bounded_decides(const float4* __restrict__ P, int m, const double (&
     return nq >= 2 ? 1 : 0;
 }
 
+// A deferred query (6 <= K1 < 30 keys inside 1 m, fewer than two other-ring points among ranks
+// 5..K1-1) has a valid plane only if NO point of ranks K1..29 lies on another ring (0..63):
+// the pick (lidarOdometry_onlyPC.cpp:180-198) takes the first such point, n becomes its rank and
+// dis2[n] >= 1 fails :207.  If none is there, n is a rank inside 1 m and the plane uses only
+// points inside 1 m.  kk is exact for every key closer than lim.  Returns 1 when the list
+// is complete (table_finish decides), 2 when an other-ring point among the exact ranks >= K1
+// decides it invalid, 0 when the ranks beyond lim are still needed.
+SSF_DEV int deferred_decides(const float4* __restrict__ P, const double (&kk)[kK], float lim) {
+    if (key_dist(kk[kK - 1]) < lim) return 1;
+    const int prow = row_of(P[key_index(kk[0])].w);
+    int dec = 0;
+#pragma unroll
+    for (int k = 5; k < kK; ++k) {
+        const float d = key_dist(kk[k]);
+        if (d >= 1.0f && d < lim) {
+            const int row = row_of(P[key_index(kk[k])].w);
+            if (row != prow && row >= 0 && row <= 63) dec = 2;
+        }
+    }
+    return dec;
+}
+
 SSF_DEV void table_finish(const float4* __restrict__ P, int m, float plane_max, int64_t o,
                           const double (&kk)[kK], float* __restrict__ normal,
                           uint8_t* __restrict__ valid) {
@@ -674,6 +696,13 @@ SSF_DEV void strip_knn_radius(const StripView<kSoa>& v, const StripLds& T, const
 #define SSF_DEFER_RINGS 6
 #endif
 constexpr int kDeferRings = SSF_DEFER_RINGS;     // deferred queries: strips within this many metres
+#ifndef SSF_DEFER_FIRST
+#define SSF_DEFER_FIRST 2
+#endif
+#ifndef SSF_DEFER_MID
+#define SSF_DEFER_MID 0
+#endif
+constexpr int kDeferFirst = SSF_DEFER_FIRST;     // ... searched first within this many metres
 
 SSF_DEV void table_deferred_walk(const float4* __restrict__ P, const float4* __restrict__ SP,
                                  const int32_t* __restrict__ SI, int m, int qi, const float4& q,
@@ -727,12 +756,28 @@ SSF_DEV void table_strip_walks(const float4* __restrict__ P, const StripView<kSo
         const int j = queue[k];
         const float4 q = v.pt(j);
         double kk[kK];
-        // within 4 m from the strips (exact when the 30th key is closer than 4 m), else the
-        // x-sorted global copy, unbounded
-        strip_knn_radius<kDeferRings>(v, T, g, j, q, kk);
-        if (!(key_dist(kk[kK - 1]) < (float)(kDeferRings * kDeferRings)))
-            table_deferred_walk(P, SP, SI, m, v.id(j), q, kk);
-        table_finish(P, m, plane_max, base + v.id(j), kk, normal, valid);
+        // within 2 m, then within kDeferRings m, from the strips: decided as soon as the exact
+        // part of the list settles it (deferred_decides); else the x-sorted global copy, unbounded
+        strip_knn_radius<kDeferFirst>(v, T, g, j, q, kk);
+        int dec = deferred_decides(P, kk, (float)(kDeferFirst * kDeferFirst));
+#if SSF_DEFER_MID
+        if (dec == 0) {
+            strip_knn_radius<SSF_DEFER_MID>(v, T, g, j, q, kk);
+            dec = deferred_decides(P, kk, (float)(SSF_DEFER_MID * SSF_DEFER_MID));
+        }
+#endif
+        if (dec == 0) {
+            strip_knn_radius<kDeferRings>(v, T, g, j, q, kk);
+            dec = deferred_decides(P, kk, (float)(kDeferRings * kDeferRings));
+        }
+        if (dec == 0) table_deferred_walk(P, SP, SI, m, v.id(j), q, kk);
+        const int64_t o = base + v.id(j);
+        if (dec == 2) {
+            normal[3 * o] = 0.f; normal[3 * o + 1] = 0.f; normal[3 * o + 2] = 0.f;
+            valid[o] = 0;
+        } else {
+            table_finish(P, m, plane_max, o, kk, normal, valid);
+        }
     }
 }
 

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--distinct", type=int, default=16)
     ap.add_argument("--chain", action="store_true", help="also plane table + registration")
     ap.add_argument("--tag", default=os.environ.get("SSF_LIB", "default"))
+    ap.add_argument("--dump", default=None, help="with --chain: write the last plane table (normals, validity) "
+                    "and registration poses to this .npz")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic library (-DSSF_SOLVE_STAMPS): print k_solve phase cycles")
     a = ap.parse_args()
@@ -58,6 +60,9 @@ def main():
                                                   "first_eval": float(lg[:, 1].mean()),
                                                   "iterations": float(lg[:, 2].mean())}}))
     t = fe.kernel_times()
+    if a.dump and a.chain:
+        import numpy as np
+        np.savez(a.dump, normal=t0[0].cpu().numpy(), valid=t0[1].cpu().numpy(), pose=res["pose_rel"].cpu().numpy())
     print(json.dumps({"tag": a.tag, "batch": B, "points": N,
                       "kernel_ms": {k: round(ms / n, 4) for k, (n, ms) in sorted(t.items())}}))
 

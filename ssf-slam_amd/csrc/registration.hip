@@ -527,7 +527,9 @@ struct StripView {
     SSF_DEV float4 pt(int c) const { return kSoa ? make_float4(X[c], X[m + c], X[2 * m + c], 0.f) : F[c]; }
     SSF_DEV float x(int c) const { return kSoa ? X[c] : F[c].x; }
     SSF_DEV float y(int c) const { return kSoa ? X[m + c] : F[c].y; }
-    SSF_DEV int id(int c) const { return kSoa ? (int)I[c] : __float_as_int(F[c].w); }
+    // 16-B layout: original index in the low 16 bits of .w; the plane table packs the point's
+    // ring code (row_code) in bits 16..23
+    SSF_DEV int id(int c) const { return kSoa ? (int)I[c] : (__float_as_int(F[c].w) & 0xFFFF); }
 };
 
 constexpr int kStripPerMax = kSortMax / kStripThreads;   // x-order points per thread (16)
@@ -715,6 +717,295 @@ SSF_DEV void table_deferred_walk(const float4* __restrict__ P, const float4* __r
     knn_walk(PtsF4{SP, SI}, m, l, q, false, kk);
 }
 
+// ---- the plane table's pick without the 30-key list (16-B strip layout) ---------------------
+// The pick (lidarOdometry_onlyPC.cpp:180-207) reads, from the sorted 30-NN list: the ranks 0..4,
+// prow = the row of rank 0, and in rank order from rank 5 the first two points on another ring
+// (0..63); n = the rank of the last one found (5 if none) must satisfy d2[n] < 1.  With K1 = the
+// number of points within 1 m (the query itself included):
+//   K1 <= 5                      -> invalid (n >= 5 >= K1);
+//   D1 < D2: the two smallest keys of other-ring points of rank >= 5 within 1 m;
+//   K1 >= 30                     -> n = rank of the last of D1, D2 whose rank (= number of keys
+//                                   below it) is < 30, else 5; always valid-gated (d2 < 1);
+//   K1 < 30, D2 found            -> n = rank(D2) < K1, D1 and D2 replace ranks 3 and 4;
+//   K1 < 30, D2 not found        -> the ranks K1..29 lie beyond 1 m: the plane is invalid iff
+//                                   an other-ring point has rank < 30, i.e. iff E, the smallest
+//                                   key of an other-ring point beyond 1 m, has fewer than
+//                                   30 - K1 keys beyond 1 m below it; else valid with D1 (if any).
+// The planes are computed from the same five points as plane_from_knn; each stage walks the
+// strips with a few registers instead of inserting every candidate into a 30-key list.
+constexpr uint32_t kRowCodeBad = 255u;
+SSF_DEV uint32_t row_code(float fi) {
+    const int r = row_of(fi);
+    return (r >= 0 && r < (int)kRowCodeBad) ? (uint32_t)r : kRowCodeBad;
+}
+SSF_DEV int pt_row(const float4& p) { return (__float_as_int(p.w) >> 16) & 0xFF; }
+SSF_DEV int pt_id(const float4& p) { return __float_as_int(p.w) & 0xFFFF; }
+
+// Visit the points of one strip with dx^2 + dy_lb^2 <= bound() (bound re-read at every step)
+// and < lim, from q's x position (start: the query's own strip position, or -1 = binary search).
+// start: in, the query's own strip position or a position found before; -1: binary search
+// (the result is stored back, so later walks of the same strip skip the search).
+template <class Bound, class Body>
+SSF_DEV void strip_visit(const StripView<false>& v, const StripLds& T, int sidx, int& start, const float4& q,
+                         float lim, Bound&& bound, Body&& body) {
+    const int a = T.start[sidx], b = T.start[sidx + 1];
+    if (a >= b) return;
+    const float yl = T.ylo[sidx], yh = T.yhi[sidx];
+    const float dyl = q.y < yl ? yl - q.y : (q.y > yh ? q.y - yh : 0.0f);
+    const float dy2 = dyl * dyl;
+    if (dy2 > bound() || dy2 >= lim) return;
+    int l = start;
+    if (l < 0) {
+        l = a;
+        int h = b;
+        while (l < h) {
+            const int mid = (l + h) >> 1;
+            if (v.F[mid].x < q.x) l = mid + 1; else h = mid;
+        }
+        start = l;
+    }
+    // the next record is read while the current one is processed (clamped: always in the strip)
+    if (l < b) {
+        float4 pn = v.F[l];
+        for (int c = l; c < b; ++c) {
+            const float4 p = pn;
+            pn = v.F[min(c + 1, b - 1)];
+            const float dx = q.x - p.x;
+            const float t = dx * dx + dy2;
+            if (t > bound() || t >= lim) break;
+            body(p);
+        }
+    }
+    if (l > a) {
+        float4 pn = v.F[l - 1];
+        for (int c = l - 1; c >= a; --c) {
+            const float4 p = pn;
+            pn = v.F[max(c - 1, a)];
+            const float dx = q.x - p.x;
+            const float t = dx * dx + dy2;
+            if (t > bound() || t >= lim) break;
+            body(p);
+        }
+    }
+}
+
+// The 1-m region: the query's strip and its two neighbours (strip width > 1 m).
+// pos[3]: the start positions in the query's strip (its own) and the neighbours (-1 until found).
+template <class Bound, class Body>
+SSF_DEV void visit_1m(const StripView<false>& v, const StripLds& T, const StripGeo& g, int (&pos)[3],
+                      const float4& q, Bound&& bound, Body&& body) {
+    const int s0 = g.strip_of(q.y);
+    strip_visit(v, T, s0, pos[0], q, 1.0f, bound, body);
+    if (s0 + 1 < g.ns) strip_visit(v, T, s0 + 1, pos[1], q, 1.0f, bound, body);
+    if (s0 - 1 >= 0) strip_visit(v, T, s0 - 1, pos[2], q, 1.0f, bound, body);
+}
+
+// Every strip outward from q's, in rings of strips, while a strip can still hold a point with
+// d2 <= bound(): strip s0 +- r has |dy| >= (r - 1) W (less 1 mm of rounding slack).
+template <class Bound, class Body>
+SSF_DEV void visit_all(const StripView<false>& v, const StripLds& T, const StripGeo& g, int self, const float4& q,
+                       Bound&& bound, Body&& body) {
+    const float inf = __builtin_inff();
+    const int s0 = g.strip_of(q.y);
+    int p0 = self;
+    strip_visit(v, T, s0, p0, q, inf, bound, body);
+    for (int r = 1; r < g.ns; ++r) {
+        const float lb = (float)(r - 1) * g.W - 0.001f;
+        if (lb > 0.0f && lb * lb > bound()) break;
+        int pu = -1, pd = -1;
+        if (s0 + r < g.ns) strip_visit(v, T, s0 + r, pu, q, inf, bound, body);
+        if (s0 - r >= 0) strip_visit(v, T, s0 - r, pd, q, inf, bound, body);
+    }
+}
+
+// The plane of the five picked points: plane_from_knn from the least-squares solve on
+// (identical arithmetic).
+SSF_DEV void plane_from_pick(const float4* __restrict__ P, const int (&v5)[5], float plane_max, float nrm[3],
+                             uint8_t& ok) {
+    float Am[3][5];
+    float pts[5][3];
+    for (int j = 0; j < 5; ++j) {
+        const float4 p = P[v5[j]];
+        pts[j][0] = p.x; pts[j][1] = p.y; pts[j][2] = p.z;
+        Am[0][j] = p.x; Am[1][j] = p.y; Am[2][j] = p.z;
+    }
+    qr_solve_5x3(Am, nrm);                                             // :219
+    float z = nrm[0] * nrm[0] + nrm[1] * nrm[1];
+    z = z + nrm[2] * nrm[2];
+    if (z > 0.0f) {                                                    // :220
+        const float sq = sqrtf(z);
+        nrm[0] = nrm[0] / sq; nrm[1] = nrm[1] / sq; nrm[2] = nrm[2] / sq;
+    }
+    ok = 1;
+    for (int k = 0; k < 4; ++k) {                                      // :222-232
+        const double vx = (double)(pts[k][0] - pts[k + 1][0]);
+        const double vy = (double)(pts[k][1] - pts[k + 1][1]);
+        const double vz = (double)(pts[k][2] - pts[k + 1][2]);
+        double dd = (double)nrm[0] * vx + (double)nrm[1] * vy;
+        dd = dd + (double)nrm[2] * vz;
+        if (fabs(dd) > (double)plane_max) { ok = 0; break; }
+    }
+}
+
+struct PickState {
+    int pos[3];         // strip start positions of the 1-m region (visit_1m)
+    double t5[5];       // ranks 0..4
+    double d1, d2;      // the first two other-ring keys of rank >= 5 within 1 m (sentinel: 1 m)
+    int K1, prow;
+};
+
+// Inside 1 m for query j, one walk: K1, the top five, and the six smallest keys of points on
+// another ring than the query's own (at most four of them can be in the top five, so D1 / D2 are
+// the first two of them above rank 4).  prow is the ring of rank 0: the query itself unless an
+// exact duplicate with a lower index precedes it -- then a second walk with that ring.
+SSF_DEV void pick_1m(const float4* __restrict__ P, const StripView<false>& v, const StripLds& T, const StripGeo& g,
+                     int j, const float4& q, PickState& s) {
+    const double sent = knn_key(1.0f, 0x7fffffff);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) s.t5[k] = sent;
+    double o6[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) o6[k] = sent;
+    const int qrow = pt_row(q);
+    int K1 = 0;
+    s.pos[0] = j; s.pos[1] = -1; s.pos[2] = -1;
+    visit_1m(v, T, g, s.pos, q, [] { return 1.0f; }, [&](const float4& p) {
+        const float d = l2_simple(q, p);
+        if (d < 1.0f) {
+            const double key = knn_key(d, pt_id(p));
+            ++K1;
+            key_insert<5>(s.t5, key);
+            const int row = pt_row(p);
+            if (row != qrow && row <= 63) key_insert<6>(o6, key);
+        }
+    });
+    s.K1 = K1;
+    s.d1 = sent; s.d2 = sent;
+    s.prow = -1;
+    if (K1 <= 5) return;
+    s.prow = row_of(P[key_index(s.t5[0])].w);
+    const double k5 = s.t5[4];
+    if (key_index(s.t5[0]) == pt_id(q) || s.prow == qrow) {
+        // D1, D2: the first two of o6 above rank 4
+        int c = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) c += o6[k] <= k5;
+        double a = sent, b = sent;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            if (k == c) { a = o6[k]; b = o6[k + 1]; }
+        }
+        s.d1 = a; s.d2 = b;
+        return;
+    }
+    const int prow = s.prow;
+    double dd[2] = {sent, sent};
+    visit_1m(v, T, g, s.pos, q, [&] { return key_dist(dd[1]); }, [&](const float4& p) {
+        const float d = l2_simple(q, p);
+        const int row = pt_row(p);
+        const double key = knn_key(d, pt_id(p));
+        if (d < 1.0f && key > k5 && row != prow && row <= 63) key_insert<2>(dd, key);
+    });
+    s.d1 = dd[0]; s.d2 = dd[1];
+}
+
+SSF_DEV void pick_finish(const float4* __restrict__ P, const PickState& s, int nvr, float plane_max, int64_t o,
+                         float* __restrict__ normal, uint8_t* __restrict__ valid) {
+    int v5[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v5[k] = key_index(s.t5[k]);
+    if (nvr == 1) v5[4] = key_index(s.d1);                             // :199-205
+    if (nvr == 2) { v5[3] = key_index(s.d1); v5[4] = key_index(s.d2); }
+    float nrm[3];
+    uint8_t ok;
+    plane_from_pick(P, v5, plane_max, nrm, ok);
+    normal[3 * o] = nrm[0]; normal[3 * o + 1] = nrm[1]; normal[3 * o + 2] = nrm[2];
+    valid[o] = ok;
+}
+
+SSF_DEV void pick_invalid(int64_t o, float* __restrict__ normal, uint8_t* __restrict__ valid) {
+    normal[3 * o] = 0.f; normal[3 * o + 1] = 0.f; normal[3 * o + 2] = 0.f;
+    valid[o] = 0;
+}
+
+// Beyond 1 m (K1 < 30, fewer than two other-ring points inside): invalid iff E, the smallest
+// key of an other-ring point beyond 1 m, has fewer than 30 - K1 keys beyond 1 m below it.
+SSF_DEV bool pick_beyond_invalid(const StripView<false>& v, const StripLds& T, const StripGeo& g, int j,
+                                 const float4& q, const PickState& s) {
+    double E = knn_key(__builtin_inff(), 0x7fffffff);
+    const int prow = s.prow;
+    visit_all(v, T, g, j, q, [&] { return key_dist(E); }, [&](const float4& p) {
+        const float d = l2_simple(q, p);
+        const int row = pt_row(p);
+        const double key = knn_key(d, pt_id(p));
+        if (d >= 1.0f && row != prow && row <= 63 && key < E) E = key;
+    });
+    if (!(key_dist(E) < __builtin_inff())) return false;          // no other-ring point at all
+    int C = 0;
+    const int need = 30 - s.K1;
+    const float lim = key_dist(E);
+    visit_all(v, T, g, j, q, [&] { return C >= need ? -1.0f : lim; }, [&](const float4& p) {
+        const float d = l2_simple(q, p);
+        C += (d >= 1.0f && knn_key(d, pt_id(p)) < E);
+    });
+    return C < need;
+}
+
+// Whole work-group: every query of the frame (m > 30, every ring code < 255).  Queries that need
+// points beyond 1 m (K1 < 30, fewer than two other-ring points inside) are queued and finished
+// afterwards, spread over the waves.
+SSF_DEV void table_pick_walks(const float4* __restrict__ P, const StripView<false>& v, const StripLds& T,
+                              const StripGeo& g, int m, float plane_max, int64_t base, float* __restrict__ normal,
+                              uint8_t* __restrict__ valid, int* queue, int qcap, int* qlen,
+                              int32_t* stamp_out = nullptr, unsigned long long stamp0 = 0) {
+    for (int j = threadIdx.x; j < m; j += blockDim.x) {
+        const float4 q = v.pt(j);
+        const int64_t o = base + v.id(j);
+        PickState s;
+        pick_1m(P, v, T, g, j, q, s);
+        if (s.K1 <= 5) { pick_invalid(o, normal, valid); continue; }
+        const bool f1 = key_dist(s.d1) < 1.0f, f2 = key_dist(s.d2) < 1.0f;
+        if (s.K1 >= 30) {
+            int r1 = 0, r2 = 0;                                            // ranks of D1, D2
+            if (f1) {
+                const double b1 = s.d1, b2 = s.d2;
+                const float lim = f2 ? key_dist(b2) : key_dist(b1);
+                visit_1m(v, T, g, s.pos, q, [&] { return lim; }, [&](const float4& p) {
+                    const double key = knn_key(l2_simple(q, p), pt_id(p));
+                    r1 += key < b1;
+                    r2 += key < b2;
+                });
+            }
+            const int nvr = (f1 && r1 < 30) + (f2 && r2 < 30);
+            pick_finish(P, s, nvr, plane_max, o, normal, valid);
+        } else if (f2) {
+            pick_finish(P, s, 2, plane_max, o, normal, valid);
+        } else {
+            const int slot = atomicAdd(qlen, 1);
+            if (slot < qcap) { queue[slot] = j; continue; }
+            if (pick_beyond_invalid(v, T, g, j, q, s)) pick_invalid(o, normal, valid);   // queue full
+            else pick_finish(P, s, f1 ? 1 : 0, plane_max, o, normal, valid);
+        }
+    }
+    __syncthreads();
+#ifdef SSF_TABLE_STAMPS
+    if (threadIdx.x == 0 && stamp_out) { stamp_out[0] = (int32_t)((__builtin_amdgcn_s_memtime() - stamp0) >> 4); stamp_out[1] = *qlen; }
+#endif
+    const int nq = min(*qlen, qcap);
+    const int nw = blockDim.x >> 6, t2 = (threadIdx.x & 63) * nw + (threadIdx.x >> 6);
+    for (int k = t2; k < nq; k += blockDim.x) {
+        const int j = queue[k];
+        const float4 q = v.pt(j);
+        const int64_t o = base + v.id(j);
+        PickState s;
+        pick_1m(P, v, T, g, j, q, s);
+        const bool f1 = key_dist(s.d1) < 1.0f;
+        const bool inval = pick_beyond_invalid(v, T, g, j, q, s);
+        if (inval) pick_invalid(o, normal, valid);
+        else pick_finish(P, s, f1 ? 1 : 0, plane_max, o, normal, valid);
+    }
+}
+
 // The deferred few (no decision inside 1 m: sparse, far regions) walk the x-sorted copy the
 // sort left in global memory (SP / SI, L2-resident), unbounded, from their x rank (binary
 // search on (x, index)): a strip ring search there would need a loop nest whose register
@@ -874,10 +1165,34 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
             table_strip_walks(P, StripView<true>{F, X, I16, m}, T, g, m, plane_max, base, normal,
                               valid, queue, qcap, qlen, SP, SI, stamp_out, st0);
         } else {
-            const StripGeo g = strips_build<false, kStripPerMax>(get, m, T, F, X, I16);
+            // 16-B records carry the ring code of every point (bits 16..23 of .w): the pick then
+            // runs without the 30-key list (table_pick_walks) unless the frame is tiny or a ring
+            // code is out of range (intensities frameFeature never writes)
+            bool rows_ok = true;
+#pragma unroll
+            for (int k = 0; k < kStripPerMax; ++k) {
+                const int r = k * kTableThreads + tid;
+                if (r < m) rows_ok = rows_ok && row_code(P[own[k]].w) != kRowCodeBad;
+            }
+            int* rflag = reinterpret_cast<int*>(lds + sizeof(lds) - 8);   // next to qlen, free here
+            if (tid == 0) *rflag = 1;
+            __syncthreads();
+            if (!rows_ok) *rflag = 0;
+            __syncthreads();
+            rows_ok = *rflag != 0;
+            auto getp = [&](int k, int) {
+                float4 p = P[own[k]];
+                p.w = __int_as_float(own[k] | (int)(row_code(p.w) << 16));
+                return p;
+            };
+            const StripGeo g = strips_build<false, kStripPerMax>(getp, m, T, F, X, I16);
             SSF_TSTAMP_BUILD();
-            table_strip_walks(P, StripView<false>{F, X, I16, m}, T, g, m, plane_max, base, normal,
-                              valid, queue, qcap, qlen, SP, SI, stamp_out, st0);
+            if (rows_ok && m > kK)
+                table_pick_walks(P, StripView<false>{F, X, I16, m}, T, g, m, plane_max, base, normal, valid,
+                                 queue, qcap, qlen, stamp_out, st0);
+            else
+                table_strip_walks(P, StripView<false>{F, X, I16, m}, T, g, m, plane_max, base, normal,
+                                  valid, queue, qcap, qlen, SP, SI, stamp_out, st0);
         }
         SSF_TSTAMP(3);
     } else {

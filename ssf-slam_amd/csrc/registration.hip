@@ -1577,25 +1577,34 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
                 const int mid = (l + h) >> 1;
                 if (v.x(mid) < qs.x) l = mid + 1; else h = mid;
             }
-            for (int c = l; c < b; ++c) {
-                const float4 pl = v.pt(c);
-                const float dx = qs.x - pl.x;
-                if (dx * dx + dy2 > best) break;
-                const float d = l2_simple(qs, pl);
-                if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
+            // the next record is read while the current one is processed (clamped into the strip)
+            if (l < b) {
+                float4 pn = v.pt(l);
+                for (int c = l; c < b; ++c) {
+                    const float4 pl = pn;
+                    pn = v.pt(min(c + 1, b - 1));
+                    const float dx = qs.x - pl.x;
+                    if (dx * dx + dy2 > best) break;
+                    const float d = l2_simple(qs, pl);
+                    if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
 #ifdef SSF_ASSOC_COUNT
-                ++vis;
+                    ++vis;
 #endif
+                }
             }
-            for (int c = l - 1; c >= a; --c) {
-                const float4 pl = v.pt(c);
-                const float dx = qs.x - pl.x;
-                if (dx * dx + dy2 > best) break;
-                const float d = l2_simple(qs, pl);
-                if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
+            if (l > a) {
+                float4 pn = v.pt(l - 1);
+                for (int c = l - 1; c >= a; --c) {
+                    const float4 pl = pn;
+                    pn = v.pt(max(c - 1, a));
+                    const float dx = qs.x - pl.x;
+                    if (dx * dx + dy2 > best) break;
+                    const float d = l2_simple(qs, pl);
+                    if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
 #ifdef SSF_ASSOC_COUNT
-                ++vis;
+                    ++vis;
 #endif
+                }
             }
         };
         const int s0 = strip_of(qs.y);

@@ -1072,6 +1072,74 @@ SSF_DEV void table_strip_walks(const float4* __restrict__ P, const StripView<kSo
     }
 }
 
+// The (x, index) bitonic sort of k_plane_table_sorted with each thread's E elements in registers
+// (element t = e kTableThreads + tid): partners 64 <= j < kTableThreads apart go through LDS (one
+// barrier per half-stage), j < 64 through wave shuffles, j >= kTableThreads within the thread.
+// The same comparator network as the LDS loop (same pairs, directions and comparisons), so the
+// same permutation for any input.  Leaves the sorted indices in idx[].
+template <int E>
+SSF_DEV void table_sort_regs(const float4* __restrict__ P, int m, float* key, int* idx) {
+    constexpr int NT = kTableThreads, NP = E * NT;
+    const int tid = threadIdx.x;
+    float k[E];
+    int ix[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int t = e * NT + tid;
+        k[e] = t < m ? P[t].x : __builtin_inff();
+        ix[e] = t;
+    }
+    for (int kk = 2; kk <= NP; kk <<= 1) {
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            if (j >= NT) {                                          // partner in this thread
+                const int je = j / NT;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int e2 = e ^ je;
+                    if (e2 > e) {
+                        const int t = e * NT + tid;
+                        const bool asc = (t & kk) == 0;
+                        const bool sw = asc ? lex_less(k[e2], ix[e2], k[e], ix[e]) : lex_less(k[e], ix[e], k[e2], ix[e2]);
+                        if (sw) {
+                            const float tk = k[e]; k[e] = k[e2]; k[e2] = tk;
+                            const int ti = ix[e]; ix[e] = ix[e2]; ix[e2] = ti;
+                        }
+                    }
+                }
+            } else if (j >= 64) {                                   // partner in another wave
+#pragma unroll
+                for (int e = 0; e < E; ++e) { key[e * NT + tid] = k[e]; idx[e * NT + tid] = ix[e]; }
+                __syncthreads();
+                const bool lower = (tid & j) == 0;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int t = e * NT + tid;
+                    const float pk = key[t ^ j];
+                    const int pi = idx[t ^ j];
+                    const bool asc = (t & kk) == 0;
+                    const bool take = (lower == asc) ? lex_less(pk, pi, k[e], ix[e]) : lex_less(k[e], ix[e], pk, pi);
+                    if (take) { k[e] = pk; ix[e] = pi; }
+                }
+                __syncthreads();
+            } else {                                                // partner in this wave
+                const bool lower = (tid & j) == 0;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int t = e * NT + tid;
+                    const float pk = __shfl_xor(k[e], j, 64);
+                    const int pi = __shfl_xor(ix[e], j, 64);
+                    const bool asc = (t & kk) == 0;
+                    const bool take = (lower == asc) ? lex_less(pk, pi, k[e], ix[e]) : lex_less(k[e], ix[e], pk, pi);
+                    if (take) { k[e] = pk; ix[e] = pi; }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) { key[e * NT + tid] = k[e]; idx[e * NT + tid] = ix[e]; }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
     const float4* __restrict__ plane, const int64_t* __restrict__ frame_off,
     const int32_t* __restrict__ count, float plane_max, float* __restrict__ normal,
@@ -1092,6 +1160,12 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
 #endif
     int np = 1;
     while (np < m) np <<= 1;
+    if (np == 4 * kTableThreads) table_sort_regs<4>(P, m, key, idx);
+    else if (np == 2 * kTableThreads) table_sort_regs<2>(P, m, key, idx);
+    else if (np == kTableThreads) table_sort_regs<1>(P, m, key, idx);
+    else if (np == 8 * kTableThreads) table_sort_regs<8>(P, m, key, idx);
+    else if (np == 16 * kTableThreads) table_sort_regs<16>(P, m, key, idx);
+    else {
     for (int r = tid; r < np; r += blockDim.x) {
         key[r] = r < m ? P[r].x : __builtin_inff();
         idx[r] = r;
@@ -1112,6 +1186,7 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
             }
             __syncthreads();
         }
+    }
     }
     float4* SP = sorted_xyzi + base;
     int32_t* SI = sorted_idx + base;

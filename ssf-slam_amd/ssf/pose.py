@@ -88,12 +88,39 @@ def slove_RT_by_SVD(src, dst, reflection: str = "raise", device=None):
     return R, t
 
 
+class MaskPose(tuple):
+    """(R, t, q_xyzw, bg_mask): the Python boundary of SURVEY §8(b).  One frame: R (3, 3) and
+    t (3, 1) as slove_RT_by_SVD returns them, q_xyzw (4,), bg_mask (device uint8); F frames (with
+    frame_sizes): the same with a leading F axis.  The batched fields are also readable by key
+    or attribute -- res["R"] [F, 3, 3], res["t"] [F, 3], res["q_xyzw"] [F, 4], res["para_t_q"]
+    [F, 7] (the published [t, q]), res["bg_mask"], res["info"] (iteration counts, labels,
+    k-means++ centres, lower bound)."""
+    def __new__(cls, values, fields):
+        obj = super().__new__(cls, values)
+        obj._fields = fields
+        return obj
+
+    def __getitem__(self, k):
+        return self._fields[k] if isinstance(k, str) else super().__getitem__(k)
+
+    def __getattr__(self, k):
+        if k.startswith("_"):
+            raise AttributeError(k)
+        try:
+            return self._fields[k]
+        except KeyError:
+            raise AttributeError(k) from None
+
+    def keys(self):
+        return self._fields.keys()
+
+
 def mask_and_pose(points, flow, mode: str = "gmm", gt_mask=None, seed: int | None = None,
                   draws=None, reflection: str = "raise", device=None, frame_sizes=None):
     """The PointCloudOdometry_noSeg.py:97-125 block for one frame (or F frames packed back to
     back with `frame_sizes`).  mode 'gmm' (GaussianMixture on [flow, xyz]), 'gt'
     (background = s_fg_mask == 0, PointCloudOdometry.py:91) or 'given' (background = mask != 0).
-    -> dict(R [F,3,3], t [F,3], q_xyzw [F,4], para_t_q [F,7], bg_mask (device u8), info)."""
+    -> MaskPose: (R, t, q_xyzw, bg_mask), plus keyed batched fields (see MaskPose)."""
     fe = _frontend(device)
     dt = _storage(points, flow)
     pts = _as_dev(points, fe.device, dt)
@@ -114,8 +141,12 @@ def mask_and_pose(points, flow, mode: str = "gmm", gt_mask=None, seed: int | Non
     for st in o[:, _abi.POSE_OUT["STATUS"]]:
         if int(st) != 0:
             _raise_status(st)
-    return dict(R=o[:, 7:16].reshape(-1, 3, 3), t=o[:, 0:3], q_xyzw=o[:, 3:7],
-                para_t_q=o[:, 0:7], bg_mask=bg,
-                info=dict(bg_label=o[:, 18], n_bg=o[:, 17], kmeans_iter=o[:, 19], em_iter=o[:, 20],
-                          converged=o[:, 21], centers=o[:, 22:24], lower_bound=o[:, 24],
-                          passes=o[:, 25]))
+    fields = dict(R=o[:, 7:16].reshape(-1, 3, 3), t=o[:, 0:3], q_xyzw=o[:, 3:7],
+                  para_t_q=o[:, 0:7], bg_mask=bg,
+                  info=dict(bg_label=o[:, 18], n_bg=o[:, 17], kmeans_iter=o[:, 19], em_iter=o[:, 20],
+                            converged=o[:, 21], centers=o[:, 22:24], lower_bound=o[:, 24],
+                            passes=o[:, 25]))
+    R, t, q = fields["R"].copy(), fields["t"].reshape(-1, 3, 1).copy(), fields["q_xyzw"].copy()
+    if frame_sizes is None:                      # one frame: the shapes of slove_RT_by_SVD
+        R, t, q = R[0], t[0], q[0]
+    return MaskPose((R, t, q, bg), fields)

@@ -253,6 +253,10 @@ def test_reference_named_python_api(dev):
     c = np.load(os.path.join(GOLDEN, "gmm_noseg_case0.npz"))
     res = ssf.mask_and_pose(c["pos1"], c["flow"], seed=int(c["seed"]))
     assert np.abs(res["para_t_q"][0] - c["para_t_q"]).max() < 1e-6
+    R1, t1, q1, bg1 = res                                       # the SURVEY §8(b) tuple
+    assert R1.shape == (3, 3) and t1.shape == (3, 1) and q1.shape == (4,)
+    assert _rot_angle(R1, c["R"]) < 1e-6 and np.abs(t1.ravel() - c["t"]).max() < 1e-5
+    assert bg1 is res["bg_mask"] and res.info["em_iter"][0] == int(c["gmm_n_iter"])
     bg_ref = (c["labels"] == int(c["bg_label"])).astype(np.uint8)
     assert np.array_equal(res["bg_mask"].cpu().numpy(), bg_ref)
     gt = ssf.mask_and_pose(c["pos1"], c["flow"], mode="gt", gt_mask=c["s_fg_mask"])

@@ -61,7 +61,7 @@ SSF_DEV int ring_id(float x, float y, float z, int n_rows) {
     return (id > -1 && id < n_rows) ? id : -1;
 }
 
-// Each thread issues all of its 16 point loads (clamped, unconditional) before the first ring
+// Each thread issues all of its kCountSteps point loads (clamped, unconditional) before the first ring
 // id: one load latency per chunk instead of one per point.
 constexpr int kCountSteps = kBinChunk / 256;
 
@@ -124,14 +124,14 @@ __global__ __launch_bounds__(64) void k_bin_scan(int n_rows, int n_chunks, int32
     if (r == n_rows - 1) ro[n_rows] = incl;
 }
 
-// Stable per-row partition of one 4096-point chunk.  Wave w owns the chunk's points
-// [1024 w, 1024 w + 1024) in 16 steps of 64: a 7-ballot "match" on the 6-bit row id gives each
+// Stable per-row partition of one kBinChunk-point chunk.  Wave w owns the chunk's points
+// [kBinChunk/4 w, kBinChunk/4 (w + 1)) in steps of 64: a 7-ballot "match" on the 6-bit row id gives each
 // point its rank among same-row lanes, and a wave-private running count per row (LDS, no
 // barrier) turns that into its rank among the wave's same-row points.  One barrier later the
 // per-wave counts are prefixed (waves in order, then rows), every point lands in a row-grouped
 // LDS tile, and the tile leaves in contiguous per-row runs: coalesced 16-B stores instead of
 // one scattered store per point (a LiDAR scan interleaves the rows point by point).
-constexpr int kScatterSteps = kBinChunk / 256;   // 16 points per thread
+constexpr int kScatterSteps = kBinChunk / 256;   // points per thread
 
 struct Xyz { float x, y, z; };                      // packed ring-ordered point (12 B)
 
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
                                                      const int32_t* __restrict__ chunk_base,
                                                      const int32_t* __restrict__ ring_off,
                                                      Xyz* __restrict__ out, float4* __restrict__ out4) {
-    __shared__ float4 tile[kBinChunk];            // 64 KiB
+    __shared__ float4 tile[kBinChunk];            // 16 B per point
     __shared__ uint8_t row_of[kBinChunk];
     __shared__ int wrun[4][kMaxRows];
     __shared__ int roff[kMaxRows + 1];            // chunk-local row offsets
@@ -159,10 +159,10 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
     }
     __syncthreads();
     // all loads first (ids, then points at clamped indices, unconditionally): one wait for the
-    // whole 16-point batch instead of one load latency per step
+    // whole kScatterSteps-point batch instead of one load latency per step
     int idr[kScatterSteps];       // row id, then row id | rank-in-wave << 8
     float px[kScatterSteps], py[kScatterSteps], pz[kScatterSteps];
-    const int64_t i0 = s + 1024 * w + (tid & 63);
+    const int64_t i0 = s + (kBinChunk / 4) * w + (tid & 63);
 #pragma unroll
     for (int st = 0; st < kScatterSteps; ++st) {
         const int64_t i = i0 + 64 * st;
@@ -224,7 +224,8 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
             const int loc = roff[id] + in_row;
             float4 v;
             v.x = px[st]; v.y = py[st]; v.z = pz[st];
-            v.w = (float)((double)(cb[id] + in_row) + rfrac[id]);   // frameFeature.cpp:77
+            // frameFeature.cpp:77, needed only by the debug ring-ordered cloud (out4 is uniform)
+            v.w = out4 ? (float)((double)(cb[id] + in_row) + rfrac[id]) : 0.0f;
             tile[loc] = v;
             row_of[loc] = (uint8_t)id;
         }
@@ -256,6 +257,9 @@ constexpr int kCurvRowsPerWG = SSF_CURV_ROWS_PER_WG;
 #define SSF_CURV_DEPTH 3
 #endif
 constexpr int kCurvDepth = SSF_CURV_DEPTH;   // 64-point groups in flight per wave (one trip)
+#ifndef SSF_CURV_PROBE
+#define SSF_CURV_PROBE 0                      // diagnostic variants only (tools/gpu scripts)
+#endif
 
 // The window holds 256 points (4 groups; point p at p & 255) plus a mirror of its first 16 at
 // [256, 272), so the 11 taps of centre j are the contiguous a[b .. b + 10], b = (j - 5) & 255:
@@ -263,19 +267,18 @@ constexpr int kCurvDepth = SSF_CURV_DEPTH;   // 64-point groups in flight per wa
 constexpr int kWin = 256;
 constexpr int kWinPad = kWin + 16;
 
-// The 11 taps of centre j from a float4 (x, y, z, -) window: 11 ds_read_b128 (16-B aligned,
+// The 11 taps t[0 .. 10] (centre t[5]) from a float4 (x, y, z, -) window: 11 ds_read_b128 (16-B aligned,
 // immediate offsets) serve all three coordinates; each coordinate's sum is evaluated left to
 // right in float exactly as frameFeature.cpp:86-105.
-SSF_DEV void stencil11w(const float4* a, int j, float& dx, float& dy, float& dz) {
-    const float4* t = a + ((j - 5) & (kWin - 1));
+SSF_DEV void stencil11t(const float4* t, float& dx, float& dy, float& dz) {
     float4 u[11];
 #pragma unroll
-    for (int k = 0; k < 11; ++k) {
-        u[k] = t[k];
-        // keep .w live: a whole-float4 read is ds_read_b128 (4 LDS cycles per wave), the
-        // x, y, z read the compiler would otherwise emit is ds_read_b96 (8 cycles)
-        asm volatile("" ::"v"(u[k].w));
-    }
+    for (int k = 0; k < 11; ++k) u[k] = t[k];
+    // keep .w live: a whole-float4 read is ds_read_b128 (4 LDS cycles per wave), the x, y, z
+    // read the compiler would otherwise emit is ds_read_b96 (8 cycles).  One statement after
+    // all eleven reads: one per read made the compiler wait for each before issuing the next.
+    asm volatile("" ::"v"(u[0].w), "v"(u[1].w), "v"(u[2].w), "v"(u[3].w), "v"(u[4].w), "v"(u[5].w),
+                 "v"(u[6].w), "v"(u[7].w), "v"(u[8].w), "v"(u[9].w), "v"(u[10].w));
     float sx = u[0].x + u[1].x, sy = u[0].y + u[1].y, sz = u[0].z + u[1].z;
 #pragma unroll
     for (int k = 2; k < 11; ++k) {
@@ -283,6 +286,11 @@ SSF_DEV void stencil11w(const float4* a, int j, float& dx, float& dy, float& dz)
         else { sx = sx + u[k].x; sy = sy + u[k].y; sz = sz + u[k].z; }
     }
     dx = sx; dy = sy; dz = sz;
+}
+
+// the taps of centre j in the circular window (t = a[(j - 5) & 255 ..], contiguous by the mirror)
+SSF_DEV void stencil11w(const float4* a, int j, float& dx, float& dy, float& dz) {
+    stencil11t(a + ((j - 5) & (kWin - 1)), dx, dy, dz);
 }
 
 // kHalves: 64-entry selection stores per trip (a trip selects <= 64 kCurvDepth / span + 1
@@ -326,7 +334,17 @@ __global__ __launch_bounds__(64 * kCurvRowsPerWG) void k_curv_select(const int64
     int32_t* sl = slist[w];
     const Xyz* src = rxyz + base;
     const int ng = (n_r + 63) >> 6;
+#if SSF_CURV_PROBE == 3
+    // diagnostic: the same bytes as lane-contiguous 16-B loads (48 lanes x 16 B = 64 points)
+    const float4* src4 = reinterpret_cast<const float4*>(reinterpret_cast<uintptr_t>(src) & ~(uintptr_t)15);
+    const int n4 = (3 * n_r + 3) / 4;
+    auto load = [&](int g) {
+        const float4 q = src4[min(48 * g + min(lane, 47), n4 - 1)];
+        return Xyz{q.x + q.w, q.y, q.z};
+    };
+#else
     auto load = [&](int g) { return src[min(64 * g + lane, n_r - 1)]; };   // clamped
+#endif
     int cnt = 0, nl = 0, jstart = 0;                           // wave-uniform
     int ecnt = 0, enl = 0, ejstart = 0;                        // wave-uniform (kEdge)
     int32_t* el = elist[kEdge ? w : 0];
@@ -341,14 +359,25 @@ __global__ __launch_bounds__(64 * kCurvRowsPerWG) void k_curv_select(const int64
         if (g == 0 || g > ng) return;                          // uniform
         const int j = 64 * (g - 1) + lane;                     // group g-1: its stencil is complete
         float v = 0.0f;
+#if SSF_CURV_PROBE == 1 || SSF_CURV_PROBE == 3
+        // diagnostic (tools/ variants only): the stream and the window, no stencil, no greedy
+        v = wv[(j - 5) & (kWin - 1)].x;
+#else
         if (j >= 5 && j < n_r - 5) {
             float dx, dy, dz;
             stencil11w(wv, j, dx, dy, dz);
             v = dx * dx + dy * dy;
             v = v + dz * dz;
         }
+#endif
         if (kCurv) curv[base + min(j, n_r - 1)] = v;   // lanes past the row write its last value, 0
         uint64_t m = __ballot(j < n_r && v < plane_min);
+#if SSF_CURV_PROBE
+        // diagnostic: no greedy walk (one selection per group keeps the ballot live)
+        if (m) { if (lane == 0) sl[nl] = 64 * (g - 1) + __ffsll((unsigned long long)m) - 1; nl++; }
+        (void)jstart;
+        if (true) return;
+#endif
         const int j0 = 64 * (g - 1);
         while (true) {
             const int lo = jstart - j0;
@@ -479,6 +508,13 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
         if (curv) { if (two) SSF_CURV_LAUNCH(true, 2, false); else SSF_CURV_LAUNCH(true, 1, false); }
         else { if (two) SSF_CURV_LAUNCH(false, 2, false); else SSF_CURV_LAUNCH(false, 1, false); }
     }
+#ifdef SSF_CURV_TWICE
+    // diagnostic (tools/ variants only): the same launch again, on data the previous kernel
+    // left settled (k_curv_select is idempotent)
+    kmark(s, "k_curv_select_again");
+    if (!edge) { if (curv) { if (two) SSF_CURV_LAUNCH(true, 2, false); else SSF_CURV_LAUNCH(true, 1, false); }
+                 else { if (two) SSF_CURV_LAUNCH(false, 2, false); else SSF_CURV_LAUNCH(false, 1, false); } }
+#endif
 #undef SSF_CURV_LAUNCH
     kmark(s, "k_compact");
     hipLaunchKernelGGL(k_compact, dim3(R, n_frames), dim3(256), 0, s, frame_off, R, ring_off,

@@ -35,7 +35,11 @@ struct DevBuf {
 // With timing off (the default) kmark is one thread-local load and a branch.
 void kmark(hipStream_t s, const char* name);
 
-constexpr int kBinChunk = 4096;   // points per binning work-group
+#ifndef SSF_BIN_CHUNK
+#define SSF_BIN_CHUNK 2048
+#endif
+constexpr int kBinChunk = SSF_BIN_CHUNK;   // points per binning work-group (2048: 8 points per
+                                           // thread; 4096 measured 11-12 % slower binning)
 constexpr int kMaxRows = 64;
 
 // Per-correspondence record written by the association kernel, read by the solver.

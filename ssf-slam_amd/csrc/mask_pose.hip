@@ -55,6 +55,10 @@ constexpr double kPi = 3.14159265358979323846;
 #define SSF_LLOYD_FULL_PASSES 4
 #endif
 constexpr int kLloydFullPasses = SSF_LLOYD_FULL_PASSES;   // full Lloyd passes before skipping
+#ifndef SSF_LLOYD_REFULL
+#define SSF_LLOYD_REFULL 4
+#endif
+constexpr int kLloydRefull = SSF_LLOYD_REFULL;   // back to a full pass when > n / this relabel
 #ifndef SSF_LLOYD_REC_DEEP
 #define SSF_LLOYD_REC_DEEP 8
 #endif
@@ -1095,7 +1099,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             for (int k = 0; k < 14; ++k) S.lsum[k] = full ? acc[k] : S.lsum[k] + acc[k];
             // the first passes move the centres most (typically 35-45 % of the points would be
             // relabelled): full passes through it = 3, then skip passes while they relabel < 1/4
-            S.lfull = full ? it < kLloydFullPasses - 1 : nlab * 4 > n;
+            S.lfull = full ? it < kLloydFullPasses - 1 : nlab * kLloydRefull > n;
 #ifdef SSF_MASK_STAMPS
             // diagnostic: cycles and relabelled points of the skip passes (k_mask_pose stamps
             // build only; reported through the k-means++ centre slots, which it overwrites)

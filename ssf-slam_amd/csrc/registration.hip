@@ -1869,7 +1869,13 @@ __global__ __launch_bounds__(kEdgeAssocThreads) void k_edge_associate(
 }
 
 // ------------------------------------------------------------------------------------------
-constexpr int kSolveThreads = 512;
+// one wave per SIMD: the per-pair solve is latency-bound (a block reduction and a 6x6 solve per
+// iteration), and 256 threads measured 0.083 ms per 256-pair launch against 0.092 at 512 and
+// 0.28 at 1024 (round 2c, tools/gpu/r2c_solve3.sh)
+#ifndef SSF_SOLVE_THREADS
+#define SSF_SOLVE_THREADS 256
+#endif
+constexpr int kSolveThreads = SSF_SOLVE_THREADS;
 constexpr int kNE = 28;  // 21 (packed upper JtWJ) + 6 (JtWr) + cost
 
 SSF_DEV int pk(int u, int v) {
@@ -2014,8 +2020,12 @@ SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4],
     for (int k = 0; k < kNE; ++k) ne[k] *= 2.0;
 }
 
-// LDS-resident correspondences, two per step (i, i + T; a missing second one is a clamped
-// duplicate weighted 0): both loads are in flight before either is used.
+// LDS-resident correspondences, kSolveStep per step (i, i + T, ...; a missing one is a clamped
+// duplicate weighted 0): all of a step's loads are in flight before the first is used.
+#ifndef SSF_SOLVE_STEP
+#define SSF_SOLVE_STEP 2
+#endif
+constexpr int kSolveStep = SSF_SOLVE_STEP;
 SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double t[3],
                       double (&ne)[kNE], double* lds, int nve = 0) {
 #pragma unroll
@@ -2023,20 +2033,19 @@ SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double 
     double R[9];
     quat_to_R(q, R);
     const int T = blockDim.x;
-    for (int i = threadIdx.x; i < nv; i += 2 * T) {
-        const int i2 = min(i + T, nv - 1);
-        const double w2 = i + T < nv ? 1.0 : 0.0;
-        float f[2][9];
+    for (int i = threadIdx.x; i < nv; i += kSolveStep * T) {
+        float f[kSolveStep][9];
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            f[0][d] = C.po[d][i]; f[0][3 + d] = C.pa[d][i]; f[0][6 + d] = C.n[d][i];
-            f[1][d] = C.po[d][i2]; f[1][3 + d] = C.pa[d][i2]; f[1][6 + d] = C.n[d][i2];
+        for (int h = 0; h < kSolveStep; ++h) {
+            const int ih = min(i + h * T, nv - 1);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) { f[h][d] = C.po[d][ih]; f[h][3 + d] = C.pa[d][ih]; f[h][6 + d] = C.n[d][ih]; }
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < kSolveStep; ++h) {
             const double po[3] = {f[h][0], f[h][1], f[h][2]}, pa[3] = {f[h][3], f[h][4], f[h][5]},
                          nn[3] = {f[h][6], f[h][7], f[h][8]};
-            accum_corr(R, t, po, pa, nn, h ? w2 : 1.0, ne);
+            accum_corr(R, t, po, pa, nn, (h == 0 || i + h * T < nv) ? 1.0 : 0.0, ne);
         }
     }
     for (int i = nv + threadIdx.x; i < nv + nve; i += T) {        // edge blocks after the planes
@@ -2047,6 +2056,36 @@ SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double 
     block_sum_rs<kNE>(ne, lds);
 #pragma unroll
     for (int k = 0; k < kNE; ++k) ne[k] *= 2.0;
+}
+
+// quat_plus for a GN step: |d| = theta < 2^-7 (a step of a converging solve) takes sin(theta) /
+// theta and cos(theta) as their Taylor polynomials in theta^2 = |d|^2 -- no sqrt, division, sin or
+// cos on the per-iteration critical path every thread runs.  The first omitted terms are below
+// 2^-95 (sinc, x2^5 / 11!) and 2^-112 (cos, x2^6 / 12!) of the results, far under one f64 ulp
+// (2^-53): the values agree with libm's to an ulp or so, as libm agrees with the oracle's glibc.
+// Larger steps take quat_plus itself.  -DSSF_QUAT_PLUS_LIBM restores libm everywhere (A/B).
+SSF_DEV void quat_plus_step(const double q[4], const double d[3], double o[4]) {
+#ifndef SSF_QUAT_PLUS_LIBM
+    const double x2 = __builtin_fma(d[2], d[2], __builtin_fma(d[1], d[1], d[0] * d[0]));
+    if (x2 > 0.0 && x2 < 0x1p-14) {
+        // Horner in x2: sinc = sum (-x2)^k / (2k + 1)!, k <= 4; cos = sum (-x2)^k / (2k)!, k <= 5
+        double sc = 1.0 / 362880.0;
+        sc = __builtin_fma(sc, x2, -1.0 / 5040.0);
+        sc = __builtin_fma(sc, x2, 1.0 / 120.0);
+        sc = __builtin_fma(sc, x2, -1.0 / 6.0);
+        sc = __builtin_fma(sc, x2, 1.0);
+        double c = -1.0 / 3628800.0;
+        c = __builtin_fma(c, x2, 1.0 / 40320.0);
+        c = __builtin_fma(c, x2, -1.0 / 720.0);
+        c = __builtin_fma(c, x2, 1.0 / 24.0);
+        c = __builtin_fma(c, x2, -0.5);
+        c = __builtin_fma(c, x2, 1.0);
+        const double dq[4] = {sc * d[0], sc * d[1], sc * d[2], c};
+        quat_mul(dq, q, o);
+        return;
+    }
+#endif
+    quat_plus(q, d, o);
 }
 
 SSF_DEV int chol_solve6(double M[6][6], const double b[6], double y[6]) {
@@ -2246,7 +2285,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
                     break;
                 }
                 double qn[4];
-                quat_plus(q, y, qn);
+                quat_plus_step(q, y, qn);
                 for (int k = 0; k < 4; ++k) q[k] = qn[k];
                 t[0] += y[3]; t[1] += y[4]; t[2] += y[5];
                 eval_at(q, t, ne);

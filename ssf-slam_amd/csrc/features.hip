@@ -105,11 +105,20 @@ __global__ __launch_bounds__(64) void k_bin_scan(int n_rows, int n_chunks, int32
     const int f = blockIdx.x, r = threadIdx.x;
     int run = 0;
     if (r < n_rows) {
+        // 16 counts loaded before any is rewritten: one memory latency per 16 chunks (a load
+        // after a store to the same array otherwise waits for the previous chunk's round trip)
         int32_t* hp = hist + (int64_t)f * n_chunks * n_rows + r;
-        for (int c = 0; c < n_chunks; ++c) {
-            int v = hp[(int64_t)c * n_rows];
-            hp[(int64_t)c * n_rows] = run;
-            run += v;
+        for (int c0 = 0; c0 < n_chunks; c0 += 16) {
+            int v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = hp[(int64_t)min(c0 + k, n_chunks - 1) * n_rows];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if (c0 + k < n_chunks) {
+                    hp[(int64_t)(c0 + k) * n_rows] = run;
+                    run += v[k];
+                }
+            }
         }
     }
     // exclusive scan of row totals across the wave

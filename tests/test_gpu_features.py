@@ -96,6 +96,20 @@ def test_full_size_frame(oracle, dev):
     _check_frame(oracle, fe, out, h_off, 1, c, 64)
 
 
+def test_chunk_and_scan_boundaries(oracle, dev):
+    """frames cut at the binning chunk (kBinChunk = 2048 points, ssf_internal.hpp) and at the
+    scan's 16-chunk batches (k_bin_scan): 2047 / 2048 / 16 x 2048 +- 1 / 32 x 2048 points, in one
+    ragged batch (every frame scans the batch's chunk count), bit-exact"""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index)
+    full = frame(4, 7, n_az=1875)[0]
+    sizes = [2047, 2048, 16 * 2048 - 1, 16 * 2048, 16 * 2048 + 1, 32 * 2048]
+    clouds = [full[:n] for n in sizes]
+    out, h_off = _run(fe, clouds, dev)
+    for f, c in enumerate(clouds):
+        _check_frame(oracle, fe, out, h_off, f, c, 64)
+
+
 @pytest.mark.parametrize("n_rows", [16, 64])
 def test_ring_ids_near_bin_edges(oracle, dev, n_rows):
     """Elevations on and within 1e-6..1e-2 deg of every bin edge (and the -8.83 switch), plus a

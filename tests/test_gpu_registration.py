@@ -125,6 +125,38 @@ def test_register_pair_per_step(oracle, dev, solver, iters, mode, brute):
     assert np.abs(got[4:] - t).max() < TOL_T and _quat_angle(got[:4], q) < TOL_R
 
 
+def test_gn_steps_both_quaternion_update_paths(oracle, dev):
+    """k_solve's GN update takes Taylor polynomials for steps theta < 2^-7 and libm sin / cos
+    above (quat_plus_step): a warm start 0.05 rad off gives both kinds of step in one solve; every
+    step's pose stays within the per-step bar of the oracle's (libm) update."""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index, solver="gn", max_iter=10)
+    clouds = [frame(0, 2, n_az=1875)[0], frame(0, 3, n_az=1875)[0]]
+    pb = _planes(fe, dev, clouds)
+    table = fe.plane_table(pb)
+    last, curr = _sub(pb, [0]), _sub(pb, [1])
+    q0 = np.array([0.0, 0.0, np.sin(0.025), np.cos(0.025)])
+    t0 = np.array([0.9, 0.01, 0.0])
+    pose = torch.tensor([[*q0, *t0]], dtype=torch.float64, device=dev)
+    res = fe.register(last, table, curr, pose, want_log=True)
+    torch.cuda.synchronize()
+    L = pb.frame(0).cpu().numpy()
+    Cc = pb.frame(1).cpu().numpy()
+    q, t, log, c = oracle.register_pair(L, Cc, 0.05, mode=1, max_iter=10, q_init=q0, t_init=t0)
+    nl = int(res["nlog"][0])
+    assert nl == log.shape[0]
+    glog = res["log"][0, :nl].cpu().numpy()
+    for k in range(nl):
+        assert glog[k, 8] == log[k, 8], f"step {k} status differs"
+        assert np.abs(glog[k, 4:7] - log[k, 4:7]).max() < TOL_T, k
+        assert _quat_angle(glog[k, :4], log[k, :4]) < TOL_R, k
+    # a step of theta turns the pose by 2 theta
+    turns = [_quat_angle(log[0, :4], q0)] + [_quat_angle(log[k, :4], log[k - 1, :4]) for k in range(1, nl)]
+    assert max(turns) > 2 * 2.0 ** -7 and min(turns) < 2 * 2.0 ** -7, turns
+    got = res["pose_rel"][0].cpu().numpy()
+    assert np.abs(got[4:] - t).max() < TOL_T and _quat_angle(got[:4], q) < TOL_R
+
+
 def test_16_row_profile_table_and_registration(oracle, dev):
     """16-beam profile (planeMax 0.15, lidarOdometry_onlyPC.cpp:314-316): plane table bit-exact
     and an LM pair within the pose bars."""

@@ -68,8 +68,8 @@ def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
                     help="ranks (one per GPU); without WORLD_SIZE in the env, bench.py starts them")
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="sequences in flight per GPU")
     ap.add_argument("--n-az", type=int, default=1875,
                     help="azimuth steps (64 x 1875 = 120k pts; 4000 -> 256k, BASELINE configs[4])")
@@ -107,6 +107,8 @@ def parse(argv=None):
                          "prints the world it sees and exits (no GPU is touched)")
     ap.add_argument("--mask-split", type=int, default=0,
                     help="work-groups per frame of the GMM fit (0: automatic, ssf_set_mask_split)")
+    ap.add_argument("--latency", action="store_true",
+                    help="BASELINE configs[1] as written: one frame pair at a time (B = 1), ms per frame")
     ap.add_argument("--mask-streams", type=int, default=3,
                     help="mask launches of consecutive steps alternate over this many streams: the "
                          "GMM of a frame depends on no other frame, so a step's slow frames overlap "
@@ -131,24 +133,51 @@ def launch_ranks(args) -> int:
 
 # ---------------------------------------------------------------------------- CPU baseline
 def _cpu_share():
+    """CPUs this job may use: OMP_NUM_THREADS / MAX_JOBS (the GPU box sets them to its per-GPU
+    CPU share, 16; nproc there shows the whole machine), else the affinity set."""
     for k in ("OMP_NUM_THREADS", "MAX_JOBS"):
         v = os.environ.get(k)
         if v and v.isdigit() and int(v) > 0:
             return int(v)
     try:
-        n = len(os.sched_getaffinity(0))
+        return len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
+        return os.cpu_count() or 1
 
 
-def _run_legs(specs, seconds):
-    """start every leg process at once; -> list of parsed JSON results"""
+def _physical_cpus(n):
+    """Up to n CPUs of this process's affinity set, at most one per physical core (SMT siblings
+    skipped; sysfs topology) -> (cpus, siblings_skipped).  Falls back to the set in order."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        return list(range(n)), False
+    seen, pick = set(), []
+    for c in allowed:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            key = (open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip())
+        except OSError:
+            key = ("cpu", str(c))
+        if key in seen:
+            continue
+        seen.add(key)
+        pick.append(c)
+        if len(pick) == n:
+            break
+    return pick, len(seen) < len(allowed)
+
+
+def _run_legs(specs, seconds, cpus=None):
+    """start every leg process at once (leg i pinned to cpus[i] when given); -> list of parsed
+    JSON results"""
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
     procs = []
-    for leg, seq, extra in specs:
+    for i, (leg, seq, extra) in enumerate(specs):
         cmd = [sys.executable, "-m", "oracle.cpu_leg", leg, "--seq", str(seq), "--seconds",
                str(seconds), *extra]
+        if cpus and leg != "sklearn":
+            cmd += ["--cpu", str(cpus[i % len(cpus)])]
         e = dict(os.environ) if leg == "sklearn" else env
         procs.append(subprocess.Popen(cmd, cwd=REPO, env=e, stdout=subprocess.PIPE,
                                       stderr=subprocess.DEVNULL, text=True))
@@ -171,10 +200,12 @@ def cpu_baseline(args):
     iters = args.iters or (10 if args.solver == "gn" else 8)
     extra = ["--rows", str(args.rows), "--n-az", str(args.n_az), "--solver", args.solver,
              "--iters", str(iters)]
-    cores = args.cpu_cores or _cpu_share()
+    share = args.cpu_cores or _cpu_share()
+    cpus, smt = _physical_cpus(share)
+    cores = len(cpus)
     T = args.cpu_seconds
-    single = _run_legs([("oracle", 0, extra)], T)[0]
-    many = _run_legs([("oracle", s, extra) for s in range(cores)], T)
+    single = _run_legs([("oracle", 0, extra)], T, cpus[:1])[0]
+    many = _run_legs([("oracle", s, extra) for s in range(cores)], T, cpus)
     skl = _run_legs([("sklearn", 0, ["--rows", str(args.rows), "--n-az", str(args.n_az)])], T)[0]
     rate = lambda r: r["frames"] / r["seconds"] if r.get("seconds") else 0.0
     agg = sum(rate(r) for r in many)
@@ -183,13 +214,16 @@ def cpu_baseline(args):
     return dict(
         value=agg, unit="frames/s", cores=cores, kind="port",
         sample=f"{sum(r['frames'] for r in many)} frames of {args.rows}-beam {N}-pt synthetic "
-               f"scans ({work}) through oracle/ssf_oracle.c, {cores} processes x 1 thread "
+               f"scans ({work}) through oracle/ssf_oracle.c (gcc -O3 -ffp-contract=off), {cores} "
+               f"processes x 1 thread, each pinned to its own physical core (SMT siblings "
+               f"{'present in the affinity set and left idle' if smt else 'not present'}) "
                f"(one sequence each, {T:.0f} s each, concurrent)",
         legs={
             "single_thread": dict(value=rate(single), cores=1, frames=single.get("frames"),
                                   seconds=single.get("seconds"), kind="port"),
             "all_cores": dict(value=agg, cores=cores, frames=sum(r["frames"] for r in many),
-                              per_process=[round(rate(r), 3) for r in many], kind="port"),
+                              per_process=[round(rate(r), 3) for r in many], cpus=cpus,
+                              smt_siblings_in_affinity_set=smt, kind="port"),
             "sklearn_mask_only": dict(value=rate(skl), cores="BLAS default",
                                       frames=skl.get("frames"), seconds=skl.get("seconds"),
                                       kind="third-party (sklearn GaussianMixture + numpy Kabsch)",
@@ -199,24 +233,25 @@ def cpu_baseline(args):
 
 
 # ---------------------------------------------------------------------------- data
-def make_data(args, dev, n_frames, rank):
+def make_data(args, dev, n_frames, rank, batch=None):
     """[n_frames] batches of B frames: pos/flow packed [B*N, 3] f32, resident in HBM.  Sequence
-    b of rank r is synth sequence r * 100000 + (b mod distinct)."""
+    b of rank r is synth sequence r * 100000 + (b mod distinct), ray-cast on the GPU
+    (ssf.synth.BatchScanner: synth.scan's scenes and sensor, one ray per thread)."""
     import torch
     from ssf import synth
-    S = max(1, min(args.distinct or args.batch, args.batch))
+    B = batch or args.batch
+    S = max(1, min(args.distinct or B, B))
     N = args.rows * args.n_az
-    pos = [torch.empty((args.batch * N, 3), dtype=torch.float32, device=dev) for _ in range(n_frames)]
-    flow = [torch.empty((args.batch * N, 3), dtype=torch.float32, device=dev) for _ in range(n_frames)]
-    for s in range(S):
-        seq_id = rank * 100000 + s
-        sc = synth.Scene(seq_id)
-        for k in range(n_frames):
-            f = synth.scan(seq_id, k, n_rows=args.rows, n_az=args.n_az, device=dev, scene=sc)
-            for b in range(s, args.batch, S):
-                pos[k][b * N:(b + 1) * N].copy_(f["pos1"])
-                flow[k][b * N:(b + 1) * N].copy_(f["flow"])
-    return list(zip(pos, flow))
+    scanner = synth.BatchScanner([rank * 100000 + (b % S) for b in range(B)], n_frames,
+                                 n_rows=args.rows, n_az=args.n_az, device=dev)
+    out = []
+    for k in range(n_frames):
+        pos = torch.empty((B * N, 3), dtype=torch.float32, device=dev)
+        flow = torch.empty((B * N, 3), dtype=torch.float32, device=dev)
+        scanner.frame(k, pos, flow)
+        out.append((pos, flow))
+    torch.cuda.synchronize(dev)
+    return out
 
 
 # ---------------------------------------------------------------------------- pipeline
@@ -249,8 +284,9 @@ class Pipeline:
         self.pose_abs = ssf.identity_poses(B, dev)
         self.last = self.last_table = None
         self.last_e = self.last_etable = None
-        self.records = []           # per step: (pose snapshot on s_reg, mask out)
-        self.gathered = []
+        self.records = []           # per timed step: the pose record this rank contributed
+        self.gathered = []          # per timed step: the all-gathered records of every rank
+        self.snaps = []             # (pose snapshot on s_reg, mask out, its streams) until exchange()
         self.ev = {k: [] for k in ("mask", "feat", "table", "reg")}
 
     def contexts(self):
@@ -258,7 +294,6 @@ class Pipeline:
 
     def step(self, k, batches, off, h_off, timing, streams=None, want_stats=False):
         import torch
-        from ssf import dist as sd
         a = self.args
         pos, flow = batches[k]
         s_mask, s_feat, s_reg = streams or (self.s_masks[k % len(self.s_masks)], self.s_feat, self.s_reg)
@@ -308,18 +343,34 @@ class Pipeline:
             snap = self.pose_abs.clone() if self.world > 1 else None   # step-k poses, on s_reg
         self.last, self.last_table = pb, table
         self.last_e, self.last_etable = eb, etable
-        if self.world > 1:   # the one exchange step: per-frame 6-DoF poses of every rank (RCCL)
-            cur = torch.cuda.current_stream(self.dev)
-            cur.wait_stream(s_mask)
-            cur.wait_stream(s_reg)
-            snap.record_stream(cur)
-            rec = sd.pose_record(snap, out)
-            self.records.append(rec)
-            self.gathered.append(sd.gather_poses(rec))
+        if self.world > 1 and timing:   # for the deferred exchange (exchange()): no per-step wait
+            self.snaps.append((snap, out, s_mask, s_reg))
         if timing:
             self.ev["mask"].append((m0, m1)); self.ev["feat"].append((es[0], es[1]))
             self.ev["table"].append((es[1], es[2])); self.ev["reg"].append((r0, r1))
         return dict(out=out, bg=bg, pb=pb, stats=stats)
+
+    def exchange(self):
+        """The one exchange step (N > 1): every step's per-frame 6-DoF pose records of every rank
+        in ONE all-gather (RCCL), after the last step -- SURVEY §8(e) "once per batch or at the
+        end of a sequence"; no step of the pipeline waits for it."""
+        from ssf import dist as sd
+        if not self.snaps:
+            return
+        import torch
+        cur = torch.cuda.current_stream(self.dev)
+        for s in {id(x[2]): x[2] for x in self.snaps}.values():
+            cur.wait_stream(s)
+        cur.wait_stream(self.s_reg)
+        recs = []
+        for snap, out, _, _ in self.snaps:
+            snap.record_stream(cur)
+            out.record_stream(cur)
+            recs.append(sd.pose_record(snap, out))
+        self.records.extend(recs)
+        g = sd.gather_pose_records(recs)                 # [K, world * B, 14]
+        self.gathered.extend(list(g))
+        self.snaps = []
 
 
 def kernel_pass(pipe, batches, off, h_off, ks, rows, row_start, row_end):
@@ -410,8 +461,124 @@ def rooflines(times, acc, B, N):
     return out, passes
 
 
+def latency(args):
+    """BASELINE configs[1] as written: ONE 120k-point frame pair at a time, the way the
+    reference's nodes see it -- PointCloudOdometry_noSeg.py:97-125 masks one frame per callback,
+    frameFeature extracts one frame (frameFeature.cpp:35-139), and cloudThread registers one
+    plane cloud against the previous one (lidarOdometry_onlyPC.cpp:281-311).  Per frame: the
+    mask (GMM + Kabsch, automatic split: G = 8 work-groups for one frame) on one stream, and
+    features -> plane table -> registration of the pair (10 GN iterations) on another; the
+    frame is done when both have finished (host wall time per frame, synchronised).  `serial`
+    runs the same calls on ONE stream (mask, then the chain), as a single-threaded node chain
+    would.  Rank 0 prints one JSON line, value = median ms per frame (overlapped)."""
+    import torch
+    import ssf
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    iters = args.iters or (10 if args.solver == "gn" else 8)
+    N = args.rows * args.n_az
+    W, K = max(2, args.warmup), args.steps
+    t_data = time.perf_counter()
+    frames = make_data(args, dev, 2 * (W + K) + 2, 0, batch=1)
+    t_data = time.perf_counter() - t_data
+    off, h_off = ssf.frame_offsets([N], dev)
+    fe_mask = ssf.Frontend(args.rows, device=0)
+    fe_mask.reserve(1, N)
+    fe_mask.mask_split(args.mask_split)
+    fe_mask.seed(20240000)
+    fe = ssf.Frontend(args.rows, device=0, solver=args.solver, max_iter=iters)
+    fe.reserve(1, N)
+    s_mask, s_chain = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def run(ks, serial, profile=False):
+        pose_rel, pose_abs = ssf.identity_poses(1, dev), ssf.identity_poses(1, dev)
+        last = last_table = None
+        wall, ev = [], []
+        if profile:
+            for c in (fe_mask, fe):
+                c.kernel_times()
+                c.profile(True)
+        for k in ks:
+            pos, flow = frames[k]
+            sm, sc = (s_chain, s_chain) if serial else (s_mask, s_chain)
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            with torch.cuda.stream(sm):
+                e[0].record(sm)
+                out, bg = fe_mask.mask_pose(pos, flow, off, h_off, mode="gmm", want_mask=True)
+                e[1].record(sm)
+            with torch.cuda.stream(sc):
+                e[2].record(sc)
+                pb = fe.extract_planes_batch(pos, off, h_off, max_points=N)
+                e[3].record(sc)
+                table = fe.plane_table(pb)
+                e[4].record(sc)
+                if last is not None:
+                    fe.register(last, last_table, pb, pose_rel, pose_abs)
+                e[5].record(sc)
+            sm.synchronize()
+            sc.synchronize()
+            wall.append((time.perf_counter() - t0) * 1e3)
+            ev.append(e)
+            last, last_table = pb, table
+        kt = {}
+        if profile:
+            for c in (fe_mask, fe):
+                for name, (n, ms) in c.kernel_times().items():
+                    a, b = kt.get(name, (0, 0.0))
+                    kt[name] = (a + n, b + ms)
+                c.profile(False)
+        stages = dict(mask=[a[0].elapsed_time(a[1]) for a in ev],
+                      features=[a[2].elapsed_time(a[3]) for a in ev],
+                      plane_table=[a[3].elapsed_time(a[4]) for a in ev],
+                      registration=[a[4].elapsed_time(a[5]) for a in ev[1:]])
+        return wall[1:], stages, kt      # the first frame of a run has no pair to register
+
+    # warm up both orders, then time K frames of one sequence each way
+    run(range(0, W), False)
+    run(range(0, W), True)
+    wall_o, st_o, _ = run(range(W, W + K), False)
+    wall_s, st_s, _ = run(range(W + K + 1, W + 2 * K + 1), True)
+    _, _, kt = run(range(W, W + min(K, 8)), True, profile=True)
+    med = lambda v: float(np.median(v)) if len(v) else 0.0
+    kernels = {name: dict(launches=n, ms=ms / n) for name, (n, ms) in sorted(kt.items(), key=lambda x: -x[1][1])}
+    cpu = None
+    if not args.no_cpu_baseline:
+        iters_s = ["--rows", str(args.rows), "--n-az", str(args.n_az), "--solver", args.solver, "--iters", str(iters)]
+        single = _run_legs([("oracle", 0, iters_s)], args.cpu_seconds)[0]
+        if single.get("seconds"):
+            cpu = dict(value=single["seconds"] / max(1, single["frames"]) * 1e3, unit="ms/frame", cores=1,
+                       kind="port", sample=f"{single['frames']} consecutive frames of one sequence through "
+                                           "oracle/ssf_oracle.c (mask + features + plane table + registration), "
+                                           "one thread")
+    line = {
+        "metric": "LiDAR front-end latency per frame pair (mask+feature+GN), 64-beam 120k pts, 1 GPU",
+        "value": med(wall_o), "unit": "ms/frame", "n_gpus": 1, "steps": K, "warmup": W,
+        "ms_per_step": med(wall_o), "higher_is_better": False, "scaling": "none", "vs_baseline": None,
+        "dtype": "f32 features / f64 mask+solve",
+        "data": "synthetic (seeded ray-cast 64-beam scans, ssf/synth.py BatchScanner; one sequence)",
+        "config": {"workload": f"configs[1] as written: one {args.rows}-beam {N}-pt frame pair per step (B = 1); "
+                               f"mask(GMM+Kabsch, automatic split) || features -> plane table -> {args.solver} "
+                               f"x{iters}; host wall per frame, synchronised",
+                   "points_per_frame": N, "solver": args.solver, "iters": iters, "batch": 1},
+        "latency_ms": {"overlapped": {"median": med(wall_o), "mean": float(np.mean(wall_o)),
+                                      "p90": float(np.percentile(wall_o, 90))},
+                       "serial_one_stream": {"median": med(wall_s), "mean": float(np.mean(wall_s)),
+                                             "p90": float(np.percentile(wall_s, 90))}},
+        "stage_event_ms": {k: med(v) for k, v in st_o.items()},
+        "stage_event_ms_serial": {k: med(v) for k, v in st_s.items()},
+        "kernels": kernels, "cpu_baseline": cpu, "data_gen_s": round(t_data, 2),
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.latency:
+        if args.gpus != 1 or os.environ.get("WORLD_SIZE", "1") != "1":
+            sys.exit("bench.py --latency is a one-GPU, one-frame-pair measurement")
+        return latency(args)
     ws = os.environ.get("WORLD_SIZE")
     if ws is None and args.gpus > 1:
         sys.exit(launch_ranks(args))
@@ -481,6 +648,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
         pipe.step(k, batches, off, h_off, True)
+    if world > 1:
+        pipe.exchange()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -516,7 +685,8 @@ def main():
     total_frames = B * args.steps * world
     value = total_frames / elapsed
     cfg_name = ("configs[2] noSeg mask-before-features" if args.mask_before_features else
-                "configs[4] 256k-pt stress" if args.n_az >= 4000 else "configs[1]/[4] 120k-pt")
+                "configs[4] 256k-pt stress" if args.n_az >= 4000 else
+                "configs[1] shape (one 120k-pt frame pair per sequence per step)")
     line = {
         "metric": METRIC,
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
@@ -548,6 +718,16 @@ def main():
             t = traffic["kernels"].get(k, {}).get("traffic_bytes_per_launch")
             if t:
                 v["traffic"] = t
+                # the PMC-measured HBM bytes over the same kernel-only duration: the fraction of
+                # the HBM peak the kernel actually moves (beside the byte model's "frac")
+                v["traffic_gbs"] = t / (v["ms"] * 1e-3) / 1e9
+                v["traffic_frac"] = v["traffic_gbs"] / HBM_PEAK_GBS
+    if "k_solve" in kernels:
+        kernels["k_solve"]["bound"] = (
+            "latency: iterates on LDS-resident correspondences (one work-group per pair); per "
+            "GN iteration one evaluation (block reduction of 28 f64 terms, 256 threads) and the "
+            "serial 6x6 solve -- 'frac' is SURVEY 8(d)'s 36 B x C x evaluations model, "
+            "'traffic_frac' the PMC-measured HBM bytes over the same duration")
     mk = kernels.get("k_mask_pose")
     if mk and "gbs" in mk:
         line["roofline"] = {"bound": "hbm", "achieved": mk["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -564,6 +744,9 @@ def main():
     ns = {k: kernels[k]["frac"] for k in ("k_curv_select", "k_solve") if k in kernels and "frac" in kernels[k]}
     if ns:
         line["north_star_kernels_hbm_frac"] = ns
+        meas = {k: kernels[k]["traffic_frac"] for k in ns if "traffic_frac" in kernels[k]}
+        if meas:
+            line["north_star_kernels_hbm_frac_pmc"] = meas
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

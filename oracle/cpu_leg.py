@@ -110,7 +110,10 @@ def main():
     ap.add_argument("--n-az", type=int, default=1875)
     ap.add_argument("--solver", default="gn")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--cpu", type=int, default=None, help="pin this process to one CPU")
     a = ap.parse_args()
+    if a.cpu is not None and hasattr(os, "sched_setaffinity"):
+        os.sched_setaffinity(0, {a.cpu})
     r = leg_oracle(a) if a.leg == "oracle" else leg_sklearn(a)
     r["leg"] = a.leg
     r["seq"] = a.seq

@@ -12,6 +12,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "ssf", "_lib")
 OBJ_DIR = os.path.join(HERE, "build")
 LIB = os.path.join(OUT_DIR, "libssf_frontend.so")
+SYNTH_LIB = os.path.join(OUT_DIR, "libssf_synth.so")
 SOURCES = ["abi.hip", "features.hip", "registration.hip", "mask_pose.hip", "mask_pose_f64.hip", "loop.hip",
            "pointnet2.hip"]
 # sources that include another source file
@@ -58,6 +59,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
         list(ex.map(run, jobs))
     if force or jobs or _stale(LIB, objs):
         run([HIPCC, *FLAGS, "-shared", *objs, "-o", LIB])
+    # bench / test data generator (ssf.synth.BatchScanner): a library of its own, not the front-end
+    syn = os.path.join(CSRC, "synth.hip")
+    if force or _stale(SYNTH_LIB, [syn]):
+        run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-shared", syn,
+             "-o", SYNTH_LIB])
     return LIB
 
 

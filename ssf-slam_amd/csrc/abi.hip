@@ -312,8 +312,8 @@ static int32_t ensure_features(ssf_ctx* c, int32_t n_frames, int64_t total, int6
     SSF_TRY_HIP(c, c->hist.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(n_frames * n_chunks * R, 1)), "alloc hist");
     SSF_TRY_HIP(c, c->ring_off.ensure(sizeof(int32_t) * (size_t)n_frames * (R + 1)), "alloc ring_off");
     SSF_TRY_HIP(c, c->ring_xyzi.ensure(3 * sizeof(float) * (size_t)std::max<int64_t>(total, 1)), "alloc ring_xyz");
-    // + 64 dump slots for the selection stores of lanes without a selection (k_curv_select)
-    SSF_TRY_HIP(c, c->sel.ensure(sizeof(int32_t) * (size_t)(std::max<int64_t>(total, 1) + 64)), "alloc sel");
+    // per-row staging slots of the selected points (float4 at ring positions, k_curv_select)
+    SSF_TRY_HIP(c, c->sel.ensure(sizeof(float4) * (size_t)std::max<int64_t>(total, 1)), "alloc sel");
     SSF_TRY_HIP(c, c->sel_cnt.ensure(sizeof(int32_t) * (size_t)n_frames * R), "alloc sel_cnt");
     return SSF_OK;
 }
@@ -356,9 +356,9 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
     ssf::EdgeSel es{};
     const bool edges = d_edge_xyzi != nullptr;
     if (edges) {
-        SSF_TRY_HIP(c, c->esel.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(total_points, 1)), "alloc esel");
+        SSF_TRY_HIP(c, c->esel.ensure(sizeof(float4) * (size_t)std::max<int64_t>(total_points, 1)), "alloc esel");
         SSF_TRY_HIP(c, c->esel_cnt.ensure(sizeof(int32_t) * (size_t)n_frames * c->cfg.n_rows), "alloc esel_cnt");
-        es = ssf::EdgeSel{c->ecfg.edge_min, c->ecfg.edge_span, c->esel.as<int32_t>(),
+        es = ssf::EdgeSel{c->ecfg.edge_min, c->ecfg.edge_span, c->esel.as<float4>(),
                           c->esel_cnt.as<int32_t>(), reinterpret_cast<float4*>(d_edge_xyzi), d_edge_count};
     }
     ProfScope prof(c, stream);
@@ -367,8 +367,7 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
     hipError_t e = ssf::launch_extract_planes(
         (hipStream_t)stream, c->cfg, n_frames, d_pts, point_stride, d_frame_off, max_frame_points,
         d_keep, c->rid.as<int8_t>(), c->hist.as<int32_t>(), roff, c->ring_xyzi.as<float>(), ring4,
-        d_curv, c->sel.as<int32_t>(),
-        c->sel.as<int32_t>() + std::max<int64_t>(total_points, 1), c->sel_cnt.as<int32_t>(),
+        d_curv, c->sel.as<float4>(), c->sel_cnt.as<int32_t>(),
         reinterpret_cast<float4*>(d_plane_xyzi), d_plane_count, edges ? &es : nullptr);
     if (e != hipSuccess) return hip_fail(c, e, "extract_planes launch");
     return SSF_OK;

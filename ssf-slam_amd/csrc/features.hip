@@ -9,12 +9,12 @@
 //                 order exactly.  The chunk is regrouped by row in LDS and stored in contiguous
 //                 per-row runs of packed xyz (12 B/pt: the ring order alone carries indexInRow,
 //                 so intensity = indexInRow + row/100.0 (:77) is recomputed where it is needed)
-//   k_curv_select one wave per (frame,row): the row streams through a circular LDS window, the
-//                 11-tap stencil (:84-107) is evaluated left to right in float, and the same
-//                 wave runs the greedy spacing rule (:110-123) with a 64-bit ballot of
-//                 candidates per 64 points (jstart is wave-uniform).
-//   k_compact     row-major concatenation of the selected points (framePlanePtr order), with
-//                 their encoded intensity.
+//   k_curv_select one work-group per (frame,row): the row in one burst into an LDS tile, the
+//                 11-tap stencil (:84-107) evaluated left to right in float, 8 centres per
+//                 thread; the greedy spacing rule (:110-123) on one wave over candidate words;
+//                 the selected points (with their encoded intensity) stored into per-row slots
+//   k_compact     one work-group per frame: the per-row runs copied into the row-major plane
+//                 cloud (framePlanePtr order).
 #include "ssf_device.hpp"
 #include "ssf_internal.hpp"
 
@@ -249,229 +249,201 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
     }
 }
 
-// One WAVE per (frame, row), four rows per work-group, no block barrier.  The wave streams its
-// row in 64-point groups (one coalesced 12-byte load per lane) into a 256-point circular LDS
-// window (point p at p & 255, see stencil11w); group g-1's 11-tap stencil (:84-107, evaluated left to
-// right in float exactly as the reference) is computed once group g has landed, and the greedy
-// spacing rule (:110-123) runs on the same wave with a 64-bit ballot of candidates per group
-// (jstart is wave-uniform).  Three register buffers with static roles (one loop trip = three
-// groups; loads clamped and unconditional) keep three groups in flight: a rotation by register
-// moves, or a load or store under a branch, makes the compiler wait for every load at each
-// group.  The selected indices collect in LDS and leave once per trip.
-#ifndef SSF_CURV_ROWS_PER_WG
-#define SSF_CURV_ROWS_PER_WG 4
-#endif
-constexpr int kCurvRowsPerWG = SSF_CURV_ROWS_PER_WG;
-#ifndef SSF_CURV_DEPTH
-#define SSF_CURV_DEPTH 3
-#endif
-constexpr int kCurvDepth = SSF_CURV_DEPTH;   // 64-point groups in flight per wave (one trip)
-#ifndef SSF_CURV_PROBE
-#define SSF_CURV_PROBE 0                      // diagnostic variants only (tools/gpu scripts)
-#endif
+// One WORK-GROUP per (frame, row).  The row is requested in one burst of 2048-point tiles
+// (each thread issues its 9 clamped 12-byte loads before the first use, as the binning kernels
+// do) into an LDS tile of x | y | z float arrays with an 8-point halo on both sides.  Every
+// thread then owns 8 consecutive centres: it reads the 24 points around them as six aligned
+// ds_read_b128 per coordinate and evaluates the 11-tap sums (:84-107) left to right in float,
+// exactly as the reference, one coordinate at a time (8 partial sums live, not 33 taps).  The
+// planar candidates (value < planeMin, the value staying 0 for j < 5 and j >= n - 5) leave as one
+// byte per thread; wave 0 then runs the greedy spacing rule (:110-123) over the tile's 64-bit
+// words in scalar code, collecting up to 64 selections in one VGPR (lane k holds the k-th) and emitting
+// them -- x, y, z from the LDS tile, intensity = indexInRow + row / 100.0 (:77) -- as float4
+// stores into the row's own staging slots (ring position + rank).  k_compact then only copies
+// contiguous per-row runs into the frame-major plane cloud.  Rows longer than a tile carry the
+// greedy state (jstart) from tile to tile.
+// kEdge (beyond the reference, off by default): wave 1 runs the edge rule -- greedy in index
+// order, curvature > edge_min, spacing edge_span, centres in [5, n - 5) (oracle/edge_oracle.c) --
+// on a second byte array, into its own staging slots.
+constexpr int kCurvTile = 2048;                 // centres per tile (one tile per 64-beam 120k row)
+constexpr int kCurvHalo = 8;                    // >= 5, and a multiple of 8 (aligned windows)
+constexpr int kCurvSpan = kCurvTile + 2 * kCurvHalo;
+constexpr int kCurvLoads = (kCurvSpan + 255) / 256;
 
-// The window holds 256 points (4 groups; point p at p & 255) plus a mirror of its first 16 at
-// [256, 272), so the 11 taps of centre j are the contiguous a[b .. b + 10], b = (j - 5) & 255:
-// one base address, immediate LDS offsets; (x, y, z) of a point in one float4.
-constexpr int kWin = 256;
-constexpr int kWinPad = kWin + 16;
-
-// The 11 taps t[0 .. 10] (centre t[5]) from a float4 (x, y, z, -) window: 11 ds_read_b128 (16-B aligned,
-// immediate offsets) serve all three coordinates; each coordinate's sum is evaluated left to
-// right in float exactly as frameFeature.cpp:86-105.
-SSF_DEV void stencil11t(const float4* t, float& dx, float& dy, float& dz) {
-    float4 u[11];
-#pragma unroll
-    for (int k = 0; k < 11; ++k) u[k] = t[k];
-    // keep .w live: a whole-float4 read is ds_read_b128 (4 LDS cycles per wave), the x, y, z
-    // read the compiler would otherwise emit is ds_read_b96 (8 cycles).  One statement after
-    // all eleven reads: one per read made the compiler wait for each before issuing the next.
-    asm volatile("" ::"v"(u[0].w), "v"(u[1].w), "v"(u[2].w), "v"(u[3].w), "v"(u[4].w), "v"(u[5].w),
-                 "v"(u[6].w), "v"(u[7].w), "v"(u[8].w), "v"(u[9].w), "v"(u[10].w));
-    float sx = u[0].x + u[1].x, sy = u[0].y + u[1].y, sz = u[0].z + u[1].z;
-#pragma unroll
-    for (int k = 2; k < 11; ++k) {
-        if (k == 5) { sx = sx - 10.0f * u[5].x; sy = sy - 10.0f * u[5].y; sz = sz - 10.0f * u[5].z; }
-        else { sx = sx + u[k].x; sy = sy + u[k].y; sz = sz + u[k].z; }
-    }
-    dx = sx; dy = sy; dz = sz;
-}
-
-// the taps of centre j in the circular window (t = a[(j - 5) & 255 ..], contiguous by the mirror)
-SSF_DEV void stencil11w(const float4* a, int j, float& dx, float& dy, float& dz) {
-    stencil11t(a + ((j - 5) & (kWin - 1)), dx, dy, dz);
-}
-
-// kHalves: 64-entry selection stores per trip (a trip selects <= 64 kCurvDepth / span + 1
-// points: one store for span >= 4, two below)
-// kEdge (beyond the reference, off by default): the same wave also runs the edge rule --
-// greedy in index order, curvature > edge_min, spacing edge_span (the mirror image of :110-123;
-// oracle/edge_oracle.c) -- into esel / esel_cnt.
-template <bool kCurv, int kHalves, bool kEdge>
-__global__ __launch_bounds__(64 * kCurvRowsPerWG) void k_curv_select(const int64_t* __restrict__ frame_off,
-                                                     int n_rows, int row_start, int row_end,
-                                                     float plane_min, int plane_span,
-                                                     const int32_t* __restrict__ ring_off,
-                                                     const Xyz* __restrict__ rxyz,
-                                                     float* __restrict__ curv,
-                                                     int32_t* __restrict__ sel,
-                                                     int32_t* __restrict__ sel_cnt,
-                                                     int32_t* __restrict__ sel_dump,
-                                                     float edge_min, int edge_span,
-                                                     int32_t* __restrict__ esel,
-                                                     int32_t* __restrict__ esel_cnt) {
-    __shared__ float4 win[kCurvRowsPerWG][kWinPad];
-    __shared__ int32_t slist[kCurvRowsPerWG][64 * kHalves];
-    __shared__ int32_t elist[kEdge ? kCurvRowsPerWG : 1][kEdge ? 64 * kHalves : 1];
-    // the wave index through readfirstlane: the compiler then knows the row, its length and
-    // every loop bound are wave-uniform (scalar loads, no exec-masked loops)
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int r = blockIdx.x * kCurvRowsPerWG + w, f = blockIdx.y;
-    if (r >= n_rows) return;                                   // wave-uniform
-    const int32_t* ro = ring_off + (int64_t)f * (n_rows + 1);
-    const int rs = ro[r], n_r = ro[r + 1] - rs;
-    const int64_t base = frame_off[f] + rs;
-    const bool in_rows = (r >= row_start) && (r < n_rows - row_end);
-    if (!in_rows || n_r == 0) {
-        if (kCurv)
-            for (int j = lane; j < n_r; j += 64) curv[base + j] = 0.0f;
-        if (lane == 0) sel_cnt[(int64_t)f * n_rows + r] = 0;
-        if (kEdge && lane == 0) esel_cnt[(int64_t)f * n_rows + r] = 0;
-        return;
-    }
-    float4* wv = win[w];
-    int32_t* sl = slist[w];
-    const Xyz* src = rxyz + base;
-    const int ng = (n_r + 63) >> 6;
-#if SSF_CURV_PROBE == 3
-    // diagnostic: the same bytes as lane-contiguous 16-B loads (48 lanes x 16 B = 64 points)
-    const float4* src4 = reinterpret_cast<const float4*>(reinterpret_cast<uintptr_t>(src) & ~(uintptr_t)15);
-    const int n4 = (3 * n_r + 3) / 4;
-    auto load = [&](int g) {
-        const float4 q = src4[min(48 * g + min(lane, 47), n4 - 1)];
-        return Xyz{q.x + q.w, q.y, q.z};
+// The greedy rule over one tile's candidate words (wave-uniform, run by ONE wave): selections at
+// ring positions >= jstart, spaced by `span`; emitted 64 at a time from the LDS tile.
+SSF_DEV void greedy_emit(const uint64_t* words, int t0, int tn, int span, int& jstart, int& cnt,
+                         const float* sx, const float* sy, const float* sz, double rfrac,
+                         float4* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    int nl = 0, selv = 0;
+    auto flush = [&]() {
+        if (lane < nl) {
+            const int p = selv - (t0 - kCurvHalo);
+            out[cnt + lane] = make_float4(sx[p], sy[p], sz[p], (float)((double)selv + rfrac));
+        }
+        cnt += nl;
+        nl = 0;
     };
-#else
-    auto load = [&](int g) { return src[min(64 * g + lane, n_r - 1)]; };   // clamped
-#endif
-    int cnt = 0, nl = 0, jstart = 0;                           // wave-uniform
-    int ecnt = 0, enl = 0, ejstart = 0;                        // wave-uniform (kEdge)
-    int32_t* el = elist[kEdge ? w : 0];
-    auto group = [&](Xyz& buf, int g) {
-        {                                                      // group g into the window
-            const int p = (64 * g + lane) & (kWin - 1);
-            const float4 q = make_float4(buf.x, buf.y, buf.z, 0.0f);
-            wv[p] = q;
-            if (p < kWinPad - kWin) wv[p + kWin] = q;
-            buf = load(g + kCurvDepth);
-        }
-        if (g == 0 || g > ng) return;                          // uniform
-        const int j = 64 * (g - 1) + lane;                     // group g-1: its stencil is complete
-        float v = 0.0f;
-#if SSF_CURV_PROBE == 1 || SSF_CURV_PROBE == 3
-        // diagnostic (tools/ variants only): the stream and the window, no stencil, no greedy
-        v = wv[(j - 5) & (kWin - 1)].x;
-#else
-        if (j >= 5 && j < n_r - 5) {
-            float dx, dy, dz;
-            stencil11w(wv, j, dx, dy, dz);
-            v = dx * dx + dy * dy;
-            v = v + dz * dz;
-        }
-#endif
-        if (kCurv) curv[base + min(j, n_r - 1)] = v;   // lanes past the row write its last value, 0
-        uint64_t m = __ballot(j < n_r && v < plane_min);
-#if SSF_CURV_PROBE
-        // diagnostic: no greedy walk (one selection per group keeps the ballot live)
-        if (m) { if (lane == 0) sl[nl] = 64 * (g - 1) + __ffsll((unsigned long long)m) - 1; nl++; }
-        (void)jstart;
-        if (true) return;
-#endif
-        const int j0 = 64 * (g - 1);
+    const int nw = (tn + 63) >> 6;
+    for (int wi = 0; wi < nw; ++wi) {
+        const uint64_t wv = words[wi];                      // LDS broadcast
+        uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wv >> 32)) << 32) |
+                     (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wv);
+        const int j0 = t0 + 64 * wi;
         while (true) {
             const int lo = jstart - j0;
             if (lo >= 64) break;
             if (lo > 0) m &= ~((1ull << lo) - 1ull);
             if (!m) break;
-            const int l = __ffsll((unsigned long long)m) - 1;
-            const int jj = __builtin_amdgcn_readfirstlane(j0 + l);
-            if (lane == 0) sl[nl] = jj;
-            nl++;
-            jstart = jj + plane_span;
+            const int jj = j0 + (int)__builtin_ctzll(m);
+            if (lane == nl) selv = jj;                 // lane nl keeps selection nl
+            jstart = jj + span;
+            if (++nl == 64) flush();
         }
-        nl = __builtin_amdgcn_readfirstlane(nl);
-        if (kEdge) {
-            uint64_t me = __ballot(j >= 5 && j < n_r - 5 && v > edge_min);
-            while (true) {
-                const int lo = ejstart - j0;
-                if (lo >= 64) break;
-                if (lo > 0) me &= ~((1ull << lo) - 1ull);
-                if (!me) break;
-                const int l = __ffsll((unsigned long long)me) - 1;
-                const int jj = __builtin_amdgcn_readfirstlane(j0 + l);
-                if (lane == 0) el[enl] = jj;
-                enl++;
-                ejstart = jj + edge_span;
-            }
-            enl = __builtin_amdgcn_readfirstlane(enl);
-        }
-    };
-    // a trip's selections (<= 64 kHalves) leave with unconditional stores; lanes without one write
-    // the row's last slot, which no selection list reaches when the row has >= 2 points (at most
-    // ceil(n_r / 2) entries for plane_span >= 2).  A ONE-point row selects its point 0, its last
-    // slot: those lanes write a 64-slot dump after the last point of the batch instead.
-    int32_t* const spare = n_r >= 2 ? sel + base + n_r - 1 : sel_dump + lane;
-    // edges never select the row's last point (j < n_r - 5), so its slot is a safe spare too
-    int32_t* const espare = kEdge ? (n_r >= 2 ? esel + base + n_r - 1 : sel_dump + lane) : nullptr;
-    // prologue loads in buffer order (the loop's waits count on b[0] being the oldest)
-    Xyz b[kCurvDepth];
-#pragma unroll
-    for (int k = 0; k < kCurvDepth; ++k) {
-        b[k] = load(k);
-        asm volatile("" ::: "memory");
     }
-    for (int g = 0; g <= ng; g += kCurvDepth) {
-#pragma unroll
-        for (int k = 0; k < kCurvDepth; ++k) group(b[k], g + k);
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int h = 0; h < kHalves; ++h)
-            *(lane + 64 * h < nl ? sel + base + cnt + 64 * h + lane : spare) = sl[64 * h + lane];
-        if (kEdge) {
-#pragma unroll
-            for (int h = 0; h < kHalves; ++h)
-                *(lane + 64 * h < enl ? esel + base + ecnt + 64 * h + lane : espare) = el[64 * h + lane];
-        }
-        __builtin_amdgcn_wave_barrier();
-        cnt += nl;
-        nl = 0;
-        ecnt += enl;
-        enl = 0;
-    }
-    if (lane == 0) sel_cnt[(int64_t)f * n_rows + r] = cnt;
-    if (kEdge && lane == 0) esel_cnt[(int64_t)f * n_rows + r] = ecnt;
+    flush();
 }
 
-__global__ __launch_bounds__(256) void k_compact(const int64_t* __restrict__ frame_off, int n_rows,
-                                                 const int32_t* __restrict__ ring_off,
-                                                 const Xyz* __restrict__ rxyz,
-                                                 const int32_t* __restrict__ sel,
-                                                 const int32_t* __restrict__ sel_cnt,
-                                                 float4* __restrict__ plane,
-                                                 int32_t* __restrict__ plane_count) {
-    const int r = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
-    const int32_t* sc = sel_cnt + (int64_t)f * n_rows;
-    int pre = 0;
-    for (int k = 0; k < r; ++k) pre += sc[k];  // <= 63 uniform loads
-    const int n = sc[r];
-    if (r == n_rows - 1 && tid == 0) plane_count[f] = pre + n;
+template <bool kCurv, bool kEdge>
+__global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__ frame_off,
+                                                     int n_rows, int row_start, int row_end,
+                                                     float plane_min, int plane_span,
+                                                     const int32_t* __restrict__ ring_off,
+                                                     const Xyz* __restrict__ rxyz,
+                                                     float* __restrict__ curv,
+                                                     float4* __restrict__ stage,
+                                                     int32_t* __restrict__ sel_cnt,
+                                                     float edge_min, int edge_span,
+                                                     float4* __restrict__ estage,
+                                                     int32_t* __restrict__ esel_cnt) {
+    __shared__ __attribute__((aligned(16))) float sx[kCurvSpan], sy[kCurvSpan], sz[kCurvSpan];
+    __shared__ __attribute__((aligned(16))) uint8_t pbits[kCurvTile / 8];
+    __shared__ __attribute__((aligned(16))) uint8_t ebits[kEdge ? kCurvTile / 8 : 16];
+    const int tid = threadIdx.x, w = tid >> 6;
+    const int r = blockIdx.x, f = blockIdx.y;
+    const int32_t* ro = ring_off + (int64_t)f * (n_rows + 1);
+    const int rs = ro[r], n_r = ro[r + 1] - rs;
+    const int64_t base = frame_off[f] + rs;
+    const bool in_rows = (r >= row_start) && (r < n_rows - row_end);
+    if (!in_rows || n_r == 0) {                                  // uniform
+        if (kCurv)
+            for (int j = tid; j < n_r; j += 256) curv[base + j] = 0.0f;
+        if (tid == 0) sel_cnt[(int64_t)f * n_rows + r] = 0;
+        if (kEdge && tid == 0) esel_cnt[(int64_t)f * n_rows + r] = 0;
+        return;
+    }
+    const double rfrac = (double)r / 100.0;                    // :77
+    const Xyz* src = rxyz + base;
+    int cnt = 0, jstart = 0;                                   // wave 0's greedy state
+    int ecnt = 0, ejstart = 0;                                 // wave 1's (kEdge)
+    for (int t0 = 0; t0 < n_r; t0 += kCurvTile) {              // uniform
+        const int tn = min(kCurvTile, n_r - t0);
+        {   // positions [t0 - halo, t0 + tile + halo), clamped into the row: all loads first
+            Xyz q[kCurvLoads];
+#pragma unroll
+            for (int k = 0; k < kCurvLoads; ++k) {
+                const int pos = t0 - kCurvHalo + tid + 256 * k;
+                q[k] = src[min(max(pos, 0), n_r - 1)];
+            }
+#pragma unroll
+            for (int k = 0; k < kCurvLoads; ++k) {
+                const int p = tid + 256 * k;
+                if (p < kCurvSpan) { sx[p] = q[k].x; sy[p] = q[k].y; sz[p] = q[k].z; }
+            }
+        }
+        __syncthreads();
+        // centres j = t0 + 8 tid + i; their taps are tile entries 8 tid + 3 + i .. 8 tid + 13 + i
+        float d0[8], d1[8];
+        float v[8];
+        auto coord = [&](const float* a, float (&d)[8]) {
+            float h[24];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const float4 x4 = *reinterpret_cast<const float4*>(a + 8 * tid + 4 * k);
+                h[4 * k] = x4.x; h[4 * k + 1] = x4.y; h[4 * k + 2] = x4.z; h[4 * k + 3] = x4.w;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float* u = h + 3 + i;                    // u[0 .. 10], centre u[5]
+                float acc = u[0] + u[1];
+#pragma unroll
+                for (int k = 2; k < 11; ++k) acc = (k == 5) ? acc - 10.0f * u[5] : acc + u[k];
+                d[i] = acc;
+            }
+        };
+        if (8 * tid < tn) {
+            coord(sx, d0);
+            coord(sy, d1);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = d0[i] * d0[i] + d1[i] * d1[i];
+            coord(sz, d0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = v[i] + d0[i] * d0[i];
+        }
+        uint32_t pb = 0, eb = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int jl = 8 * tid + i, j = t0 + jl;
+            if (jl < tn) {
+                const bool inner = j >= 5 && j < n_r - 5;
+                const float val = inner ? v[i] : 0.0f;
+                if (kCurv) curv[base + j] = val;
+                pb |= (uint32_t)(val < plane_min) << i;
+                if (kEdge) eb |= (uint32_t)(inner && val > edge_min) << i;
+            }
+        }
+        if (8 * tid < kCurvTile) pbits[tid] = (uint8_t)pb;
+        if (kEdge && 8 * tid < kCurvTile) ebits[tid] = (uint8_t)eb;
+        __syncthreads();
+        if (w == 0)
+            greedy_emit(reinterpret_cast<const uint64_t*>(pbits), t0, tn, plane_span, jstart, cnt,
+                        sx, sy, sz, rfrac, stage + base);
+        else if (kEdge && w == 1)
+            greedy_emit(reinterpret_cast<const uint64_t*>(ebits), t0, tn, edge_span, ejstart, ecnt,
+                        sx, sy, sz, rfrac, estage + base);
+        __syncthreads();                                       // the tile is read; next tile
+    }
+    if (tid == 0) sel_cnt[(int64_t)f * n_rows + r] = cnt;
+    if (kEdge && tid == 64) esel_cnt[(int64_t)f * n_rows + r] = ecnt;
+}
+
+// One work-group per frame: the row counts' prefix in LDS, then every output slot of the frame's
+// plane cloud (row-major, framePlanePtr order) copies its float4 from its row's staging run.
+__global__ __launch_bounds__(1024) void k_compact(const int64_t* __restrict__ frame_off, int n_rows,
+                                                  const int32_t* __restrict__ ring_off,
+                                                  const float4* __restrict__ stage,
+                                                  const int32_t* __restrict__ sel_cnt,
+                                                  float4* __restrict__ plane,
+                                                  int32_t* __restrict__ plane_count) {
+    __shared__ int pre[kMaxRows + 1];
+    __shared__ int rbeg[kMaxRows];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    if (tid < 64) {
+        const int c = tid < n_rows ? sel_cnt[(int64_t)f * n_rows + tid] : 0;
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (tid >= o) incl += y;
+        }
+        if (tid < n_rows) {
+            pre[tid] = incl - c;
+            rbeg[tid] = ring_off[(int64_t)f * (n_rows + 1) + tid];
+        }
+        if (tid == 63) pre[n_rows] = incl;
+    }
+    __syncthreads();
+    const int total = pre[n_rows];
     const int64_t fb = frame_off[f];
-    const int64_t base = fb + ring_off[(int64_t)f * (n_rows + 1) + r];
-    const double rfrac = (double)r / 100.0;
-    for (int k = tid; k < n; k += blockDim.x) {
-        const int j = sel[base + k];                 // indexInRow
-        const Xyz p = rxyz[base + j];
-        plane[fb + pre + k] = make_float4(p.x, p.y, p.z, (float)((double)j + rfrac));   // :77
+    if (tid == 0) plane_count[f] = total;
+    for (int k = tid; k < total; k += blockDim.x) {
+        int lo = 0, hi = n_rows - 1;                           // the row r with pre[r] <= k < pre[r + 1]
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (pre[mid] <= k) lo = mid; else hi = mid - 1;
+        }
+        plane[fb + k] = stage[fb + rbeg[lo] + (k - pre[lo])];
     }
 }
 
@@ -479,12 +451,12 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
                                  const float* pts, int stride, const int64_t* frame_off,
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
                                  int32_t* ring_off, float* ring_xyz, float4* ring_xyzi, float* curv,
-                                 int32_t* sel,
-                                 int32_t* sel_dump, int32_t* sel_cnt, float4* plane,
+                                 float4* stage, int32_t* sel_cnt, float4* plane,
                                  int32_t* plane_count, const EdgeSel* edge) {
     const int R = cfg.n_rows;
     const int n_chunks = (int)((max_pts + kBinChunk - 1) / kBinChunk);
     if (n_frames <= 0) return hipSuccess;
+    if (R > kMaxRows) return hipErrorInvalidValue;
     if (n_chunks > 0) {
         kmark(s, "k_bin_count");
         hipLaunchKernelGGL(k_bin_count, dim3(n_chunks, n_frames), dim3(256), 0, s, pts, stride,
@@ -498,40 +470,27 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
                            frame_off, R, n_chunks, rid, hist, ring_off,
                            reinterpret_cast<Xyz*>(ring_xyz), ring_xyzi);
     }
-    const dim3 cgrid((R + kCurvRowsPerWG - 1) / kCurvRowsPerWG, n_frames);
+    const dim3 cgrid(R, n_frames);
     kmark(s, "k_curv_select");
     const Xyz* rx = reinterpret_cast<const Xyz*>(ring_xyz);
-    const bool two = cfg.plane_span < 4 || (edge && edge->span < 4);
     const float emin = edge ? edge->min_curv : 0.f;
     const int espan = edge ? edge->span : 1;
-    int32_t* esel = edge ? edge->sel : nullptr;
+    float4* estage = edge ? edge->stage : nullptr;
     int32_t* ecnt = edge ? edge->sel_cnt : nullptr;
-#define SSF_CURV_LAUNCH(C, H, E)                                                                  \
-    hipLaunchKernelGGL((k_curv_select<C, H, E>), cgrid, dim3(64 * kCurvRowsPerWG), 0, s, frame_off, \
-                       R, cfg.row_start, cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off, rx,  \
-                       curv, sel, sel_cnt, sel_dump, emin, espan, esel, ecnt)
-    if (edge) {
-        if (curv) { if (two) SSF_CURV_LAUNCH(true, 2, true); else SSF_CURV_LAUNCH(true, 1, true); }
-        else { if (two) SSF_CURV_LAUNCH(false, 2, true); else SSF_CURV_LAUNCH(false, 1, true); }
-    } else {
-        if (curv) { if (two) SSF_CURV_LAUNCH(true, 2, false); else SSF_CURV_LAUNCH(true, 1, false); }
-        else { if (two) SSF_CURV_LAUNCH(false, 2, false); else SSF_CURV_LAUNCH(false, 1, false); }
-    }
-#ifdef SSF_CURV_TWICE
-    // diagnostic (tools/ variants only): the same launch again, on data the previous kernel
-    // left settled (k_curv_select is idempotent)
-    kmark(s, "k_curv_select_again");
-    if (!edge) { if (curv) { if (two) SSF_CURV_LAUNCH(true, 2, false); else SSF_CURV_LAUNCH(true, 1, false); }
-                 else { if (two) SSF_CURV_LAUNCH(false, 2, false); else SSF_CURV_LAUNCH(false, 1, false); } }
-#endif
+#define SSF_CURV_LAUNCH(C, E)                                                                      \
+    hipLaunchKernelGGL((k_curv_select<C, E>), cgrid, dim3(256), 0, s, frame_off, R, cfg.row_start,  \
+                       cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off, rx, curv, stage, sel_cnt, \
+                       emin, espan, estage, ecnt)
+    if (edge) { if (curv) SSF_CURV_LAUNCH(true, true); else SSF_CURV_LAUNCH(false, true); }
+    else { if (curv) SSF_CURV_LAUNCH(true, false); else SSF_CURV_LAUNCH(false, false); }
 #undef SSF_CURV_LAUNCH
     kmark(s, "k_compact");
-    hipLaunchKernelGGL(k_compact, dim3(R, n_frames), dim3(256), 0, s, frame_off, R, ring_off,
-                       rx, sel, sel_cnt, plane, plane_count);
+    hipLaunchKernelGGL(k_compact, dim3(n_frames), dim3(1024), 0, s, frame_off, R, ring_off, stage,
+                       sel_cnt, plane, plane_count);
     if (edge) {
         kmark(s, "k_compact_edges");
-        hipLaunchKernelGGL(k_compact, dim3(R, n_frames), dim3(256), 0, s, frame_off, R, ring_off,
-                           rx, edge->sel, edge->sel_cnt, edge->out, edge->count);
+        hipLaunchKernelGGL(k_compact, dim3(n_frames), dim3(1024), 0, s, frame_off, R, ring_off,
+                           edge->stage, edge->sel_cnt, edge->out, edge->count);
     }
     return hipGetLastError();
 }

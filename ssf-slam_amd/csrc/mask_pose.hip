@@ -513,8 +513,28 @@ struct Split {
     int64_t r0, r1;            // its points [r0, r1) of the frame
     double* part;              // the frame's slots [kMaxExchanges][G][kSlot]
     uint32_t* arrive;          // the frame's arrival counter (monotonic over its exchanges)
+    uint32_t* fail;            // the frame's failure word: set by any part whose wait timed out
     uint32_t seq;              // exchanges done (uniform)
 };
+
+// SSF_MASK_XCHG_FENCES=1 (A/B only): an agent-scope release fence before the arrival add and an
+// agent-scope acquire after the poll, on top of the write-through form below.
+#ifndef SSF_MASK_XCHG_FENCES
+#define SSF_MASK_XCHG_FENCES 0
+#endif
+
+// lane 0: wait until the frame's arrival counter reaches `target` (relaxed sc1 polls with
+// s_sleep back-off); false when a partner reported a timeout or the spin bound ran out
+SSF_DEV bool wait_arrivals(const Split& X, uint32_t target) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(X.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > kSpinLimit ||
+            __hip_atomic_load(X.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+            return false;
+    }
+    return true;
+}
 
 template <int N, bool kMin = false>
 SSF_DEV bool exchange(Split& X, double (&v)[N], double* tmp, int* okflag) {
@@ -530,20 +550,27 @@ SSF_DEV bool exchange(Split& X, double (&v)[N], double* tmp, int* okflag) {
                                __HIP_MEMORY_SCOPE_AGENT);
     X.seq += 1u;
     if (threadIdx.x < 64) {                        // wave 0 stored every value
+        // drain the write-through stores before the signal (R1); the asm is also the compiler
+        // barrier that keeps them above the add
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (threadIdx.x == 0) {
+#if SSF_MASK_XCHG_FENCES
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
             __hip_atomic_fetch_add(X.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t target = (uint32_t)X.G * X.seq;
-            uint32_t spins = 0;
-            int ok = 1;
-            while (__hip_atomic_load(X.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > kSpinLimit) { ok = 0; break; }
-            }
+            const int ok = wait_arrivals(X, (uint32_t)X.G * X.seq) ? 1 : 0;
+#if SSF_MASK_XCHG_FENCES
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
             *okflag = ok;
         }
     }
     __syncthreads();
+    // no instruction: keeps the compiler from moving the slot loads above the poll and the
+    // barrier (the sc1 loads themselves stand in for the acquire: Guideline 16, Valid forms row 1)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (!*okflag) return false;                    // uniform
     if (threadIdx.x < (unsigned)N) {
         double acc = kMin ? __builtin_inf() : 0.0;
@@ -618,12 +645,18 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     }
     X.part = parts + (size_t)f * kMaxExchanges * (size_t)G * kSlot;
     X.arrive = sync + 4 + f;
+    X.fail = sync + 4 + n_frames + f;
     X.seq = 0;
     const int64_t r0 = X.r0, r1 = X.r1;
     auto sync_failed = [&]() {                 // a partner never arrived: report, never hang
-        if (tid == 0 && g == 0) {
-            for (int i = 0; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
-            out[SSF_POSE_OUT_STATUS] = SSF_POSE_SYNC_FAILED;
+        if (tid == 0) {
+            // every part reports, so part 0 never publishes a frame whose other parts stopped
+            // before their share of the mask (the done round below)
+            __hip_atomic_store(X.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (g == 0) {
+                for (int i = 0; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
+                out[SSF_POSE_OUT_STATUS] = SSF_POSE_SYNC_FAILED;
+            }
         }
     };
     if (tid == 0) {
@@ -1339,6 +1372,19 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     if (bg_mask && S.bg != S.bg_pred) {
         for (int64_t i = r0 + tid; i < r1; i += blockDim.x) bg_mask[fb + i] ^= 1;
     }
+    if (G > 1) {
+        // done round: part 0's success status stands only once every part has finished its
+        // share of the mask (a part whose wait timed out returned early and set the failure word)
+        __syncthreads();
+        if (tid == 0) {
+            __hip_atomic_fetch_add(X.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            X.seq += 1u;
+            if (g == 0 && !wait_arrivals(X, (uint32_t)G * X.seq)) {
+                for (int i = 0; i < SSF_POSE_OUT_STRIDE; ++i) out[i] = 0.0;
+                out[SSF_POSE_OUT_STATUS] = SSF_POSE_SYNC_FAILED;
+            }
+        }
+    }
     SSF_STAMP(5);
     }();                                       // the frame part
     }                                          // tickets
@@ -1379,7 +1425,8 @@ int mask_pose_slots(int device) {
     return cus * per;
 }
 
-size_t mask_sync_bytes(int n_frames) { return (size_t)(4 + n_frames) * sizeof(uint32_t); }
+// ticket words, then per frame its arrival counter and its failure word
+size_t mask_sync_bytes(int n_frames) { return (size_t)(4 + 2 * n_frames) * sizeof(uint32_t); }
 size_t mask_parts_bytes(int n_frames, int G) {
     return G > 1 ? (size_t)n_frames * kMaxExchanges * G * kSlot * sizeof(double) : 0;
 }

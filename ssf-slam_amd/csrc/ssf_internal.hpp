@@ -51,12 +51,12 @@ struct alignas(16) CorrRec {
 
 // ---- launchers (features.hip) ----
 // Edge selection of launch_extract_planes (beyond the reference; nullptr = planes only):
-// selection indices / per-row counts in ctx scratch, the compacted edge cloud (float4 x, y, z,
-// intensity at the frame offsets) and per-frame counts out.
+// per-row staging slots (float4 per point) / per-row counts in ctx scratch, the compacted edge
+// cloud (float4 x, y, z, intensity at the frame offsets) and per-frame counts out.
 struct EdgeSel {
     float min_curv;
     int span;
-    int32_t* sel;
+    float4* stage;
     int32_t* sel_cnt;
     float4* out;
     int32_t* count;
@@ -65,8 +65,7 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
                                  const float* pts, int stride, const int64_t* frame_off,
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
                                  int32_t* ring_off, float* ring_xyz, float4* ring_xyzi,
-                                 float* curv, int32_t* sel, int32_t* sel_dump, int32_t* sel_cnt,
-                                 float4* plane,
+                                 float* curv, float4* stage, int32_t* sel_cnt, float4* plane,
                                  int32_t* plane_count, const EdgeSel* edge = nullptr);
 
 // ---- launchers (registration.hip) ----

@@ -29,6 +29,19 @@ def pose_record(pose_abs: torch.Tensor, mask_out: torch.Tensor | None = None) ->
     return torch.cat(parts, 1).contiguous()
 
 
+def gather_pose_records(records, group=None) -> torch.Tensor:
+    """Deferred exchange: the records of K steps ([K] x [n, k], one per step, each from
+    pose_record) stacked and all-gathered in ONE collective -> [K, world * n, k], step-major,
+    ranks in order within a step.  Used at the end of a run (or every K steps) so that no step
+    of the pipeline waits on its streams for a collective (once per batch or
+    at the end of a sequence)."""
+    stack = torch.stack(list(records), 0).contiguous()          # [K, n, k]
+    K, n, k = stack.shape
+    allr = gather_poses(stack.view(K, n * k), group)             # [world * K, n * k]
+    world = allr.shape[0] // K
+    return allr.view(world, K, n, k).transpose(0, 1).reshape(K, world * n, k)
+
+
 def gather_poses(local: torch.Tensor, group=None) -> torch.Tensor:
     """All-gather equal-shaped per-rank pose records -> [world * n, k] in rank order."""
     if not dist.is_available() or not dist.is_initialized():

@@ -67,7 +67,8 @@ def _ros_pointcloud_odometry(a, mode):
     rospy = rosbridge.require()[0]
     rospy.init_node("velodyne_points_odometry_node", anonymous=True)
     topics = ["/velodyne_points"] + ([] if mode == "none" else ["/frame_odom1"])
-    pub = rosbridge.RosPublisher(topics)
+    # PointCloudOdometry_onlyPC.py:15 advertises velodyne_points with queue 10, the others 100
+    pub = rosbridge.RosPublisher(topics, queue={"/velodyne_points": 10} if mode == "none" else None)
     rate = rospy.Rate(a.rate)
     rospy.loginfo("\033[1;32m----> PointCloudOdometry Started.\033[0m")
     root = rospy.get_param("~DATASET_PATH") if rospy.has_param("~DATASET_PATH") else "."
@@ -126,7 +127,8 @@ def node_main(exe: str, argv=None):
         path = rospy.get_param("~RESULT_PATH") if rospy.has_param("~RESULT_PATH") else None
         pub = rosbridge.RosPublisher(["/map_odom_res3", "/map_frame_res3", "/map_laser_path_res3"])
         node = nodes.MapOptimizationNode(pub, device=a.device, tum_path=path)
-        rospy.Subscriber("/plane_frame_cloud2", sensor_msgs.PointCloud2, node.on_plane_cloud, queue_size=100)
+        rospy.Subscriber("/plane_frame_cloud2", sensor_msgs.PointCloud2, node.on_plane_cloud,
+                         queue_size=10)                               # mapOptmization.cpp:473
         rospy.Subscriber("/frame_odom2", nav_msgs.Odometry,
                          lambda m: node.on_odom(rosbridge.from_ros_odometry(m)), queue_size=100)
     rospy.loginfo(f"\033[1;32m----> {name} Started.\033[0m")

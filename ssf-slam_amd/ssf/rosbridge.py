@@ -107,7 +107,8 @@ def to_ros_array(std_msgs, msg):
 
 # topic -> (message class attribute path, converter kind); queue sizes from the reference
 TOPICS = {
-    "/velodyne_points": ("sensor_msgs", "PointCloud2", "cloud", 100),   # PointCloudOdometry_noSeg.py:41
+    "/velodyne_points": ("sensor_msgs", "PointCloud2", "cloud", 100),   # PointCloudOdometry_noSeg.py:42
+    #                                          (PointCloudOdometry_onlyPC.py:15 uses 10: queue= below)
     "/frame_odom1": ("std_msgs", "Float64MultiArray", "array", 100),    # :42
     "/plane_frame_cloud1": ("sensor_msgs", "PointCloud2", "cloud", 100),  # frameFeature.cpp:162
     "/org_frame_cloud1": ("sensor_msgs", "PointCloud2", "cloud", 100),    # :163
@@ -115,7 +116,7 @@ TOPICS = {
     "/frame_odom2": ("nav_msgs", "Odometry", "odom", 100),                # :326
     "/frame_odom_path2": ("nav_msgs", "Path", "path", 100),               # :327
     "/map_odom_res3": ("nav_msgs", "Odometry", "odom", 100),              # mapOptmization.cpp:471-478
-    "/map_frame_res3": ("sensor_msgs", "PointCloud2", "cloud", 100),
+    "/map_frame_res3": ("sensor_msgs", "PointCloud2", "cloud", 10),       # mapOptmization.cpp:475
     "/map_laser_path_res3": ("nav_msgs", "Path", "path", 100),
 }
 
@@ -123,11 +124,13 @@ TOPICS = {
 class RosPublisher:
     """publish(topic, stand-in message) -> the real publisher of that topic, converted."""
 
-    def __init__(self, topics, mods=None):
+    def __init__(self, topics, mods=None, queue=None):
+        """queue: {topic: size} where the publishing script's own line differs from TOPICS"""
         self.rospy, self.sensor_msgs, self.std_msgs, self.nav_msgs, self.geometry_msgs = mods or require()
         self.pubs = {}
         for t in topics:
             pkg, cls, kind, q = TOPICS[t]
+            q = (queue or {}).get(t, q)
             klass = getattr(getattr(self, pkg), cls)
             self.pubs[t] = (self.rospy.Publisher(t.lstrip("/"), klass, queue_size=q), kind)
 

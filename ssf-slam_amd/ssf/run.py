@@ -27,11 +27,17 @@ def main(argv=None):
                     help="also run mapOptmization (loop closure) and write its RESULT_PATH TUM file")
     a = ap.parse_args(argv)
     from .nodes import run_sequence
+    import os
+    import sys
+    if a.tum and os.path.exists(a.tum) and not a.truncate:
+        print(f"ssf.run: appending to the existing {a.tum} (the reference's std::ios::app); "
+              f"--truncate starts a new file", file=sys.stderr)
     torch.cuda.set_device(a.device)
     res = run_sequence(a.dataset_path, a.tum, n_rows=a.rows, solver=a.solver, max_iter=a.iters,
                        seed=a.seed, launch=a.launch, map_tum_path=a.map_tum,
                        truncate_results=a.truncate)
-    print(json.dumps({"launch": a.launch, "frames": len(res["stamps"]),
+    print(json.dumps({"launch": a.launch, "tum": a.tum, "tum_mode": "truncate" if a.truncate else "append",
+                      "frames": len(res["stamps"]),
                       "odom1_poses": int(res["odom1"].shape[0]),
                       "odom2_poses": int(res["odom2"].shape[0]),
                       "final_t": res["odom2"][-1, 0:3].tolist() if len(res["odom2"]) else None,

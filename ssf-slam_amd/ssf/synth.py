@@ -180,6 +180,85 @@ def scan(seq: int, frame: int, n_rows: int = 64, n_az: int = 1875, device="cpu",
     return dict(pos1=pos1f, flow=flow, s_fg_mask=m.to(torch.uint8))
 
 
+_SYNTH_LIB = None
+
+
+def _synth_lib():
+    """libssf_synth.so (csrc/synth.hip): the batched GPU form of scan(), for bench data."""
+    global _SYNTH_LIB
+    if _SYNTH_LIB is None:
+        import ctypes as C
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libssf_synth.so")
+        lib = C.CDLL(path)
+        lib.ssf_synth_scan_batch.restype = C.c_int
+        lib.ssf_synth_scan_batch.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                             C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                             C.c_void_p, C.c_void_p, C.c_void_p]
+        _SYNTH_LIB = lib
+    return _SYNTH_LIB
+
+
+def ego_poses(seq: int, n_frames: int, speed: float = 1.0, yaw_rate: float = 0.004):
+    """ego_pose(seq, k) for k < n_frames at once -> (R [n,3,3], p [n,3]) numpy float64."""
+    import numpy as np
+    yaw0 = 0.002 * ((seq * 7919) % 11 - 5)
+    y = yaw0 + yaw_rate * np.arange(n_frames, dtype=np.float64)
+    step = speed * np.stack([np.cos(y), np.sin(y), np.zeros_like(y)], 1)
+    p = np.concatenate([np.zeros((1, 3)), np.cumsum(step, 0)[:-1]], 0)
+    c, s = np.cos(y), np.sin(y)
+    R = np.zeros((n_frames, 3, 3))
+    R[:, 0, 0], R[:, 0, 1], R[:, 1, 0], R[:, 1, 1], R[:, 2, 2] = c, -s, s, c, 1.0
+    return R, p
+
+
+class BatchScanner:
+    """scan() for S sequences at once on the GPU (libssf_synth.so): the same scenes, sensor and
+    ego motion as scan(), one ray per thread; the range noise and the jitter come from a
+    counter-based hash instead of torch's CPU generator.  Bench / test data only."""
+
+    def __init__(self, seqs, n_frames: int, n_rows: int = 64, n_az: int = 1875, device="cuda"):
+        import numpy as np
+        self.seqs, self.n_rows, self.n_az, self.device = list(seqs), n_rows, n_az, torch.device(device)
+        self.scenes = [Scene(s) for s in self.seqs]
+        self.poses = [ego_poses(s, n_frames + 1) for s in self.seqs]
+        sc = self.scenes[0]
+        self.n_box, self.n_pole, self.n_car = sc.boxes.shape[0], sc.poles.shape[0], sc.cars.shape[0]
+        self.rec = 25 + 6 * self.n_box + 4 * self.n_pole + 9 * self.n_car
+        self.elev = (elevations_deg(n_rows) * (math.pi / 180.0)).to(self.device)
+        self._np = np
+
+    def frame(self, k: int, pos: torch.Tensor, flow: torch.Tensor):
+        """frame k of every sequence into pos / flow [S * N, 3] f32 (device, contiguous)."""
+        import ctypes as C
+        np = self._np
+        S, N = len(self.seqs), self.n_rows * self.n_az
+        assert pos.shape == (S * N, 3) and flow.shape == (S * N, 3) and pos.is_contiguous() and flow.is_contiguous()
+        prm = np.zeros((S, self.rec))
+        seeds = np.zeros(S, dtype=np.uint64)
+        for j, (seq, sc) in enumerate(zip(self.seqs, self.scenes)):
+            R, p = self.poses[j]
+            az0 = 2 * math.pi * torch.rand(1, generator=_gen(SEED_BASE + seq * 10000 + k),
+                                           dtype=torch.float64).item() / self.n_az
+            car = sc.car_boxes(k).numpy()
+            carv = np.concatenate([sc.cars[:, 2:4].numpy(), np.zeros((self.n_car, 1))], 1)
+            prm[j] = np.concatenate([R[k].ravel(), p[k], R[k + 1].ravel(), p[k + 1], [az0],
+                                     sc.boxes.numpy().ravel(), sc.poles.numpy().ravel(), car.ravel(),
+                                     carv.ravel()])
+            seeds[j] = (SEED_BASE + seq * 10000 + k) * 0x9E3779B97F4A7C15 % (1 << 64)
+        d_prm = torch.from_numpy(prm).to(self.device)
+        d_seeds = torch.from_numpy(seeds.view(np.int64)).to(self.device)
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        rc = _synth_lib().ssf_synth_scan_batch(
+            C.c_void_p(st), S, self.n_rows, self.n_az, C.c_void_p(self.elev.data_ptr()),
+            C.c_void_p(d_prm.data_ptr()), self.rec, self.n_box, self.n_pole, self.n_car,
+            C.c_void_p(d_seeds.data_ptr()), C.c_void_p(pos.data_ptr()), C.c_void_p(flow.data_ptr()))
+        if rc != 0:
+            raise RuntimeError(f"ssf_synth_scan_batch failed: hipError {rc}")
+        d_prm.record_stream(torch.cuda.current_stream(self.device))
+        d_seeds.record_stream(torch.cuda.current_stream(self.device))
+
+
 def relative_pose(seq: int, frame_last: int, frame_curr: int):
     """Ground-truth T_last<-curr as (q_xyzw, t) float64 tuples (lidarOdometry q_last_curr)."""
     Rl, pl = ego_pose(seq, frame_last)

@@ -36,12 +36,27 @@ def _worker(rank, world, port, n_seq, q):
         mask_out[:, 0] = torch.tensor([100.0 + s for s in mine])
         rec = sd.pose_record(pose_abs, mask_out)
         allp = sd.gather_poses(rec)
+        # deferred exchange (bench.py, N > 1): K steps' records in one all-gather at the end
+        steps = []
+        for k in range(3):
+            pk = pose_abs.clone()
+            pk[:, 5] = 10.0 * k + rank                              # t.y = step, rank
+            steps.append(sd.pose_record(pk, mask_out))
+        defer = sd.gather_pose_records(steps)
         # max-over-ranks timing reduction used by bench.py
         t = torch.tensor([float(rank + 1)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        q.put((rank, list(mine), allp.numpy().tolist(), float(t.item())))
+        q.put((rank, list(mine), allp.numpy().tolist(), float(t.item()), defer.numpy().tolist()))
     finally:
         dist.destroy_process_group()
+
+
+def sd_shard(n, w, r):
+    import sys
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(here, "ssf-slam_amd"))
+    import ssf.dist as sd
+    return sd.sequence_shard(n, w, r)
 
 
 def test_sequence_shard_covers_all():
@@ -66,8 +81,14 @@ def test_gloo_world2_pose_allgather():
         p.join(timeout=30)
         assert p.exitcode == 0
     res.sort()
-    for rank, mine, allp, tmax in res:
+    for rank, mine, allp, tmax, defer in res:
         assert tmax == 2.0
+        # [K, n_seq, 14]: step-major, ranks in order within a step
+        assert len(defer) == 3 and all(len(d) == n_seq for d in defer)
+        for k in range(3):
+            assert [row[4] for row in defer[k]] == [float(s) for s in range(n_seq)]
+            owners = [r for r in range(world) for _ in sd_shard(n_seq, world, r)]
+            assert [row[5] for row in defer[k]] == [10.0 * k + r for r in owners]
         assert len(allp) == n_seq
         assert [row[4] for row in allp] == [float(s) for s in range(n_seq)]
         assert [row[7] for row in allp] == [100.0 + s for s in range(n_seq)]

@@ -31,7 +31,7 @@ def _pair(b, a, c):
     return last, curr
 
 
-@pytest.mark.parametrize("rows,n_az", [(64, 1875), (16, 1800)])
+@pytest.mark.parametrize("rows,n_az", [(64, 1875), (16, 1800), (16, 4500)])
 def test_edge_features_bitexact(oracle, dev, rows, n_az):
     import ssf
     fe = ssf.Frontend(rows, device=dev.index)

@@ -110,6 +110,20 @@ def test_chunk_and_scan_boundaries(oracle, dev):
         _check_frame(oracle, fe, out, h_off, f, c, 64)
 
 
+@pytest.mark.parametrize("n_rows,n_az", [(16, 2047), (16, 2048), (16, 2049), (16, 4500), (64, 4097)])
+def test_rows_across_curvature_tiles(oracle, dev, n_rows, n_az):
+    """k_curv_select streams a row in 2048-point tiles with an 8-point halo and carries the greedy
+    state (jstart) from tile to tile: rows of one tile exactly, one point over, 2-3 tiles, and the
+    16-beam span (3) whose selections cross every tile edge; curvature bits and plane lists
+    bit-exact vs the oracle"""
+    import ssf
+    fe = ssf.Frontend(n_rows, device=dev.index)
+    c = frame(5, 1, n_rows=n_rows, n_az=n_az)[0]
+    out, h_off = _run(fe, [c[: len(c) // 2], c], dev)
+    _check_frame(oracle, fe, out, h_off, 0, c[: len(c) // 2], n_rows)
+    _check_frame(oracle, fe, out, h_off, 1, c, n_rows)
+
+
 @pytest.mark.parametrize("n_rows", [16, 64])
 def test_ring_ids_near_bin_edges(oracle, dev, n_rows):
     """Elevations on and within 1e-6..1e-2 deg of every bin edge (and the -8.83 switch), plus a

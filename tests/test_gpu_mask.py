@@ -116,6 +116,61 @@ def test_frame_split_full_size_vs_oracle(oracle, dev, G):
         assert np.abs(o[0:3] - ref["t"]).max() < 1e-5
 
 
+def test_frame_split_work_groups_take_several_tickets(oracle, dev):
+    """Split G = 8 with n_frames * 8 > the resident work-groups (mask_pose_slots): the grid is
+    capped at the slots, so work-groups take several (frame, part) tickets in order and reuse
+    their LDS state across frames.  Every frame must equal the same frame fitted alone (one
+    ticket per work-group: the per-part sums and their exchange order are the same), also with
+    two such launches on two streams at once."""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index)
+    fe.mask_split(8)
+    props = torch.cuda.get_device_properties(dev)
+    n_fr = props.multi_processor_count // 8 + 3          # 8 x n_fr > one work-group per CU
+    batches = []
+    for b in range(2):
+        fr = [frame(40 + 50 * b + k, k % 3, n_az=60) for k in range(n_fr)]
+        draws = np.array([[0.05 + 0.9 * ((k * 7 + b) % 11) / 11, 0.37, 0.81] for k in range(n_fr)])
+        batches.append((fr, draws))
+    # reference: every frame alone (8 work-groups, one ticket each)
+    ref = []
+    for fr, draws in batches:
+        rows = []
+        for k, f in enumerate(fr):
+            o, bg, _ = _run(fe, dev, [f[0]], [f[1]], draws=draws[k:k + 1])
+            rows.append((o[0][:26], bg))
+        ref.append(rows)
+    # one launch per batch, both batches on two streams at once
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    inputs = []
+    for fr, draws in batches:
+        pts = torch.from_numpy(np.concatenate([f[0] for f in fr])).to(dev)
+        fl = torch.from_numpy(np.concatenate([f[1] for f in fr])).to(dev)
+        off, h_off = ssf.frame_offsets([f[0].shape[0] for f in fr], dev)
+        inputs.append((pts, fl, off, h_off, draws))
+    torch.cuda.synchronize()
+    outs = []
+    for b, (pts, fl, off, h_off, draws) in enumerate(inputs):
+        with torch.cuda.stream(streams[b]):
+            o, bg = fe.mask_pose(pts, fl, off, h_off, draws=draws)
+        outs.append((o, bg, h_off))
+    torch.cuda.synchronize()
+    for b, (o, bg, h_off) in enumerate(outs):
+        o, bg = o.cpu().numpy(), bg.cpu().numpy()
+        for k in range(n_fr):
+            a, e = int(h_off[k]), int(h_off[k + 1])
+            ro, rbg = ref[b][k]
+            assert o[k, 16] == 0, (b, k, o[k, 16])
+            assert np.array_equal(o[k, :26], ro), (b, k)
+            assert np.array_equal(bg[a:e], rbg), (b, k)
+    # and the fits are the reference's (sanity on a few frames)
+    fr, draws = batches[0]
+    o = outs[0][0].cpu().numpy()
+    for k in (0, n_fr - 1):
+        r = oracle.mask_and_pose(fr[k][0], fr[k][1], draws[k])
+        assert int(o[k, 19]) == int(r["info"]["kmeans_iter"]) and int(o[k, 20]) == int(r["info"]["em_iter"])
+
+
 def test_concurrent_streams_one_context(dev):
     """ssf_mask_pose_batch from one context on two streams back to back (the bench overlaps
     consecutive batches this way): every launch stages its draws in its own slot, so each result

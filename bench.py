@@ -5,7 +5,7 @@ path (BASELINE.json north_star):
   * scene-flow dynamic-point mask: GaussianMixture(2) fit + Kabsch pose + quaternion
     (PointCloudOdometry_noSeg.py:97-125)                       -> k_mask_pose         [mask streams]
   * frameFeature: ring binning, curvature, planar selection (frameFeature.cpp:45-123)
-                                                               -> k_bin_* / k_curv_select / k_compact
+                                                               -> k_bin_* / k_curv / k_select
   * plane table of the new frame (it is the next step's last frame)    -> k_plane_table_sorted
                                                                                       [feature stream]
   * registration of the pair (previous frame, new frame): association + 10 Gauss-Newton
@@ -107,6 +107,10 @@ def parse(argv=None):
                          "prints the world it sees and exits (no GPU is touched)")
     ap.add_argument("--mask-split", type=int, default=0,
                     help="work-groups per frame of the GMM fit (0: automatic, ssf_set_mask_split)")
+    ap.add_argument("--consecutive", type=int, default=0,
+                    help="BASELINE configs[2] as written: K consecutive frame pairs of each sequence "
+                         "per step (mask of K frames in one launch, masked features, K chained "
+                         "registrations); --batch sequences side by side")
     ap.add_argument("--latency", action="store_true",
                     help="BASELINE configs[1] as written: one frame pair at a time (B = 1), ms per frame")
     ap.add_argument("--mask-streams", type=int, default=3,
@@ -431,9 +435,11 @@ def rooflines(times, acc, B, N):
         "k_bin_count": 13.0 * acc["points"],                        # xyz read, row id written
         "k_bin_scatter": 13.0 * acc["points"] + 12.0 * acc["kept"], # xyz + id read, packed xyz written
         # §8(d) counts 16 B per point of the rows in range (12 B xyz read + a 4-B curvature
-        # write); the product path writes no curvature, only the selected indices
-        "k_curv_select": 12.0 * acc["in_range"] + 4.0 * acc["plane"],
-        "k_compact": 20.0 * acc["plane"],                           # index + xyz read, xyzi written
+        # write); the product path writes no curvature, only one candidate bit per point
+        "k_curv": 12.0 * acc["in_range"] + acc["in_range"] / 8.0,
+        # candidate bits read, per plane point: its index written and read back (4 + 4 B), its
+        # xyz gathered (12 B) and the xyzi record written (16 B)
+        "k_select": acc["in_range"] / 8.0 + 36.0 * acc["plane"],
         "k_plane_table_sorted": 49.0 * acc["plane"],
         "k_associate_lds": 64.0 * acc["plane_reg"],
         "k_associate_lds_soa": 64.0 * acc["plane_reg"],
@@ -456,8 +462,8 @@ def rooflines(times, acc, B, N):
                               evaluations_per_pair=acc["corr_evals"] / max(1, acc["corr"]),
                               note="corr = valid correspondences counted on device (ncorr); "
                                    "evaluations = 1 + logged iterations (nlog)")
-    if "k_curv_select" in out:
-        out["k_curv_select"]["in_range_points_per_launch"] = acc["in_range"] / out["k_curv_select"]["launches"]
+    if "k_curv" in out:
+        out["k_curv"]["in_range_points_per_launch"] = acc["in_range"] / out["k_curv"]["launches"]
     return out, passes
 
 
@@ -470,7 +476,9 @@ def latency(args):
     features -> plane table -> registration of the pair (10 GN iterations) on another; the
     frame is done when both have finished (host wall time per frame, synchronised).  `serial`
     runs the same calls on ONE stream (mask, then the chain), as a single-threaded node chain
-    would.  Rank 0 prints one JSON line, value = median ms per frame (overlapped)."""
+    would.  The frame's plane table (needed only by the NEXT pair) is launched after its
+    registration, so the latency is frame in -> both poses out; frame_period adds the table.
+    Rank 0 prints one JSON line, value = median ms per frame (overlapped)."""
     import torch
     import ssf
     dev = torch.device("cuda", 0)
@@ -490,6 +498,8 @@ def latency(args):
     fe.reserve(1, N)
     s_mask, s_chain = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
 
+    self_period = []
+
     def run(ks, serial, profile=False):
         pose_rel, pose_abs = ssf.identity_poses(1, dev), ssf.identity_poses(1, dev)
         last = last_table = None
@@ -498,6 +508,7 @@ def latency(args):
             for c in (fe_mask, fe):
                 c.kernel_times()
                 c.profile(True)
+        period = []
         for k in ks:
             pos, flow = frames[k]
             sm, sc = (s_chain, s_chain) if serial else (s_mask, s_chain)
@@ -512,14 +523,18 @@ def latency(args):
                 e[2].record(sc)
                 pb = fe.extract_planes_batch(pos, off, h_off, max_points=N)
                 e[3].record(sc)
-                table = fe.plane_table(pb)
-                e[4].record(sc)
                 if last is not None:
                     fe.register(last, last_table, pb, pose_rel, pose_abs)
+                e[4].record(sc)
+                # the plane table of this frame is needed by the NEXT pair only: it runs after
+                # this frame's pose is out, off the frame's critical path
+                table = fe.plane_table(pb)
                 e[5].record(sc)
-            sm.synchronize()
+            e[1].synchronize()
+            e[4].synchronize()
+            wall.append((time.perf_counter() - t0) * 1e3)      # both poses of the frame are out
             sc.synchronize()
-            wall.append((time.perf_counter() - t0) * 1e3)
+            period.append((time.perf_counter() - t0) * 1e3)    # + the table for the next pair
             ev.append(e)
             last, last_table = pb, table
         kt = {}
@@ -531,14 +546,17 @@ def latency(args):
                 c.profile(False)
         stages = dict(mask=[a[0].elapsed_time(a[1]) for a in ev],
                       features=[a[2].elapsed_time(a[3]) for a in ev],
-                      plane_table=[a[3].elapsed_time(a[4]) for a in ev],
-                      registration=[a[4].elapsed_time(a[5]) for a in ev[1:]])
+                      registration=[a[3].elapsed_time(a[4]) for a in ev[1:]],
+                      plane_table=[a[4].elapsed_time(a[5]) for a in ev])
+        self_period.extend(period[1:])
         return wall[1:], stages, kt      # the first frame of a run has no pair to register
 
     # warm up both orders, then time K frames of one sequence each way
     run(range(0, W), False)
     run(range(0, W), True)
+    self_period.clear()
     wall_o, st_o, _ = run(range(W, W + K), False)
+    period_o = list(self_period)
     wall_s, st_s, _ = run(range(W + K + 1, W + 2 * K + 1), True)
     _, _, kt = run(range(W, W + min(K, 8)), True, profile=True)
     med = lambda v: float(np.median(v)) if len(v) else 0.0
@@ -563,12 +581,131 @@ def latency(args):
                                f"x{iters}; host wall per frame, synchronised",
                    "points_per_frame": N, "solver": args.solver, "iters": iters, "batch": 1},
         "latency_ms": {"overlapped": {"median": med(wall_o), "mean": float(np.mean(wall_o)),
-                                      "p90": float(np.percentile(wall_o, 90))},
+                                      "p90": float(np.percentile(wall_o, 90)),
+                                      "note": "frame in -> SSF pose (mask + Kabsch) and registration pose out; "
+                                              "the frame's plane table (needed by the next pair) runs after"},
+                       "frame_period_overlapped": {"median": med(period_o),
+                                                   "note": "latency + the plane table: one frame after "
+                                                           "another on one GPU, nothing pipelined across frames"},
                        "serial_one_stream": {"median": med(wall_s), "mean": float(np.mean(wall_s)),
                                              "p90": float(np.percentile(wall_s, 90))}},
         "stage_event_ms": {k: med(v) for k, v in st_o.items()},
         "stage_event_ms_serial": {k: med(v) for k, v in st_s.items()},
         "kernels": kernels, "cpu_baseline": cpu, "data_gen_s": round(t_data, 2),
+    }
+    print(json.dumps(line), flush=True)
+
+
+def consecutive(args):
+    """BASELINE configs[2] as written: the PointCloudOdometry_noSeg.py path with the scene-flow
+    mask applied before the features, on a batch of K consecutive frame pairs of ONE sequence
+    (--consecutive K; --batch B runs B such sequences side by side).  One step = the next K frames
+    of every sequence: one mask launch (GMM + Kabsch) for the B x K frames, masked features and the
+    plane table of those frames in one launch each, then the K chained registrations (the warm
+    start of pair k is the solution of pair k - 1, lidarOdometry_onlyPC.cpp:164-169,251-252), one
+    launch of B pairs each.  Masks of consecutive steps alternate over --mask-streams streams, and
+    the registrations of step j overlap the mask of step j + 1.  Prints one JSON line."""
+    import torch
+    import ssf
+    from ssf import synth
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    K, B = args.consecutive, args.batch
+    iters = args.iters or (10 if args.solver == "gn" else 8)
+    N = args.rows * args.n_az
+    W, S = max(1, args.warmup), args.steps
+    n_steps = W + S
+    t_data = time.perf_counter()
+    # frame 0 of every sequence (the prologue), then per step K frames, frame-major:
+    # buffer index kk * B + b holds frame j K + kk + 1 of sequence b
+    scanner = synth.BatchScanner(list(range(B)), K * n_steps + 1, n_rows=args.rows, n_az=args.n_az, device=dev)
+    pro = (torch.empty((B * N, 3), dtype=torch.float32, device=dev),
+           torch.empty((B * N, 3), dtype=torch.float32, device=dev))
+    scanner.frame(0, *pro)
+    steps = []
+    for j in range(n_steps):
+        pos = torch.empty((K * B * N, 3), dtype=torch.float32, device=dev)
+        flow = torch.empty_like(pos)
+        for kk in range(K):
+            scanner.frame(j * K + kk + 1, pos[kk * B * N:(kk + 1) * B * N], flow[kk * B * N:(kk + 1) * B * N])
+        steps.append((pos, flow))
+    torch.cuda.synchronize(dev)
+    t_data = time.perf_counter() - t_data
+    off1, h1 = ssf.frame_offsets([N] * B, dev)
+    offK, hK = ssf.frame_offsets([N] * (K * B), dev)
+    fe_mask = ssf.Frontend(args.rows, device=0)
+    fe_mask.reserve(K * B, N)
+    fe_mask.mask_split(args.mask_split)
+    fe_mask.seed(20240000)
+    fe_feat = ssf.Frontend(args.rows, device=0, solver=args.solver, max_iter=iters)
+    fe_feat.reserve(K * B, N)
+    fe_reg = ssf.Frontend(args.rows, device=0, solver=args.solver, max_iter=iters)
+    fe_reg.reserve(B, N)
+    s_masks = [torch.cuda.Stream(dev) for _ in range(max(1, args.mask_streams))]
+    s_feat = torch.cuda.Stream(dev, priority=args.feat_priority)
+    s_reg = torch.cuda.Stream(dev, priority=args.feat_priority)
+    rel, ab = ssf.identity_poses(B, dev), ssf.identity_poses(B, dev)
+
+    def view(pb, table, kk):
+        """the B frames of buffer slot kk as a PlaneBatch (+ the table arrays, shared)"""
+        return ssf.PlaneBatch(pb.xyzi, pb.count[kk * B:(kk + 1) * B], pb.off[kk * B:(kk + 1) * B + 1],
+                              pb.h_off[kk * B:(kk + 1) * B + 1], pb.max_points), table
+
+    # prologue: frame 0 -> the first last frames
+    with torch.cuda.stream(s_feat):
+        _, bg0 = fe_mask.mask_pose(pro[0], pro[1], off1, h1, mode="gmm", want_mask=True)
+        pb0 = fe_feat.extract_planes_batch(pro[0], off1, h1, max_points=N, keep=bg0)
+        last = (pb0, fe_feat.plane_table(pb0))
+    torch.cuda.synchronize(dev)
+
+    def step(j, ev=None):
+        nonlocal last
+        pos, flow = steps[j]
+        sm = s_masks[j % len(s_masks)]
+        with torch.cuda.stream(sm):
+            out, bg = fe_mask.mask_pose(pos, flow, offK, hK, mode="gmm", want_mask=True)
+            done = torch.cuda.Event()
+            done.record(sm)
+        s_feat.wait_event(done)
+        bg.record_stream(s_feat)
+        with torch.cuda.stream(s_feat):
+            pb = fe_feat.extract_planes_batch(pos, offK, hK, max_points=N, keep=bg)
+            table = fe_feat.plane_table(pb)
+            tdone = torch.cuda.Event()
+            tdone.record(s_feat)
+        s_reg.wait_event(tdone)
+        for t in (pb.xyzi, pb.count, *[x for x in table if isinstance(x, torch.Tensor)]):
+            t.record_stream(s_reg)
+        with torch.cuda.stream(s_reg):
+            for kk in range(K):
+                cur = view(pb, table, kk)
+                (lpb, ltab) = last
+                fe_reg.register(lpb, ltab, cur[0], rel, ab)
+                last = cur
+        return out
+
+    for j in range(W):
+        step(j)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for j in range(W, W + S):
+        step(j)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    frames = B * K * S
+    line = {
+        "metric": METRIC, "value": frames / elapsed, "unit": "frames/s", "n_gpus": 1, "steps": S,
+        "warmup": W, "ms_per_step": elapsed / S * 1e3, "higher_is_better": True, "scaling": "none",
+        "vs_baseline": None, "dtype": "f32 features / f64 mask+solve",
+        "data": f"synthetic (seeded ray-cast {args.rows}-beam scans, ssf/synth.py BatchScanner; {B} sequence(s))",
+        "config": {"workload": f"configs[2] as written: PointCloudOdometry_noSeg path, mask before features, "
+                               f"{K} consecutive frame pairs of each of {B} sequence(s) per step: one mask "
+                               f"launch of {K * B} frames, masked features + plane table of them, {K} chained "
+                               f"registrations ({args.solver} x{iters})",
+                   "consecutive_pairs": K, "sequences": B, "points_per_frame": N, "solver": args.solver,
+                   "iters": iters, "mask_before_features": True},
+        "data_gen_s": round(t_data, 2),
+        "final_t_norm": float(ab[:, 4:].norm(dim=1).mean()),
     }
     print(json.dumps(line), flush=True)
 
@@ -579,6 +716,10 @@ def main():
         if args.gpus != 1 or os.environ.get("WORLD_SIZE", "1") != "1":
             sys.exit("bench.py --latency is a one-GPU, one-frame-pair measurement")
         return latency(args)
+    if args.consecutive:
+        if args.gpus != 1 or os.environ.get("WORLD_SIZE", "1") != "1":
+            sys.exit("bench.py --consecutive is a one-GPU measurement (configs[2])")
+        return consecutive(args)
     ws = os.environ.get("WORLD_SIZE")
     if ws is None and args.gpus > 1:
         sys.exit(launch_ranks(args))
@@ -684,7 +825,8 @@ def main():
 
     total_frames = B * args.steps * world
     value = total_frames / elapsed
-    cfg_name = ("configs[2] noSeg mask-before-features" if args.mask_before_features else
+    cfg_name = ("configs[2] shape, noSeg mask-before-features, B sequences x 1 frame per step "
+                "(--consecutive K runs K consecutive pairs of one sequence)" if args.mask_before_features else
                 "configs[4] 256k-pt stress" if args.n_az >= 4000 else
                 "configs[1] shape (one 120k-pt frame pair per sequence per step)")
     line = {
@@ -741,7 +883,7 @@ def main():
             line["roofline_f64"] = {"bound": "valu_f64", "achieved": tf, "peak": F64_PEAK_TFLOPS,
                                     "unit": "TFLOP/s", "frac": tf / F64_PEAK_TFLOPS,
                                     "kernel": "k_mask_pose", "flops_source": os.path.basename(F64_JSON)}
-    ns = {k: kernels[k]["frac"] for k in ("k_curv_select", "k_solve") if k in kernels and "frac" in kernels[k]}
+    ns = {k: kernels[k]["frac"] for k in ("k_curv", "k_solve") if k in kernels and "frac" in kernels[k]}
     if ns:
         line["north_star_kernels_hbm_frac"] = ns
         meas = {k: kernels[k]["traffic_frac"] for k in ns if "traffic_frac" in kernels[k]}

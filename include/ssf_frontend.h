@@ -310,7 +310,7 @@ int32_t ssf_mask_pose_batch_f64(ssf_ctx* ctx, void* stream, int32_t n_frames, co
                                 double* d_out);
 /* Work-groups per frame of the GMM fit in ssf_mask_pose_batch (no reference counterpart;
  * results do not depend on it beyond f64 summation order): 0 = automatic (as many as keep the
- * chip full: ~256 / frames, at most 8; 1 for 256 frames and more), 1..8 = fixed.  With more
+ * chip full: ~256 / frames, at most 32; 1 for 256 frames and more), 1..32 = fixed.  With more
  * than one, a frame's points are cut into contiguous parts whose per-pass sums are exchanged
  * in global memory; a partner that never arrives gives status SSF_POSE_SYNC_FAILED. */
 int32_t ssf_set_mask_split(ssf_ctx* ctx, int32_t parts_per_frame);

@@ -48,7 +48,7 @@ struct ssf_ctx {
     ssf_config cfg{};
     std::string err;
     // frameFeature scratch
-    DevBuf rid, hist, ring_off, ring_xyzi, sel, sel_cnt, plane1, off1, cnt1;
+    DevBuf rid, hist, ring_off, ring_xyzi, sel, sel_cnt /* candidate bits */, plane1, off1, cnt1;
     // registration scratch
     DevBuf corr;
     // ssf_register_pair: offsets, counts, the last frame's plane table + search index, pose, log
@@ -67,7 +67,7 @@ struct ssf_ctx {
     static constexpr int kDrawSlots = 4;
     // edge features (beyond the reference): selection scratch, correspondence records
     ssf_edge_config ecfg{};
-    DevBuf esel, esel_cnt, ecorr;
+    DevBuf esel, esel_cnt /* edge candidate bits */, ecorr;
     int mask_split = 0;                // ssf_set_mask_split: 0 = automatic
     int mask_slots = -1;               // resident k_mask_pose work-groups (queried once)
     DrawSlot dslot[kDrawSlots];
@@ -278,7 +278,7 @@ int32_t ssf_profile_read(ssf_ctx* c, ssf_kernel_time* out, int32_t cap, int32_t*
 const char* ssf_last_error(const ssf_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int32_t ssf_set_mask_split(ssf_ctx* c, int32_t parts_per_frame) {
-    if (!c || parts_per_frame < 0 || parts_per_frame > 8) return SSF_E_ARG;
+    if (!c || parts_per_frame < 0 || parts_per_frame > ssf::kMaskMaxSplit) return SSF_E_ARG;
     c->mask_split = parts_per_frame;
     return SSF_OK;
 }
@@ -312,9 +312,9 @@ static int32_t ensure_features(ssf_ctx* c, int32_t n_frames, int64_t total, int6
     SSF_TRY_HIP(c, c->hist.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(n_frames * n_chunks * R, 1)), "alloc hist");
     SSF_TRY_HIP(c, c->ring_off.ensure(sizeof(int32_t) * (size_t)n_frames * (R + 1)), "alloc ring_off");
     SSF_TRY_HIP(c, c->ring_xyzi.ensure(3 * sizeof(float) * (size_t)std::max<int64_t>(total, 1)), "alloc ring_xyz");
-    // per-row staging slots of the selected points (float4 at ring positions, k_curv_select)
-    SSF_TRY_HIP(c, c->sel.ensure(sizeof(float4) * (size_t)std::max<int64_t>(total, 1)), "alloc sel");
-    SSF_TRY_HIP(c, c->sel_cnt.ensure(sizeof(int32_t) * (size_t)n_frames * R), "alloc sel_cnt");
+    // per-row selection slots (indexInRow at ring positions, k_select) + the candidate bits
+    SSF_TRY_HIP(c, c->sel.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(total, 1)), "alloc sel");
+    SSF_TRY_HIP(c, c->sel_cnt.ensure(sizeof(uint64_t) * ssf::cand_words(total, n_frames)), "alloc cand bits");
     return SSF_OK;
 }
 
@@ -331,7 +331,7 @@ int32_t ssf_reserve(ssf_ctx* c, int32_t max_frames, int64_t max_points_per_frame
         SSF_TRY_HIP(c, ds.sync.ensure(ssf::mask_sync_bytes(std::max(max_frames, 1)) + 16), "alloc mask sync");
         // exchange slots of the automatic split for max_frames (a fixed split grows them on demand)
         if (c->mask_slots < 0) c->mask_slots = ssf::mask_pose_slots(c->device);
-        const int g_auto = std::max(1, std::min(8, c->mask_slots > 0 ? c->mask_slots / std::max(max_frames, 1) : 1));
+        const int g_auto = std::max(1, std::min(ssf::kMaskMaxSplit, c->mask_slots > 0 ? c->mask_slots / std::max(max_frames, 1) : 1));
         const size_t pb = ssf::mask_parts_bytes(std::max(max_frames, 1), g_auto);
         if (pb) SSF_TRY_HIP(c, ds.parts.ensure(pb), "alloc mask parts");
     }
@@ -356,10 +356,10 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
     ssf::EdgeSel es{};
     const bool edges = d_edge_xyzi != nullptr;
     if (edges) {
-        SSF_TRY_HIP(c, c->esel.ensure(sizeof(float4) * (size_t)std::max<int64_t>(total_points, 1)), "alloc esel");
-        SSF_TRY_HIP(c, c->esel_cnt.ensure(sizeof(int32_t) * (size_t)n_frames * c->cfg.n_rows), "alloc esel_cnt");
-        es = ssf::EdgeSel{c->ecfg.edge_min, c->ecfg.edge_span, c->esel.as<float4>(),
-                          c->esel_cnt.as<int32_t>(), reinterpret_cast<float4*>(d_edge_xyzi), d_edge_count};
+        SSF_TRY_HIP(c, c->esel.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(total_points, 1)), "alloc esel");
+        SSF_TRY_HIP(c, c->esel_cnt.ensure(sizeof(uint64_t) * ssf::cand_words(total_points, n_frames)), "alloc edge bits");
+        es = ssf::EdgeSel{c->ecfg.edge_min, c->ecfg.edge_span, c->esel_cnt.as<uint64_t>(),
+                          c->esel.as<int32_t>(), reinterpret_cast<float4*>(d_edge_xyzi), d_edge_count};
     }
     ProfScope prof(c, stream);
     float4* ring4 = reinterpret_cast<float4*>(d_ring_xyzi);   // debug output only (nullable)
@@ -367,7 +367,7 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
     hipError_t e = ssf::launch_extract_planes(
         (hipStream_t)stream, c->cfg, n_frames, d_pts, point_stride, d_frame_off, max_frame_points,
         d_keep, c->rid.as<int8_t>(), c->hist.as<int32_t>(), roff, c->ring_xyzi.as<float>(), ring4,
-        d_curv, c->sel.as<float4>(), c->sel_cnt.as<int32_t>(),
+        d_curv, c->sel_cnt.as<uint64_t>(), c->sel.as<int32_t>(),
         reinterpret_cast<float4*>(d_plane_xyzi), d_plane_count, edges ? &es : nullptr);
     if (e != hipSuccess) return hip_fail(c, e, "extract_planes launch");
     return SSF_OK;
@@ -662,7 +662,7 @@ static int32_t mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const
     if (c->mask_slots < 0) c->mask_slots = ssf::mask_pose_slots(c->device);
     int G = c->mask_split;
     if (G <= 0) G = c->mask_slots > 0 ? c->mask_slots / n_frames : 1;
-    G = std::max(1, std::min(G, 8));
+    G = std::max(1, std::min(G, ssf::kMaskMaxSplit));
     if (mode != SSF_MASK_GMM) G = 1;
     const size_t sync_need = G > 1 ? ssf::mask_sync_bytes(n_frames) + 16 : 0;
     const size_t parts_need = G > 1 ? ssf::mask_parts_bytes(n_frames, G) : 0;

@@ -9,12 +9,12 @@
 //                 order exactly.  The chunk is regrouped by row in LDS and stored in contiguous
 //                 per-row runs of packed xyz (12 B/pt: the ring order alone carries indexInRow,
 //                 so intensity = indexInRow + row/100.0 (:77) is recomputed where it is needed)
-//   k_curv_select one work-group per (frame,row): the row in one burst into an LDS tile, the
-//                 11-tap stencil (:84-107) evaluated left to right in float, 8 centres per
-//                 thread; the greedy spacing rule (:110-123) on one wave over candidate words;
-//                 the selected points (with their encoded intensity) stored into per-row slots
-//   k_compact     one work-group per frame: the per-row runs copied into the row-major plane
-//                 cloud (framePlanePtr order).
+//   k_curv        the 11-tap stencil (:84-107) as a stream over 2048-point chunks of the ring
+//                 cloud, evaluated left to right in float, 8 centres per thread; planar
+//                 candidates out as a per-frame bit array
+//   k_select      one work-group per frame: the greedy spacing rule (:110-123) with one row per
+//                 lane, then the selected points (and their encoded intensity) written in
+//                 framePlanePtr order (row major).
 #include "ssf_device.hpp"
 #include "ssf_internal.hpp"
 
@@ -249,113 +249,82 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
     }
 }
 
-// One WORK-GROUP per (frame, row).  The row is requested in one burst of 2048-point tiles
-// (each thread issues its 9 clamped 12-byte loads before the first use, as the binning kernels
-// do) into an LDS tile of x | y | z float arrays with an 8-point halo on both sides.  Every
-// thread then owns 8 consecutive centres: it reads the 24 points around them as six aligned
-// ds_read_b128 per coordinate and evaluates the 11-tap sums (:84-107) left to right in float,
-// exactly as the reference, one coordinate at a time (8 partial sums live, not 33 taps).  The
-// planar candidates (value < planeMin, the value staying 0 for j < 5 and j >= n - 5) leave as one
-// byte per thread; wave 0 then runs the greedy spacing rule (:110-123) over the tile's 64-bit
-// words in scalar code, collecting up to 64 selections in one VGPR (lane k holds the k-th) and emitting
-// them -- x, y, z from the LDS tile, intensity = indexInRow + row / 100.0 (:77) -- as float4
-// stores into the row's own staging slots (ring position + rank).  k_compact then only copies
-// contiguous per-row runs into the frame-major plane cloud.  Rows longer than a tile carry the
-// greedy state (jstart) from tile to tile.
-// kEdge (beyond the reference, off by default): wave 1 runs the edge rule -- greedy in index
-// order, curvature > edge_min, spacing edge_span, centres in [5, n - 5) (oracle/edge_oracle.c) --
-// on a second byte array, into its own staging slots.
-constexpr int kCurvTile = 2048;                 // centres per tile (one tile per 64-beam 120k row)
+// k_curv: the 11-tap curvature (:84-107) as a pure stream over the frame's ring-ordered cloud,
+// one work-group per 2048-point chunk of the rows in range (rows are contiguous there, row after
+// row).  Each thread issues its 9 clamped 12-byte loads (the chunk and an 8-point halo on both
+// sides) before the first use, the chunk lands in an LDS tile of x | y | z float arrays, and
+// every thread owns 8 consecutive centres: it reads the 24 points around them as six aligned
+// ds_read_b128 per coordinate and evaluates the sums left to right in float, exactly as the
+// reference, one coordinate at a time.  A centre's row comes from the frame's row offsets (LDS);
+// its value stays 0 for j < 5 and j >= n - 5 (never computed, :85).  The planar candidates
+// (value < planeMin) leave as one byte per thread of a per-frame bit array (bit = ring position);
+// the greedy spacing rule runs in k_select.  kEdge (beyond the reference, off by default): the
+// edge candidates (curvature > edge_min, centres in [5, n - 5), oracle/edge_oracle.c) into a
+// second bit array.  kCurv (debug / parity output): the curvature of every point, 0 outside the
+// rows in range.
+#ifndef SSF_CURV_PROBE
+#define SSF_CURV_PROBE 0   // diagnostic variants only (tools/gpu): 2 = no stencil
+#endif
+constexpr int kCurvChunk = 2048;                // centres per work-group
 constexpr int kCurvHalo = 8;                    // >= 5, and a multiple of 8 (aligned windows)
-constexpr int kCurvSpan = kCurvTile + 2 * kCurvHalo;
-constexpr int kCurvLoads = (kCurvSpan + 255) / 256;
+constexpr int kCurvLoads = (kCurvChunk + 2 * kCurvHalo + 255) / 256;   // 9
 
-// The greedy rule over one tile's candidate words (wave-uniform, run by ONE wave): selections at
-// ring positions >= jstart, spaced by `span`; emitted 64 at a time from the LDS tile.
-SSF_DEV void greedy_emit(const uint64_t* words, int t0, int tn, int span, int& jstart, int& cnt,
-                         const float* sx, const float* sy, const float* sz, double rfrac,
-                         float4* __restrict__ out) {
-    const int lane = threadIdx.x & 63;
-    int nl = 0, selv = 0;
-    auto flush = [&]() {
-        if (lane < nl) {
-            const int p = selv - (t0 - kCurvHalo);
-            out[cnt + lane] = make_float4(sx[p], sy[p], sz[p], (float)((double)selv + rfrac));
-        }
-        cnt += nl;
-        nl = 0;
-    };
-    const int nw = (tn + 63) >> 6;
-    for (int wi = 0; wi < nw; ++wi) {
-        const uint64_t wv = words[wi];                      // LDS broadcast
-        uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wv >> 32)) << 32) |
-                     (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wv);
-        const int j0 = t0 + 64 * wi;
-        while (true) {
-            const int lo = jstart - j0;
-            if (lo >= 64) break;
-            if (lo > 0) m &= ~((1ull << lo) - 1ull);
-            if (!m) break;
-            const int jj = j0 + (int)__builtin_ctzll(m);
-            if (lane == nl) selv = jj;                 // lane nl keeps selection nl
-            jstart = jj + span;
-            if (++nl == 64) flush();
-        }
-    }
-    flush();
-}
+// 64-bit word where frame f's candidate bits start (frame-local bit i -> word + (i >> 6)):
+// 8-byte aligned per frame, and frames never share a word
+SSF_DEV int64_t cand_word0(const int64_t* frame_off, int f) { return (frame_off[f] >> 6) + f; }
 
 template <bool kCurv, bool kEdge>
-__global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__ frame_off,
-                                                     int n_rows, int row_start, int row_end,
-                                                     float plane_min, int plane_span,
-                                                     const int32_t* __restrict__ ring_off,
-                                                     const Xyz* __restrict__ rxyz,
-                                                     float* __restrict__ curv,
-                                                     float4* __restrict__ stage,
-                                                     int32_t* __restrict__ sel_cnt,
-                                                     float edge_min, int edge_span,
-                                                     float4* __restrict__ estage,
-                                                     int32_t* __restrict__ esel_cnt) {
-    __shared__ __attribute__((aligned(16))) float sx[kCurvSpan], sy[kCurvSpan], sz[kCurvSpan];
-    __shared__ __attribute__((aligned(16))) uint8_t pbits[kCurvTile / 8];
-    __shared__ __attribute__((aligned(16))) uint8_t ebits[kEdge ? kCurvTile / 8 : 16];
-    const int tid = threadIdx.x, w = tid >> 6;
-    const int r = blockIdx.x, f = blockIdx.y;
-    const int32_t* ro = ring_off + (int64_t)f * (n_rows + 1);
-    const int rs = ro[r], n_r = ro[r + 1] - rs;
-    const int64_t base = frame_off[f] + rs;
-    const bool in_rows = (r >= row_start) && (r < n_rows - row_end);
-    if (!in_rows || n_r == 0) {                                  // uniform
-        if (kCurv)
-            for (int j = tid; j < n_r; j += 256) curv[base + j] = 0.0f;
-        if (tid == 0) sel_cnt[(int64_t)f * n_rows + r] = 0;
-        if (kEdge && tid == 0) esel_cnt[(int64_t)f * n_rows + r] = 0;
-        return;
-    }
-    const double rfrac = (double)r / 100.0;                    // :77
-    const Xyz* src = rxyz + base;
-    int cnt = 0, jstart = 0;                                   // wave 0's greedy state
-    int ecnt = 0, ejstart = 0;                                 // wave 1's (kEdge)
-    for (int t0 = 0; t0 < n_r; t0 += kCurvTile) {              // uniform
-        const int tn = min(kCurvTile, n_r - t0);
-        {   // positions [t0 - halo, t0 + tile + halo), clamped into the row: all loads first
-            Xyz q[kCurvLoads];
+__global__ __launch_bounds__(256) void k_curv(const int64_t* __restrict__ frame_off, int n_rows,
+                                              int row_start, int row_end, float plane_min,
+                                              const int32_t* __restrict__ ring_off,
+                                              const Xyz* __restrict__ rxyz,
+                                              float* __restrict__ curv,
+                                              uint8_t* __restrict__ pbits, float edge_min,
+                                              uint8_t* __restrict__ ebits) {
+    __shared__ __attribute__((aligned(16))) float sx[256 * kCurvLoads], sy[256 * kCurvLoads], sz[256 * kCurvLoads];
+    __shared__ int ro[kMaxRows + 1];
+    const int tid = threadIdx.x, c = blockIdx.x, f = blockIdx.y;
+    // the chunk's bounds from uniform (scalar) loads, so the point loads issue after ONE memory
+    // latency; the row table for the centres follows into LDS while they are in flight
+    const int64_t fb = frame_off[f];
+    const int32_t* rof = ring_off + (int64_t)f * (n_rows + 1);
+    const int nr_tot = rof[n_rows];
+    // the rows in range (every point for the debug curvature, which is 0 outside them); chunks
+    // start at a multiple of 8 points, so every thread's 8 centres are one byte of the bit array
+    const int lo = kCurv ? 0 : (rof[row_start] & ~7), hi = kCurv ? nr_tot : rof[n_rows - row_end];
+    const int c0 = lo + c * kCurvChunk;                        // uniform
+    if (c0 >= hi) return;
+    const Xyz* src = rxyz + fb;
+    {   // positions [c0 - halo, c0 + chunk + halo), clamped into the frame: all loads first
+        Xyz q[kCurvLoads];
 #pragma unroll
-            for (int k = 0; k < kCurvLoads; ++k) {
-                const int pos = t0 - kCurvHalo + tid + 256 * k;
-                q[k] = src[min(max(pos, 0), n_r - 1)];
-            }
-#pragma unroll
-            for (int k = 0; k < kCurvLoads; ++k) {
-                const int p = tid + 256 * k;
-                if (p < kCurvSpan) { sx[p] = q[k].x; sy[p] = q[k].y; sz[p] = q[k].z; }
-            }
+        for (int k = 0; k < kCurvLoads; ++k) {
+            const int pos = c0 - kCurvHalo + tid + 256 * k;
+            q[k] = src[min(max(pos, 0), nr_tot - 1)];
         }
-        __syncthreads();
-        // centres j = t0 + 8 tid + i; their taps are tile entries 8 tid + 3 + i .. 8 tid + 13 + i
+        if (tid <= n_rows) ro[tid] = rof[tid];
+        // every store unconditional (the tail lands in the pad): a store under a branch made the
+        // compiler wait for the last load right after issuing it
+#pragma unroll
+        for (int k = 0; k < kCurvLoads; ++k) {
+            const int p = tid + 256 * k;
+            sx[p] = q[k].x; sy[p] = q[k].y; sz[p] = q[k].z;
+        }
+    }
+    __syncthreads();
+    const int i0 = c0 + 8 * tid;                               // this thread's 8 centres
+    if (i0 >= hi) return;
+    // its first centre's row: the last r with ro[r] <= i0
+    int r = 0;
+#pragma unroll
+    for (int st = 32; st > 0; st >>= 1)
+        if (r + st <= n_rows && ro[r + st] <= i0) r += st;
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.0f;
+    if (SSF_CURV_PROBE != 2) {
+        // centres i0 + i; their taps are tile entries 8 tid + 3 + i .. 8 tid + 13 + i
         float d0[8], d1[8];
-        float v[8];
         auto coord = [&](const float* a, float (&d)[8]) {
             float h[24];
 #pragma unroll
@@ -372,78 +341,151 @@ __global__ __launch_bounds__(256) void k_curv_select(const int64_t* __restrict__
                 d[i] = acc;
             }
         };
-        if (8 * tid < tn) {
-            coord(sx, d0);
-            coord(sy, d1);
+        coord(sx, d0);
+        coord(sy, d1);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = d0[i] * d0[i] + d1[i] * d1[i];
-            coord(sz, d0);
+        for (int i = 0; i < 8; ++i) v[i] = d0[i] * d0[i] + d1[i] * d1[i];
+        coord(sz, d0);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = v[i] + d0[i] * d0[i];
-        }
-        uint32_t pb = 0, eb = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int jl = 8 * tid + i, j = t0 + jl;
-            if (jl < tn) {
-                const bool inner = j >= 5 && j < n_r - 5;
-                const float val = inner ? v[i] : 0.0f;
-                if (kCurv) curv[base + j] = val;
-                pb |= (uint32_t)(val < plane_min) << i;
-                if (kEdge) eb |= (uint32_t)(inner && val > edge_min) << i;
-            }
-        }
-        if (8 * tid < kCurvTile) pbits[tid] = (uint8_t)pb;
-        if (kEdge && 8 * tid < kCurvTile) ebits[tid] = (uint8_t)eb;
-        __syncthreads();
-        if (w == 0)
-            greedy_emit(reinterpret_cast<const uint64_t*>(pbits), t0, tn, plane_span, jstart, cnt,
-                        sx, sy, sz, rfrac, stage + base);
-        else if (kEdge && w == 1)
-            greedy_emit(reinterpret_cast<const uint64_t*>(ebits), t0, tn, edge_span, ejstart, ecnt,
-                        sx, sy, sz, rfrac, estage + base);
-        __syncthreads();                                       // the tile is read; next tile
+        for (int i = 0; i < 8; ++i) v[i] = v[i] + d0[i] * d0[i];
     }
-    if (tid == 0) sel_cnt[(int64_t)f * n_rows + r] = cnt;
-    if (kEdge && tid == 64) esel_cnt[(int64_t)f * n_rows + r] = ecnt;
+    uint32_t pb = 0, eb = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int ii = i0 + i;
+        while (r < n_rows - 1 && ii >= ro[r + 1]) ++r;         // rows of >= 1 point ahead
+        const int j = ii - ro[r], n_r = ro[r + 1] - ro[r];
+        const bool row_in = r >= row_start && r < n_rows - row_end;
+        const bool inner = j >= 5 && j < n_r - 5;
+        const float val = inner ? v[i] : 0.0f;
+        if (ii < hi) {
+            if (kCurv) curv[fb + ii] = row_in ? val : 0.0f;
+            pb |= (uint32_t)(row_in && val < plane_min) << i;
+            if (kEdge) eb |= (uint32_t)(row_in && inner && val > edge_min) << i;
+        }
+    }
+    const int64_t byte0 = cand_word0(frame_off, f) * 8 + (i0 >> 3);
+    pbits[byte0] = (uint8_t)pb;
+    if (kEdge) ebits[byte0] = (uint8_t)eb;
 }
 
-// One work-group per frame: the row counts' prefix in LDS, then every output slot of the frame's
-// plane cloud (row-major, framePlanePtr order) copies its float4 from its row's staging run.
-__global__ __launch_bounds__(1024) void k_compact(const int64_t* __restrict__ frame_off, int n_rows,
-                                                  const int32_t* __restrict__ ring_off,
-                                                  const float4* __restrict__ stage,
-                                                  const int32_t* __restrict__ sel_cnt,
-                                                  float4* __restrict__ plane,
-                                                  int32_t* __restrict__ plane_count) {
-    __shared__ int pre[kMaxRows + 1];
-    __shared__ int rbeg[kMaxRows];
-    const int f = blockIdx.x, tid = threadIdx.x;
-    if (tid < 64) {
-        const int c = tid < n_rows ? sel_cnt[(int64_t)f * n_rows + tid] : 0;
-        int incl = c;
+// k_select: one work-group per frame.  The greedy spacing rule (:110-123) for every row at once,
+// ONE ROW PER LANE of wave 0 (wave 1: the edge rule, kEdge): each lane walks its row's candidate
+// bits from the frame's bit array staged in LDS -- next candidate at or after jstart by a
+// count-trailing-zeros of the word, jstart = selection + planeSpan -- so 64 rows advance in one
+// VALU instruction stream (a scalar walk per row was ~180 cycles per step).  The selections
+// (indexInRow) go to per-row slots in global scratch; after one barrier the row counts are
+// prefixed and every thread of the work-group emits output slots in framePlanePtr order (row
+// major): x, y, z gathered from the ring-ordered cloud, intensity = indexInRow + row / 100.0 (:77).
+constexpr int kSelThreads = 1024;
+constexpr int kSelWordsLds = 6144;              // candidate words staged per array (48 KiB: 393k points)
+
+template <bool kEdge>
+__global__ __launch_bounds__(kSelThreads) void k_select(const int64_t* __restrict__ frame_off, int n_rows,
+                                                        int row_start, int row_end, int plane_span,
+                                                        const int32_t* __restrict__ ring_off,
+                                                        const Xyz* __restrict__ rxyz,
+                                                        const uint64_t* __restrict__ pbits,
+                                                        int32_t* __restrict__ sel,
+                                                        float4* __restrict__ plane,
+                                                        int32_t* __restrict__ plane_count,
+                                                        int edge_span, const uint64_t* __restrict__ ebits,
+                                                        int32_t* __restrict__ esel,
+                                                        float4* __restrict__ edge,
+                                                        int32_t* __restrict__ edge_count) {
+    __shared__ uint64_t wl[kEdge ? 2 : 1][kSelWordsLds];
+    __shared__ int ro[kMaxRows + 1];
+    __shared__ int pre[2][kMaxRows + 1];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int f = blockIdx.x;
+    const int64_t fb = frame_off[f];
+    const int nf = (int)(frame_off[f + 1] - fb);
+    const int nw = (nf + 63) >> 6;
+    const int64_t wb = cand_word0(frame_off, f);
+    if (tid <= n_rows) ro[tid] = ring_off[(int64_t)f * (n_rows + 1) + tid];
+    for (int k = tid; k < min(nw, kSelWordsLds); k += kSelThreads) {
+        wl[0][k] = pbits[wb + k];
+        if (kEdge) wl[kEdge ? 1 : 0][k] = ebits[wb + k];
+    }
+    __syncthreads();
+    if (w < (kEdge ? 2 : 1)) {                                 // uniform: wave 0 planes, wave 1 edges
+        const int r = lane;
+        const bool e = kEdge && w == 1;
+        const uint64_t* W = wl[e ? 1 : 0];
+        const uint64_t* G = (e ? ebits : pbits) + wb;
+        const int span = e ? edge_span : plane_span;
+        int32_t* out = e ? esel : sel;
+        int cnt = 0;
+        if (r < n_rows && r >= row_start && r < n_rows - row_end) {
+            const int rs = ro[r], n_r = ro[r + 1] - rs;
+            if (n_r > 0) {
+                auto word = [&](int k) { return k < kSelWordsLds ? W[k] : G[k]; };
+                int js = 0;                                     // jstart, row-relative
+                const int kend = (rs + n_r - 1) >> 6;
+                uint64_t nxt = word(rs >> 6);
+                for (int k = rs >> 6; k <= kend; ++k) {         // the row's words in order
+                    uint64_t wv = nxt;
+                    nxt = word(min(k + 1, kend));               // the next word in flight
+                    const int gb = k * 64;
+                    int low = rs + js - gb;                     // bits below jstart
+                    if (low >= 64) continue;
+                    if (low > 0) wv &= ~0ull << low;
+                    const int top = rs + n_r - gb;              // bits past the row's end
+                    if (top < 64) wv &= (1ull << top) - 1ull;
+                    while (wv) {
+                        const int j = gb + (int)__builtin_ctzll(wv) - rs;
+                        out[fb + rs + cnt] = j;
+                        ++cnt;
+                        js = j + span;
+                        low = rs + js - gb;
+                        wv = low >= 64 ? 0ull : (wv & (~0ull << low));
+                    }
+                }
+            }
+        }
+        int incl = cnt;                                         // prefix over the rows
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int y = __shfl_up(incl, o, 64);
-            if (tid >= o) incl += y;
+            if (lane >= o) incl += y;
         }
-        if (tid < n_rows) {
-            pre[tid] = incl - c;
-            rbeg[tid] = ring_off[(int64_t)f * (n_rows + 1) + tid];
-        }
-        if (tid == 63) pre[n_rows] = incl;
+        if (lane < n_rows) pre[e ? 1 : 0][lane] = incl - cnt;
+        if (lane == 63) pre[e ? 1 : 0][n_rows] = incl;
     }
     __syncthreads();
-    const int total = pre[n_rows];
-    const int64_t fb = frame_off[f];
-    if (tid == 0) plane_count[f] = total;
-    for (int k = tid; k < total; k += blockDim.x) {
-        int lo = 0, hi = n_rows - 1;                           // the row r with pre[r] <= k < pre[r + 1]
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (pre[mid] <= k) lo = mid; else hi = mid - 1;
+#pragma unroll
+    for (int e = 0; e < (kEdge ? 2 : 1); ++e) {
+        const int* P = pre[e];
+        const int total = P[n_rows];
+        if (tid == 0) (e ? edge_count : plane_count)[f] = total;
+        const int32_t* S = e ? esel : sel;
+        float4* O = e ? edge : plane;
+        // four output slots per thread per trip, each stage's loads issued together (the
+        // selection index, then the gathered point): three memory latencies per trip
+        constexpr int U = 4;
+        for (int k0 = 0; k0 < total; k0 += U * kSelThreads) {   // uniform
+            int kk[U], rr[U], jj[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                kk[u] = min(k0 + u * kSelThreads + tid, total - 1);
+                int a = 0;                                      // the row r with P[r] <= k < P[r + 1]
+#pragma unroll
+                for (int st = 32; st > 0; st >>= 1)
+                    if (a + st < n_rows && P[a + st] <= kk[u]) a += st;
+                rr[u] = a;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) jj[u] = S[fb + ro[rr[u]] + (kk[u] - P[rr[u]])];
+            Xyz q[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) q[u] = rxyz[fb + ro[rr[u]] + jj[u]];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (k0 + u * kSelThreads + tid < total)
+                    O[fb + kk[u]] = make_float4(q[u].x, q[u].y, q[u].z,
+                                                (float)((double)jj[u] + (double)rr[u] / 100.0));
         }
-        plane[fb + k] = stage[fb + rbeg[lo] + (k - pre[lo])];
     }
 }
 
@@ -451,7 +493,7 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
                                  const float* pts, int stride, const int64_t* frame_off,
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
                                  int32_t* ring_off, float* ring_xyz, float4* ring_xyzi, float* curv,
-                                 float4* stage, int32_t* sel_cnt, float4* plane,
+                                 uint64_t* bits, int32_t* sel, float4* plane,
                                  int32_t* plane_count, const EdgeSel* edge) {
     const int R = cfg.n_rows;
     const int n_chunks = (int)((max_pts + kBinChunk - 1) / kBinChunk);
@@ -470,28 +512,29 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
                            frame_off, R, n_chunks, rid, hist, ring_off,
                            reinterpret_cast<Xyz*>(ring_xyz), ring_xyzi);
     }
-    const dim3 cgrid(R, n_frames);
-    kmark(s, "k_curv_select");
+    // k_curv: chunks of the rows in range (every point with the debug curvature)
+    const int cchunks = (int)((max_pts + kCurvChunk - 1) / kCurvChunk);
+    const dim3 cgrid(max(cchunks, 1), n_frames);
+    kmark(s, "k_curv");
     const Xyz* rx = reinterpret_cast<const Xyz*>(ring_xyz);
     const float emin = edge ? edge->min_curv : 0.f;
-    const int espan = edge ? edge->span : 1;
-    float4* estage = edge ? edge->stage : nullptr;
-    int32_t* ecnt = edge ? edge->sel_cnt : nullptr;
+    uint8_t* eb8 = edge ? reinterpret_cast<uint8_t*>(edge->bits) : nullptr;
 #define SSF_CURV_LAUNCH(C, E)                                                                      \
-    hipLaunchKernelGGL((k_curv_select<C, E>), cgrid, dim3(256), 0, s, frame_off, R, cfg.row_start,  \
-                       cfg.row_end, cfg.plane_min, cfg.plane_span, ring_off, rx, curv, stage, sel_cnt, \
-                       emin, espan, estage, ecnt)
+    hipLaunchKernelGGL((k_curv<C, E>), cgrid, dim3(256), 0, s, frame_off, R, cfg.row_start,         \
+                       cfg.row_end, cfg.plane_min, ring_off, rx, curv,                             \
+                       reinterpret_cast<uint8_t*>(bits), emin, eb8)
     if (edge) { if (curv) SSF_CURV_LAUNCH(true, true); else SSF_CURV_LAUNCH(false, true); }
     else { if (curv) SSF_CURV_LAUNCH(true, false); else SSF_CURV_LAUNCH(false, false); }
 #undef SSF_CURV_LAUNCH
-    kmark(s, "k_compact");
-    hipLaunchKernelGGL(k_compact, dim3(n_frames), dim3(1024), 0, s, frame_off, R, ring_off, stage,
-                       sel_cnt, plane, plane_count);
-    if (edge) {
-        kmark(s, "k_compact_edges");
-        hipLaunchKernelGGL(k_compact, dim3(n_frames), dim3(1024), 0, s, frame_off, R, ring_off,
-                           edge->stage, edge->sel_cnt, edge->out, edge->count);
-    }
+    kmark(s, "k_select");
+    if (edge)
+        hipLaunchKernelGGL(k_select<true>, dim3(n_frames), dim3(kSelThreads), 0, s, frame_off, R,
+                           cfg.row_start, cfg.row_end, cfg.plane_span, ring_off, rx, bits, sel, plane,
+                           plane_count, edge->span, edge->bits, edge->sel, edge->out, edge->count);
+    else
+        hipLaunchKernelGGL(k_select<false>, dim3(n_frames), dim3(kSelThreads), 0, s, frame_off, R,
+                           cfg.row_start, cfg.row_end, cfg.plane_span, ring_off, rx, bits, sel, plane,
+                           plane_count, 1, nullptr, nullptr, nullptr, nullptr);
     return hipGetLastError();
 }
 

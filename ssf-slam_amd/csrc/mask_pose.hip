@@ -502,7 +502,7 @@ __device__ __noinline__ int kabsch_finish(const double* k, const double cs[3], c
 // work-group that becomes free (no wait on a work-group that cannot be dispatched).  A bounded
 // spin turns a lost partner into status SSF_POSE_SYNC_FAILED, never a hang.
 constexpr int kSlot = 32;                         // doubles per part and exchange
-constexpr int kMaxSplit = 8;                      // parts per frame at most
+constexpr int kMaxSplit = kMaskMaxSplit;          // parts per frame at most (32)
 constexpr uint32_t kSpinLimit = 1u << 24;         // x s_sleep 2 (~128 cycles): ~1 s
 // exchanges per frame at most: pass 0, 3 in k-means++, one per Lloyd iteration (<= 300), the
 // GMM init, one per EM iteration (<= 100), the final pass
@@ -572,12 +572,19 @@ SSF_DEV bool exchange(Split& X, double (&v)[N], double* tmp, int* okflag) {
     // barrier (the sc1 loads themselves stand in for the acquire: Guideline 16, Valid forms row 1)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (!*okflag) return false;                    // uniform
+    // every (part, value) on its own thread: one load latency for the G x N values (a loop over
+    // the parts per value waited for G loads in a row); tmp holds kMaxSplit x kSlot doubles
+    for (int t = threadIdx.x; t < X.G * N; t += blockDim.x) {
+        const int gg = t / N, k = t - gg * N;
+        tmp[kSlot + t] = __longlong_as_double((long long)__hip_atomic_load(
+            reinterpret_cast<unsigned long long*>(slot + gg * kSlot + k), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT));
+    }
+    __syncthreads();
     if (threadIdx.x < (unsigned)N) {
         double acc = kMin ? __builtin_inf() : 0.0;
-        for (int gg = 0; gg < X.G; ++gg) {
-            const double x = __longlong_as_double((long long)__hip_atomic_load(
-                reinterpret_cast<unsigned long long*>(slot + gg * kSlot + threadIdx.x), __ATOMIC_RELAXED,
-                __HIP_MEMORY_SCOPE_AGENT));
+        for (int gg = 0; gg < X.G; ++gg) {                 // part order: the same bits everywhere
+            const double x = tmp[kSlot + gg * N + threadIdx.x];
             acc = kMin ? (x < acc ? x : acc) : acc + x;
         }
         tmp[threadIdx.x] = acc;
@@ -585,6 +592,55 @@ SSF_DEV bool exchange(Split& X, double (&v)[N], double* tmp, int* okflag) {
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < N; ++k) v[k] = tmp[k];
+    __syncthreads();
+    return true;
+}
+
+// One value per part; every part reads the G values in part order -> the sum over the parts
+// before this one and the total (the k-means++ cumulative potential).  Same protocol as exchange.
+SSF_DEV bool exchange_prefix(Split& X, double v, double* tmp, int* okflag, double& before, double& total) {
+    if (X.seq >= (uint32_t)kMaxExchanges) return false;
+    double* slot = X.part + (size_t)X.seq * (size_t)X.G * kSlot;
+    if (threadIdx.x == 0)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(slot + X.g * kSlot),
+                           (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    X.seq += 1u;
+    if (threadIdx.x < 64) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) {
+#if SSF_MASK_XCHG_FENCES
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+            __hip_atomic_fetch_add(X.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int ok = wait_arrivals(X, (uint32_t)X.G * X.seq) ? 1 : 0;
+#if SSF_MASK_XCHG_FENCES
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+            *okflag = ok;
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!*okflag) return false;                    // uniform
+    if (threadIdx.x < (unsigned)X.G)
+        tmp[kSlot + threadIdx.x] = __longlong_as_double((long long)__hip_atomic_load(
+            reinterpret_cast<unsigned long long*>(slot + threadIdx.x * kSlot), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double b = 0.0, t = 0.0;
+        for (int gg = 0; gg < X.G; ++gg) {
+            const double x = tmp[kSlot + gg];
+            if (gg < X.g) b += x;
+            t += x;
+        }
+        tmp[0] = b; tmp[1] = t;
+    }
+    __syncthreads();
+    before = tmp[0];
+    total = tmp[1];
     __syncthreads();
     return true;
 }
@@ -614,7 +670,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     __shared__ unsigned long long cand_lds[2];
     __shared__ double bsum[kKppBlocks];   // k-means++ per-64-point-block distance totals
     __shared__ uint32_t lq[kNW * kLQ];     // Lloyd skip passes: per-wave relabel entries of a trip
-    __shared__ double xtmp[kSlot];          // exchange totals
+    __shared__ double xtmp[kSlot + kMaxSplit * kSlot];   // exchange totals + the gathered parts
     __shared__ int tk, okflag;
     const int tid = threadIdx.x;
     // G == 1: work-group = frame.  G > 1: (frame, part) tickets in order (see Split).
@@ -814,14 +870,9 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         for (int k = 0; k < nw; ++k) { if (k == w) carry = pot; pot += red[k]; }
         if (G > 1) {
             // the in-order cumulative sum runs over the parts in order: part g starts after the
-            // potentials of parts 0..g-1 (part totals exchanged as a G-vector)
-            double tv[kMaxSplit];
-#pragma unroll
-            for (int k = 0; k < kMaxSplit; ++k) tv[k] = k == g ? pot : 0.0;
-            if (!exchange<kMaxSplit>(X, tv, xtmp, &okflag)) { sync_failed(); return; }
+            // potentials of parts 0..g-1 (one value per part; every part reads all G in order)
             double before = 0.0, total = 0.0;
-#pragma unroll
-            for (int k = 0; k < kMaxSplit; ++k) { if (k < g) before += tv[k]; total += tv[k]; }
+            if (!exchange_prefix(X, pot, xtmp, &okflag, before, total)) { sync_failed(); return; }
             carry += before;
             pot = total;
         }

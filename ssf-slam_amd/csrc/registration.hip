@@ -1642,13 +1642,14 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
 #ifdef SSF_ASSOC_COUNT
         int vis = 0;
 #endif
-        auto search = [&](int sidx) __attribute__((always_inline)) {
+        // walks stop at min(best, lim): lim = R^2 of the current search radius
+        auto search = [&](int sidx, float lim) __attribute__((always_inline)) {
             const int a = T.start[sidx], b = T.start[sidx + 1];
             if (a >= b) return;
             const float yl = T.ylo[sidx], yh = T.yhi[sidx];
             const float dyl = qs.y < yl ? yl - qs.y : (qs.y > yh ? qs.y - yh : 0.0f);
             const float dy2 = dyl * dyl;
-            if (dy2 > best) return;
+            if (dy2 > fminf(best, lim)) return;
             int l = a, h = b;                                            // first x >= qs.x
             while (l < h) {
                 const int mid = (l + h) >> 1;
@@ -1661,7 +1662,7 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
                     const float4 pl = pn;
                     pn = v.pt(min(c + 1, b - 1));
                     const float dx = qs.x - pl.x;
-                    if (dx * dx + dy2 > best) break;
+                    if (dx * dx + dy2 > fminf(best, lim)) break;
                     const float d = l2_simple(qs, pl);
                     if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
 #ifdef SSF_ASSOC_COUNT
@@ -1675,7 +1676,7 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
                     const float4 pl = pn;
                     pn = v.pt(max(c - 1, a));
                     const float dx = qs.x - pl.x;
-                    if (dx * dx + dy2 > best) break;
+                    if (dx * dx + dy2 > fminf(best, lim)) break;
                     const float d = l2_simple(qs, pl);
                     if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
 #ifdef SSF_ASSOC_COUNT
@@ -1684,23 +1685,35 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
                 }
             }
         };
+        // Radius doubling (R = 2, 4, 8, ... m, then unbounded): a level visits, strip ring by
+        // strip ring from the query's, every point with dx^2 + dymin^2 <= min(best, R^2).  Once
+        // best <= R^2 every point as close as best has been seen (its lower bound is <= its
+        // distance <= best <= R^2), so the 1-NN is exact; a query in an empty region (a masked
+        // hole, BASELINE configs[2]) therefore walks the points within ~2x its 1-NN distance,
+        // not every point within the distance of the first point its own strip happens to hold.
         const int s0 = strip_of(qs.y);
-        search(s0);
-        bool up = true, dn = true;
-        for (int rr = 1; up || dn; ++rr) {
-            if (up) {
-                const int su = s0 + rr;
-                // every point of strips >= su has y >= y0 + su W (less float slack)
-                const float gap = (y0 + (float)su * W) - qs.y - 1e-3f;
-                if (su >= ns || (gap > 0.0f && gap * gap > best)) up = false;
-                else search(su);
+        for (float R = 2.0f;; R *= 2.0f) {
+            const bool unbounded = R > 4096.0f;                          // uniform per lane
+            const float lim = unbounded ? __builtin_inff() : R * R;
+            search(s0, lim);
+            bool up = true, dn = true;
+            for (int rr = 1; up || dn; ++rr) {
+                const float bnd = fminf(best, lim);
+                if (up) {
+                    const int su = s0 + rr;
+                    // every point of strips >= su has y >= y0 + su W (less float slack)
+                    const float gap = (y0 + (float)su * W) - qs.y - 1e-3f;
+                    if (su >= ns || (gap > 0.0f && gap * gap > bnd)) up = false;
+                    else search(su, lim);
+                }
+                if (dn) {
+                    const int sd = s0 - rr;
+                    const float gap = qs.y - (y0 + (float)(sd + 1) * W) - 1e-3f;
+                    if (sd < 0 || (gap > 0.0f && gap * gap > bnd)) dn = false;
+                    else search(sd, lim);
+                }
             }
-            if (dn) {
-                const int sd = s0 - rr;
-                const float gap = qs.y - (y0 + (float)(sd + 1) * W) - 1e-3f;
-                if (sd < 0 || (gap > 0.0f && gap * gap > best)) dn = false;
-                else search(sd);
-            }
+            if (best <= lim || unbounded) break;
         }
         assoc_finish(L, lo, last_normal, last_valid, pc, v.id(max(bc, 0)), corr, nn_out, co + i);
 #ifdef SSF_ASSOC_COUNT

@@ -41,6 +41,9 @@ void kmark(hipStream_t s, const char* name);
 constexpr int kBinChunk = SSF_BIN_CHUNK;   // points per binning work-group (2048: 8 points per
                                            // thread; 4096 measured 11-12 % slower binning)
 constexpr int kMaxRows = 64;
+constexpr int kMaskMaxSplit = 32;          // work-groups per frame of the GMM fit at most
+// candidate bit arrays of a batch (k_curv / k_select): 64-bit words, per frame 8-byte aligned
+inline size_t cand_words(int64_t total, int n_frames) { return (size_t)((total >> 6) + n_frames + 2); }
 
 // Per-correspondence record written by the association kernel, read by the solver.
 struct alignas(16) CorrRec {
@@ -51,13 +54,13 @@ struct alignas(16) CorrRec {
 
 // ---- launchers (features.hip) ----
 // Edge selection of launch_extract_planes (beyond the reference; nullptr = planes only):
-// per-row staging slots (float4 per point) / per-row counts in ctx scratch, the compacted edge
+// the candidate bit array and the per-row selection slots in ctx scratch, the compacted edge
 // cloud (float4 x, y, z, intensity at the frame offsets) and per-frame counts out.
 struct EdgeSel {
     float min_curv;
     int span;
-    float4* stage;
-    int32_t* sel_cnt;
+    uint64_t* bits;
+    int32_t* sel;
     float4* out;
     int32_t* count;
 };
@@ -65,7 +68,7 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
                                  const float* pts, int stride, const int64_t* frame_off,
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
                                  int32_t* ring_off, float* ring_xyz, float4* ring_xyzi,
-                                 float* curv, float4* stage, int32_t* sel_cnt, float4* plane,
+                                 float* curv, uint64_t* bits, int32_t* sel, float4* plane,
                                  int32_t* plane_count, const EdgeSel* edge = nullptr);
 
 // ---- launchers (registration.hip) ----

@@ -110,7 +110,7 @@ class Frontend:
         return {buf[i].name.decode(): (int(buf[i].launches), float(buf[i].total_ms)) for i in range(n.value)}
 
     def mask_split(self, parts_per_frame: int = 0):
-        """Work-groups per frame of the GMM fit (0 = automatic, 1..8 fixed)."""
+        """Work-groups per frame of the GMM fit (0 = automatic, 1..32 fixed)."""
         self._check(_abi.lib().ssf_set_mask_split(self._h, int(parts_per_frame)), "ssf_set_mask_split")
 
     def edge_config(self, **kw):

@@ -9,7 +9,7 @@ repository and there is no network, so scans are ray-cast here:
 * azimuth-major emission order (all beams per azimuth step, like a spinning sensor);
 * world: ground plane z = -2.5, a street of box buildings, poles (vertical cylinders), a
   100 m "sky dome" for rays that hit nothing, and moving cars (dynamic points, ~8 %);
-* ego motion ~1 m/frame with a small yaw rate; range noise sigma 0.01 m plus 1e-4 m jitter so
+* ego motion ~1 m/frame with a bounded heading (ego_yaw); range noise sigma 0.01 m plus 1e-4 m jitter so
   k-NN distances are tie-free;
 * flow = pos1 expressed in frame k+1 coordinates minus pos1 (Generate_Sceneflow.py
   semantics); dynamic points include their object's motion.  s_fg_mask = 1 on movers.
@@ -67,7 +67,8 @@ class Scene:
         self.poles = torch.stack([px, py, 0.15 + 0.1 * u(n_poles), torch.full((n_poles,), 3.5)], 1)
         cars = []
         for c in range(n_cars):
-            lane = [-3.0, 3.0, -1.5, 1.5][c % 4]
+            # lanes clear of the ego path (|y| <~ 2 m, ego_yaw) and of the poles (|y| ~ 6.5)
+            lane = [-3.5, 3.5, -5.0, 5.0][c % 4]
             x0 = 5.0 + 25.0 * c + 10.0 * float(u(1))
             vx = (1.6 + 0.8 * float(u(1))) * (1.0 if lane > 0 else -1.0)
             cars.append([x0, lane, vx, 0.05 * (float(u(1)) - 0.5)])
@@ -84,14 +85,27 @@ class Scene:
         return torch.cat([lo, hi], 1)
 
 
-def ego_pose(seq: int, frame: int, speed: float = 1.0, yaw_rate: float = 0.004):
-    """Sensor pose in the world: (R [3,3], p [3]) float64.  Constant speed, slow yaw."""
+def ego_yaw(seq: int, frame: int, yaw_rate: float = 0.004) -> float:
+    """Heading of frame k: yaw0 + yaw_rate k for the first 15 frames, then a triangle wave of the
+    same slope between +/- c0 (c0 = the heading reached at frame 15), whose mean is zero, so the
+    lateral offset stays within ~2 m of the street axis however long the sequence (a constant
+    yaw rate drove long sequences into the buildings, |y| > 9 m, after ~70 frames)."""
     yaw0 = 0.002 * ((seq * 7919) % 11 - 5)
+    if frame <= 15:
+        return yaw0 + yaw_rate * frame
+    c0 = yaw0 + 15 * yaw_rate
+    half = 2.0 * c0 / yaw_rate                      # frames from +c0 down to -c0
+    u = math.fmod(frame - 15, 2.0 * half)
+    return c0 - yaw_rate * u if u <= half else -c0 + yaw_rate * (u - half)
+
+
+def ego_pose(seq: int, frame: int, speed: float = 1.0, yaw_rate: float = 0.004):
+    """Sensor pose in the world: (R [3,3], p [3]) float64.  Constant speed, bounded heading."""
     p = torch.zeros(3, dtype=torch.float64)
     for k in range(frame):
-        yk = yaw0 + yaw_rate * k
+        yk = ego_yaw(seq, k, yaw_rate)
         p = p + speed * torch.tensor([math.cos(yk), math.sin(yk), 0.0], dtype=torch.float64)
-    y = yaw0 + yaw_rate * frame
+    y = ego_yaw(seq, frame, yaw_rate)
     c, s = math.cos(y), math.sin(y)
     R = torch.tensor([[c, -s, 0.0], [s, c, 0.0], [0.0, 0.0, 1.0]], dtype=torch.float64)
     return R, p
@@ -202,8 +216,7 @@ def _synth_lib():
 def ego_poses(seq: int, n_frames: int, speed: float = 1.0, yaw_rate: float = 0.004):
     """ego_pose(seq, k) for k < n_frames at once -> (R [n,3,3], p [n,3]) numpy float64."""
     import numpy as np
-    yaw0 = 0.002 * ((seq * 7919) % 11 - 5)
-    y = yaw0 + yaw_rate * np.arange(n_frames, dtype=np.float64)
+    y = np.array([ego_yaw(seq, k, yaw_rate) for k in range(n_frames)], dtype=np.float64)
     step = speed * np.stack([np.cos(y), np.sin(y), np.zeros_like(y)], 1)
     p = np.concatenate([np.zeros((1, 3)), np.cumsum(step, 0)[:-1]], 0)
     c, s = np.cos(y), np.sin(y)

@@ -112,10 +112,10 @@ def test_chunk_and_scan_boundaries(oracle, dev):
 
 @pytest.mark.parametrize("n_rows,n_az", [(16, 2047), (16, 2048), (16, 2049), (16, 4500), (64, 4097)])
 def test_rows_across_curvature_tiles(oracle, dev, n_rows, n_az):
-    """k_curv_select streams a row in 2048-point tiles with an 8-point halo and carries the greedy
-    state (jstart) from tile to tile: rows of one tile exactly, one point over, 2-3 tiles, and the
-    16-beam span (3) whose selections cross every tile edge; curvature bits and plane lists
-    bit-exact vs the oracle"""
+    """k_curv streams the ring cloud in 2048-point chunks with an 8-point halo (a row spans
+    several chunks, a chunk several rows) and k_select walks each row's candidate words: rows of
+    one chunk exactly, one point over, 2-3 chunks, and the 16-beam span (3) whose selections cross
+    every chunk and word edge; curvature bits and plane lists bit-exact vs the oracle"""
     import ssf
     fe = ssf.Frontend(n_rows, device=dev.index)
     c = frame(5, 1, n_rows=n_rows, n_az=n_az)[0]

@@ -336,3 +336,7 @@ def test_asf_f32_block(oracle, dev, case):
     assert (bg == bg_ref).mean() >= ASF_BARS["agree"]
     assert np.abs(res["R"][0] - g[f"R_{case}"]).max() < ASF_BARS["R"]
     assert np.abs(res["t"][0] - g[f"t_{case}"]).max() < ASF_BARS["t"]
+    # per frame against the float32 reference's own sensitivity (a19, make_asf_sensitivity.py):
+    # stable frames -> identical mask and EM iteration count, pose = the exact Kabsch of that mask
+    from test_oracle_golden import asf_check
+    asf_check(case, bg, res["info"]["em_iter"][0], res["t"][0])

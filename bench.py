@@ -5,7 +5,7 @@ path (BASELINE.json north_star):
   * scene-flow dynamic-point mask: GaussianMixture(2) fit + Kabsch pose + quaternion
     (PointCloudOdometry_noSeg.py:97-125)                       -> k_mask_pose         [mask streams]
   * frameFeature: ring binning, curvature, planar selection (frameFeature.cpp:45-123)
-                                                               -> k_bin_* / k_curv / k_select
+                                                               -> k_bin_count / k_bin_scan / k_bin_curv / k_select
   * plane table of the new frame (it is the next step's last frame)    -> k_plane_table_sorted
                                                                                       [feature stream]
   * registration of the pair (previous frame, new frame): association + 10 Gauss-Newton
@@ -433,13 +433,13 @@ def rooflines(times, acc, B, N):
     model = {   # DESIGN.md §5 / SURVEY §8(d) per-unit figures
         "k_mask_pose": B * N * (24.0 * passes + 1.0) * n_mask,     # [flow,xyz] f32 per pass + mask
         "k_bin_count": 13.0 * acc["points"],                        # xyz read, row id written
-        "k_bin_scatter": 13.0 * acc["points"] + 12.0 * acc["kept"], # xyz + id read, packed xyz written
-        # §8(d) counts 16 B per point of the rows in range (12 B xyz read + a 4-B curvature
-        # write); the product path writes no curvature, only one candidate bit per point
-        "k_curv": 12.0 * acc["in_range"] + acc["in_range"] / 8.0,
-        # candidate bits read, per plane point: its index written and read back (4 + 4 B), its
-        # xyz gathered (12 B) and the xyzi record written (16 B)
-        "k_select": acc["in_range"] / 8.0 + 36.0 * acc["plane"],
+        # the stable partition fused with the 11-tap curvature: xyz + row id read once per point
+        # (the halo's re-reads of neighbouring chunks are L2 hits, not algorithmic), per kept
+        # point its input index (4 B) and candidate flag byte written at its ring position
+        "k_bin_curv": 13.0 * acc["points"] + 5.0 * acc["kept"],
+        # flag bytes read, per plane point: its index written and read back (4 + 4 B), its ring
+        # index (4 B) and xyz (12 B) gathered and the xyzi record written (16 B)
+        "k_select": 1.0 * acc["kept"] + 40.0 * acc["plane"],
         "k_plane_table_sorted": 49.0 * acc["plane"],
         "k_associate_lds": 64.0 * acc["plane_reg"],
         "k_associate_lds_soa": 64.0 * acc["plane_reg"],
@@ -462,8 +462,8 @@ def rooflines(times, acc, B, N):
                               evaluations_per_pair=acc["corr_evals"] / max(1, acc["corr"]),
                               note="corr = valid correspondences counted on device (ncorr); "
                                    "evaluations = 1 + logged iterations (nlog)")
-    if "k_curv" in out:
-        out["k_curv"]["in_range_points_per_launch"] = acc["in_range"] / out["k_curv"]["launches"]
+    if "k_bin_curv" in out:
+        out["k_bin_curv"]["kept_points_per_launch"] = acc["kept"] / out["k_bin_curv"]["launches"]
     return out, passes
 
 
@@ -883,7 +883,7 @@ def main():
             line["roofline_f64"] = {"bound": "valu_f64", "achieved": tf, "peak": F64_PEAK_TFLOPS,
                                     "unit": "TFLOP/s", "frac": tf / F64_PEAK_TFLOPS,
                                     "kernel": "k_mask_pose", "flops_source": os.path.basename(F64_JSON)}
-    ns = {k: kernels[k]["frac"] for k in ("k_curv", "k_solve") if k in kernels and "frac" in kernels[k]}
+    ns = {k: kernels[k]["frac"] for k in ("k_bin_curv", "k_solve") if k in kernels and "frac" in kernels[k]}
     if ns:
         line["north_star_kernels_hbm_frac"] = ns
         meas = {k: kernels[k]["traffic_frac"] for k in ns if "traffic_frac" in kernels[k]}

@@ -48,7 +48,7 @@ struct ssf_ctx {
     ssf_config cfg{};
     std::string err;
     // frameFeature scratch
-    DevBuf rid, hist, ring_off, ring_xyzi, sel, sel_cnt /* candidate bits */, plane1, off1, cnt1;
+    DevBuf rid, hist, ring_off, ring_xyzi /* ring index */, sel, sel_cnt /* candidate flags */, fix, plane1, off1, cnt1;
     // registration scratch
     DevBuf corr;
     // ssf_register_pair: offsets, counts, the last frame's plane table + search index, pose, log
@@ -67,7 +67,7 @@ struct ssf_ctx {
     static constexpr int kDrawSlots = 4;
     // edge features (beyond the reference): selection scratch, correspondence records
     ssf_edge_config ecfg{};
-    DevBuf esel, esel_cnt /* edge candidate bits */, ecorr;
+    DevBuf esel, ecorr;
     int mask_split = 0;                // ssf_set_mask_split: 0 = automatic
     int mask_slots = -1;               // resident k_mask_pose work-groups (queried once)
     DrawSlot dslot[kDrawSlots];
@@ -221,10 +221,10 @@ int32_t ssf_create(int32_t device, const ssf_config* cfg, ssf_ctx** out) {
 void ssf_destroy(ssf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    DevBuf* bufs[] = {&c->rid, &c->hist, &c->ring_off, &c->ring_xyzi, &c->sel, &c->sel_cnt,
+    DevBuf* bufs[] = {&c->rid, &c->hist, &c->ring_off, &c->ring_xyzi, &c->sel, &c->sel_cnt, &c->fix,
                       &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->pair, &c->start1, &c->vg,
                       &c->icp_cur, &c->icp_key, &c->icp_st, &c->icp_guess, &c->esel,
-                      &c->esel_cnt, &c->ecorr};
+                      &c->ecorr};
     for (auto& ds : c->dslot) {
         if (ds.used) { (void)hipEventSynchronize(ds.used); (void)hipEventDestroy(ds.used); }
         if (ds.copied) { (void)hipEventSynchronize(ds.copied); (void)hipEventDestroy(ds.copied); }
@@ -311,10 +311,12 @@ static int32_t ensure_features(ssf_ctx* c, int32_t n_frames, int64_t total, int6
     SSF_TRY_HIP(c, c->rid.ensure((size_t)std::max<int64_t>(total, 1)), "alloc rid");
     SSF_TRY_HIP(c, c->hist.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(n_frames * n_chunks * R, 1)), "alloc hist");
     SSF_TRY_HIP(c, c->ring_off.ensure(sizeof(int32_t) * (size_t)n_frames * (R + 1)), "alloc ring_off");
-    SSF_TRY_HIP(c, c->ring_xyzi.ensure(3 * sizeof(float) * (size_t)std::max<int64_t>(total, 1)), "alloc ring_xyz");
-    // per-row selection slots (indexInRow at ring positions, k_select) + the candidate bits
+    // ring index (input index per ring position), per-row selection slots (indexInRow at ring
+    // positions, k_select), candidate flag bytes, curvature fix-up list
+    SSF_TRY_HIP(c, c->ring_xyzi.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(total, 1)), "alloc ring index");
     SSF_TRY_HIP(c, c->sel.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(total, 1)), "alloc sel");
-    SSF_TRY_HIP(c, c->sel_cnt.ensure(sizeof(uint64_t) * ssf::cand_words(total, n_frames)), "alloc cand bits");
+    SSF_TRY_HIP(c, c->sel_cnt.ensure(ssf::flag_bytes(total, n_frames)), "alloc cand flags");
+    SSF_TRY_HIP(c, c->fix.ensure(ssf::fix_bytes(total, n_frames)), "alloc curvature fix-up list");
     return SSF_OK;
 }
 
@@ -349,6 +351,8 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
     if (n_frames < 0 || point_stride < 3 || total_points < 0 || max_frame_points < 0 ||
         (n_frames > 0 && (!d_pts || !d_frame_off || !d_plane_xyzi || !d_plane_count)))
         return fail(c, SSF_E_ARG, "extract_planes_batch: bad arguments");
+    if (max_frame_points >= ((int64_t)1 << 24))
+        return fail(c, SSF_E_ARG, "extract_planes_batch: frames of at most 16777215 points (24-bit ring positions)");
     if (n_frames == 0) return SSF_OK;
     SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
     int32_t rc = ensure_features(c, n_frames, total_points, max_frame_points);
@@ -357,8 +361,7 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
     const bool edges = d_edge_xyzi != nullptr;
     if (edges) {
         SSF_TRY_HIP(c, c->esel.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(total_points, 1)), "alloc esel");
-        SSF_TRY_HIP(c, c->esel_cnt.ensure(sizeof(uint64_t) * ssf::cand_words(total_points, n_frames)), "alloc edge bits");
-        es = ssf::EdgeSel{c->ecfg.edge_min, c->ecfg.edge_span, c->esel_cnt.as<uint64_t>(),
+        es = ssf::EdgeSel{c->ecfg.edge_min, c->ecfg.edge_span,
                           c->esel.as<int32_t>(), reinterpret_cast<float4*>(d_edge_xyzi), d_edge_count};
     }
     ProfScope prof(c, stream);
@@ -366,8 +369,8 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
     int32_t* roff = d_ring_off ? d_ring_off : c->ring_off.as<int32_t>();
     hipError_t e = ssf::launch_extract_planes(
         (hipStream_t)stream, c->cfg, n_frames, d_pts, point_stride, d_frame_off, max_frame_points,
-        d_keep, c->rid.as<int8_t>(), c->hist.as<int32_t>(), roff, c->ring_xyzi.as<float>(), ring4,
-        d_curv, c->sel_cnt.as<uint64_t>(), c->sel.as<int32_t>(),
+        d_keep, c->rid.as<int8_t>(), c->hist.as<int32_t>(), roff, c->ring_xyzi.as<int32_t>(), ring4,
+        d_curv, c->sel_cnt.as<uint8_t>(), c->fix.p, c->sel.as<int32_t>(),
         reinterpret_cast<float4*>(d_plane_xyzi), d_plane_count, edges ? &es : nullptr);
     if (e != hipSuccess) return hip_fail(c, e, "extract_planes launch");
     return SSF_OK;

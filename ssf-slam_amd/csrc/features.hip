@@ -1,20 +1,21 @@
 // features.hip -- frameFeature::cloudHandler (src/frameFeature.cpp:35-139) on gfx950.
 //
-// Four kernels per batch of frames, all HBM-streaming:
+// Four kernels per batch of frames:
 //   k_bin_count   ring id per point (frameFeature.cpp:57-72) + per-chunk ring histogram
 //   k_bin_scan    per-frame exclusive scans -> per-(chunk,row) bases and row offsets
-//   k_bin_scatter stable per-row partition (:73-80): wave ballot "match" on the 6-bit row id
-//                 gives each point its rank among same-row points; waves own contiguous
-//                 quarters of the chunk and are prefixed in order -> the reference's push_back
-//                 order exactly.  The chunk is regrouped by row in LDS and stored in contiguous
-//                 per-row runs of packed xyz (12 B/pt: the ring order alone carries indexInRow,
-//                 so intensity = indexInRow + row/100.0 (:77) is recomputed where it is needed)
-//   k_curv        the 11-tap stencil (:84-107) as a stream over 2048-point chunks of the ring
-//                 cloud, evaluated left to right in float, 8 centres per thread; planar
-//                 candidates out as a per-frame bit array
-//   k_select      one work-group per frame: the greedy spacing rule (:110-123) with one row per
-//                 lane, then the selected points (and their encoded intensity) written in
-//                 framePlanePtr order (row major).
+//   k_bin_curv    the stable per-row partition (:73-80) AND the 11-tap curvature (:84-107) of
+//                 one 2048-point input chunk: the chunk plus a halo of input points on both
+//                 sides is ranked per row (wave ballot "match" on the 6-bit row id, waves in
+//                 order -> the reference's push_back order), regrouped by row in LDS, and each
+//                 chunk point's stencil is read from its row's run in that tile.  Out: per ring
+//                 position the point's input index (4 B) and a candidate flag byte (planar, and
+//                 edge when asked) -- the ring-ordered cloud itself is never written (debug only)
+//   k_select      one work-group per frame: the flag bytes packed to bits in LDS, the stencils
+//                 the halo did not cover (a row with < 5 points in the window, e.g. input not in
+//                 azimuth order: the frame's fix-up list, normally empty) computed through the
+//                 ring indices and OR-ed in, the greedy
+//                 spacing rule (:110-123) with one row per lane, then the selected points (and
+//                 their encoded intensity) gathered from the input in framePlanePtr order.
 #include "ssf_device.hpp"
 #include "ssf_internal.hpp"
 
@@ -99,10 +100,13 @@ __global__ __launch_bounds__(256) void k_bin_count(const float* __restrict__ pts
     if (threadIdx.x < n_rows) hist[((int64_t)f * n_chunks + c) * n_rows + threadIdx.x] = h[threadIdx.x];
 }
 
-// One wave per frame: thread r scans its row's chunk counts in chunk order.
+// One wave per frame: thread r scans its row's chunk counts in chunk order.  It also clears the
+// frame's fix-up list count for the k_bin_curv launch that follows on this stream.
 __global__ __launch_bounds__(64) void k_bin_scan(int n_rows, int n_chunks, int32_t* __restrict__ hist,
-                                                 int32_t* __restrict__ ring_off) {
+                                                 int32_t* __restrict__ ring_off,
+                                                 uint32_t* __restrict__ fix_count) {
     const int f = blockIdx.x, r = threadIdx.x;
+    if (r == 0) fix_count[f] = 0u;
     int run = 0;
     if (r < n_rows) {
         // 16 counts loaded before any is rewritten: one memory latency per 16 chunks (a load
@@ -133,57 +137,132 @@ __global__ __launch_bounds__(64) void k_bin_scan(int n_rows, int n_chunks, int32
     if (r == n_rows - 1) ro[n_rows] = incl;
 }
 
-// Stable per-row partition of one kBinChunk-point chunk.  Wave w owns the chunk's points
-// [kBinChunk/4 w, kBinChunk/4 (w + 1)) in steps of 64: a 7-ballot "match" on the 6-bit row id gives each
-// point its rank among same-row lanes, and a wave-private running count per row (LDS, no
-// barrier) turns that into its rank among the wave's same-row points.  One barrier later the
-// per-wave counts are prefixed (waves in order, then rows), every point lands in a row-grouped
-// LDS tile, and the tile leaves in contiguous per-row runs: coalesced 16-B stores instead of
-// one scattered store per point (a LiDAR scan interleaves the rows point by point).
-constexpr int kScatterSteps = kBinChunk / 256;   // points per thread
+// ---- k_bin_curv ------------------------------------------------------------------------------
+// One work-group per (frame, 2048-point input chunk).  Its WINDOW is the chunk plus kCurvHalo
+// input points on each side (clamped to the frame).  A row's points inside the window are
+// consecutive ring positions of that row (the partition is stable and the window a contiguous
+// input range), so once the window is regrouped by row, a chunk point's 11 taps are its
+// neighbours in its row's run of the tile -- whenever the run holds 5 points on each side of it.
+// With a 64-beam scan in azimuth order a row has a point every 64 inputs, so 384 halo points
+// hold 6 per row; a stencil the halo does not cover goes to the frame's fix-up list (k_select).
+//   rank   waves own contiguous quarters of the window; a 7-ballot match on the row id ranks a
+//          point among same-row lanes, a wave-private running count per row among the wave's
+//          points, the per-wave counts are prefixed (waves in order, then rows): the tile
+//          position.  Halo-before points per row are counted on the side (LDS adds).
+//   place  every point decides at once, from its row's record (one ds_read_b128), its tile
+//          slot, its ring position and its class: halo / chunk point whose stencil lies in the
+//          window / chunk point with curvature 0 (row out of range, or within 5 of the row's
+//          ends, :85) / chunk point whose taps the window lacks; one 32-bit word per tile entry
+//          {ring position : 24, class : 2, flags : 2} and its window position (u16)
+//   curv   ONE float array, filled with x, then y, then z (the points stay in registers):
+//          every thread owns kCE consecutive tile entries and reads their taps as 7 aligned
+//          ds_read_b128 per coordinate; sums left to right in float, exactly as the reference
+//          (and the oracle), one coordinate at a time
+//   out    per chunk point, at its ring position: the input index (frame-local, int32), and a
+//          flag byte: bit 0 = planar candidate (row in range and curvature < planeMin, the
+//          curvature being 0 outside [5, n - 5) as :85 leaves it), bit 1 = edge candidate
+//          (kEdge, beyond the reference: row in range, centre in [5, n - 5), curvature >
+//          edge_min, oracle/edge_oracle.c); tile order = contiguous per-row runs.  Debug only:
+//          the ring-ordered cloud (x, y, z, intensity = indexInRow + row / 100.0, :77) and the
+//          curvature of every point.
+// Blocks are mapped XCD-aware: the dispatcher deals blocks round-robin over the 8 XCDs, so
+// block b runs logical block (b % 8) * Q + b / 8 -- each XCD walks a contiguous range of
+// chunks in order and a window's halo is the neighbouring chunk its own L2 just read.
+#ifndef SSF_CURV_HALO
+#define SSF_CURV_HALO 384
+#endif
+constexpr int kCurvHalo = SSF_CURV_HALO;                 // multiple of 64, <= kBinChunk
+constexpr int kWin = kBinChunk + 2 * kCurvHalo;          // window points at most
+constexpr int kWinQ = ((kWin + 3) / 4 + 63) / 64;        // 64-point steps per wave quarter
+constexpr int kCE = ((kWin + 255) / 256 + 3) & ~3;       // tile entries per thread (12)
+constexpr int kTileE = kCE * 256;                        // tile entries (>= kWin)
+constexpr int kTilePad = 8;
+static_assert(kCurvHalo % 64 == 0 && kCurvHalo <= kBinChunk, "halo");
+static_assert(kWin < 4096, "window positions and run lengths use 12 bits");
+// tile entry classes (meta bits 24..25)
+constexpr uint32_t kClsHalo = 0, kClsStencil = 1, kClsZero = 2, kClsOpen = 3;
 
-struct Xyz { float x, y, z; };                      // packed ring-ordered point (12 B)
+// byte where frame f's flag bytes start: 64-byte aligned per frame, frames disjoint
+// (buffer: total + 64 F + 64 bytes)
+SSF_DEV int64_t flag_base(const int64_t* frame_off, int f) { return (frame_off[f] & ~(int64_t)63) + 64 * (int64_t)f; }
 
-__global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ pts, int stride,
-                                                     const int64_t* __restrict__ frame_off,
-                                                     int n_rows, int n_chunks,
-                                                     const int8_t* __restrict__ rid,
-                                                     const int32_t* __restrict__ chunk_base,
-                                                     const int32_t* __restrict__ ring_off,
-                                                     Xyz* __restrict__ out, float4* __restrict__ out4) {
-    __shared__ float4 tile[kBinChunk];            // 16 B per point
-    __shared__ uint8_t row_of[kBinChunk];
+// the 11-tap sum of one coordinate, left to right (u[5] is the centre): frameFeature.cpp:88-97
+SSF_DEV float tap11(const float* u) {
+    float acc = u[0] + u[1];
+#pragma unroll
+    for (int k = 2; k < 11; ++k) acc = (k == 5) ? acc - 10.0f * u[5] : acc + u[k];
+    return acc;
+}
+
+SSF_DEV uint8_t cand_flags(bool row_in, bool inner, float v, float plane_min, bool edge, float edge_min) {
+    const float val = inner ? v : 0.0f;
+    return (uint8_t)((row_in && val < plane_min) ? 1 : 0) |
+           (uint8_t)((edge && row_in && inner && v > edge_min) ? 2 : 0);
+}
+
+template <bool kDebug, bool kEdge>
+__global__ __launch_bounds__(256) void k_bin_curv(const float* __restrict__ pts, int stride,
+                                                  const int64_t* __restrict__ frame_off,
+                                                  int n_frames, int n_rows, int n_chunks,
+                                                  int row_start, int row_end, float plane_min,
+                                                  float edge_min,
+                                                  const int8_t* __restrict__ rid,
+                                                  const int32_t* __restrict__ chunk_base,
+                                                  const int32_t* __restrict__ ring_off,
+                                                  int32_t* __restrict__ ring_idx,
+                                                  uint8_t* __restrict__ flags,
+                                                  int32_t* __restrict__ fix, uint32_t* __restrict__ fix_count,
+                                                  float4* __restrict__ out4, float* __restrict__ curv) {
+    __shared__ __attribute__((aligned(16))) float sc[kTileE + 2 * kTilePad];   // x, then y, then z
+    __shared__ uint32_t meta[kTileE];
+    __shared__ uint16_t wpos[kTileE];
     __shared__ int wrun[4][kMaxRows];
-    __shared__ int roff[kMaxRows + 1];            // chunk-local row offsets
-    __shared__ int64_t rbase[kMaxRows];           // global index of row r's first chunk point - roff[r]
-    __shared__ double rfrac[kMaxRows];            // id / 100.0, the f64 division done once per row
-    const int f = blockIdx.y, c = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
+    __shared__ int nb[kMaxRows];                  // halo-before points per row
+    __shared__ int4 rinfo[kMaxRows];              // {run offset | run length << 12, cb - nb, ring offset, n_r}
+    __shared__ int ntot;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // XCD-aware logical block (see above)
+    const int64_t nblk = (int64_t)n_chunks * n_frames;
+    const int64_t q8 = (nblk + 7) / 8;
+    const int64_t lb = (int64_t)(blockIdx.x % 8) * q8 + blockIdx.x / 8;
+    if (lb >= nblk) return;
+    const int f = (int)(lb / n_chunks), c = (int)(lb - (int64_t)f * n_chunks);
     const int64_t fb = frame_off[f], e = frame_off[f + 1];
     const int64_t s = fb + (int64_t)c * kBinChunk;
-    if (s >= e) return;  // uniform
+    if (s >= e) return;                           // uniform
     const int64_t t = min(e, s + (int64_t)kBinChunk);
+    const int64_t ws = max(fb, s - (int64_t)kCurvHalo), we = min(e, t + (int64_t)kCurvHalo);
+    const int L = (int)(we - ws), hb = (int)(s - ws), he = (int)(t - ws);   // own: [hb, he)
+    const int qlen = ((L + 3) / 4 + 63) / 64 * 64;                          // <= 64 kWinQ
     if (tid < kMaxRows) {
         wrun[0][tid] = wrun[1][tid] = wrun[2][tid] = wrun[3][tid] = 0;
-        rfrac[tid] = (double)tid / 100.0;
+        nb[tid] = 0;
+    }
+    // the rows' chunk bases and ring offsets, loaded now by wave 0 (used after the ranking):
+    // their latency hides behind the point loads instead of stalling the work-group later
+    int cbr = 0, ro0 = 0, ro1 = 0;
+    if (tid < n_rows) {
+        cbr = chunk_base[((int64_t)f * n_chunks + c) * n_rows + tid];
+        const int32_t* ro = ring_off + (int64_t)f * (n_rows + 1);
+        ro0 = ro[tid]; ro1 = ro[tid + 1];
     }
     __syncthreads();
-    // all loads first (ids, then points at clamped indices, unconditionally): one wait for the
-    // whole kScatterSteps-point batch instead of one load latency per step
-    int idr[kScatterSteps];       // row id, then row id | rank-in-wave << 8
-    float px[kScatterSteps], py[kScatterSteps], pz[kScatterSteps];
-    const int64_t i0 = s + (kBinChunk / 4) * w + (tid & 63);
+    // all loads first (ids, then points at clamped indices, unconditionally)
+    const int q0 = w * qlen, q1 = min(L, q0 + qlen);
+    int idr[kWinQ];
+    float px[kWinQ], py[kWinQ], pz[kWinQ];
 #pragma unroll
-    for (int st = 0; st < kScatterSteps; ++st) {
-        const int64_t i = i0 + 64 * st;
-        idr[st] = (i < t) ? (int)rid[i] : -1;
+    for (int st = 0; st < kWinQ; ++st) {
+        const int p = q0 + lane + 64 * st;
+        idr[st] = (p < q1) ? (int)rid[ws + p] : -1;
     }
 #pragma unroll
-    for (int st = 0; st < kScatterSteps; ++st) {
-        const float* p = pts + min(i0 + 64 * st, t - 1) * stride;
-        px[st] = p[0]; py[st] = p[1]; pz[st] = p[2];
+    for (int st = 0; st < kWinQ; ++st) {
+        const float* pp = pts + (ws + min(q0 + lane + 64 * st, L - 1)) * stride;
+        px[st] = pp[0]; py[st] = pp[1]; pz[st] = pp[2];
     }
 #pragma unroll
-    for (int st = 0; st < kScatterSteps; ++st) {
+    for (int st = 0; st < kWinQ; ++st) {
         const int id = idr[st];
         uint64_t m = __ballot(id >= 0);
 #pragma unroll
@@ -198,12 +277,11 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
             const int before = wrun[w][id];                  // read by every lane first,
             rank = before + rin;
             if (rin == 0) wrun[w][id] = before + __popcll(m);   // then the group leader adds
+            if (q0 + lane + 64 * st < hb) atomicAdd(&nb[id], 1);
         }
         idr[st] = (id & 0xff) | (rank << 8);
     }
     __syncthreads();
-    const int32_t* cb = chunk_base + ((int64_t)f * n_chunks + c) * n_rows;
-    const int32_t* ro = ring_off + (int64_t)f * (n_rows + 1);
     if (tid < 64) {                                          // rows on the lanes of wave 0
         const int r = tid;
         int tot = 0;
@@ -218,179 +296,164 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const float* __restrict__ p
             const int y = __shfl_up(incl, o, 64);
             if (r >= o) incl += y;
         }
-        if (r < n_rows) {
-            roff[r] = incl - tot;
-            rbase[r] = fb + ro[r] + cb[r] - (incl - tot);
-        }
-        if (r == 63) roff[kMaxRows] = incl;
+        if (r < n_rows) rinfo[r] = make_int4((incl - tot) | (tot << 12), cbr - nb[r], ro0, ro1 - ro0);
+        if (r == 63) ntot = incl;
     }
     __syncthreads();
+    const int nt = ntot;                                     // kept points in the window
+    // ---- place: tile slot, ring position and class of every point; x into the tile
+    int loc[kWinQ];
 #pragma unroll
-    for (int st = 0; st < kScatterSteps; ++st) {
+    for (int st = 0; st < kWinQ; ++st) {
         const int id = (int)(int8_t)(idr[st] & 0xff);
+        loc[st] = kTileE;                                    // no point: the pad slot
         if (id >= 0) {
-            const int in_row = wrun[w][id] + (idr[st] >> 8);    // rank among the chunk's row-id points
-            const int loc = roff[id] + in_row;
-            float4 v;
-            v.x = px[st]; v.y = py[st]; v.z = pz[st];
-            // frameFeature.cpp:77, needed only by the debug ring-ordered cloud (out4 is uniform)
-            v.w = out4 ? (float)((double)(cb[id] + in_row) + rfrac[id]) : 0.0f;
-            tile[loc] = v;
-            row_of[loc] = (uint8_t)id;
+            const int4 ri = rinfo[id];
+            const int p = wrun[w][id] + (idr[st] >> 8);      // position in the row's window run
+            const int k = (ri.x & 0xfff) + p;
+            const int j = ri.y + p;                          // row-relative ring index
+            const int wp = q0 + lane + 64 * st;
+            const int nr = ri.w, wl = ri.x >> 12;
+            const bool own = wp >= hb && wp < he;
+            const bool row_in = id >= row_start && id < n_rows - row_end;
+            const bool inner = j >= 5 && j < nr - 5;
+            const bool covered = p >= 5 && p + 5 < wl;
+            const uint32_t cls = !own ? kClsHalo : !(row_in && inner) ? kClsZero : covered ? kClsStencil : kClsOpen;
+            // curvature-0 points: the flags now (:85 leaves their curvature at 0)
+            const uint32_t fl = cls == kClsZero ? (uint32_t)cand_flags(row_in, false, 0.0f, plane_min, kEdge, edge_min) : 0u;
+            meta[k] = (uint32_t)(ri.z + j) | (cls << 24) | (fl << 26);
+            wpos[k] = (uint16_t)wp;
+            sc[kTilePad + k] = px[st];
+            loc[st] = k;
+            if (kDebug && own) {
+                const int64_t g = fb + ri.z + j;
+                if (out4) out4[g] = make_float4(px[st], py[st], pz[st], (float)((double)j + (double)id / 100.0));
+                if (curv && cls == kClsZero) curv[g] = 0.0f;
+            }
         }
     }
     __syncthreads();
-    const int total = roff[kMaxRows];
-    for (int k = tid; k < total; k += 256) {
-        const float4 v = tile[k];
-        const int64_t o = rbase[row_of[k]] + k;
-        out[o] = Xyz{v.x, v.y, v.z};
-        if (out4) out4[o] = v;                      // debug ring-ordered cloud (x, y, z, intensity)
-    }
-}
-
-// k_curv: the 11-tap curvature (:84-107) as a pure stream over the frame's ring-ordered cloud,
-// one work-group per 2048-point chunk of the rows in range (rows are contiguous there, row after
-// row).  Each thread issues its 9 clamped 12-byte loads (the chunk and an 8-point halo on both
-// sides) before the first use, the chunk lands in an LDS tile of x | y | z float arrays, and
-// every thread owns 8 consecutive centres: it reads the 24 points around them as six aligned
-// ds_read_b128 per coordinate and evaluates the sums left to right in float, exactly as the
-// reference, one coordinate at a time.  A centre's row comes from the frame's row offsets (LDS);
-// its value stays 0 for j < 5 and j >= n - 5 (never computed, :85).  The planar candidates
-// (value < planeMin) leave as one byte per thread of a per-frame bit array (bit = ring position);
-// the greedy spacing rule runs in k_select.  kEdge (beyond the reference, off by default): the
-// edge candidates (curvature > edge_min, centres in [5, n - 5), oracle/edge_oracle.c) into a
-// second bit array.  kCurv (debug / parity output): the curvature of every point, 0 outside the
-// rows in range.
-#ifndef SSF_CURV_PROBE
-#define SSF_CURV_PROBE 0   // diagnostic variants only (tools/gpu): 2 = no stencil
-#endif
-constexpr int kCurvChunk = 2048;                // centres per work-group
-constexpr int kCurvHalo = 8;                    // >= 5, and a multiple of 8 (aligned windows)
-constexpr int kCurvLoads = (kCurvChunk + 2 * kCurvHalo + 255) / 256;   // 9
-
-// 64-bit word where frame f's candidate bits start (frame-local bit i -> word + (i >> 6)):
-// 8-byte aligned per frame, and frames never share a word
-SSF_DEV int64_t cand_word0(const int64_t* frame_off, int f) { return (frame_off[f] >> 6) + f; }
-
-template <bool kCurv, bool kEdge>
-__global__ __launch_bounds__(256) void k_curv(const int64_t* __restrict__ frame_off, int n_rows,
-                                              int row_start, int row_end, float plane_min,
-                                              const int32_t* __restrict__ ring_off,
-                                              const Xyz* __restrict__ rxyz,
-                                              float* __restrict__ curv,
-                                              uint8_t* __restrict__ pbits, float edge_min,
-                                              uint8_t* __restrict__ ebits) {
-    __shared__ __attribute__((aligned(16))) float sx[256 * kCurvLoads], sy[256 * kCurvLoads], sz[256 * kCurvLoads];
-    __shared__ int ro[kMaxRows + 1];
-    const int tid = threadIdx.x, c = blockIdx.x, f = blockIdx.y;
-    // the chunk's bounds from uniform (scalar) loads, so the point loads issue after ONE memory
-    // latency; the row table for the centres follows into LDS while they are in flight
-    const int64_t fb = frame_off[f];
-    const int32_t* rof = ring_off + (int64_t)f * (n_rows + 1);
-    const int nr_tot = rof[n_rows];
-    // the rows in range (every point for the debug curvature, which is 0 outside them); chunks
-    // start at a multiple of 8 points, so every thread's 8 centres are one byte of the bit array
-    const int lo = kCurv ? 0 : (rof[row_start] & ~7), hi = kCurv ? nr_tot : rof[n_rows - row_end];
-    const int c0 = lo + c * kCurvChunk;                        // uniform
-    if (c0 >= hi) return;
-    const Xyz* src = rxyz + fb;
-    {   // positions [c0 - halo, c0 + chunk + halo), clamped into the frame: all loads first
-        Xyz q[kCurvLoads];
+    // ---- curvature of this thread's kCE tile entries, one coordinate at a time
+    const int k0 = kCE * tid;
+    float v[kCE];
+    auto coord = [&](float (&d)[kCE]) {
+        float h[kCE + 16];                                   // tile entries k0 - 8 .. k0 + kCE + 8
 #pragma unroll
-        for (int k = 0; k < kCurvLoads; ++k) {
-            const int pos = c0 - kCurvHalo + tid + 256 * k;
-            q[k] = src[min(max(pos, 0), nr_tot - 1)];
+        for (int k = 0; k < (kCE + 16) / 4; ++k) {
+            const float4 x4 = *reinterpret_cast<const float4*>(sc + k0 + 4 * k);
+            h[4 * k] = x4.x; h[4 * k + 1] = x4.y; h[4 * k + 2] = x4.z; h[4 * k + 3] = x4.w;
         }
-        if (tid <= n_rows) ro[tid] = rof[tid];
-        // every store unconditional (the tail lands in the pad): a store under a branch made the
-        // compiler wait for the last load right after issuing it
 #pragma unroll
-        for (int k = 0; k < kCurvLoads; ++k) {
-            const int p = tid + 256 * k;
-            sx[p] = q[k].x; sy[p] = q[k].y; sz[p] = q[k].z;
+        for (int i = 0; i < kCE; ++i) d[i] = tap11(h + 3 + i);   // centre h[8 + i]
+    };
+    {
+        float d0[kCE], d1[kCE];
+        coord(d0);
+        __syncthreads();
+#pragma unroll
+        for (int st = 0; st < kWinQ; ++st) sc[kTilePad + loc[st]] = py[st];
+        __syncthreads();
+        coord(d1);
+#pragma unroll
+        for (int i = 0; i < kCE; ++i) v[i] = d0[i] * d0[i] + d1[i] * d1[i];
+        __syncthreads();
+#pragma unroll
+        for (int st = 0; st < kWinQ; ++st) sc[kTilePad + loc[st]] = pz[st];
+        __syncthreads();
+        coord(d0);
+#pragma unroll
+        for (int i = 0; i < kCE; ++i) v[i] = v[i] + d0[i] * d0[i];
+    }
+    uint32_t mt[kCE];
+#pragma unroll
+    for (int i = 0; i < kCE; ++i) mt[i] = meta[min(k0 + i, kTileE - 1)];
+    uint32_t fixm = 0;                                       // open stencils (bit i)
+#pragma unroll
+    for (int i = 0; i < kCE; ++i) {
+        const uint32_t cls = (mt[i] >> 24) & 3u;
+        if (k0 + i < nt && cls == kClsStencil) {
+            const uint32_t fl = cand_flags(true, true, v[i], plane_min, kEdge, edge_min);
+            meta[k0 + i] = mt[i] | (fl << 26);
+            if (kDebug && curv) curv[fb + (mt[i] & 0xFFFFFFu)] = v[i];
+        }
+        fixm |= (k0 + i < nt && cls == kClsOpen) ? 1u << i : 0u;
+    }
+    // fix-up list (rare): wave-aggregated reservation
+    const int nfx = __popc(fixm);
+    int incl = nfx;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const int wtot = __shfl(incl, 63, 64);
+    if (wtot > 0) {                                          // wave-uniform
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&fix_count[f], (uint32_t)wtot);
+        base = __shfl(base, 0, 64) + (uint32_t)(incl - nfx);
+        while (fixm) {
+            const int i = __builtin_ctz(fixm);
+            fixm &= fixm - 1u;
+            fix[fb + base++] = (int32_t)(mt[i] & 0xFFFFFFu);
         }
     }
     __syncthreads();
-    const int i0 = c0 + 8 * tid;                               // this thread's 8 centres
-    if (i0 >= hi) return;
-    // its first centre's row: the last r with ro[r] <= i0
-    int r = 0;
-#pragma unroll
-    for (int st = 32; st > 0; st >>= 1)
-        if (r + st <= n_rows && ro[r + st] <= i0) r += st;
-    float v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = 0.0f;
-    if (SSF_CURV_PROBE != 2) {
-        // centres i0 + i; their taps are tile entries 8 tid + 3 + i .. 8 tid + 13 + i
-        float d0[8], d1[8];
-        auto coord = [&](const float* a, float (&d)[8]) {
-            float h[24];
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                const float4 x4 = *reinterpret_cast<const float4*>(a + 8 * tid + 4 * k);
-                h[4 * k] = x4.x; h[4 * k + 1] = x4.y; h[4 * k + 2] = x4.z; h[4 * k + 3] = x4.w;
-            }
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float* u = h + 3 + i;                    // u[0 .. 10], centre u[5]
-                float acc = u[0] + u[1];
-#pragma unroll
-                for (int k = 2; k < 11; ++k) acc = (k == 5) ? acc - 10.0f * u[5] : acc + u[k];
-                d[i] = acc;
-            }
-        };
-        coord(sx, d0);
-        coord(sy, d1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = d0[i] * d0[i] + d1[i] * d1[i];
-        coord(sz, d0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = v[i] + d0[i] * d0[i];
+    // ---- chunk points out, in tile order (contiguous per-row runs of ring positions)
+    const int64_t fl0 = flag_base(frame_off, f);
+    const int32_t ib = (int32_t)(ws - fb);
+#pragma unroll 4
+    for (int k = tid; k < nt; k += 256) {
+        const uint32_t mk = meta[k];
+        const int wp = wpos[k];
+        if (((mk >> 24) & 3u) == kClsHalo) continue;
+        const int g = (int)(mk & 0xFFFFFFu);
+        ring_idx[fb + g] = ib + wp;
+        flags[fl0 + g] = (uint8_t)(mk >> 26);
     }
-    uint32_t pb = 0, eb = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int ii = i0 + i;
-        while (r < n_rows - 1 && ii >= ro[r + 1]) ++r;         // rows of >= 1 point ahead
-        const int j = ii - ro[r], n_r = ro[r + 1] - ro[r];
-        const bool row_in = r >= row_start && r < n_rows - row_end;
-        const bool inner = j >= 5 && j < n_r - 5;
-        const float val = inner ? v[i] : 0.0f;
-        if (ii < hi) {
-            if (kCurv) curv[fb + ii] = row_in ? val : 0.0f;
-            pb |= (uint32_t)(row_in && val < plane_min) << i;
-            if (kEdge) eb |= (uint32_t)(row_in && inner && val > edge_min) << i;
-        }
-    }
-    const int64_t byte0 = cand_word0(frame_off, f) * 8 + (i0 >> 3);
-    pbits[byte0] = (uint8_t)pb;
-    if (kEdge) ebits[byte0] = (uint8_t)eb;
 }
 
-// k_select: one work-group per frame.  The greedy spacing rule (:110-123) for every row at once,
-// ONE ROW PER LANE of wave 0 (wave 1: the edge rule, kEdge): each lane walks its row's candidate
-// bits from the frame's bit array staged in LDS -- next candidate at or after jstart by a
+// k_select: one work-group per frame.  The frame's flag bytes are packed into bit words in LDS
+// (64 flags -> one word: byte LSBs gathered by a multiply); the stencils k_bin_curv left open (the
+// frame's fix-up list) are evaluated through the ring index -- same taps, same sums, same order --
+// and their flags OR-ed into the words; then the greedy spacing rule
+// (:110-123) runs for every row at once, ONE ROW PER LANE of wave 0 (wave 1: the edge rule,
+// kEdge): each lane walks its row's candidate bits -- next candidate at or after jstart by a
 // count-trailing-zeros of the word, jstart = selection + planeSpan -- so 64 rows advance in one
-// VALU instruction stream (a scalar walk per row was ~180 cycles per step).  The selections
-// (indexInRow) go to per-row slots in global scratch; after one barrier the row counts are
-// prefixed and every thread of the work-group emits output slots in framePlanePtr order (row
-// major): x, y, z gathered from the ring-ordered cloud, intensity = indexInRow + row / 100.0 (:77).
+// VALU instruction stream.  The selections (indexInRow) go to per-row slots in global scratch;
+// after one barrier the row counts are prefixed and every thread of the work-group emits
+// output slots in framePlanePtr order (row major): x, y, z gathered from the input through the
+// ring index, intensity = indexInRow + row / 100.0 (:77).
 constexpr int kSelThreads = 1024;
 constexpr int kSelWordsLds = 6144;              // candidate words staged per array (48 KiB: 393k points)
 
+// bit b of the result = bit `bit` of byte b of x (bytes' bits gathered by one multiply: the
+// products 2^(8k + 7m + 7) never collide, so no carries)
+SSF_DEV uint32_t pack8(uint64_t x, int bit) {
+    return (uint32_t)((((x >> bit) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+}
+
+SSF_DEV uint64_t pack64(const uint64_t* b8, int bit) {
+    uint64_t wv = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wv |= (uint64_t)pack8(b8[k], bit) << (8 * k);
+    return wv;
+}
+
 template <bool kEdge>
-__global__ __launch_bounds__(kSelThreads) void k_select(const int64_t* __restrict__ frame_off, int n_rows,
+__global__ __launch_bounds__(kSelThreads) void k_select(const float* __restrict__ pts, int stride,
+                                                        const int64_t* __restrict__ frame_off, int n_rows,
                                                         int row_start, int row_end, int plane_span,
+                                                        float plane_min, float edge_min,
                                                         const int32_t* __restrict__ ring_off,
-                                                        const Xyz* __restrict__ rxyz,
-                                                        const uint64_t* __restrict__ pbits,
+                                                        const int32_t* __restrict__ ring_idx,
+                                                        uint8_t* __restrict__ flags,
+                                                        const int32_t* __restrict__ fix,
+                                                        const uint32_t* __restrict__ fix_count,
+                                                        float* __restrict__ curv,
                                                         int32_t* __restrict__ sel,
                                                         float4* __restrict__ plane,
                                                         int32_t* __restrict__ plane_count,
-                                                        int edge_span, const uint64_t* __restrict__ ebits,
-                                                        int32_t* __restrict__ esel,
+                                                        int edge_span, int32_t* __restrict__ esel,
                                                         float4* __restrict__ edge,
                                                         int32_t* __restrict__ edge_count) {
     __shared__ uint64_t wl[kEdge ? 2 : 1][kSelWordsLds];
@@ -400,27 +463,62 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const int64_t* __restric
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int f = blockIdx.x;
     const int64_t fb = frame_off[f];
-    const int nf = (int)(frame_off[f + 1] - fb);
-    const int nw = (nf + 63) >> 6;
-    const int64_t wb = cand_word0(frame_off, f);
     if (tid <= n_rows) ro[tid] = ring_off[(int64_t)f * (n_rows + 1) + tid];
+    __syncthreads();
+    const int nr = ro[n_rows];                                 // kept points (ring positions)
+    const int nw = (nr + 63) >> 6;
+    uint8_t* F8 = flags + flag_base(frame_off, f);
+    const uint64_t* F = reinterpret_cast<const uint64_t*>(F8);
+    const uint32_t nfix = fix_count[f];
     for (int k = tid; k < min(nw, kSelWordsLds); k += kSelThreads) {
-        wl[0][k] = pbits[wb + k];
-        if (kEdge) wl[kEdge ? 1 : 0][k] = ebits[wb + k];
+        uint64_t b8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) b8[u] = F[8 * k + u];
+        wl[0][k] = pack64(b8, 0);
+        if (kEdge) wl[kEdge ? 1 : 0][k] = pack64(b8, 1);
     }
     __syncthreads();
+    if (nfix > 0) {                                            // uniform; normally not taken
+        for (uint32_t q = tid; q < nfix; q += kSelThreads) {
+            const int g = fix[fb + q];                         // in range and inner: 5 <= j < n_r - 5
+            float ux[11], uy[11], uz[11];
+#pragma unroll
+            for (int m = 0; m < 11; ++m) {
+                const float* p = pts + (fb + ring_idx[fb + g - 5 + m]) * stride;
+                ux[m] = p[0]; uy[m] = p[1]; uz[m] = p[2];
+            }
+            const float d0 = tap11(ux), d1 = tap11(uy), d2 = tap11(uz);
+            float v = d0 * d0 + d1 * d1;
+            v = v + d2 * d2;
+            const uint8_t fl = cand_flags(true, true, v, plane_min, kEdge, edge_min);
+            if (curv) curv[fb + g] = v;
+            if ((g >> 6) < kSelWordsLds) {
+                if (fl & 1) atomicOr((unsigned long long*)&wl[0][g >> 6], 1ull << (g & 63));
+                if (kEdge && (fl & 2)) atomicOr((unsigned long long*)&wl[kEdge ? 1 : 0][g >> 6], 1ull << (g & 63));
+            } else {
+                F8[g] = fl;                                    // read back by the walk below
+            }
+        }
+        __syncthreads();
+    }
     if (w < (kEdge ? 2 : 1)) {                                 // uniform: wave 0 planes, wave 1 edges
         const int r = lane;
         const bool e = kEdge && w == 1;
         const uint64_t* W = wl[e ? 1 : 0];
-        const uint64_t* G = (e ? ebits : pbits) + wb;
         const int span = e ? edge_span : plane_span;
         int32_t* out = e ? esel : sel;
         int cnt = 0;
         if (r < n_rows && r >= row_start && r < n_rows - row_end) {
             const int rs = ro[r], n_r = ro[r + 1] - rs;
             if (n_r > 0) {
-                auto word = [&](int k) { return k < kSelWordsLds ? W[k] : G[k]; };
+                // beyond the LDS stage (frames > 393k points): the word straight from the flags
+                auto word = [&](int k) {
+                    if (k < kSelWordsLds) return W[k];
+                    uint64_t b8[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) b8[u] = F[8 * k + u];
+                    return pack64(b8, e ? 1 : 0);
+                };
                 int js = 0;                                     // jstart, row-relative
                 const int kend = (rs + n_r - 1) >> 6;
                 uint64_t nxt = word(rs >> 6);
@@ -462,10 +560,10 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const int64_t* __restric
         const int32_t* S = e ? esel : sel;
         float4* O = e ? edge : plane;
         // four output slots per thread per trip, each stage's loads issued together (the
-        // selection index, then the gathered point): three memory latencies per trip
+        // selection index, the ring index, then the gathered point)
         constexpr int U = 4;
         for (int k0 = 0; k0 < total; k0 += U * kSelThreads) {   // uniform
-            int kk[U], rr[U], jj[U];
+            int kk[U], rr[U], jj[U], ii[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 kk[u] = min(k0 + u * kSelThreads + tid, total - 1);
@@ -477,64 +575,74 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const int64_t* __restric
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) jj[u] = S[fb + ro[rr[u]] + (kk[u] - P[rr[u]])];
-            Xyz q[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) q[u] = rxyz[fb + ro[rr[u]] + jj[u]];
+            for (int u = 0; u < U; ++u) ii[u] = ring_idx[fb + ro[rr[u]] + jj[u]];
+            float q[U][3];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float* p = pts + (fb + ii[u]) * stride;
+                q[u][0] = p[0]; q[u][1] = p[1]; q[u][2] = p[2];
+            }
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 if (k0 + u * kSelThreads + tid < total)
-                    O[fb + kk[u]] = make_float4(q[u].x, q[u].y, q[u].z,
+                    O[fb + kk[u]] = make_float4(q[u][0], q[u][1], q[u][2],
                                                 (float)((double)jj[u] + (double)rr[u] / 100.0));
         }
     }
 }
 
+size_t flag_bytes(int64_t total, int n_frames) { return (size_t)(total + 64 * (int64_t)n_frames + 64); }
+// per-frame fix-up counts (64-byte aligned block), then the entries at the frame offsets
+static size_t fix_head(int n_frames) { return ((size_t)n_frames * sizeof(uint32_t) + 63) & ~(size_t)63; }
+size_t fix_bytes(int64_t total, int n_frames) { return fix_head(n_frames) + sizeof(int32_t) * (size_t)(total + 1); }
+
 hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_frames,
                                  const float* pts, int stride, const int64_t* frame_off,
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
-                                 int32_t* ring_off, float* ring_xyz, float4* ring_xyzi, float* curv,
-                                 uint64_t* bits, int32_t* sel, float4* plane,
+                                 int32_t* ring_off, int32_t* ring_idx, float4* ring_xyzi, float* curv,
+                                 uint8_t* flags, void* fix, int32_t* sel, float4* plane,
                                  int32_t* plane_count, const EdgeSel* edge) {
     const int R = cfg.n_rows;
     const int n_chunks = (int)((max_pts + kBinChunk - 1) / kBinChunk);
     if (n_frames <= 0) return hipSuccess;
     if (R > kMaxRows) return hipErrorInvalidValue;
+    if (max_pts >= (int64_t)1 << 24) return hipErrorInvalidValue;   // ring positions: 24 bits
+    // fix-up lists: per-frame counts, then the entries at the frame offsets
+    uint32_t* fix_count = reinterpret_cast<uint32_t*>(fix);
+    int32_t* fixl = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(fix) + fix_head(n_frames));
     if (n_chunks > 0) {
         kmark(s, "k_bin_count");
         hipLaunchKernelGGL(k_bin_count, dim3(n_chunks, n_frames), dim3(256), 0, s, pts, stride,
                            frame_off, R, n_chunks, keep, rid, hist);
     }
     kmark(s, "k_bin_scan");
-    hipLaunchKernelGGL(k_bin_scan, dim3(n_frames), dim3(64), 0, s, R, n_chunks, hist, ring_off);
-    if (n_chunks > 0) {
-        kmark(s, "k_bin_scatter");
-        hipLaunchKernelGGL(k_bin_scatter, dim3(n_chunks, n_frames), dim3(256), 0, s, pts, stride,
-                           frame_off, R, n_chunks, rid, hist, ring_off,
-                           reinterpret_cast<Xyz*>(ring_xyz), ring_xyzi);
-    }
-    // k_curv: chunks of the rows in range (every point with the debug curvature)
-    const int cchunks = (int)((max_pts + kCurvChunk - 1) / kCurvChunk);
-    const dim3 cgrid(max(cchunks, 1), n_frames);
-    kmark(s, "k_curv");
-    const Xyz* rx = reinterpret_cast<const Xyz*>(ring_xyz);
+    hipLaunchKernelGGL(k_bin_scan, dim3(n_frames), dim3(64), 0, s, R, n_chunks, hist, ring_off, fix_count);
+    const bool dbg = curv != nullptr || ring_xyzi != nullptr;
     const float emin = edge ? edge->min_curv : 0.f;
-    uint8_t* eb8 = edge ? reinterpret_cast<uint8_t*>(edge->bits) : nullptr;
-#define SSF_CURV_LAUNCH(C, E)                                                                      \
-    hipLaunchKernelGGL((k_curv<C, E>), cgrid, dim3(256), 0, s, frame_off, R, cfg.row_start,         \
-                       cfg.row_end, cfg.plane_min, ring_off, rx, curv,                             \
-                       reinterpret_cast<uint8_t*>(bits), emin, eb8)
-    if (edge) { if (curv) SSF_CURV_LAUNCH(true, true); else SSF_CURV_LAUNCH(false, true); }
-    else { if (curv) SSF_CURV_LAUNCH(true, false); else SSF_CURV_LAUNCH(false, false); }
-#undef SSF_CURV_LAUNCH
+    if (n_chunks > 0) {
+        const int64_t nblk = (int64_t)n_chunks * n_frames;
+        const dim3 grid((unsigned)((nblk + 7) / 8 * 8));
+        kmark(s, "k_bin_curv");
+#define SSF_BC_LAUNCH(D, E)                                                                        \
+        hipLaunchKernelGGL((k_bin_curv<D, E>), grid, dim3(256), 0, s, pts, stride, frame_off,       \
+                           n_frames, R, n_chunks, cfg.row_start, cfg.row_end, cfg.plane_min, emin,  \
+                           rid, hist, ring_off, ring_idx, flags, fixl, fix_count, ring_xyzi, curv)
+        if (edge) { if (dbg) SSF_BC_LAUNCH(true, true); else SSF_BC_LAUNCH(false, true); }
+        else { if (dbg) SSF_BC_LAUNCH(true, false); else SSF_BC_LAUNCH(false, false); }
+#undef SSF_BC_LAUNCH
+    }
     kmark(s, "k_select");
     if (edge)
-        hipLaunchKernelGGL(k_select<true>, dim3(n_frames), dim3(kSelThreads), 0, s, frame_off, R,
-                           cfg.row_start, cfg.row_end, cfg.plane_span, ring_off, rx, bits, sel, plane,
-                           plane_count, edge->span, edge->bits, edge->sel, edge->out, edge->count);
+        hipLaunchKernelGGL(k_select<true>, dim3(n_frames), dim3(kSelThreads), 0, s, pts, stride, frame_off,
+                           R, cfg.row_start, cfg.row_end, cfg.plane_span, cfg.plane_min, emin, ring_off,
+                           ring_idx, flags, fixl, fix_count, curv, sel, plane, plane_count, edge->span,
+                           edge->sel, edge->out, edge->count);
     else
-        hipLaunchKernelGGL(k_select<false>, dim3(n_frames), dim3(kSelThreads), 0, s, frame_off, R,
-                           cfg.row_start, cfg.row_end, cfg.plane_span, ring_off, rx, bits, sel, plane,
-                           plane_count, 1, nullptr, nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL(k_select<false>, dim3(n_frames), dim3(kSelThreads), 0, s, pts, stride, frame_off,
+                           R, cfg.row_start, cfg.row_end, cfg.plane_span, cfg.plane_min, emin, ring_off,
+                           ring_idx, flags, fixl, fix_count, curv, sel, plane, plane_count, 1, nullptr,
+                           nullptr, nullptr);
     return hipGetLastError();
 }
 

@@ -1264,7 +1264,22 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
             };
             const StripGeo g = strips_build<false, kStripPerMax>(getp, m, T, F, X, I16);
             SSF_TSTAMP_BUILD();
-            if (rows_ok && m > kK)
+            // results staged in LDS at their original index and stored coalesced at the end when
+            // 13 B per point fit behind the strip image with a queue of m / 4 entries (m <= ~5000):
+            // scattered 12-B normal and 1-B validity stores each cost a 64-B write request
+            const int soff = ((int)sizeof(lds) - 16 - 13 * m) & ~15;
+            const bool stage = (soff - qoff) / 4 >= m / 4 + 64;              // uniform
+            if (rows_ok && m > kK && stage) {
+                float* nl = reinterpret_cast<float*>(lds + soff);
+                uint8_t* vl = reinterpret_cast<uint8_t*>(lds + soff + 12 * m);
+                table_pick_walks(P, StripView<false>{F, X, I16, m}, T, g, m, plane_max, 0, nl, vl,
+                                 queue, (soff - qoff) / 4, qlen, stamp_out, st0);
+                __syncthreads();
+                float* gn = normal + 3 * base;
+                uint8_t* gv = valid + base;
+                for (int k = tid; k < 3 * m; k += kTableThreads) gn[k] = nl[k];
+                for (int k = tid; k < m; k += kTableThreads) gv[k] = vl[k];
+            } else if (rows_ok && m > kK)
                 table_pick_walks(P, StripView<false>{F, X, I16, m}, T, g, m, plane_max, base, normal, valid,
                                  queue, qcap, qlen, stamp_out, st0);
             else
@@ -1886,7 +1901,9 @@ __global__ __launch_bounds__(kEdgeAssocThreads) void k_edge_associate(
 // ------------------------------------------------------------------------------------------
 // one wave per SIMD: the per-pair solve is latency-bound (a block reduction and a 6x6 solve per
 // iteration), and 256 threads measured 0.083 ms per 256-pair launch against 0.092 at 512 and
-// 0.28 at 1024 (round 2c, tools/gpu/r2c_solve3.sh)
+// 0.28 at 1024 (round 2c, tools/gpu/r2c_solve3.sh).  For a launch of ONE pair (BASELINE
+// configs[1] as written) 512 threads were slower too: 0.083 against 0.073 ms (round 3,
+// tools/gpu/r3g.sh; 1024 threads cap the solve at 128 VGPRs and spill).
 #ifndef SSF_SOLVE_THREADS
 #define SSF_SOLVE_THREADS 256
 #endif
@@ -2191,8 +2208,8 @@ SSF_DEV void write_log(double* log, int max_iter, int p, int idx, const double q
 
 // kEdges: point-to-line blocks (ecorr at ecurr_off / ecurr_count) join every evaluation; they
 // are compacted into the same LDS arrays after the planes.
-template <bool kEdges>
-__global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restrict__ corr,
+template <bool kEdges, int NT>
+__global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
                                                          const int64_t* __restrict__ curr_off,
                                                          const int32_t* __restrict__ curr_count,
                                                          const int32_t* __restrict__ last_count,
@@ -2207,9 +2224,9 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(const CorrRec* __restri
                                                          const int32_t* __restrict__ ecurr_count,
                                                          int32_t* __restrict__ ncorr_edge_out) {
     __shared__ SolveShared S;
-    __shared__ double red[(kSolveThreads / 64) * kNE];
+    __shared__ double red[(NT / 64) * kNE];
     __shared__ CorrLds C;
-    __shared__ int wtot[kSolveThreads / 64];
+    __shared__ int wtot[NT / 64];
     const int p = blockIdx.x, tid = threadIdx.x;
     const int n = curr_count[p];
     const CorrRec* rec = corr + curr_off[p];
@@ -2526,15 +2543,16 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
                            edge->corr, cap);
     }
     kmark(s, "k_solve");
+#define SSF_SOLVE_LAUNCH(E, NT, ...)                                                               \
+    hipLaunchKernelGGL((k_solve<E, NT>), dim3(n_pairs), dim3(NT), 0, s, corr, curr_off, curr_count, \
+                       last_count, cfg.solver, cfg.max_iter, pose_rel, pose_abs, log, nlog, ncorr,  \
+                       __VA_ARGS__)
     if (edge)
-        hipLaunchKernelGGL(k_solve<true>, dim3(n_pairs), dim3(kSolveThreads), 0, s, corr, curr_off,
-                           curr_count, last_count, cfg.solver, cfg.max_iter, pose_rel, pose_abs, log,
-                           nlog, ncorr, edge->corr, edge->curr_off, edge->curr_count, edge->ncorr);
+        SSF_SOLVE_LAUNCH(true, kSolveThreads, edge->corr, edge->curr_off, edge->curr_count, edge->ncorr);
     else
-        hipLaunchKernelGGL(k_solve<false>, dim3(n_pairs), dim3(kSolveThreads), 0, s, corr, curr_off,
-                           curr_count, last_count, cfg.solver, cfg.max_iter, pose_rel, pose_abs, log,
-                           nlog, ncorr, (const CorrRec*)nullptr, (const int64_t*)nullptr,
-                           (const int32_t*)nullptr, (int32_t*)nullptr);
+        SSF_SOLVE_LAUNCH(false, kSolveThreads, (const CorrRec*)nullptr, (const int64_t*)nullptr,
+                         (const int32_t*)nullptr, (int32_t*)nullptr);
+#undef SSF_SOLVE_LAUNCH
     return hipGetLastError();
 }
 

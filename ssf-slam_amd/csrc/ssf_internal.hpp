@@ -42,8 +42,11 @@ constexpr int kBinChunk = SSF_BIN_CHUNK;   // points per binning work-group (204
                                            // thread; 4096 measured 11-12 % slower binning)
 constexpr int kMaxRows = 64;
 constexpr int kMaskMaxSplit = 32;          // work-groups per frame of the GMM fit at most
-// candidate bit arrays of a batch (k_curv / k_select): 64-bit words, per frame 8-byte aligned
-inline size_t cand_words(int64_t total, int n_frames) { return (size_t)((total >> 6) + n_frames + 2); }
+// candidate flag bytes of a batch (k_bin_curv -> k_select, one per ring position, per frame
+// 64-byte aligned) and the curvature fix-up lists (per-frame counts, then ring positions at the
+// frame offsets)
+size_t flag_bytes(int64_t total, int n_frames);
+size_t fix_bytes(int64_t total, int n_frames);
 
 // Per-correspondence record written by the association kernel, read by the solver.
 struct alignas(16) CorrRec {
@@ -54,12 +57,12 @@ struct alignas(16) CorrRec {
 
 // ---- launchers (features.hip) ----
 // Edge selection of launch_extract_planes (beyond the reference; nullptr = planes only):
-// the candidate bit array and the per-row selection slots in ctx scratch, the compacted edge
-// cloud (float4 x, y, z, intensity at the frame offsets) and per-frame counts out.
+// the per-row selection slots in ctx scratch, the compacted edge cloud (float4 x, y, z,
+// intensity at the frame offsets) and per-frame counts out (the candidates ride in bit 1 of
+// the planar flag bytes).
 struct EdgeSel {
     float min_curv;
     int span;
-    uint64_t* bits;
     int32_t* sel;
     float4* out;
     int32_t* count;
@@ -67,8 +70,8 @@ struct EdgeSel {
 hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_frames,
                                  const float* pts, int stride, const int64_t* frame_off,
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
-                                 int32_t* ring_off, float* ring_xyz, float4* ring_xyzi,
-                                 float* curv, uint64_t* bits, int32_t* sel, float4* plane,
+                                 int32_t* ring_off, int32_t* ring_idx, float4* ring_xyzi,
+                                 float* curv, uint8_t* flags, void* fix, int32_t* sel, float4* plane,
                                  int32_t* plane_count, const EdgeSel* edge = nullptr);
 
 // ---- launchers (registration.hip) ----

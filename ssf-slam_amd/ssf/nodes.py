@@ -89,7 +89,7 @@ def _single_batch(xyzi: torch.Tensor, device) -> PlaneBatch:
 
 
 class FrameFeatureNode:
-    """src/frameFeature.cpp cloudHandler on the device (k_bin_* / k_curv / k_select)."""
+    """src/frameFeature.cpp cloudHandler on the device (k_bin_count / k_bin_scan / k_bin_curv / k_select)."""
 
     def __init__(self, publish, n_rows: int = 64, device=None, frontend: Frontend | None = None):
         self.fe = frontend or Frontend(n_rows, device=device)

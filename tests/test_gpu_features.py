@@ -112,7 +112,7 @@ def test_chunk_and_scan_boundaries(oracle, dev):
 
 @pytest.mark.parametrize("n_rows,n_az", [(16, 2047), (16, 2048), (16, 2049), (16, 4500), (64, 4097)])
 def test_rows_across_curvature_tiles(oracle, dev, n_rows, n_az):
-    """k_curv streams the ring cloud in 2048-point chunks with an 8-point halo (a row spans
+    """k_bin_curv works on 2048-point input chunks with a halo of input points (a row spans
     several chunks, a chunk several rows) and k_select walks each row's candidate words: rows of
     one chunk exactly, one point over, 2-3 chunks, and the 16-beam span (3) whose selections cross
     every chunk and word edge; curvature bits and plane lists bit-exact vs the oracle"""
@@ -222,3 +222,53 @@ def test_masked_rows_with_0_1_2_points(oracle, dev):
         assert np.array_equal(pb.frame(f).cpu().numpy().view(np.uint32), ref.view(np.uint32)), f
     out, h2 = _run(fe, [pts[keep != 0]], dev)
     _check_frame(oracle, fe, out, h2, 0, pts[keep != 0], 64)
+
+
+def _planes_product(fe, clouds, dev):
+    """the product path (no debug outputs: k_bin_curv<false> / k_curv_fixup<false>)"""
+    import ssf
+    t = torch.from_numpy(np.ascontiguousarray(np.concatenate(clouds))).to(dev)
+    off, h_off = ssf.frame_offsets([c.shape[0] for c in clouds], dev)
+    pb = fe.extract_planes_batch(t, off, h_off)
+    return [pb.frame(f).cpu().numpy() for f in range(len(clouds))]
+
+
+def test_curvature_halo_and_fixup_orders(oracle, dev):
+    """k_bin_curv reads a stencil from its window (the chunk +- 384 input points) when the row
+    has 5 points on each side there, and leaves the rest to k_curv_fixup (taps through the ring
+    index).  Input orders that exercise every case: azimuth order with whole azimuth columns
+    missing in some rows (sparse rows: a few stencils open), row-major order (a chunk is one or
+    two rows: every stencil in the window), a fully shuffled frame (almost every stencil open),
+    and a frame whose first half is shuffled.  Debug outputs (curvature bits, ring cloud) and the
+    product path's plane lists, bit-exact vs the oracle."""
+    import ssf
+    O = oracle
+    base = frame(6, 2, n_az=1875)[0]
+    rid = O.ring_ids(base, 64)
+    rng = np.random.default_rng(5)
+    # sparse rows: rows 20..27 keep only 1 azimuth column in 9 (a row point every ~576 inputs)
+    drop = np.isin(rid, np.arange(20, 28)) & (rng.random(len(base)) < 8 / 9)
+    sparse = base[~drop]
+    rowmajor = base[np.argsort(rid, kind="stable")]
+    half = base.copy()
+    half[: len(half) // 2] = shuffled(half[: len(half) // 2], 9)
+    clouds = [sparse, rowmajor, shuffled(base, 4), half]
+    fe = ssf.Frontend(64, device=dev.index or 0)
+    out, h_off = _run(fe, clouds, dev)
+    for f, c in enumerate(clouds):
+        _check_frame(O, fe, out, h_off, f, c, 64)
+    got = _planes_product(fe, clouds, dev)
+    for f, c in enumerate(clouds):
+        assert np.array_equal(got[f].view(np.uint32), O.extract_planes(c, 64).view(np.uint32)), f
+
+
+def test_product_path_equals_debug_path(oracle, dev):
+    """the product instantiation (no ring cloud, no curvature out) selects the same planes as the
+    debug one, on a full 120k-point frame and a 16-beam frame, bit for bit (and both = oracle)"""
+    import ssf
+    for n_rows, n_az in [(64, 1875), (16, 4500)]:
+        c = frame(7, 3, n_rows=n_rows, n_az=n_az)[0]
+        fe = ssf.Frontend(n_rows, device=dev.index or 0)
+        got = _planes_product(fe, [c, c[: len(c) // 3]], dev)
+        assert np.array_equal(got[0].view(np.uint32), oracle.extract_planes(c, n_rows).view(np.uint32))
+        assert np.array_equal(got[1].view(np.uint32), oracle.extract_planes(c[: len(c) // 3], n_rows).view(np.uint32))

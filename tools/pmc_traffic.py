@@ -21,7 +21,7 @@ import csv
 import json
 from collections import defaultdict
 
-KERNELS = ("k_mask_pose", "k_bin_count", "k_bin_scan", "k_bin_scatter", "k_curv", "k_select",
+KERNELS = ("k_mask_pose", "k_bin_count", "k_bin_scan", "k_bin_curv", "k_select",
            "k_plane_table_sorted", "k_associate_strips", "k_associate_lds", "k_associate_sorted", "k_solve")
 
 

@@ -517,10 +517,15 @@ struct Split {
     uint32_t seq;              // exchanges done (uniform)
 };
 
-// SSF_MASK_XCHG_FENCES=1 (A/B only): an agent-scope release fence before the arrival add and an
-// agent-scope acquire after the poll, on top of the write-through form below.
+// The write-through form below matches a measured valid hand-off (MI355X_MICROARCH.md "Valid
+// forms", row 1), which the guide marks as measured on gfx950 / ROCm 7.2, not an architectural
+// guarantee.  So the exchange also carries the architectural pair: an agent-scope release fence
+// before the arrival add and an agent-scope acquire after the poll (round 3).  Cost,
+// same box A/B: configs[1] latency 0.554 -> 0.574 ms, configs[2] as written 4868 -> 4715
+// frames/s (tools/gpu/r3i.sh); B = 256 runs G = 1 and never exchanges.  -DSSF_MASK_XCHG_FENCES=0
+// drops the pair (A/B only).
 #ifndef SSF_MASK_XCHG_FENCES
-#define SSF_MASK_XCHG_FENCES 0
+#define SSF_MASK_XCHG_FENCES 1
 #endif
 
 // lane 0: wait until the frame's arrival counter reaches `target` (relaxed sc1 polls with

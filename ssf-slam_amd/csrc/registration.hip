@@ -25,10 +25,15 @@ namespace ssf {
 // qr_solve_5x3 (oracle/ssf_oracle.c), float, no FMA contraction.
 SSF_DEV float sqnorm_f(const float* v, int n) {
     float s = 0.0f;
+#pragma unroll
     for (int i = 0; i < n; ++i) s = s + v[i] * v[i];
     return s;
 }
 
+// Every loop is unrolled and every runtime index (the pivot column, the permutation, the rank)
+// is applied as a predicate on compile-time indices: the 5x3 system stays in registers (with
+// runtime indices it lived in scratch, ~90 B of private-memory traffic per plane point).  The
+// floating-point operations and their order are those of the oracle's loops.
 SSF_DEV void qr_solve_5x3(float m[3][5], float x[3]) {
     float hc[3] = {0.f, 0.f, 0.f};
     int tr[3] = {0, 1, 2};
@@ -36,49 +41,63 @@ SSF_DEV void qr_solve_5x3(float m[3][5], float x[3]) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) { nd[k] = sqrtf(sqnorm_f(m[k], 5)); nu[k] = nd[k]; }
     float mx = nu[0];
+#pragma unroll
     for (int k = 1; k < 3; ++k) if (nu[k] > mx) mx = nu[k];
     float th = mx * FLT_EPSILON;
     th = (th * th) / 5.0f;
     const float ndt = sqrtf(FLT_EPSILON);
     int nz = 3;
+#pragma unroll
     for (int k = 0; k < 3; ++k) {
         int bi = k;
         float bv = nu[k];
+#pragma unroll
         for (int j = k + 1; j < 3; ++j) if (nu[j] > bv) { bv = nu[j]; bi = j; }
         const float bsq = bv * bv;
         if (nz == 3 && bsq < th * (float)(5 - k)) nz = k;
         tr[k] = bi;
-        if (k != bi) {
-            for (int r = 0; r < 5; ++r) { float t = m[k][r]; m[k][r] = m[bi][r]; m[bi][r] = t; }
-            float t = nu[k]; nu[k] = nu[bi]; nu[bi] = t;
-            t = nd[k]; nd[k] = nd[bi]; nd[bi] = t;
+#pragma unroll
+        for (int j = k + 1; j < 3; ++j) {
+            if (j == bi) {
+#pragma unroll
+                for (int r = 0; r < 5; ++r) { float t = m[k][r]; m[k][r] = m[j][r]; m[j][r] = t; }
+                float t = nu[k]; nu[k] = nu[j]; nu[j] = t;
+                t = nd[k]; nd[k] = nd[j]; nd[j] = t;
+            }
         }
-        const int L = 5 - k;
+        constexpr int L0 = 5;
+        const int L = L0 - k;
         float* v = &m[k][k];
         const float tail = sqnorm_f(v + 1, L - 1);
         const float c0 = v[0];
         float beta, tau;
         if (tail <= FLT_MIN) {
             tau = 0.0f; beta = c0;
+#pragma unroll
             for (int i = 1; i < L; ++i) v[i] = 0.0f;
         } else {
             beta = sqrtf(c0 * c0 + tail);
             if (c0 >= 0.0f) beta = -beta;
             const float den = c0 - beta;
+#pragma unroll
             for (int i = 1; i < L; ++i) v[i] = v[i] / den;
             tau = (beta - c0) / beta;
         }
         hc[k] = tau;
         v[0] = beta;
         if (tau != 0.0f) {
+#pragma unroll
             for (int c = k + 1; c < 3; ++c) {
                 float tmp = 0.0f;
+#pragma unroll
                 for (int i = 1; i < L; ++i) tmp = tmp + v[i] * m[c][k + i];
                 tmp = tmp + m[c][k];
                 m[c][k] = m[c][k] - tau * tmp;
+#pragma unroll
                 for (int i = 1; i < L; ++i) m[c][k + i] = m[c][k + i] - (tau * v[i]) * tmp;
             }
         }
+#pragma unroll
         for (int j = k + 1; j < 3; ++j) {
             if (nu[j] != 0.0f) {
                 float t = fabsf(m[j][k]) / nu[j];
@@ -96,31 +115,48 @@ SSF_DEV void qr_solve_5x3(float m[3][5], float x[3]) {
         }
     }
     int perm[3] = {0, 1, 2};
-    for (int k = 0; k < 3; ++k) { int t = perm[k]; perm[k] = perm[tr[k]]; perm[tr[k]] = t; }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {                       // swap perm[k] and perm[tr[k]] (tr[k] >= k)
+        const int pk0 = perm[k];
+        int pt = pk0;
+#pragma unroll
+        for (int j = k; j < 3; ++j) if (j == tr[k]) pt = perm[j];
+#pragma unroll
+        for (int j = k; j < 3; ++j) if (j == tr[k]) perm[j] = pk0;
+        perm[k] = pt;
+    }
     x[0] = x[1] = x[2] = 0.0f;
     if (nz == 0) return;
     float c[5] = {-1.0f, -1.0f, -1.0f, -1.0f, -1.0f};
-    for (int k = 0; k < nz; ++k) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (k >= nz) break;
         const float tau = hc[k];
         const int L = 5 - k;
-        if (L == 1) {
-            c[k] = c[k] * (1.0f - tau);
-        } else if (tau != 0.0f) {
+        if (tau != 0.0f) {
             const float* v = &m[k][k];
             float tmp = 0.0f;
+#pragma unroll
             for (int i = 1; i < L; ++i) tmp = tmp + v[i] * c[k + i];
             tmp = tmp + c[k];
             c[k] = c[k] - tau * tmp;
+#pragma unroll
             for (int i = 1; i < L; ++i) c[k + i] = c[k + i] - (tau * v[i]) * tmp;
         }
     }
-    for (int i = nz - 1; i >= 0; --i) {
-        if (c[i] != 0.0f) {
+#pragma unroll
+    for (int i = 2; i >= 0; --i) {
+        if (i < nz && c[i] != 0.0f) {
             c[i] = c[i] / m[i][i];
-            for (int s = 0; s < i; ++s) c[s] = c[s] - c[i] * m[i][s];
+#pragma unroll
+            for (int s2 = 0; s2 < i; ++s2) c[s2] = c[s2] - c[i] * m[i][s2];
         }
     }
-    for (int i = 0; i < nz; ++i) x[perm[i]] = c[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int p2 = 0; p2 < 3; ++p2)
+            if (i < nz && perm[i] == p2) x[p2] = c[i];
 }
 
 constexpr int kKnnTile = 2048;
@@ -193,6 +229,7 @@ SSF_DEV void plane_from_knn(const float4* __restrict__ P, const double (&kk)[30]
     if (!(dn < 1.0f)) return;                                          // :207
     float Am[3][5];
     float pts[5][3];
+#pragma unroll
     for (int j = 0; j < 5; ++j) {
         const float4 p = P[v5[j]];
         pts[j][0] = p.x; pts[j][1] = p.y; pts[j][2] = p.z;
@@ -206,6 +243,7 @@ SSF_DEV void plane_from_knn(const float4* __restrict__ P, const double (&kk)[30]
         nrm[0] = nrm[0] / sq; nrm[1] = nrm[1] / sq; nrm[2] = nrm[2] / sq;
     }
     ok = 1;
+#pragma unroll
     for (int k = 0; k < 4; ++k) {                                      // :222-232
         const double vx = (double)(pts[k][0] - pts[k + 1][0]);
         const double vy = (double)(pts[k][1] - pts[k + 1][1]);
@@ -826,6 +864,7 @@ SSF_DEV void plane_from_pick(const float4* __restrict__ P, const int (&v5)[5], f
                              uint8_t& ok) {
     float Am[3][5];
     float pts[5][3];
+#pragma unroll
     for (int j = 0; j < 5; ++j) {
         const float4 p = P[v5[j]];
         pts[j][0] = p.x; pts[j][1] = p.y; pts[j][2] = p.z;
@@ -839,6 +878,7 @@ SSF_DEV void plane_from_pick(const float4* __restrict__ P, const int (&v5)[5], f
         nrm[0] = nrm[0] / sq; nrm[1] = nrm[1] / sq; nrm[2] = nrm[2] / sq;
     }
     ok = 1;
+#pragma unroll
     for (int k = 0; k < 4; ++k) {                                      // :222-232
         const double vx = (double)(pts[k][0] - pts[k + 1][0]);
         const double vy = (double)(pts[k][1] - pts[k + 1][1]);

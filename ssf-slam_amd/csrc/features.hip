@@ -214,7 +214,7 @@ __global__ __launch_bounds__(256) void k_bin_curv(const float* __restrict__ pts,
                                                   int32_t* __restrict__ fix, uint32_t* __restrict__ fix_count,
                                                   float4* __restrict__ out4, float* __restrict__ curv) {
     __shared__ __attribute__((aligned(16))) float sc[kTileE + 2 * kTilePad];   // x, then y, then z
-    __shared__ uint32_t meta[kTileE];
+    __shared__ __attribute__((aligned(16))) uint32_t meta[kTileE];
     __shared__ uint16_t wpos[kTileE];
     __shared__ int wrun[4][kMaxRows];
     __shared__ int nb[kMaxRows];                  // halo-before points per row
@@ -252,13 +252,13 @@ __global__ __launch_bounds__(256) void k_bin_curv(const float* __restrict__ pts,
     int idr[kWinQ];
     float px[kWinQ], py[kWinQ], pz[kWinQ];
 #pragma unroll
-    for (int st = 0; st < kWinQ; ++st) {
-        const int p = q0 + lane + 64 * st;
-        idr[st] = (p < q1) ? (int)rid[ws + p] : -1;
-    }
+    for (int st = 0; st < kWinQ; ++st) idr[st] = (int)rid[ws + min(q0 + lane + 64 * st, L - 1)];   // clamped: no branch
+#pragma unroll
+    for (int st = 0; st < kWinQ; ++st) if (q0 + lane + 64 * st >= q1) idr[st] = -1;
+    const float* pw = pts + ws * stride;                     // the window's first point
 #pragma unroll
     for (int st = 0; st < kWinQ; ++st) {
-        const float* pp = pts + (ws + min(q0 + lane + 64 * st, L - 1)) * stride;
+        const float* pp = pw + (uint32_t)(min(q0 + lane + 64 * st, L - 1) * stride);   // < 2^32 floats
         px[st] = pp[0]; py[st] = pp[1]; pz[st] = pp[2];
     }
 #pragma unroll
@@ -366,7 +366,10 @@ __global__ __launch_bounds__(256) void k_bin_curv(const float* __restrict__ pts,
     }
     uint32_t mt[kCE];
 #pragma unroll
-    for (int i = 0; i < kCE; ++i) mt[i] = meta[min(k0 + i, kTileE - 1)];
+    for (int i = 0; i < kCE; i += 4) {                       // k0 + kCE <= kTileE: 3 ds_read_b128
+        const uint4 m4 = *reinterpret_cast<const uint4*>(meta + k0 + i);
+        mt[i] = m4.x; mt[i + 1] = m4.y; mt[i + 2] = m4.z; mt[i + 3] = m4.w;
+    }
     uint32_t fixm = 0;                                       // open stencils (bit i)
 #pragma unroll
     for (int i = 0; i < kCE; ++i) {

@@ -1660,7 +1660,10 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     int lds_cap) {
     extern __shared__ float4 SL[];                  // [ml] strip-major, x-sorted in each strip
     __shared__ StripLds T;
+    // gridDim.y work-groups per pair (few pairs in a launch): each stages the whole last frame
+    // and answers every gridDim.y-th block of kStripThreads queries
     const int p = blockIdx.x, tid = threadIdx.x;
+    const int q0 = tid + (int)blockIdx.y * kStripThreads, qstep = kStripThreads * (int)gridDim.y;
     const int mc = curr_count[p], ml = last_count[p];
     if (mc <= 0 || ml <= 10) return;                                    // uniform (:158)
     const int64_t lo = last_off[p], co = curr_off[p];
@@ -1671,7 +1674,7 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     const float4* L = last + lo;
     if (ml > lds_cap) {                                                 // uniform
         const PtsF4 g{SP, SI};
-        for (int i = tid; i < mc; i += kStripThreads) {
+        for (int i = q0; i < mc; i += qstep) {
             const float4 pc = curr[co + i];
             const float4 qs = assoc_query_point(pc, q, t);
             float best = __builtin_inff();
@@ -1689,7 +1692,8 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     const int ns = geo.ns;
     auto strip_of = [&](float y) { return geo.strip_of(y); };
     const StripView<kSoa> v{SL, SX, SI16, ml};
-    for (int i = tid; i < mc; i += kStripThreads) {
+    if (q0 >= mc) return;                                               // (after the barriers of the build)
+    for (int i = q0; i < mc; i += qstep) {
         const float4 pc = curr[co + i];
         const float4 qs = assoc_query_point(pc, q, t);
         float best = __builtin_inff();
@@ -2546,9 +2550,14 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
             const bool soa = max_m > kAssocStripF4Max;
             const int cap = (int)std::min<int64_t>(max_m, soa ? kAssocStripSoaMax : kAssocStripF4Max);
             const size_t lds = soa ? (size_t)cap * 14 + 16 : (size_t)cap * sizeof(float4);
+            // few pairs (a node's one pair, configs[2]'s chained pairs): up to 8 work-groups per
+            // pair, each staging the last frame and taking a share of the queries, so the launch
+            // spreads over ~256 CUs instead of n_pairs
+            const int qsplit = (int)std::max<int64_t>(1, std::min<int64_t>({8, 256 / n_pairs,
+                                                                 (max_m + kStripThreads - 1) / kStripThreads}));
             kmark(s, soa ? "k_associate_strips_soa" : "k_associate_strips");
             hipLaunchKernelGGL(soa ? k_associate_strips<true> : k_associate_strips<false>,
-                               dim3(n_pairs), dim3(kStripThreads), lds, s, last, last_off, last_count,
+                               dim3(n_pairs, qsplit), dim3(kStripThreads), lds, s, last, last_off, last_count,
                                last_normal, last_valid, last_sorted, last_sidx, curr, curr_off,
                                curr_count, pose_rel, corr, nn, cap);
         } else

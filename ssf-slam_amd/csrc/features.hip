@@ -145,7 +145,7 @@ __global__ __launch_bounds__(64) void k_bin_scan(int n_rows, int n_chunks, int32
 // neighbours in its row's run of the tile -- whenever the run holds 5 points on each side of it.
 // With a 64-beam scan in azimuth order a row has a point every 64 inputs, so 384 halo points
 // hold 6 per row; a stencil the halo does not cover goes to the frame's fix-up list (k_select).
-//   rank   waves own contiguous quarters of the window; a 7-ballot match on the row id ranks a
+//   rank   waves own contiguous parts of the window; a 7-ballot match on the row id ranks a
 //          point among same-row lanes, a wave-private running count per row among the wave's
 //          points, the per-wave counts are prefixed (waves in order, then rows): the tile
 //          position.  Halo-before points per row are counted on the side (LDS adds).
@@ -171,14 +171,22 @@ __global__ __launch_bounds__(64) void k_bin_scan(int n_rows, int n_chunks, int32
 #ifndef SSF_CURV_HALO
 #define SSF_CURV_HALO 384
 #endif
+#ifndef SSF_CURV_SUB
+#define SSF_CURV_SUB 1
+#endif
 constexpr int kCurvHalo = SSF_CURV_HALO;                 // multiple of 64, <= kBinChunk
-constexpr int kWin = kBinChunk + 2 * kCurvHalo;          // window points at most
-constexpr int kWinQ = ((kWin + 3) / 4 + 63) / 64;        // 64-point steps per wave quarter
-constexpr int kCE = ((kWin + 255) / 256 + 3) & ~3;       // tile entries per thread (12)
-constexpr int kTileE = kCE * 256;                        // tile entries (>= kWin)
+constexpr int kCurvSub = SSF_CURV_SUB;                   // binning chunks per work-group
+constexpr int kCurvNT = 256 * kCurvSub;                  // threads per work-group
+constexpr int kCurvNW = kCurvNT / 64;
+constexpr int kCurvOwn = kBinChunk * kCurvSub;           // chunk points per work-group
+constexpr int kWin = kCurvOwn + 2 * kCurvHalo;           // window points at most
+constexpr int kWinQ = ((kWin + kCurvNW - 1) / kCurvNW + 63) / 64;   // 64-point steps per wave part
+constexpr int kCE = ((kWin + kCurvNT - 1) / kCurvNT + 3) & ~3;      // tile entries per thread (12)
+constexpr int kTileE = kCE * kCurvNT;                    // tile entries (>= kWin)
 constexpr int kTilePad = 8;
 static_assert(kCurvHalo % 64 == 0 && kCurvHalo <= kBinChunk, "halo");
-static_assert(kWin < 4096, "window positions and run lengths use 12 bits");
+static_assert(kWin < 4096 || kCurvSub > 1, "");
+static_assert(kWin < 8192, "window positions and run lengths use 13 bits");
 // tile entry classes (meta bits 24..25)
 constexpr uint32_t kClsHalo = 0, kClsStencil = 1, kClsZero = 2, kClsOpen = 3;
 
@@ -201,7 +209,7 @@ SSF_DEV uint8_t cand_flags(bool row_in, bool inner, float v, float plane_min, bo
 }
 
 template <bool kDebug, bool kEdge>
-__global__ __launch_bounds__(256) void k_bin_curv(const float* __restrict__ pts, int stride,
+__global__ __launch_bounds__(kCurvNT) void k_bin_curv(const float* __restrict__ pts, int stride,
                                                   const int64_t* __restrict__ frame_off,
                                                   int n_frames, int n_rows, int n_chunks,
                                                   int row_start, int row_end, float plane_min,
@@ -216,26 +224,28 @@ __global__ __launch_bounds__(256) void k_bin_curv(const float* __restrict__ pts,
     __shared__ __attribute__((aligned(16))) float sc[kTileE + 2 * kTilePad];   // x, then y, then z
     __shared__ __attribute__((aligned(16))) uint32_t meta[kTileE];
     __shared__ uint16_t wpos[kTileE];
-    __shared__ int wrun[4][kMaxRows];
+    __shared__ int wrun[kCurvNW][kMaxRows];
     __shared__ int nb[kMaxRows];                  // halo-before points per row
     __shared__ int4 rinfo[kMaxRows];              // {run offset | run length << 12, cb - nb, ring offset, n_r}
     __shared__ int ntot;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     // XCD-aware logical block (see above)
-    const int64_t nblk = (int64_t)n_chunks * n_frames;
+    const int nc2 = (n_chunks + kCurvSub - 1) / kCurvSub;      // work-group chunks per frame
+    const int64_t nblk = (int64_t)nc2 * n_frames;
     const int64_t q8 = (nblk + 7) / 8;
     const int64_t lb = (int64_t)(blockIdx.x % 8) * q8 + blockIdx.x / 8;
     if (lb >= nblk) return;
-    const int f = (int)(lb / n_chunks), c = (int)(lb - (int64_t)f * n_chunks);
+    const int f = (int)(lb / nc2), c = (int)(lb - (int64_t)f * nc2) * kCurvSub;   // first binning chunk
     const int64_t fb = frame_off[f], e = frame_off[f + 1];
     const int64_t s = fb + (int64_t)c * kBinChunk;
     if (s >= e) return;                           // uniform
-    const int64_t t = min(e, s + (int64_t)kBinChunk);
+    const int64_t t = min(e, s + (int64_t)kCurvOwn);
     const int64_t ws = max(fb, s - (int64_t)kCurvHalo), we = min(e, t + (int64_t)kCurvHalo);
     const int L = (int)(we - ws), hb = (int)(s - ws), he = (int)(t - ws);   // own: [hb, he)
-    const int qlen = ((L + 3) / 4 + 63) / 64 * 64;                          // <= 64 kWinQ
+    const int qlen = ((L + kCurvNW - 1) / kCurvNW + 63) / 64 * 64;        // <= 64 kWinQ
     if (tid < kMaxRows) {
-        wrun[0][tid] = wrun[1][tid] = wrun[2][tid] = wrun[3][tid] = 0;
+#pragma unroll
+        for (int k = 0; k < kCurvNW; ++k) wrun[k][tid] = 0;
         nb[tid] = 0;
     }
     // the rows' chunk bases and ring offsets, loaded now by wave 0 (used after the ranking):
@@ -287,7 +297,7 @@ __global__ __launch_bounds__(256) void k_bin_curv(const float* __restrict__ pts,
         int tot = 0;
         if (r < n_rows) {
             int acc = 0;
-            for (int k = 0; k < 4; ++k) { const int v = wrun[k][r]; wrun[k][r] = acc; acc += v; }
+            for (int k = 0; k < kCurvNW; ++k) { const int v = wrun[k][r]; wrun[k][r] = acc; acc += v; }
             tot = acc;
         }
         int incl = tot;
@@ -296,7 +306,7 @@ __global__ __launch_bounds__(256) void k_bin_curv(const float* __restrict__ pts,
             const int y = __shfl_up(incl, o, 64);
             if (r >= o) incl += y;
         }
-        if (r < n_rows) rinfo[r] = make_int4((incl - tot) | (tot << 12), cbr - nb[r], ro0, ro1 - ro0);
+        if (r < n_rows) rinfo[r] = make_int4((incl - tot) | (tot << 13), cbr - nb[r], ro0, ro1 - ro0);
         if (r == 63) ntot = incl;
     }
     __syncthreads();
@@ -310,10 +320,10 @@ __global__ __launch_bounds__(256) void k_bin_curv(const float* __restrict__ pts,
         if (id >= 0) {
             const int4 ri = rinfo[id];
             const int p = wrun[w][id] + (idr[st] >> 8);      // position in the row's window run
-            const int k = (ri.x & 0xfff) + p;
+            const int k = (ri.x & 0x1fff) + p;
             const int j = ri.y + p;                          // row-relative ring index
             const int wp = q0 + lane + 64 * st;
-            const int nr = ri.w, wl = ri.x >> 12;
+            const int nr = ri.w, wl = ri.x >> 13;
             const bool own = wp >= hb && wp < he;
             const bool row_in = id >= row_start && id < n_rows - row_end;
             const bool inner = j >= 5 && j < nr - 5;
@@ -405,7 +415,7 @@ __global__ __launch_bounds__(256) void k_bin_curv(const float* __restrict__ pts,
     const int64_t fl0 = flag_base(frame_off, f);
     const int32_t ib = (int32_t)(ws - fb);
 #pragma unroll 4
-    for (int k = tid; k < nt; k += 256) {
+    for (int k = tid; k < nt; k += kCurvNT) {
         const uint32_t mk = meta[k];
         const int wp = wpos[k];
         if (((mk >> 24) & 3u) == kClsHalo) continue;
@@ -624,11 +634,11 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
     const bool dbg = curv != nullptr || ring_xyzi != nullptr;
     const float emin = edge ? edge->min_curv : 0.f;
     if (n_chunks > 0) {
-        const int64_t nblk = (int64_t)n_chunks * n_frames;
+        const int64_t nblk = (int64_t)((n_chunks + kCurvSub - 1) / kCurvSub) * n_frames;
         const dim3 grid((unsigned)((nblk + 7) / 8 * 8));
         kmark(s, "k_bin_curv");
 #define SSF_BC_LAUNCH(D, E)                                                                        \
-        hipLaunchKernelGGL((k_bin_curv<D, E>), grid, dim3(256), 0, s, pts, stride, frame_off,       \
+        hipLaunchKernelGGL((k_bin_curv<D, E>), grid, dim3(kCurvNT), 0, s, pts, stride, frame_off,       \
                            n_frames, R, n_chunks, cfg.row_start, cfg.row_end, cfg.plane_min, emin,  \
                            rid, hist, ring_off, ring_idx, flags, fixl, fix_count, ring_xyzi, curv)
         if (edge) { if (dbg) SSF_BC_LAUNCH(true, true); else SSF_BC_LAUNCH(false, true); }

@@ -41,7 +41,10 @@ void kmark(hipStream_t s, const char* name);
 constexpr int kBinChunk = SSF_BIN_CHUNK;   // points per binning work-group (2048: 8 points per
                                            // thread; 4096 measured 11-12 % slower binning)
 constexpr int kMaxRows = 64;
-constexpr int kMaskMaxSplit = 32;          // work-groups per frame of the GMM fit at most
+#ifndef SSF_MASK_MAX_SPLIT
+#define SSF_MASK_MAX_SPLIT 32
+#endif
+constexpr int kMaskMaxSplit = SSF_MASK_MAX_SPLIT;   // work-groups per frame of the GMM fit at most
 // candidate flag bytes of a batch (k_bin_curv -> k_select, one per ring position, per frame
 // 64-byte aligned) and the curvature fix-up lists (per-frame counts, then ring positions at the
 // frame offsets)

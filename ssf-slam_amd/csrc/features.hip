@@ -145,7 +145,7 @@ __global__ __launch_bounds__(64) void k_bin_scan(int n_rows, int n_chunks, int32
 // neighbours in its row's run of the tile -- whenever the run holds 5 points on each side of it.
 // With a 64-beam scan in azimuth order a row has a point every 64 inputs, so 384 halo points
 // hold 6 per row; a stencil the halo does not cover goes to the frame's fix-up list (k_select).
-//   rank   waves own contiguous parts of the window; a 7-ballot match on the row id ranks a
+//   rank   waves own contiguous parts of the window; a per-row lane word (LDS OR) ranks a
 //          point among same-row lanes, a wave-private running count per row among the wave's
 //          points, the per-wave counts are prefixed (waves in order, then rows): the tile
 //          position.  Halo-before points per row are counted on the side (LDS adds).
@@ -224,9 +224,15 @@ __global__ __launch_bounds__(kCurvNT) void k_bin_curv(const float* __restrict__ 
     __shared__ __attribute__((aligned(16))) float sc[kTileE + 2 * kTilePad];   // x, then y, then z
     __shared__ __attribute__((aligned(16))) uint32_t meta[kTileE];
     __shared__ uint16_t wpos[kTileE];
-    __shared__ int wrun[kCurvNW][kMaxRows];
+    __shared__ int wrun[kCurvNW][kMaxRows + 1];   // (+1: the slot of points in no row)
+    __shared__ unsigned long long gmask[kCurvNW][kMaxRows + 1];   // a step's lanes per row (rank)
     __shared__ int nb[kMaxRows];                  // halo-before points per row
-    __shared__ int4 rinfo[kMaxRows];              // {run offset | run length << 12, cb - nb, ring offset, n_r}
+    // per (wave, row), in the rank space of the wave's points of that row: tile slot base, ring
+    // position base, the ranks whose centre is in [5, n_r - 5) of a row in range (inner), and the
+    // ranks whose 11 taps the window holds (covered)
+    __shared__ int4 wrec[kCurvNW][kMaxRows];      // {k base, ring base, inner lo, inner hi}
+    __shared__ int2 wcov[kCurvNW][kMaxRows];      // {covered lo, covered hi}
+    __shared__ int4 rinfo[kMaxRows];              // debug: {run offset, cb - nb, ring offset, n_r}
     __shared__ int ntot;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     // XCD-aware logical block (see above)
@@ -245,9 +251,10 @@ __global__ __launch_bounds__(kCurvNT) void k_bin_curv(const float* __restrict__ 
     const int qlen = ((L + kCurvNW - 1) / kCurvNW + 63) / 64 * 64;        // <= 64 kWinQ
     if (tid < kMaxRows) {
 #pragma unroll
-        for (int k = 0; k < kCurvNW; ++k) wrun[k][tid] = 0;
+        for (int k = 0; k < kCurvNW; ++k) { wrun[k][tid] = 0; gmask[k][tid] = 0ull; }
         nb[tid] = 0;
     }
+    if (tid < kCurvNW) { wrun[tid][kMaxRows] = 0; gmask[tid][kMaxRows] = 0ull; }
     // the rows' chunk bases and ring offsets, loaded now by wave 0 (used after the ranking):
     // their latency hides behind the point loads instead of stalling the work-group later
     int cbr = 0, ro0 = 0, ro1 = 0;
@@ -271,25 +278,27 @@ __global__ __launch_bounds__(kCurvNT) void k_bin_curv(const float* __restrict__ 
         const float* pp = pw + (uint32_t)(min(q0 + lane + 64 * st, L - 1) * stride);   // < 2^32 floats
         px[st] = pp[0]; py[st] = pp[1]; pz[st] = pp[2];
     }
+    // same-row lanes of a step: every lane ORs its bit into its row's 64-bit word of the wave
+    // (ds_or_b64), reads the word back (the wave's LDS instructions complete in order, so every
+    // OR of the step is in), ranks itself by the lanes below it, and the row's first lane clears
+    // the word for the next step -- exact and order-free (OR commutes); the 6-bit ballot match it
+    // replaces cost ~45 VALU instructions per step
 #pragma unroll
     for (int st = 0; st < kWinQ; ++st) {
         const int id = idr[st];
-        uint64_t m = __ballot(id >= 0);
-#pragma unroll
-        for (int bit = 0; bit < 6; ++bit) {
-            const bool on = (id >> bit) & 1;
-            const uint64_t bb = __ballot(on);
-            m &= on ? bb : ~bb;
-        }
+        const int rs = id >= 0 ? id : kMaxRows;              // points in no row: a spare slot
+        unsigned long long* gm = &gmask[w][rs];
+        __hip_atomic_fetch_or(gm, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint64_t m = __hip_atomic_load(gm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const int rin = __popcll(m & lanemask_lt());
-        int rank = 0;
-        if (id >= 0) {
-            const int before = wrun[w][id];                  // read by every lane first,
-            rank = before + rin;
-            if (rin == 0) wrun[w][id] = before + __popcll(m);   // then the group leader adds
-            if (q0 + lane + 64 * st < hb) atomicAdd(&nb[id], 1);
+        const int before = wrun[w][rs];                      // read by every lane first,
+        if (rin == 0) {                                      // then the group leader adds, clears
+            wrun[w][rs] = before + __popcll(m);
+            __hip_atomic_store(gm, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        idr[st] = (id & 0xff) | (rank << 8);
+        if (q0 + 64 * st < hb)                               // uniform: a step with halo-before points
+            if (id >= 0 && q0 + lane + 64 * st < hb) atomicAdd(&nb[id], 1);
+        idr[st] = (id & 0xff) | ((before + rin) << 8);       // rank among the wave's row points
     }
     __syncthreads();
     if (tid < 64) {                                          // rows on the lanes of wave 0
@@ -306,37 +315,50 @@ __global__ __launch_bounds__(kCurvNT) void k_bin_curv(const float* __restrict__ 
             const int y = __shfl_up(incl, o, 64);
             if (r >= o) incl += y;
         }
-        if (r < n_rows) rinfo[r] = make_int4((incl - tot) | (tot << 13), cbr - nb[r], ro0, ro1 - ro0);
+        if (r < n_rows) {
+            const int run0 = incl - tot, jb = cbr - nb[r], nr = ro1 - ro0;
+            const bool row_in = r >= row_start && r < n_rows - row_end;
+            if (kDebug) rinfo[r] = make_int4(run0, jb, ro0, nr);
+#pragma unroll
+            for (int k = 0; k < kCurvNW; ++k) {
+                const int pw = wrun[k][r];                   // the wave's first position in the run
+                // rank q of wave k: run position p = pw + q, row index j = jb + pw + q
+                wrec[k][r] = make_int4(run0 + pw, ro0 + jb + pw,
+                                       row_in ? 5 - jb - pw : 0, row_in ? nr - 5 - jb - pw : 0);
+                wcov[k][r] = make_int2(5 - pw, tot - 5 - pw);
+            }
+        }
         if (r == 63) ntot = incl;
     }
     __syncthreads();
     const int nt = ntot;                                     // kept points in the window
     // ---- place: tile slot, ring position and class of every point; x into the tile
     int loc[kWinQ];
+    // flags of a chunk point whose curvature is 0 (row in range, j outside [5, n_r - 5): :85)
+    const uint32_t flz = (uint32_t)cand_flags(true, false, 0.0f, plane_min, kEdge, edge_min);
 #pragma unroll
     for (int st = 0; st < kWinQ; ++st) {
         const int id = (int)(int8_t)(idr[st] & 0xff);
         loc[st] = kTileE;                                    // no point: the pad slot
         if (id >= 0) {
-            const int4 ri = rinfo[id];
-            const int p = wrun[w][id] + (idr[st] >> 8);      // position in the row's window run
-            const int k = (ri.x & 0x1fff) + p;
-            const int j = ri.y + p;                          // row-relative ring index
+            const int q = idr[st] >> 8;                      // rank among the wave's row points
+            const int4 rw = wrec[w][id];
+            const int2 cv = wcov[w][id];
+            const int k = rw.x + q;
             const int wp = q0 + lane + 64 * st;
-            const int nr = ri.w, wl = ri.x >> 13;
             const bool own = wp >= hb && wp < he;
+            const bool inner = q >= rw.z && q < rw.w;        // row in range, centre in [5, n_r - 5)
+            const bool covered = q >= cv.x && q < cv.y;
             const bool row_in = id >= row_start && id < n_rows - row_end;
-            const bool inner = j >= 5 && j < nr - 5;
-            const bool covered = p >= 5 && p + 5 < wl;
-            const uint32_t cls = !own ? kClsHalo : !(row_in && inner) ? kClsZero : covered ? kClsStencil : kClsOpen;
-            // curvature-0 points: the flags now (:85 leaves their curvature at 0)
-            const uint32_t fl = cls == kClsZero ? (uint32_t)cand_flags(row_in, false, 0.0f, plane_min, kEdge, edge_min) : 0u;
-            meta[k] = (uint32_t)(ri.z + j) | (cls << 24) | (fl << 26);
+            const uint32_t cls = !own ? kClsHalo : !inner ? kClsZero : covered ? kClsStencil : kClsOpen;
+            const uint32_t fl = cls == kClsZero && row_in ? flz : 0u;
+            meta[k] = (uint32_t)(rw.y + q) | (cls << 24) | (fl << 26);
             wpos[k] = (uint16_t)wp;
             sc[kTilePad + k] = px[st];
             loc[st] = k;
             if (kDebug && own) {
-                const int64_t g = fb + ri.z + j;
+                const int j = rw.y + q - rinfo[id].z;
+                const int64_t g = fb + rw.y + q;
                 if (out4) out4[g] = make_float4(px[st], py[st], pz[st], (float)((double)j + (double)id / 100.0));
                 if (curv && cls == kClsZero) curv[g] = 0.0f;
             }
@@ -391,7 +413,8 @@ __global__ __launch_bounds__(kCurvNT) void k_bin_curv(const float* __restrict__ 
         }
         fixm |= (k0 + i < nt && cls == kClsOpen) ? 1u << i : 0u;
     }
-    // fix-up list (rare): wave-aggregated reservation
+    // fix-up list (rare): wave-aggregated reservation, skipped by a wave with no open stencil
+    if (__ballot(fixm != 0u)) {                              // wave-uniform
     const int nfx = __popc(fixm);
     int incl = nfx;
 #pragma unroll
@@ -400,7 +423,7 @@ __global__ __launch_bounds__(kCurvNT) void k_bin_curv(const float* __restrict__ 
         if (lane >= o) incl += y;
     }
     const int wtot = __shfl(incl, 63, 64);
-    if (wtot > 0) {                                          // wave-uniform
+    {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(&fix_count[f], (uint32_t)wtot);
         base = __shfl(base, 0, 64) + (uint32_t)(incl - nfx);
@@ -409,6 +432,7 @@ __global__ __launch_bounds__(kCurvNT) void k_bin_curv(const float* __restrict__ 
             fixm &= fixm - 1u;
             fix[fb + base++] = (int32_t)(mt[i] & 0xFFFFFFu);
         }
+    }
     }
     __syncthreads();
     // ---- chunk points out, in tile order (contiguous per-row runs of ring positions)

@@ -331,7 +331,7 @@ class Pipeline:
             # the plane batch and its table are read on s_reg in this step and the next: keep
             # the caching allocator from handing their blocks to s_feat until s_reg is done
             extra = (eb.xyzi, eb.count, *etable) if a.edges else ()
-            for t in (pb.xyzi, pb.count, *[x for x in table if isinstance(x, torch.Tensor)], *extra):
+            for t in (pb.xyzi, pb.count, *table.tensors(), *extra):
                 t.record_stream(s_reg)
         stats = None
         with torch.cuda.stream(s_reg):
@@ -674,7 +674,7 @@ def consecutive(args):
             tdone = torch.cuda.Event()
             tdone.record(s_feat)
         s_reg.wait_event(tdone)
-        for t in (pb.xyzi, pb.count, *[x for x in table if isinstance(x, torch.Tensor)]):
+        for t in (pb.xyzi, pb.count, *table.tensors()):
             t.record_stream(s_reg)
         with torch.cuda.stream(s_reg):
             for kk in range(K):

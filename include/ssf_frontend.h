@@ -132,13 +132,18 @@ int32_t ssf_extract_planes(ssf_ctx* ctx, void* stream, const float* d_pts, int64
  *             ssf_register_batch when this frame is the last frame.  When they are NULL, or
  *             max_plane_points exceeds SSF_SORTED_MAX, both calls fall back to brute-force k-NN.
  *             Use the same max_plane_points bound for a frame's table and its registration.
+ *   d_strip_xyzi / d_strip_head  out (nullable, both or neither; needs the sorted buffers):
+ *             float32 x4 and int32 per plane point (frame offsets).  The table's y-strip image of
+ *             the frame (the association's search structure), kept so that ssf_register_batch
+ *             stages it instead of rebuilding it when this frame is the last frame.  Frames of
+ *             773..6144 plane points carry an image; others are rebuilt as before.
  */
 #define SSF_SORTED_MAX 16384
 int32_t ssf_plane_table_batch(ssf_ctx* ctx, void* stream, int32_t n_frames,
                               const float* d_plane_xyzi, const int64_t* d_frame_off,
                               const int32_t* d_plane_count, int64_t max_plane_points,
                               float* d_normal, uint8_t* d_valid, float* d_sorted_xyzi,
-                              int32_t* d_sorted_idx);
+                              int32_t* d_sorted_idx, float* d_strip_xyzi, int32_t* d_strip_head);
 
 /* ---------------------------------------------------------------------------------------
  * lidarOdometry_onlyPC: replaces frameRegistration() (src/lidarOdometry_onlyPC.cpp:147-252)
@@ -155,6 +160,9 @@ int32_t ssf_plane_table_batch(ssf_ctx* ctx, void* stream, int32_t n_frames,
  *   d_log      nullable [P*max_iter*10] doubles per iteration: q(4) t(3) cost status radius
  *   d_nlog     nullable [P] iterations logged;  d_ncorr nullable [P] correspondences used
  *              (-1 when skipped);  d_nn nullable: per curr point 1-NN index into last.
+ *   d_last_strip_xyzi / d_last_strip_head  nullable (both or neither): the strip image the
+ *              last frames' ssf_plane_table_batch call wrote (same max_plane_points).  The results
+ *              are identical with or without it; with it the association skips its strip build.
  */
 int32_t ssf_register_batch(ssf_ctx* ctx, void* stream, int32_t n_pairs,
                            const float* d_last_xyzi, const int64_t* d_last_off,
@@ -164,7 +172,8 @@ int32_t ssf_register_batch(ssf_ctx* ctx, void* stream, int32_t n_pairs,
                            const int64_t* d_curr_off, const int32_t* d_curr_count,
                            int64_t curr_total_points, int64_t max_plane_points,
                            double* d_pose_rel, double* d_pose_abs,
-                           double* d_log, int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_nn);
+                           double* d_log, int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_nn,
+                           const float* d_last_strip_xyzi, const int32_t* d_last_strip_head);
 
 /* Single-pair form with the SURVEY §8(b) signature: frameRegistration() on the globals
  * lastFramePlanePtr / currFramePlanePtr / para_q / para_t (src/lidarOdometry_onlyPC.cpp:51-71,
@@ -242,7 +251,8 @@ int32_t ssf_edge_table_batch(ssf_ctx* ctx, void* stream, int32_t n_frames,
                              const int32_t* d_edge_count, int64_t max_edge_points,
                              float* d_line, uint8_t* d_line_valid);
 /* ssf_register_batch with point-to-line blocks added to every pair's problem (same LM/GN loop,
- * same pose / log outputs).  Edge clouds at their own offsets; d_ncorr_edge nullable [P]. */
+ * same pose / log outputs).  Edge clouds at their own offsets; d_ncorr_edge nullable [P]; the
+ * strip image as in ssf_register_batch. */
 int32_t ssf_register_batch_edges(ssf_ctx* ctx, void* stream, int32_t n_pairs,
                                  const float* d_last_xyzi, const int64_t* d_last_off,
                                  const int32_t* d_last_count, const float* d_last_normal,
@@ -256,7 +266,8 @@ int32_t ssf_register_batch_edges(ssf_ctx* ctx, void* stream, int32_t n_pairs,
                                  const int64_t* d_curr_edge_off, const int32_t* d_curr_edge_count,
                                  int64_t curr_edge_total, int64_t max_edge_points,
                                  double* d_pose_rel, double* d_pose_abs, double* d_log,
-                                 int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_ncorr_edge);
+                                 int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_ncorr_edge,
+                                 const float* d_last_strip_xyzi, const int32_t* d_last_strip_head);
 
 /* ---------------------------------------------------------------------------------------
  * PointCloudOdometry{,_noSeg}.py: replaces the dynamic-point mask + slove_RT_by_SVD + Quaternion

@@ -461,18 +461,22 @@ int32_t ssf_extract_planes(ssf_ctx* c, void* stream, const float* d_pts, int64_t
 int32_t ssf_plane_table_batch(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_plane_xyzi,
                               const int64_t* d_frame_off, const int32_t* d_plane_count,
                               int64_t max_plane_points, float* d_normal, uint8_t* d_valid,
-                              float* d_sorted_xyzi, int32_t* d_sorted_idx) {
+                              float* d_sorted_xyzi, int32_t* d_sorted_idx, float* d_strip_xyzi,
+                              int32_t* d_strip_head) {
     if (!c) return SSF_E_ARG;
     if (n_frames < 0 || max_plane_points < 0 ||
         (n_frames > 0 && (!d_plane_xyzi || !d_frame_off || !d_plane_count || !d_normal || !d_valid)))
         return fail(c, SSF_E_ARG, "plane_table_batch: bad arguments");
+    if (!d_strip_xyzi != !d_strip_head || (d_strip_xyzi && (!d_sorted_xyzi || !d_sorted_idx)))
+        return fail(c, SSF_E_ARG, "plane_table_batch: the strip image needs both strip buffers and the sorted buffers");
     if (n_frames == 0) return SSF_OK;
     SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
     ProfScope prof(c, stream);
     hipError_t e = ssf::launch_plane_table((hipStream_t)stream, c->cfg, n_frames,
                                            reinterpret_cast<const float4*>(d_plane_xyzi), d_frame_off,
                                            d_plane_count, max_plane_points, d_normal, d_valid,
-                                           reinterpret_cast<float4*>(d_sorted_xyzi), d_sorted_idx);
+                                           reinterpret_cast<float4*>(d_sorted_xyzi), d_sorted_idx,
+                                           reinterpret_cast<float4*>(d_strip_xyzi), d_strip_head);
     if (e != hipSuccess) return hip_fail(c, e, "plane_table launch");
     return SSF_OK;
 }
@@ -484,12 +488,16 @@ int32_t ssf_register_batch(ssf_ctx* c, void* stream, int32_t n_pairs, const floa
                            const float* d_curr_xyzi, const int64_t* d_curr_off,
                            const int32_t* d_curr_count, int64_t curr_total_points,
                            int64_t max_plane_points, double* d_pose_rel, double* d_pose_abs,
-                           double* d_log, int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_nn) {
+                           double* d_log, int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_nn,
+                           const float* d_last_strip_xyzi, const int32_t* d_last_strip_head) {
     if (!c) return SSF_E_ARG;
     if (n_pairs < 0 || curr_total_points < 0 || max_plane_points < 0 ||
         (n_pairs > 0 && (!d_last_xyzi || !d_last_off || !d_last_count || !d_last_normal ||
                          !d_last_valid || !d_curr_xyzi || !d_curr_off || !d_curr_count || !d_pose_rel)))
         return fail(c, SSF_E_ARG, "register_batch: bad arguments");
+    if (!d_last_strip_xyzi != !d_last_strip_head ||
+        (d_last_strip_xyzi && (!d_last_sorted_xyzi || !d_last_sorted_idx)))
+        return fail(c, SSF_E_ARG, "register_batch: the strip image needs both strip buffers and the sorted buffers");
     if (n_pairs == 0) return SSF_OK;
     SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
     SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(curr_total_points, 1)), "alloc corr");
@@ -499,7 +507,8 @@ int32_t ssf_register_batch(ssf_ctx* c, void* stream, int32_t n_pairs, const floa
         d_last_count, d_last_normal, d_last_valid, reinterpret_cast<const float4*>(d_last_sorted_xyzi),
         d_last_sorted_idx, reinterpret_cast<const float4*>(d_curr_xyzi), d_curr_off,
         d_curr_count, max_plane_points, c->corr.as<ssf::CorrRec>(), d_pose_rel, d_pose_abs, d_log,
-        d_nlog, d_ncorr, d_nn);
+        d_nlog, d_ncorr, d_nn, nullptr, reinterpret_cast<const float4*>(d_last_strip_xyzi),
+        d_last_strip_head);
     if (e != hipSuccess) return hip_fail(c, e, "register launch");
     return SSF_OK;
 }
@@ -517,8 +526,12 @@ int32_t ssf_register_batch_edges(ssf_ctx* c, void* stream, int32_t n_pairs,
                                  const int64_t* d_curr_edge_off, const int32_t* d_curr_edge_count,
                                  int64_t curr_edge_total, int64_t max_edge_points,
                                  double* d_pose_rel, double* d_pose_abs, double* d_log,
-                                 int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_ncorr_edge) {
+                                 int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_ncorr_edge,
+                                 const float* d_last_strip_xyzi, const int32_t* d_last_strip_head) {
     if (!c) return SSF_E_ARG;
+    if (!d_last_strip_xyzi != !d_last_strip_head ||
+        (d_last_strip_xyzi && (!d_last_sorted_xyzi || !d_last_sorted_idx)))
+        return fail(c, SSF_E_ARG, "register_batch_edges: the strip image needs both strip buffers and the sorted buffers");
     if (n_pairs < 0 || curr_total_points < 0 || max_plane_points < 0 || curr_edge_total < 0 ||
         max_edge_points < 0 ||
         (n_pairs > 0 && (!d_last_xyzi || !d_last_off || !d_last_count || !d_last_normal ||
@@ -544,7 +557,8 @@ int32_t ssf_register_batch_edges(ssf_ctx* c, void* stream, int32_t n_pairs,
         d_last_count, d_last_normal, d_last_valid, reinterpret_cast<const float4*>(d_last_sorted_xyzi),
         d_last_sorted_idx, reinterpret_cast<const float4*>(d_curr_xyzi), d_curr_off,
         d_curr_count, max_plane_points, c->corr.as<ssf::CorrRec>(), d_pose_rel, d_pose_abs, d_log,
-        d_nlog, d_ncorr, nullptr, &er);
+        d_nlog, d_ncorr, nullptr, &er, reinterpret_cast<const float4*>(d_last_strip_xyzi),
+        d_last_strip_head);
     if (e != hipSuccess) return hip_fail(c, e, "register_edges launch");
     return SSF_OK;
 }
@@ -580,7 +594,9 @@ int32_t ssf_register_pair(ssf_ctx* c, void* stream, const float* d_last_xyzi, in
     const size_t o_val = al(o_nrm + 3 * sizeof(float) * (size_t)m_last);
     const size_t o_srt = al(o_val + (size_t)m_last);
     const size_t o_sid = al(o_srt + sizeof(float4) * (size_t)m_last);
-    const size_t bytes = al(o_sid + sizeof(int32_t) * (size_t)m_last);
+    const size_t o_sim = al(o_sid + sizeof(int32_t) * (size_t)m_last);
+    const size_t o_shd = al(o_sim + sizeof(float4) * (size_t)m_last);
+    const size_t bytes = al(o_shd + sizeof(int32_t) * (size_t)m_last);
     SSF_TRY_HIP(c, c->pair.ensure(bytes), "alloc pair scratch");
     char* P = c->pair.as<char>();
     int64_t* d_off = reinterpret_cast<int64_t*>(P + o_off);     // [0, m_last] and [0, m_curr]
@@ -592,6 +608,8 @@ int32_t ssf_register_pair(ssf_ctx* c, void* stream, const float* d_last_xyzi, in
     uint8_t* d_val = reinterpret_cast<uint8_t*>(P + o_val);
     float* d_srt = reinterpret_cast<float*>(P + o_srt);
     int32_t* d_sid = reinterpret_cast<int32_t*>(P + o_sid);
+    float* d_sim = reinterpret_cast<float*>(P + o_sim);        // the table's strip image
+    int32_t* d_shd = reinterpret_cast<int32_t*>(P + o_shd);
     struct { int64_t off[4]; int32_t cnt[4]; double pose[7]; } h;
     h.off[0] = 0; h.off[1] = m_last; h.off[2] = 0; h.off[3] = m_curr;
     h.cnt[0] = (int32_t)m_last; h.cnt[1] = (int32_t)m_curr; h.cnt[2] = h.cnt[3] = 0;
@@ -599,11 +617,12 @@ int32_t ssf_register_pair(ssf_ctx* c, void* stream, const float* d_last_xyzi, in
     SSF_TRY_HIP(c, hipMemcpyAsync(d_off, h.off, sizeof(h.off), hipMemcpyHostToDevice, s), "H2D off");
     SSF_TRY_HIP(c, hipMemcpyAsync(d_cnt, h.cnt, sizeof(h.cnt), hipMemcpyHostToDevice, s), "H2D counts");
     SSF_TRY_HIP(c, hipMemcpyAsync(d_pose, h.pose, sizeof(h.pose), hipMemcpyHostToDevice, s), "H2D pose");
-    int32_t rc = ssf_plane_table_batch(c, stream, 1, d_last_xyzi, d_off, d_cnt, mx, d_nrm, d_val, d_srt, d_sid);
+    int32_t rc = ssf_plane_table_batch(c, stream, 1, d_last_xyzi, d_off, d_cnt, mx, d_nrm, d_val, d_srt, d_sid,
+                                       d_sim, d_shd);
     if (rc) return rc;
     rc = ssf_register_batch(c, stream, 1, d_last_xyzi, d_off, d_cnt, d_nrm, d_val, d_srt, d_sid,
                             d_curr_xyzi, d_off + 2, d_cnt + 1, m_curr, mx, d_pose, nullptr,
-                            d_log, d_nl, d_nl + 1, nullptr);
+                            d_log, d_nl, d_nl + 1, nullptr, d_sim, d_shd);
     if (rc) return rc;
     std::vector<double> hl((size_t)std::max(max_iter, 1) * 10);
     int32_t hn[2] = {0, 0};

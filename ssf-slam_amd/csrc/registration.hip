@@ -556,6 +556,46 @@ struct StripGeo {
     SSF_DEV int strip_of(float y) const { return min(ns - 1, max(0, (int)((y - y0) * invW))); }
 };
 
+// The plane table's strip image, kept for the association of the pairs whose LAST frame it is
+// (strips_build is deterministic and both kernels run it on the same x-sorted points with the
+// same work-group size, so the image is the one the association would build).  Per frame of
+// m points, at the frame's offset: m float4 strip-major points (original index in the low 16
+// bits of .w), and kStripHeadWords int32 words {start[kStripMax + 1], ylo[kStripMax],
+// yhi[kStripMax], y0, W, invW, ns}.  Frames with kStripHeadWords <= m <= kAssocStripF4Max only
+// (the header lives in the frame's own m words; the association stages float4 up to there).
+constexpr int kStripHeadWords = (kStripMax + 1) + 2 * kStripMax + 4;
+SSF_DEV bool strip_image_frame(int m) { return m >= kStripHeadWords && m <= kAssocStripF4Max; }
+
+SSF_DEV void strip_image_store(const float4* F, const StripLds& T, const StripGeo& g, int m,
+                               float4* __restrict__ img, int32_t* __restrict__ head) {
+    for (int r = threadIdx.x; r < m; r += blockDim.x) img[r] = F[r];
+    for (int j = threadIdx.x; j <= kStripMax; j += blockDim.x) head[j] = T.start[j];
+    for (int j = threadIdx.x; j < g.ns; j += blockDim.x) {
+        head[kStripMax + 1 + j] = __float_as_int(T.ylo[j]);
+        head[2 * kStripMax + 1 + j] = __float_as_int(T.yhi[j]);
+    }
+    if (threadIdx.x == 0) {
+        int32_t* gh = head + 3 * kStripMax + 1;
+        gh[0] = __float_as_int(g.y0); gh[1] = __float_as_int(g.W); gh[2] = __float_as_int(g.invW); gh[3] = g.ns;
+    }
+}
+
+// The association's side: the image into its LDS (F, T), the geometry returned.
+SSF_DEV StripGeo strip_image_load(const float4* __restrict__ img, const int32_t* __restrict__ head, int m,
+                                  float4* F, StripLds& T) {
+    const int32_t* gh = head + 3 * kStripMax + 1;
+    StripGeo g;
+    g.y0 = __int_as_float(gh[0]); g.W = __int_as_float(gh[1]); g.invW = __int_as_float(gh[2]); g.ns = gh[3];
+    for (int r = threadIdx.x; r < m; r += blockDim.x) F[r] = img[r];
+    for (int j = threadIdx.x; j <= kStripMax; j += blockDim.x) T.start[j] = head[j];
+    for (int j = threadIdx.x; j < g.ns; j += blockDim.x) {
+        T.ylo[j] = __int_as_float(head[kStripMax + 1 + j]);
+        T.yhi[j] = __int_as_float(head[2 * kStripMax + 1 + j]);
+    }
+    __syncthreads();
+    return g;
+}
+
 // The strip-major points, either layout: float4 (x, y, z, original index in .w) or x | y | z
 // float arrays + a u16 original index.
 template <bool kSoa>
@@ -1185,7 +1225,8 @@ SSF_DEV void table_sort_regs(const float4* __restrict__ P, int m, float* key, in
 __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
     const float4* __restrict__ plane, const int64_t* __restrict__ frame_off,
     const int32_t* __restrict__ count, float plane_max, float* __restrict__ normal,
-    uint8_t* __restrict__ valid, float4* __restrict__ sorted_xyzi, int32_t* __restrict__ sorted_idx) {
+    uint8_t* __restrict__ valid, float4* __restrict__ sorted_xyzi, int32_t* __restrict__ sorted_idx,
+    float4* __restrict__ strip_xyzi, int32_t* __restrict__ strip_head) {
     // 160 KiB of LDS: [0, 64K) keys, [64K, 128K) permutation, [128K, 160K) spare.  After the
     // sort, frames <= kTableStripSoaMax rebuild the whole image as y-strips of the sorted points
     // + the strip table + the deferred queue; larger frames walk the sorted copy in global memory.
@@ -1325,6 +1366,9 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
             else
                 table_strip_walks(P, StripView<false>{F, X, I16, m}, T, g, m, plane_max, base, normal,
                                   valid, queue, qcap, qlen, SP, SI, stamp_out, st0);
+            // the walks only read F and T: the image leaves as it is (uniform condition)
+            if (strip_xyzi && strip_image_frame(m))
+                strip_image_store(F, T, g, m, strip_xyzi + base, strip_head + base);
         }
         SSF_TSTAMP(3);
     } else {
@@ -1657,7 +1701,7 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     const int32_t* __restrict__ last_sidx, const float4* __restrict__ curr,
     const int64_t* __restrict__ curr_off, const int32_t* __restrict__ curr_count,
     const double* __restrict__ pose_rel, CorrRec* __restrict__ corr, int32_t* __restrict__ nn_out,
-    int lds_cap) {
+    int lds_cap, const float4* __restrict__ strip_xyzi, const int32_t* __restrict__ strip_head) {
     extern __shared__ float4 SL[];                  // [ml] strip-major, x-sorted in each strip
     __shared__ StripLds T;
     // gridDim.y work-groups per pair (few pairs in a launch): each stages the whole last frame
@@ -1686,8 +1730,12 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     }
     float* SX = reinterpret_cast<float*>(SL);
     uint16_t* SI16 = reinterpret_cast<uint16_t*>(SX + 3 * ml);
-    const StripGeo geo = strips_build<kSoa, kStripPerMax>(
-        [&](int, int r) { float4 pt = SP[r]; pt.w = __int_as_float(SI[r]); return pt; }, ml, T, SL, SX, SI16);
+    // the plane table's image of this last frame when the caller kept it (a copy: ~4 us of the
+    // ~40 us build), otherwise the build
+    const StripGeo geo = (!kSoa && strip_xyzi && strip_image_frame(ml))
+        ? strip_image_load(strip_xyzi + lo, strip_head + lo, ml, SL, T)
+        : strips_build<kSoa, kStripPerMax>(
+              [&](int, int r) { float4 pt = SP[r]; pt.w = __int_as_float(SI[r]); return pt; }, ml, T, SL, SX, SI16);
     const float y0 = geo.y0, W = geo.W;
     const int ns = geo.ns;
     auto strip_of = [&](float y) { return geo.strip_of(y); };
@@ -2520,12 +2568,13 @@ __global__ void k_accumulate(int n, const double* __restrict__ rel, const double
 hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames,
                               const float4* plane, const int64_t* frame_off, const int32_t* count,
                               int64_t max_m, float* normal, uint8_t* valid, float4* sorted_xyzi,
-                              int32_t* sorted_idx) {
+                              int32_t* sorted_idx, float4* strip_xyzi, int32_t* strip_head) {
     if (n_frames <= 0 || max_m <= 0) return hipSuccess;
     if (max_m <= kSortMax && sorted_xyzi && sorted_idx) {
         kmark(s, "k_plane_table_sorted");
         hipLaunchKernelGGL(k_plane_table_sorted, dim3(n_frames), dim3(kTableThreads), 0, s, plane,
-                           frame_off, count, cfg.plane_max, normal, valid, sorted_xyzi, sorted_idx);
+                           frame_off, count, cfg.plane_max, normal, valid, sorted_xyzi, sorted_idx,
+                           strip_head ? strip_xyzi : nullptr, strip_head);
     } else {
         const int bx = (int)((max_m + 255) / 256);
         kmark(s, "k_plane_table");
@@ -2541,7 +2590,8 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
                            const float4* last_sorted, const int32_t* last_sidx, const float4* curr,
                            const int64_t* curr_off, const int32_t* curr_count, int64_t max_m,
                            CorrRec* corr, double* pose_rel, double* pose_abs, double* log,
-                           int32_t* nlog, int32_t* ncorr, int32_t* nn, const EdgeReg* edge) {
+                           int32_t* nlog, int32_t* ncorr, int32_t* nn, const EdgeReg* edge,
+                           const float4* last_strip_xyzi, const int32_t* last_strip_head) {
     if (n_pairs <= 0) return hipSuccess;
     if (max_m > 0) {
         const int bx = (int)((max_m + 255) / 256);
@@ -2559,7 +2609,8 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
             hipLaunchKernelGGL(soa ? k_associate_strips<true> : k_associate_strips<false>,
                                dim3(n_pairs, qsplit), dim3(kStripThreads), lds, s, last, last_off, last_count,
                                last_normal, last_valid, last_sorted, last_sidx, curr, curr_off,
-                               curr_count, pose_rel, corr, nn, cap);
+                               curr_count, pose_rel, corr, nn, cap,
+                               last_strip_head ? last_strip_xyzi : nullptr, last_strip_head);
         } else
 #endif
         if (max_m <= kAssocSoaMax && last_sorted && last_sidx) {

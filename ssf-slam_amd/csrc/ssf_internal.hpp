@@ -81,7 +81,8 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
 hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames,
                               const float4* plane, const int64_t* frame_off, const int32_t* count,
                               int64_t max_m, float* normal, uint8_t* valid, float4* sorted_xyzi,
-                              int32_t* sorted_idx);
+                              int32_t* sorted_idx, float4* strip_xyzi = nullptr,
+                              int32_t* strip_head = nullptr);
 // Point-to-line blocks of launch_register (beyond the reference; nullptr = planes only): the
 // edge clouds, the last frames' line table (6 floats per edge: centroid, direction) and the
 // correspondence scratch / per-pair counts.
@@ -105,7 +106,8 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
                            const int64_t* curr_off, const int32_t* curr_count, int64_t max_m,
                            CorrRec* corr, double* pose_rel, double* pose_abs, double* log,
                            int32_t* nlog, int32_t* ncorr, int32_t* nn,
-                           const EdgeReg* edge = nullptr);
+                           const EdgeReg* edge = nullptr, const float4* last_strip_xyzi = nullptr,
+                           const int32_t* last_strip_head = nullptr);
 hipError_t launch_edge_table(hipStream_t s, const ssf_edge_config& ec, int n_frames,
                              const float4* edges, const int64_t* frame_off, const int32_t* count,
                              int64_t max_m, float* line, uint8_t* valid);

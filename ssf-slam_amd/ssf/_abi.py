@@ -118,10 +118,10 @@ def lib():
     L.ssf_extract_planes_batch_masked.restype = i32
     L.ssf_extract_planes.argtypes = [vp, vp, vp, i64, i32, i32, vp, C.POINTER(i64), i64]
     L.ssf_extract_planes.restype = i32
-    L.ssf_plane_table_batch.argtypes = [vp, vp, i32, vp, vp, vp, i64, vp, vp, vp, vp]
+    L.ssf_plane_table_batch.argtypes = [vp, vp, i32, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]
     L.ssf_plane_table_batch.restype = i32
     L.ssf_register_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64,
-                                     vp, vp, vp, vp, vp, vp]
+                                     vp, vp, vp, vp, vp, vp, vp, vp]
     L.ssf_register_batch.restype = i32
     L.ssf_register_pair.argtypes = [vp, vp, vp, i64, vp, i64, vp, vp, vp, vp, C.POINTER(StepLog)]
     L.ssf_register_pair.restype = i32
@@ -144,7 +144,7 @@ def lib():
     L.ssf_edge_table_batch.argtypes = [vp, vp, i32, vp, vp, vp, i64, vp, vp]
     L.ssf_edge_table_batch.restype = i32
     L.ssf_register_batch_edges.argtypes = ([vp, vp, i32] + [vp] * 10 + [i64, i64] + [vp] * 8 +
-                                           [i64, i64] + [vp] * 6)
+                                           [i64, i64] + [vp] * 8)
     L.ssf_register_batch_edges.restype = i32
     L.ssf_accumulate_sequence.argtypes = [vp, vp, i32, vp, vp, vp]
     L.ssf_accumulate_sequence.restype = i32

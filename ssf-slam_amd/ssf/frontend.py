@@ -57,6 +57,20 @@ class PlaneBatch:
         return self.xyzi[o:o + c]
 
 
+class PlaneTable(tuple):
+    """(normal, valid, sorted_xyzi, sorted_idx) of ssf_plane_table_batch; .strips = (strip_xyzi,
+    strip_head), the y-strip image the association of the next pairs stages, or None."""
+
+    def __new__(cls, normal, valid, sx, si, strips=None):
+        t = super().__new__(cls, (normal, valid, sx, si))
+        t.strips = strips
+        return t
+
+    def tensors(self):
+        """every device tensor the table holds (for record_stream across streams)"""
+        return [x for x in (*self, *(self.strips or ())) if isinstance(x, torch.Tensor)]
+
+
 class Frontend:
     """One C-ABI context (one device, one parameter profile)."""
 
@@ -226,23 +240,28 @@ class Frontend:
         return out[:m.value]
 
     # ------------------------------------------------------------------ lidarOdometry_onlyPC
-    def plane_table(self, pb: PlaneBatch, brute_force: bool = False):
-        """-> (normal [total,3] f32, valid [total] u8, sorted_xyzi, sorted_idx) -- the plane table
-        of frames that will be LAST frames, plus their x-sorted search index (None, None when
-        brute_force=True)."""
+    def plane_table(self, pb: PlaneBatch, brute_force: bool = False, strips: bool = True):
+        """-> PlaneTable (normal [total,3] f32, valid [total] u8, sorted_xyzi, sorted_idx) -- the
+        plane table of frames that will be LAST frames, plus their x-sorted search index (None,
+        None when brute_force=True); .strips = the y-strip image (strip_xyzi [total,4] f32,
+        strip_head [total] i32) that register() hands to the association, or None."""
         total = pb.xyzi.shape[0]
         normal = torch.empty((total, 3), dtype=torch.float32, device=self.device)
         valid = torch.empty(total, dtype=torch.uint8, device=self.device)
-        sx = si = None
+        sx = si = st = None
         if not brute_force:
             sx = torch.empty((total, 4), dtype=torch.float32, device=self.device)
             si = torch.empty(total, dtype=torch.int32, device=self.device)
+            if strips:
+                st = (torch.empty((total, 4), dtype=torch.float32, device=self.device),
+                      torch.empty(total, dtype=torch.int32, device=self.device))
         rc = _abi.lib().ssf_plane_table_batch(self._h, _stream(self.device), pb.count.numel(),
                                               _ptr(pb.xyzi), _ptr(pb.off), _ptr(pb.count),
                                               pb.max_points, _ptr(normal), _ptr(valid), _ptr(sx),
-                                              _ptr(si))
+                                              _ptr(si), _ptr(st[0] if st else None),
+                                              _ptr(st[1] if st else None))
         self._check(rc, "ssf_plane_table_batch")
-        return normal, valid, sx, si
+        return PlaneTable(normal, valid, sx, si, st)
 
     def register_pair(self, last_xyzi, curr_xyzi, q_init=(0.0, 0.0, 0.0, 1.0),
                       t_init=(0.0, 0.0, 0.0)):
@@ -280,6 +299,7 @@ class Frontend:
         if pose_abs is not None:
             pose_abs = self._dev(pose_abs, torch.float64)
         normal, valid, sx, si = last_table
+        st = getattr(last_table, "strips", None) or (None, None)
         log = nlog = nn = None
         ncorr = torch.empty(P, dtype=torch.int32, device=self.device)
         if want_log:
@@ -295,7 +315,7 @@ class Frontend:
                 _ptr(normal), _ptr(valid), _ptr(sx), _ptr(si), _ptr(curr.xyzi), _ptr(curr.off),
                 _ptr(curr.count),
                 int(curr.h_off[-1]), mx, _ptr(pose_rel), _ptr(pose_abs), _ptr(log), _ptr(nlog),
-                _ptr(ncorr), _ptr(nn))
+                _ptr(ncorr), _ptr(nn), _ptr(st[0]), _ptr(st[1]))
             self._check(rc, "ssf_register_batch")
             return dict(pose_rel=pose_rel, pose_abs=pose_abs, ncorr=ncorr, log=log, nlog=nlog, nn=nn)
         last_e, (line, lvalid), curr_e = edges
@@ -309,7 +329,8 @@ class Frontend:
             _ptr(curr.count), int(curr.h_off[-1]), mx,
             _ptr(last_e.xyzi), _ptr(last_e.off), _ptr(last_e.count), _ptr(line), _ptr(lvalid),
             _ptr(curr_e.xyzi), _ptr(curr_e.off), _ptr(curr_e.count), int(curr_e.h_off[-1]), mxe,
-            _ptr(pose_rel), _ptr(pose_abs), _ptr(log), _ptr(nlog), _ptr(ncorr), _ptr(ncorr_e))
+            _ptr(pose_rel), _ptr(pose_abs), _ptr(log), _ptr(nlog), _ptr(ncorr), _ptr(ncorr_e),
+            _ptr(st[0]), _ptr(st[1]))
         self._check(rc, "ssf_register_batch_edges")
         return dict(pose_rel=pose_rel, pose_abs=pose_abs, ncorr=ncorr, ncorr_edge=ncorr_e, log=log,
                     nlog=nlog, nn=None)

@@ -300,3 +300,41 @@ def test_ssf_register_pair_skip_and_empty(dev):
     empty = torch.zeros((0, 4), dtype=torch.float32, device=dev)
     q, t, steps, nc = fe.register_pair(curr, empty, q0, t0)
     assert q == q0 and t == t0 and nc == 0
+
+
+@pytest.mark.parametrize("n_pairs", [1, 3])
+def test_strip_image_reuse_identical(dev, n_pairs):
+    """The association staging the plane table's strip image (PlaneTable.strips) answers exactly
+    as the one building its own strips: identical 1-NN indices, correspondence counts and pose
+    bits, for one pair (8 work-groups per pair) and several, with a last frame below the image's
+    773-point minimum (rebuilt) in the same launch."""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index)
+    full = [frame(s, 4 + s, n_az=1875)[0] for s in range(n_pairs)]
+    nxt = [frame(s, 5 + s, n_az=1875)[0] for s in range(n_pairs)]
+    pb = _planes(fe, dev, full + nxt)
+    if n_pairs > 1:                                   # pair 0's last frame: a 600-point cut
+        P0 = pb.frame(0)[:600].clone()
+        rest = [pb.frame(f) for f in range(1, 2 * n_pairs)]
+        xyzi = torch.cat([P0, *rest]).contiguous()
+        counts = [600] + [int(r.shape[0]) for r in rest]
+        off, h_off = ssf.frame_offsets(counts, dev)
+        pb = ssf.PlaneBatch(xyzi, torch.tensor(counts, dtype=torch.int32, device=dev), off, h_off,
+                            max(counts))
+    m = [int(c) for c in pb.count.cpu()]
+    assert any(773 <= c <= 6144 for c in m[:n_pairs]), m
+    t_img = fe.plane_table(pb)
+    t_new = fe.plane_table(pb, strips=False)
+    assert t_img.strips is not None and t_new.strips is None
+    last, curr = _sub(pb, list(range(n_pairs))), _sub(pb, list(range(n_pairs, 2 * n_pairs)))
+    q0 = np.array([0.0, 0.0, 0.002, 1.0]); q0 /= np.linalg.norm(q0)
+    pose0 = torch.tensor([[*q0, 0.8, 0.02, 0.0]] * n_pairs, dtype=torch.float64, device=dev)
+    out = []
+    for tb in (t_img, t_new):
+        pose = pose0.clone()
+        r = fe.register(last, tb, curr, pose, want_nn=True)
+        torch.cuda.synchronize()
+        out.append((r["nn"].cpu().numpy(), r["ncorr"].cpu().numpy(), r["pose_rel"].cpu().numpy()))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
+    assert np.array_equal(out[0][2].view(np.uint64), out[1][2].view(np.uint64))

@@ -88,6 +88,9 @@ struct MaskShared {
     float lb1[512], lb2[512];   // this pass's drift bounds against pass r (9-bit index)
     int64_t c0, c1;
     double dg_cyc, dg_n, dg_lab, dg_wfull, dg_full1;   // diagnostic build only
+#ifdef SSF_MASK_STAMPS
+    double dg_e[3];            // EM pass: points + block sum, exchange, M-step (cycles, summed)
+#endif
     double passes;             // algorithmic bytes / (24 B x n): 1 per full pass (see the Lloyd loop)
     int km_iter, em_iter, strict, converged, done, status, label0, bg, bg_pred, lfull;
     double hnk[2], hq[2], hpm[12];   // gmm_params2: per-component results of lanes 0 / 1
@@ -1284,6 +1287,10 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         // mantissa * 2^pexp (frexp per point: the product never overflows, one log per thread)
         double prod = 1.0;
         int pexp = 0;
+#ifdef SSF_MASK_STAMPS
+        if (it == 1 && tid == 0) S.dg_e[0] = S.dg_e[1] = S.dg_e[2] = 0.0;
+        const unsigned long long e_t0 = __builtin_amdgcn_s_memtime();
+#endif
         for_point_pairs(P, Fl, r0, r1, [&](const double* xa, const double* xb, double wb) {
             // Aq / bq are re-read from LDS once per PAIR of points (lds_laundered)
             const LdsDouble* Aq = lds_laundered(S.Aq);
@@ -1317,7 +1324,13 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         });
         acc[28] += log(prod) + (double)pexp * 0.69314718055994530942;
         block_sum_rs<29>(acc, red);
+#ifdef SSF_MASK_STAMPS
+        const unsigned long long e_t1 = __builtin_amdgcn_s_memtime();
+#endif
         if (!exchange<29>(X, acc, xtmp, &okflag)) { sync_failed(); return; }
+#ifdef SSF_MASK_STAMPS
+        const unsigned long long e_t2 = __builtin_amdgcn_s_memtime();
+#endif
         if (tid < 2) {                           // lanes 0 / 1: the two components
             double prev = 0.0;
             if (tid == 0) {
@@ -1334,6 +1347,12 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             }
         }
         __syncthreads();
+#ifdef SSF_MASK_STAMPS
+        if (tid == 0) {
+            S.dg_e[0] += (double)(e_t1 - e_t0); S.dg_e[1] += (double)(e_t2 - e_t1);
+            S.dg_e[2] += (double)(__builtin_amdgcn_s_memtime() - e_t2);
+        }
+#endif
         if (S.done) break;
     }
 
@@ -1418,6 +1437,8 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
                 out[SSF_POSE_OUT_CENTER1] = S.dg_n > 0.0 ? S.dg_lab / (S.dg_n * (double)n) : 0.0;
                 out[SSF_POSE_OUT_CONVERGED] = S.dg_wfull;
                 out[SSF_POSE_OUT_NBG] = S.dg_full1;
+                // EM pass split: points + block sum, exchange, M-step (cycles per pass)
+                for (int k = 0; k < 3; ++k) out[SSF_POSE_OUT_T + k] = S.em_iter > 0 ? S.dg_e[k] / S.em_iter : 0.0;
 #endif
                 out[SSF_POSE_OUT_LOWER_BOUND] = S.lb;
                 out[SSF_POSE_OUT_PASSES] = S.passes;

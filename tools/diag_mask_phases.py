@@ -42,6 +42,8 @@ def main():
     print(f"  frame cycles min {st[:, 5].min():.3e} max {st[:, 5].max():.3e} (slowest: km_iter "
           f"{o[slow, 19]:.0f} em_iter {o[slow, 20]:.0f}); kernel wall {wall_ms:.3f} ms -> "
           f"{st[:, 5].max() / wall_ms / 1e6:.2f} G stamp-cycles/s over the slowest frame")
+    print(f"  EM pass split (diag slots 0-2): points + block sum {o[:, 0].mean():.3e}, exchange "
+          f"{o[:, 1].mean():.3e}, M-step {o[:, 2].mean():.3e} cycles")
     for k, nme in enumerate(names):
         per = ""
         if nme == "lloyd":

@@ -49,6 +49,9 @@ constexpr int kNW = kMaskThreads / 64;
 #define SSF_LLOYD_DEEP 2
 #endif
 constexpr int kLloydDeep = SSF_LLOYD_DEEP;   // points in flight per thread in the Lloyd passes
+#ifndef SSF_KPP_DEEP
+#define SSF_KPP_DEEP 2
+#endif
 constexpr int kKppBlocks = 4096;             // k-means++ block totals in LDS (frames up to ~262k points)
 constexpr double kPi = 3.14159265358979323846;
 #ifndef SSF_LLOYD_FULL_PASSES
@@ -842,23 +845,45 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         const int64_t ws = r0 + (int64_t)w * seg, we = ws + seg < r1 ? ws + seg : r1;
         // D(i) = squared distance to the first centre; recomputed (same expression, same bits)
         // wherever it is needed instead of being stored
-        auto dist0 = [&](int64_t i) {
-            double x[6], dt = 0.0, xs = 0.0;
-            load_x(P, Fl, i, x);
+        auto dist0x = [&](const double* x) {
+            double dt = 0.0, xs = 0.0;
 #pragma unroll
             for (int d = 0; d < 6; ++d) { const double v = x[d] - mean[d]; dt += c0[d] * v; xs += v * v; }
             const double v = (-2.0 * dt + cn0) + xs;
             return v > 0.0 ? v : 0.0;
         };
+        auto dist0 = [&](int64_t i) {
+            double x[6];
+            load_x(P, Fl, i, x);
+            return dist0x(x);
+        };
+        // the wave's segment streamed with the next kKppDeep blocks' points in flight (raw floats,
+        // loads clamped and unconditional): each block was one dependent load latency before.
+        // Diag stamps, B = 256: k-means++ 0.75 -> 0.56 M cycles per frame at depth 2; depth 4
+        // 0.58 (tools/gpu/r3y.sh, r3z.sh)
+        constexpr int kKppDeep = SSF_KPP_DEEP;
+        const int64_t wlast = we > ws ? we - 1 : ws;
         // per 64-point block: the in-block inclusive scan's total (lane 63) goes to LDS, so the
         // draw search below only re-scans the one block that holds the draw
         const int64_t spw = seg / 64;                            // blocks per wave segment
         const bool use_blocks = spw * nw <= kKppBlocks;          // uniform
         double wsum = 0.0;
-#pragma unroll 2
-        for (int64_t b = ws; b < we; b += 64) {
+        T kb[kKppDeep][6];
+        if (ws < we) {
+#pragma unroll
+            for (int k = 0; k < kKppDeep; ++k) load_raw(P, Fl, min(ws + 64 * k + lane, wlast), kb[k]);
+        }
+        for (int64_t b0 = ws; b0 < we; b0 += 64 * kKppDeep)
+#pragma unroll
+        for (int k = 0; k < kKppDeep; ++k) {
+            const int64_t b = b0 + 64 * k;
+            if (b >= we) break;                                  // uniform
             const int64_t i = b + lane;
-            const double d = i < we ? dist0(i) : 0.0;
+            double x[6];
+#pragma unroll
+            for (int d = 0; d < 6; ++d) x[d] = (double)kb[k][d];
+            load_raw(P, Fl, min(i + 64 * kKppDeep, wlast), kb[k]);
+            const double d = i < we ? dist0x(x) : 0.0;
             wsum += d;
             if (use_blocks) {
                 double v = d;
@@ -957,12 +982,22 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             for (int d = 0; d < 6; ++d) { cc[j][d] = x[d] - mean[d]; ccn[j] += cc[j][d] * cc[j][d]; }
         }
         double cp[2] = {0.0, 0.0};
-#pragma unroll 4
-        for (int64_t b = ws; b < we; b += 64) {
+        if (ws < we) {
+#pragma unroll
+            for (int k = 0; k < kKppDeep; ++k) load_raw(P, Fl, min(ws + 64 * k + lane, wlast), kb[k]);
+        }
+        for (int64_t b0 = ws; b0 < we; b0 += 64 * kKppDeep)
+#pragma unroll
+        for (int k = 0; k < kKppDeep; ++k) {
+            const int64_t b = b0 + 64 * k;
+            if (b >= we) break;                                  // uniform
             const int64_t i = b + lane;
+            double x[6];
+#pragma unroll
+            for (int d = 0; d < 6; ++d) x[d] = (double)kb[k][d];
+            load_raw(P, Fl, min(i + 64 * kKppDeep, wlast), kb[k]);
             if (i < we) {
-                double x[6], xs = 0.0, dt0 = 0.0, dt1 = 0.0, dtc = 0.0;
-                load_x(P, Fl, i, x);
+                double xs = 0.0, dt0 = 0.0, dt1 = 0.0, dtc = 0.0;
 #pragma unroll
                 for (int d = 0; d < 6; ++d) {
                     const double v = x[d] - mean[d];

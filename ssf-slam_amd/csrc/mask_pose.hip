@@ -783,14 +783,16 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         double a[27];
 #pragma unroll
         for (int i = 0; i < 27; ++i) a[i] = 0.0;
-        for_points(P, Fl, r0, r1, [&](int64_t i, const double* x) {
-            double v[6];
+        // two points in flight per thread (for_points_deep: the same per-thread order, so the
+        // same sums); a slot past r1 adds zeros
+        for_points_deep<kLloydDeep>(P, Fl, r0, r1, [&](int64_t, const double* x, bool val) {
+            double v[6], vw[6];
 #pragma unroll
-            for (int d = 0; d < 6; ++d) { v[d] = x[d] - x0[d]; a[d] += v[d]; }
+            for (int d = 0; d < 6; ++d) { v[d] = x[d] - x0[d]; vw[d] = val ? v[d] : 0.0; a[d] += vw[d]; }
 #pragma unroll
             for (int r = 0; r < 6; ++r)
 #pragma unroll
-                for (int c = r; c < 6; ++c) a[6 + up(r, c)] += v[r] * v[c];
+                for (int c = r; c < 6; ++c) a[6 + up(r, c)] += vw[r] * v[c];
         });
         block_sum_rs<27>(a, red);
         if (!exchange<27>(X, a, xtmp, &okflag)) { sync_failed(); return; }
@@ -1275,12 +1277,12 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         double acc[28];
 #pragma unroll
         for (int k = 0; k < 28; ++k) acc[k] = 0.0;
-        for_points(P, Fl, r0, r1, [&](int64_t, const double* x) {
+        for_points_deep<kLloydDeep>(P, Fl, r0, r1, [&](int64_t, const double* x, bool val) {
             double v[6], dt0 = 0.0, dt1 = 0.0;
 #pragma unroll
             for (int d = 0; d < 6; ++d) { v[d] = x[d] - mean[d]; dt0 += v[d] * cen[d]; dt1 += v[d] * cen[6 + d]; }
             const int l = (-2.0 * dt1 + csn1) < (-2.0 * dt0 + csn0) ? 1 : 0;
-            const double w1 = (double)l;
+            const double w1 = val ? (double)l : 0.0;
             acc[0] += w1;
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
@@ -1406,7 +1408,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         for (int i = 0; i < 16; ++i) k1[i] = 0.0;
         if (tid == 0) S.label0 = 0;
         __syncthreads();
-        for_points(P, Fl, r0, r1, [&](int64_t i, const double* x) {
+        for_points_deep<kLloydDeep>(P, Fl, r0, r1, [&](int64_t i, const double* x, bool val) {
             // Aq / bq are re-read from LDS (broadcast ds_reads) for every point (lds_laundered)
             const LdsDouble* Aq = lds_laundered(S.Aq);
             const LdsDouble* bq = lds_laundered(S.bq);
@@ -1414,9 +1416,10 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
 #pragma unroll
             for (int a = 0; a < 6; ++a) v[a] = x[a] - mean[a];
             const int l = em_delta1(v, Aq, bq, cq) > 0.0 ? 1 : 0;   // a1 > a0
-            if (bg_mask) bg_mask[fb + i] = (uint8_t)(l == pred);
+            // a slot past r1 holds point r1 - 1 again: its byte is rewritten with the same value
+            if (bg_mask) bg_mask[fb + (val ? i : r1 - 1)] = (uint8_t)(l == pred);
             if (i == 0) S.label0 = l;
-            const double w1 = (double)l;
+            const double w1 = val ? (double)l : 0.0;
             double sv[3], dv[3];
 #pragma unroll
             for (int r = 0; r < 3; ++r) { dv[r] = x[3 + r] - x0[3 + r]; sv[r] = dv[r] + (x[r] - x0[r]); }

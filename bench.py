@@ -46,8 +46,8 @@ F64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector, spec (AMD datasheet); f64 MFMA
 # HBM bytes per launch of every kernel / f64 FLOPs per k_mask_pose launch, measured with rocprofv3
 # PMC passes on a serial run of this bench (tools/pmc_traffic.py, tools/pmc_f64.py); used when
 # their workload config matches the run's.
-TRAFFIC_JSON = os.path.join(REPO, "profiles", "r03e_traffic.json")
-F64_JSON = os.path.join(REPO, "profiles", "r03e_k_mask_pose_f64.json")
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "r03ac_traffic.json")
+F64_JSON = os.path.join(REPO, "profiles", "r03ac_f64.json")
 METRIC = "LiDAR front-end frames/sec (mask+feature+GN), 64-beam 120k pts, 1/2/4/8 GPUs"
 
 
@@ -440,7 +440,9 @@ def rooflines(times, acc, B, N):
         # flag bytes read, per plane point: its index written and read back (4 + 4 B), its ring
         # index (4 B) and xyz (12 B) gathered and the xyzi record written (16 B)
         "k_select": 1.0 * acc["kept"] + 40.0 * acc["plane"],
-        "k_plane_table_sorted": 49.0 * acc["plane"],
+        # plane point read (16 B), x-sorted copy + permutation (16 + 4), normal + validity
+        # (12 + 1), and the y-strip image the next pair's association stages (16 + 4)
+        "k_plane_table_sorted": 69.0 * acc["plane"],
         "k_associate_lds": 64.0 * acc["plane_reg"],
         "k_associate_lds_soa": 64.0 * acc["plane_reg"],
         "k_associate_strips": 64.0 * acc["plane_reg"],

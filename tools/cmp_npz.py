@@ -12,3 +12,11 @@ for k in a.files:
     same = x.shape == y.shape and np.array_equal(x, y)
     nd = int((x != y).sum()) if x.shape == y.shape else -1
     print(f"{k}: identical={same} differing={nd} size={x.size}")
+    if not same and x.shape == y.shape and x.ndim == 2:
+        cols = sorted(set(np.nonzero(x != y)[1].tolist()))
+        print(f"  differing columns {cols}")
+        if a[k].dtype.kind == "f":
+            for c in cols[:8]:
+                d = np.abs(a[k][:, c] - b[k][:, c])
+                rel = d / np.maximum(np.abs(a[k][:, c]), 1e-300)
+                print(f"  col {c}: max abs diff {d.max():.3e}, max rel {rel.max():.3e}")

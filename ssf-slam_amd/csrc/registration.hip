@@ -18,6 +18,8 @@
 
 #include <float.h>
 
+#include <rocprim/block/block_radix_sort.hpp>
+
 namespace ssf {
 
 // ------------------------------------------------------------------------------------------
@@ -1222,6 +1224,31 @@ SSF_DEV void table_sort_regs(const float4* __restrict__ P, int m, float* key, in
     __syncthreads();
 }
 
+// The same (x, index) order by a stable LSD radix sort of the x bits (rocPRIM
+// block_radix_sort, keys and the index in registers, E per thread in blocked order, so equal
+// keys keep index order): x + 0 turns -0 into +0 (lex_less compares them equal), the sign-flip
+// encoding orders the floats as unsigned words, and slots past m take the largest key.
+// -DSSF_TABLE_BITONIC restores the bitonic network (A/B).
+template <int E>
+SSF_DEV void table_sort_radix(const float4* __restrict__ P, int m, void* storage, int* idx) {
+    using Sort = rocprim::block_radix_sort<unsigned int, kTableThreads, E, int>;
+    auto& st = *reinterpret_cast<typename Sort::storage_type*>(storage);
+    const int tid = threadIdx.x;
+    unsigned int k[E];
+    int ix[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int t = tid * E + e;
+        const unsigned int b = __float_as_uint(t < m ? P[t].x + 0.0f : 0.0f);
+        k[e] = t < m ? (b ^ ((b >> 31) ? 0xFFFFFFFFu : 0x80000000u)) : 0xFFFFFFFFu;
+        ix[e] = t;
+    }
+    Sort().sort(k, ix, st);
+#pragma unroll
+    for (int e = 0; e < E; ++e) idx[tid * E + e] = ix[e];
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
     const float4* __restrict__ plane, const int64_t* __restrict__ frame_off,
     const int32_t* __restrict__ count, float plane_max, float* __restrict__ normal,
@@ -1243,6 +1270,14 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
 #endif
     int np = 1;
     while (np < m) np <<= 1;
+#ifndef SSF_TABLE_BITONIC
+    // the key region [0, 64 KiB) holds the radix sort's storage (the keys stay in registers)
+    if (np <= kTableThreads) table_sort_radix<1>(P, m, lds, idx);
+    else if (np == 2 * kTableThreads) table_sort_radix<2>(P, m, lds, idx);
+    else if (np == 4 * kTableThreads) table_sort_radix<4>(P, m, lds, idx);
+    else if (np == 8 * kTableThreads) table_sort_radix<8>(P, m, lds, idx);
+    else
+#endif
     if (np == 4 * kTableThreads) table_sort_regs<4>(P, m, key, idx);
     else if (np == 2 * kTableThreads) table_sort_regs<2>(P, m, key, idx);
     else if (np == kTableThreads) table_sort_regs<1>(P, m, key, idx);

@@ -1088,6 +1088,10 @@ SSF_DEV void table_pick_walks(const float4* __restrict__ P, const StripView<fals
         if (inval) pick_invalid(o, normal, valid);
         else pick_finish(P, s, f1 ? 1 : 0, plane_max, o, normal, valid);
     }
+#ifdef SSF_TABLE_STAMPS
+    __syncthreads();
+    if (threadIdx.x == 0 && stamp_out) stamp_out[4] = (int32_t)((__builtin_amdgcn_s_memtime() - stamp0) >> 4);
+#endif
 }
 
 // The deferred few (no decision inside 1 m: sparse, far regions) walk the x-sorted copy the

@@ -24,11 +24,11 @@ def main():
         torch.cuda.synchronize()
     si = t[3].cpu().numpy()
     cnt = pb.count.cpu().numpy()
-    st = np.array([si[int(h_off[f]) + cnt[f]: int(h_off[f]) + cnt[f] + 5] for f in range(B)]).astype(np.float64)
-    st[:, [0, 1, 3, 4]] *= 16
+    st = np.array([si[int(h_off[f]) + cnt[f]: int(h_off[f]) + cnt[f] + 6] for f in range(B)]).astype(np.float64)
+    st[:, [0, 1, 3, 4, 5]] *= 16
     for name, red in (("mean", np.mean), ("p90", lambda a: np.percentile(a, 90)), ("max", np.max)):
         print(f"B={B} {name}: m {red(cnt):.0f}; cycles: sort {red(st[:,0]):.3e}  bounded-walks-end "
-              f"{red(st[:,1]):.3e} (queue {red(st[:,2]):.0f})  strips-built {red(st[:,4]):.3e}  end {red(st[:,3]):.3e}")
+              f"{red(st[:,1]):.3e} (queue {red(st[:,2]):.0f})  strips-built {red(st[:,4]):.3e}  queue-done {red(st[:,5]):.3e}  end {red(st[:,3]):.3e}")
     f = int(np.argmax(st[:, 3]))
     print(f"slowest frame {f}: m {cnt[f]} sort {st[f,0]:.3e} bounded {st[f,1]:.3e} queue {st[f,2]:.0f} end {st[f,3]:.3e}")
 

@@ -338,3 +338,26 @@ def test_strip_image_reuse_identical(dev, n_pairs):
     assert np.array_equal(out[0][0], out[1][0])
     assert np.array_equal(out[0][1], out[1][1])
     assert np.array_equal(out[0][2].view(np.uint64), out[1][2].view(np.uint64))
+
+
+def test_strip_image_argument_checks(dev):
+    """The strip image travels as a pair (image and header) and only with the sorted buffers:
+    anything else is SSF_E_ARG with a message, before any launch."""
+    import ssf
+    from ssf import _abi
+    from ssf.frontend import _ptr, _stream
+    fe = ssf.Frontend(64, device=dev.index)
+    pb = _planes(fe, dev, [frame(0, 6, n_az=1875)[0]])
+    total = pb.xyzi.shape[0]
+    t = lambda *shape, dt=torch.float32: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
+    normal, valid = t(total, 3), t(total, dt=torch.uint8)
+    sx, si, img, head = t(total, 4), t(total, dt=torch.int32), t(total, 4), t(total, dt=torch.int32)
+    L = _abi.lib()
+    base = (fe._h, _stream(dev), 1, _ptr(pb.xyzi), _ptr(pb.off), _ptr(pb.count), pb.max_points,
+            _ptr(normal), _ptr(valid))
+    for args in ((_ptr(sx), _ptr(si), _ptr(img), None), (_ptr(sx), _ptr(si), None, _ptr(head)),
+                 (None, None, _ptr(img), _ptr(head))):
+        assert L.ssf_plane_table_batch(*base, *args) != 0
+        assert b"strip image" in L.ssf_last_error(fe._h)
+    assert L.ssf_plane_table_batch(*base, _ptr(sx), _ptr(si), _ptr(img), _ptr(head)) == 0
+    torch.cuda.synchronize()

@@ -5,8 +5,8 @@
 //   k_bin_scan    per-frame exclusive scans -> per-(chunk,row) bases and row offsets
 //   k_bin_curv    the stable per-row partition (:73-80) AND the 11-tap curvature (:84-107) of
 //                 one 2048-point input chunk: the chunk plus a halo of input points on both
-//                 sides is ranked per row (wave ballot "match" on the 6-bit row id, waves in
-//                 order -> the reference's push_back order), regrouped by row in LDS, and each
+//                 sides is ranked per row (per-row lane words in LDS, waves in order -> the
+//                 reference's push_back order), regrouped by row in LDS, and each
 //                 chunk point's stencil is read from its row's run in that tile.  Out: per ring
 //                 position the point's input index (4 B) and a candidate flag byte (planar, and
 //                 edge when asked) -- the ring-ordered cloud itself is never written (debug only)

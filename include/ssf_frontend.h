@@ -319,6 +319,25 @@ int32_t ssf_mask_pose_batch_f64(ssf_ctx* ctx, void* stream, int32_t n_frames, co
                                 const int64_t* h_frame_off, int32_t mode, const uint8_t* d_mask_in,
                                 const double* h_draws, int32_t reflection, uint8_t* d_bg_mask,
                                 double* d_out);
+/* slove_RT_by_SVD + Quaternion(matrix=R) on FLOAT32 arrays, per frame, as numpy runs them when
+ * the inputs are float32: the ASF block on the network's float32 flow
+ * (scripts/ActiveSceneFlow/main_sju_occ_ros.py:273-284, slove_RT_by_SVD :455-473).
+ * Replaces the f64 tail that ssf_mask_pose_batch computes (the reference's behaviour on float64
+ * inputs) with the reference's float32 arithmetic: f32 src = dst + flow, row-order f32 means,
+ * f32 centring, R and t rounded to f32 (oracle/ssf_oracle.c orc_kabsch_f32 restates each step).
+ *   source rows: d_flow != NULL -> f32(d_dst + d_flow) (target = points + move_gt, :273), with
+ *                d_src ignored; d_flow == NULL -> d_src (slove_RT_by_SVD(src, dst) directly).
+ *   d_mask   nullable uint8 per point: rows with mask != 0 (the background of ssf_mask_pose_batch's
+ *            d_bg_mask); NULL = every row.
+ *   after_mask 1: d_out holds ssf_mask_pose_batch's results for these frames (same stream, before
+ *            this call); T, Q, R, NBG and STATUS are replaced, the fit fields kept, and frames with
+ *            SSF_POSE_GMM_FAILED / SSF_POSE_SYNC_FAILED left as they are.  0: d_out is written whole.
+ *   d_out    [F * SSF_POSE_OUT_STRIDE] doubles (SSF_POSE_OUT_* below); R / t hold float32 values.
+ * Asynchronous on stream.  One work-group per frame; the two means are serial in row order. */
+int32_t ssf_kabsch_f32_batch(ssf_ctx* ctx, void* stream, int32_t n_frames, const float* d_src,
+                             const float* d_dst, const float* d_flow, const int64_t* d_frame_off,
+                             const uint8_t* d_mask, int32_t reflection, int32_t after_mask,
+                             double* d_out);
 /* Work-groups per frame of the GMM fit in ssf_mask_pose_batch (no reference counterpart;
  * results do not depend on it beyond f64 summation order): 0 = automatic (as many as keep the
  * chip full: ~256 / frames, at most 32; 1 for 256 frames and more), 1..32 = fixed.  With more

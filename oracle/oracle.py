@@ -112,6 +112,8 @@ def lib():
     L.orc_kabsch.restype = C.c_int32
     L.orc_quat_from_R.argtypes = [f64p, f64p]
     L.orc_quat_from_R.restype = C.c_int32
+    L.orc_kabsch_f32.argtypes = [f32p, f32p, C.c_int64, C.c_void_p, C.c_int32, f64p, f64p, f64p]
+    L.orc_kabsch_f32.restype = C.c_int32
     L.orc_svd3.argtypes = [f64p, f64p, f64p, f64p]
     L.orc_voxel_grid.argtypes = [f32p, C.c_int64, C.c_float, f32p]
     L.orc_voxel_grid.restype = C.c_int64
@@ -418,12 +420,30 @@ def svd3(A):
     return U.reshape(3, 3), S, Vt.reshape(3, 3)
 
 
-def mask_and_pose(points, flow, draws):
+def kabsch_f32(pos, flow, mask=None, reflection=0):
+    """slove_RT_by_SVD(points[bg] + flow[bg], points[bg]) + Quaternion on float32 arrays, as the
+    ASF block runs it (main_sju_occ_ros.py:273-284, :455-473); see orc_kabsch_f32.
+    -> rc, R (3, 3) f32 values, t (3,) f32 values, q_xyzw (4,)"""
+    pos = np.ascontiguousarray(pos, np.float32)
+    flow = np.ascontiguousarray(flow, np.float32)
+    R = np.zeros(9); t = np.zeros(3); q = np.zeros(4)
+    m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    rc = lib().orc_kabsch_f32(pos.reshape(-1), flow.reshape(-1), pos.shape[0],
+                              m.ctypes.data if m is not None else None, reflection, R, t, q)
+    return rc, R.reshape(3, 3), t, q
+
+
+def mask_and_pose(points, flow, draws, kabsch_dtype="float64"):
     """PointCloudOdometry_noSeg.py:97-125 restated: GMM mask, Kabsch(points+flow, points),
-    quaternion.  -> dict(labels, bg_mask, R, t, q_xyzw, info, rc)"""
+    quaternion.  kabsch_dtype "float32": the Kabsch + quaternion tail on float32 arrays, as the
+    ASF block runs it on float32 network flow (kabsch_f32).
+    -> dict(labels, bg_mask, R, t, q_xyzw, info, rc)"""
     X = np.concatenate([np.asarray(flow, np.float64), np.asarray(points, np.float64)], axis=1)
     lab, info, means = gmm_labels(X, draws)
     bg = (lab == int(info["bg_label"])).astype(np.uint8)
+    if kabsch_dtype == "float32":
+        rc, R, t, q = kabsch_f32(points, flow, bg)
+        return dict(labels=lab, bg_mask=bg, R=R, t=t, q_xyzw=q, info=info, means=means, rc=rc)
     p = np.asarray(points, np.float64)
     rc, R, t = kabsch(p + np.asarray(flow, np.float64), p, bg)
     qrc, q = quat_from_R(R) if rc == 0 else (rc, np.zeros(4))

@@ -1219,3 +1219,112 @@ int32_t orc_quat_from_R(const double R[9], double q[4]) {
     q[0] = x * f; q[1] = y * f; q[2] = z * f; q[3] = w * f;
     return 0;
 }
+
+/* The ASF block's float32 tail (main_sju_occ_ros.py:273-284): the network flow is
+ * float32, so `target = points[bg] + move_gt[bg]` (:273) and every line of slove_RT_by_SVD
+ * (:455-473) run on float32 arrays.  Restated step by step:
+ *   - src = f32(pos + flow), dst = pos (the numpy f32 add of :273-274);
+ *   - src.mean(axis=0): numpy's add.reduce over axis 0 of a C-ordered (n, 3) array accumulates
+ *     row after row into the f32 output, starting from the first row (no pairwise summation on
+ *     that axis); _mean then divides by the intp count (f64 loop, stored to f32: out=ret);
+ *   - centred f32 arrays (:461-462);
+ *   - H = src.T @ dst (:463) is an OpenBLAS sgemm whose summation order is not pinned: the exact
+ *     f32 products are summed in f64 here (measured 2e-7 from the fixture's R, tests);
+ *   - svd (LAPACK sgesdd on f32 H, unpinned) -> the f64 Jacobi SVD, R rounded to f32;
+ *   - det(R) < 0 as in orc_kabsch (:467-470);
+ *   - t = -R @ src_mean.T + dst_mean.T (:472): the 3-term f32 product rounded once, then the f32
+ *     add.
+ * R and t are returned as the f32 values (in doubles).  q: pyquaternion on the f32 R (recalled,
+ * parity unpinned): allclose(dot(R, R^T), I) with the dot in f32, the trace-method
+ * terms in f32, the 0.5 / sqrt(t) scale in f64.  Returns 0, -1 (no rows), -2 (reflection,
+ * reflection == 0) or -3 (not orthogonal); q is zero unless 0 is returned. */
+int32_t orc_kabsch_f32(const float* pos, const float* flow, int64_t n, const uint8_t* mask,
+                       int32_t reflection, double R_out[9], double t_out[3], double q[4]) {
+    float ss[3] = {0, 0, 0}, sd[3] = {0, 0, 0};
+    int64_t cnt = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (mask && !mask[i]) continue;
+        for (int d = 0; d < 3; ++d) {
+            const float s = pos[3 * i + d] + flow[3 * i + d];
+            const float p = pos[3 * i + d];
+            if (cnt == 0) { ss[d] = s; sd[d] = p; }
+            else { ss[d] = ss[d] + s; sd[d] = sd[d] + p; }
+        }
+        cnt++;
+    }
+    for (int k = 0; k < 4; ++k) q[k] = 0.0;
+    if (cnt == 0) return -1;
+    float ms[3], md[3];
+    for (int d = 0; d < 3; ++d) {
+        ms[d] = (float)((double)ss[d] / (double)cnt);
+        md[d] = (float)((double)sd[d] / (double)cnt);
+    }
+    double H[9] = {0};
+    for (int64_t i = 0; i < n; ++i) {
+        if (mask && !mask[i]) continue;
+        float a[3], b[3];
+        for (int d = 0; d < 3; ++d) {
+            a[d] = (pos[3 * i + d] + flow[3 * i + d]) - ms[d];
+            b[d] = pos[3 * i + d] - md[d];
+        }
+        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) H[r * 3 + c] += (double)a[r] * (double)b[c];
+    }
+    double U[9], S[3], Vt[9], R[9];
+    orc_svd3(H, U, S, Vt);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            double s = 0.0;
+            for (int k = 0; k < 3; ++k) s += Vt[k * 3 + r] * U[c * 3 + k];
+            R[r * 3 + c] = s;
+        }
+    int32_t rc = 0;
+    if (det3(R) < 0) {
+        if (!reflection) rc = -2;
+        for (int k = 0; k < 3; ++k) Vt[2 * 3 + k] *= -1.0;
+        if (reflection)
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) {
+                    double s = 0.0;
+                    for (int k = 0; k < 3; ++k) s += Vt[k * 3 + r] * U[c * 3 + k];
+                    R[r * 3 + c] = s;
+                }
+    }
+    float R32[9], t32[3];
+    for (int k = 0; k < 9; ++k) R32[k] = (float)R[k];
+    for (int r = 0; r < 3; ++r) {
+        const double dot = (double)R32[r * 3] * ms[0] + (double)R32[r * 3 + 1] * ms[1] + (double)R32[r * 3 + 2] * ms[2];
+        t32[r] = (float)(-dot) + md[r];
+    }
+    for (int k = 0; k < 9; ++k) R_out[k] = R32[k];
+    for (int r = 0; r < 3; ++r) t_out[r] = t32[r];
+    if (rc != 0) return rc;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            const float s = (R32[i * 3] * R32[j * 3] + R32[i * 3 + 1] * R32[j * 3 + 1]) + R32[i * 3 + 2] * R32[j * 3 + 2];
+            const double e = (i == j) ? 1.0 : 0.0;
+            if (!(fabs((double)s - e) <= 1e-8 + 1e-5 * fabs(e))) return -3;
+        }
+    float m[3][3];
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) m[i][j] = R32[j * 3 + i];
+    float t, w, x, y, z;
+    if (m[2][2] < 0) {
+        if (m[0][0] > m[1][1]) {
+            t = ((1.0f + m[0][0]) - m[1][1]) - m[2][2];
+            w = m[1][2] - m[2][1]; x = t; y = m[0][1] + m[1][0]; z = m[2][0] + m[0][2];
+        } else {
+            t = ((1.0f - m[0][0]) + m[1][1]) - m[2][2];
+            w = m[2][0] - m[0][2]; x = m[0][1] + m[1][0]; y = t; z = m[1][2] + m[2][1];
+        }
+    } else {
+        if (m[0][0] < -m[1][1]) {
+            t = ((1.0f - m[0][0]) - m[1][1]) + m[2][2];
+            w = m[0][1] - m[1][0]; x = m[2][0] + m[0][2]; y = m[1][2] + m[2][1]; z = t;
+        } else {
+            t = ((1.0f + m[0][0]) + m[1][1]) + m[2][2];
+            w = t; x = m[1][2] - m[2][1]; y = m[2][0] - m[0][2]; z = m[0][1] - m[1][0];
+        }
+    }
+    const double f = 0.5 / sqrt((double)t);
+    q[0] = (double)x * f; q[1] = (double)y * f; q[2] = (double)z * f; q[3] = (double)w * f;
+    return 0;
+}

@@ -126,6 +126,10 @@ int32_t orc_kabsch(const double* src, const double* dst, int64_t n, const uint8_
                    int32_t reflection, double R[9], double t[3]);
 /* pyquaternion Quaternion(matrix=R) trace method -> q (x,y,z,w); -3 if not orthogonal */
 int32_t orc_quat_from_R(const double R[9], double q[4]);
+/* slove_RT_by_SVD + Quaternion on float32 arrays (the ASF block, main_sju_occ_ros.py:273-284):
+ * src = pos + flow in f32, dst = pos, mask rows only; R, t are the f32 results */
+int32_t orc_kabsch_f32(const float* pos, const float* flow, int64_t n, const uint8_t* mask,
+                       int32_t reflection, double R[9], double t[3], double q[4]);
 void orc_svd3(const double A[9], double U[9], double S[3], double Vt[9]);
 
 /* ---- mapOptmization loop closure, oracle/loop_oracle.c ---- */

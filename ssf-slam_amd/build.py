@@ -13,8 +13,8 @@ OUT_DIR = os.path.join(HERE, "ssf", "_lib")
 OBJ_DIR = os.path.join(HERE, "build")
 LIB = os.path.join(OUT_DIR, "libssf_frontend.so")
 SYNTH_LIB = os.path.join(OUT_DIR, "libssf_synth.so")
-SOURCES = ["abi.hip", "features.hip", "registration.hip", "mask_pose.hip", "mask_pose_f64.hip", "loop.hip",
-           "pointnet2.hip"]
+SOURCES = ["abi.hip", "features.hip", "registration.hip", "mask_pose.hip", "mask_pose_f64.hip", "kabsch_f32.hip",
+           "loop.hip", "pointnet2.hip"]
 # sources that include another source file
 SRC_DEPS = {"mask_pose_f64.hip": ["mask_pose.hip"]}
 HEADERS = ["ssf_device.hpp", "ssf_internal.hpp", "svd3.hpp", os.path.join("..", "..", "include", "ssf_frontend.h"),

@@ -747,6 +747,23 @@ int32_t ssf_mask_pose_batch_f64(ssf_ctx* c, void* stream, int32_t n_frames, cons
                            d_mask_in, h_draws, reflection, d_bg_mask, d_out);
 }
 
+int32_t ssf_kabsch_f32_batch(ssf_ctx* c, void* stream, int32_t n_frames, const float* d_src,
+                             const float* d_dst, const float* d_flow, const int64_t* d_frame_off,
+                             const uint8_t* d_mask, int32_t reflection, int32_t after_mask,
+                             double* d_out) {
+    if (!c) return SSF_E_ARG;
+    if (n_frames < 0 || (n_frames > 0 && (!d_dst || (!d_flow && !d_src) || !d_frame_off || !d_out)))
+        return fail(c, SSF_E_ARG, "kabsch_f32_batch: bad arguments");
+    if (n_frames == 0) return SSF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    ProfScope prof(c, stream);
+    hipError_t e = ssf::launch_kabsch_f32(s, n_frames, d_src, d_dst, d_flow, d_frame_off, d_mask,
+                                          reflection ? 1 : 0, after_mask ? 1 : 0, d_out);
+    if (e != hipSuccess) return hip_fail(c, e, "kabsch_f32 launch");
+    return SSF_OK;
+}
+
 int32_t ssf_accumulate_sequence(ssf_ctx* c, void* stream, int32_t n, const double* d_rel,
                                 const double* h_start, double* d_abs) {
     if (!c) return SSF_E_ARG;

@@ -127,6 +127,12 @@ hipError_t launch_mask_pose(hipStream_t s, int n_frames, const double* pts, cons
                             const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
                             double* out, int G, int slots, uint32_t* sync, double* parts);
 int mask_pose_slots(int device);
+// ---- launcher (kabsch_f32.hip): the float32 slove_RT_by_SVD + Quaternion tail per frame; source
+// rows = dst + flow (f32) when flow is given, else src; keep_failures: leave frames whose status
+// is SSF_POSE_GMM_FAILED / SSF_POSE_SYNC_FAILED (a k_mask_pose output) untouched.
+hipError_t launch_kabsch_f32(hipStream_t s, int n_frames, const float* src, const float* dst,
+                             const float* flow, const int64_t* frame_off, const uint8_t* mask,
+                             int reflection, int keep_failures, double* out);
 size_t mask_sync_bytes(int n_frames);
 size_t mask_parts_bytes(int n_frames, int G);
 

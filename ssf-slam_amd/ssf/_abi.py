@@ -32,7 +32,7 @@ EXPORTS = [
     "ssf_extract_planes_batch_masked", "ssf_register_pair", "ssf_profile_enable",
     "ssf_profile_read", "ssf_set_mask_split", "ssf_mask_pose_batch_f64",
     "ssf_edge_config_default", "ssf_set_edge_config", "ssf_extract_features_batch",
-    "ssf_edge_table_batch", "ssf_register_batch_edges",
+    "ssf_edge_table_batch", "ssf_register_batch_edges", "ssf_kabsch_f32_batch",
 ]
 # Every symbol include/ssf_pointnet2.h declares (TFlow point-set operators).
 PN2_EXPORTS = [
@@ -135,6 +135,8 @@ def lib():
     L.ssf_mask_pose_batch.restype = i32
     L.ssf_mask_pose_batch_f64.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, i32, vp, vp]
     L.ssf_mask_pose_batch_f64.restype = i32
+    L.ssf_kabsch_f32_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, i32, i32, vp]
+    L.ssf_kabsch_f32_batch.restype = i32
     L.ssf_edge_config_default.argtypes = [i32, C.POINTER(EdgeConfig)]
     L.ssf_edge_config_default.restype = i32
     L.ssf_set_edge_config.argtypes = [vp, C.POINTER(EdgeConfig)]

@@ -364,6 +364,27 @@ class Frontend:
         self._check(rc, name)
         return out[:F], (bg[:total] if bg is not None else None)
 
+    def kabsch_f32(self, dst, off, h_off, src=None, flow=None, mask=None, reflection=0, out=None):
+        """slove_RT_by_SVD + Quaternion on float32 arrays per frame (ssf_kabsch_f32_batch, the ASF
+        block's arithmetic, main_sju_occ_ros.py:273-284): source rows dst + flow (f32) or src;
+        rows with mask != 0.  out: mask_pose()'s output for the same frames (its fit fields are
+        kept, T / Q / R / NBG / STATUS replaced in place), or None for a fresh [F, 32] tensor."""
+        dst = self._dev(dst, torch.float32)
+        src = None if src is None else self._dev(src, torch.float32)
+        flow = None if flow is None else self._dev(flow, torch.float32)
+        if (src is None) == (flow is None):
+            raise SSFError("kabsch_f32: give exactly one of src / flow")
+        mask = None if mask is None else self._dev(mask, torch.uint8)
+        F = h_off.numel() - 1
+        after = out is not None
+        if out is None:
+            out = torch.empty((max(F, 1), _abi.POSE_OUT_STRIDE), dtype=torch.float64, device=self.device)
+        rc = _abi.lib().ssf_kabsch_f32_batch(self._h, _stream(self.device), F, _ptr(src), _ptr(dst),
+                                             _ptr(flow), _ptr(off), _ptr(mask), int(reflection),
+                                             1 if after else 0, _ptr(out))
+        self._check(rc, "ssf_kabsch_f32_batch")
+        return out[:F]
+
     def accumulate_sequence(self, rel, start=None):
         rel = self._dev(rel, torch.float64)
         n = rel.shape[0]

@@ -66,12 +66,28 @@ def _raise_status(st):
         raise ValueError("Fitting the mixture model failed (ill-defined empirical covariance)")
 
 
-def slove_RT_by_SVD(src, dst, reflection: str = "raise", device=None):
+def _check_kabsch_dtype(kabsch_dtype):
+    if kabsch_dtype not in ("float64", "float32"):
+        raise ValueError(f"kabsch_dtype must be 'float64' or 'float32', not {kabsch_dtype!r}")
+
+
+def slove_RT_by_SVD(src, dst, reflection: str = "raise", device=None, kabsch_dtype: str = "float64"):
     """R (3,3), t (3,1) minimising |R src + t - dst| (reference signature, float64 results).
     float64 inputs run the f64-storage kernel (no input rounding); float32 inputs the f32 one.
     The kernel takes (pos, flow) = (dst, src - dst) and forms src = pos + flow in f64: exact
-    for f32 inputs, and within an ulp of src for f64 inputs."""
+    for f32 inputs, and within an ulp of src for f64 inputs.
+    kabsch_dtype "float32": numpy's float32 arithmetic on float32 arrays (ssf_kabsch_f32_batch;
+    the inputs are rounded to float32 first), R / t hold float32 values."""
+    _check_kabsch_dtype(kabsch_dtype)
     fe = _frontend(device)
+    if kabsch_dtype == "float32":
+        dst_t = _as_dev(dst, fe.device, torch.float32)
+        src_t = _as_dev(src, fe.device, torch.float32)
+        off, h_off = frame_offsets([dst_t.shape[0]], fe.device)
+        o = fe.kabsch_f32(dst_t, off, h_off, src=src_t, reflection=1 if reflection == "fix" else 0)[0].cpu().numpy()
+        if int(o[_abi.POSE_OUT["STATUS"]]) == _abi.POSE_REFLECTION and reflection != "fix":
+            _raise_status(o[_abi.POSE_OUT["STATUS"]])
+        return o[7:16].reshape(3, 3).copy(), o[0:3].reshape(3, 1).copy()
     dt = _storage(src, dst)
     dst_t = _as_dev(dst, fe.device, dt)
     src_t = _as_dev(src, fe.device, dt)
@@ -116,13 +132,19 @@ class MaskPose(tuple):
 
 
 def mask_and_pose(points, flow, mode: str = "gmm", gt_mask=None, seed: int | None = None,
-                  draws=None, reflection: str = "raise", device=None, frame_sizes=None):
+                  draws=None, reflection: str = "raise", device=None, frame_sizes=None,
+                  kabsch_dtype: str = "float64"):
     """The PointCloudOdometry_noSeg.py:97-125 block for one frame (or F frames packed back to
     back with `frame_sizes`).  mode 'gmm' (GaussianMixture on [flow, xyz]), 'gt'
     (background = s_fg_mask == 0, PointCloudOdometry.py:91) or 'given' (background = mask != 0).
+    kabsch_dtype "float64" (default): the Kabsch + quaternion tail in f64, the reference's
+    arithmetic on float64 arrays; "float32": the reference's float32 arithmetic, as the ASF block
+    runs it on float32 network flow (main_sju_occ_ros.py:273-284; inputs stored as float32,
+    ssf_kabsch_f32_batch after the mask kernel, same stream).
     -> MaskPose: (R, t, q_xyzw, bg_mask), plus keyed batched fields (see MaskPose)."""
+    _check_kabsch_dtype(kabsch_dtype)
     fe = _frontend(device)
-    dt = _storage(points, flow)
+    dt = torch.float32 if kabsch_dtype == "float32" else _storage(points, flow)
     pts = _as_dev(points, fe.device, dt)
     fl = _as_dev(flow, fe.device, dt)
     sizes = [pts.shape[0]] if frame_sizes is None else list(frame_sizes)
@@ -137,6 +159,9 @@ def mask_and_pose(points, flow, mode: str = "gmm", gt_mask=None, seed: int | Non
         m = m.to(fe.device, torch.uint8).contiguous()
     out, bg = fe.mask_pose(pts, fl, off, h_off, mode=mode, mask_in=m, draws=draws,
                            reflection=1 if reflection == "fix" else 0)
+    if kabsch_dtype == "float32":
+        fe.kabsch_f32(pts, off, h_off, flow=fl, mask=bg, reflection=1 if reflection == "fix" else 0,
+                      out=out)
     o = out.cpu().numpy()
     for st in o[:, _abi.POSE_OUT["STATUS"]]:
         if int(st) != 0:

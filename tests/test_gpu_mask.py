@@ -340,3 +340,61 @@ def test_asf_f32_block(oracle, dev, case):
     # stable frames -> identical mask and EM iteration count, pose = the exact Kabsch of that mask
     from test_oracle_golden import asf_check
     asf_check(case, bg, res["info"]["em_iter"][0], res["t"][0])
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_asf_f32_kabsch_tail(oracle, dev, case):
+    """a19 closed: the GMM on device + ssf_kabsch_f32_batch, the float32
+    slove_RT_by_SVD / Quaternion tail of main_sju_occ_ros.py:273-284.  Against the oracle's
+    float32 restatement (orc_kabsch_f32) on the same inputs, and on the stable frames against the
+    reference's own float32 R / t within 1e-6 (tests/test_oracle_golden.py F32_TAIL_BAR)."""
+    import ssf
+    from test_oracle_golden import F32_TAIL_BAR, asf_case_bars
+    g = np.load(os.path.join(GOLDEN, "gmm_asf_f32.npz"))
+    p, f, d = g[f"pos1_{case}"], g[f"flow_{case}"], g[f"draws_{case}"]
+    res = ssf.mask_and_pose(p, f, draws=d[None, :], kabsch_dtype="float32")
+    ref = oracle.mask_and_pose(p, f, d, kabsch_dtype="float32")
+    bg = res["bg_mask"].cpu().numpy()
+    assert ref["rc"] == 0
+    if np.array_equal(bg, ref["bg_mask"]):          # same rows: the same float32 arithmetic
+        assert np.abs(res["R"][0] - ref["R"]).max() < 1e-6
+        assert np.abs(res["t"][0] - ref["t"]).max() < 1e-6
+        assert np.abs(res["q_xyzw"][0] - ref["q_xyzw"]).max() < 1e-6
+    assert np.array_equal(res["R"][0], res["R"][0].astype(np.float32))   # float32 values
+    b = asf_case_bars(case)
+    bg_ref = (g[f"labels_{case}"] == int(g[f"bg_label_{case}"])).astype(np.uint8)
+    if b["stable"]:
+        assert np.array_equal(bg, bg_ref)
+        assert int(res["info"]["em_iter"][0]) == b["n_iter"]
+        assert np.abs(res["R"][0] - g[f"R_{case}"]).max() < F32_TAIL_BAR["R"]
+        assert np.abs(res["t"][0] - g[f"t_{case}"]).max() < F32_TAIL_BAR["t"]
+    else:
+        assert np.abs(res["t"][0] - g[f"t_{case}"]).max() <= b["t_spread"]
+    # the fit fields of the mask kernel are kept
+    assert int(res["info"]["em_iter"][0]) >= 1 and res["info"]["n_bg"][0] == bg.sum()
+
+
+def test_slove_RT_by_SVD_float32(oracle, dev):
+    """slove_RT_by_SVD(src, dst, kabsch_dtype='float32') on float32 arrays = numpy's own float32
+    run of the reference function's lines (:455-473), ValueError on a reflection, on no rows."""
+    import ssf
+    rng = np.random.default_rng(11)
+    dst = (rng.standard_normal((6000, 3)) * 20).astype(np.float32)
+    ang = 0.03
+    Rt = np.array([[np.cos(ang), -np.sin(ang), 0], [np.sin(ang), np.cos(ang), 0], [0, 0, 1]])
+    src = (dst @ Rt.T + np.array([0.8, -0.1, 0.02]) + rng.standard_normal((6000, 3)) * 0.01).astype(np.float32)
+    R, t = ssf.slove_RT_by_SVD(src, dst, kabsch_dtype="float32")
+    sm, dm = src.mean(axis=0, keepdims=True), dst.mean(axis=0, keepdims=True)
+    U, S, Vt = np.linalg.svd((src - sm).T @ (dst - dm))
+    Rn = Vt.T @ U.T
+    tn = -Rn @ sm.T + dm.T
+    assert R.shape == (3, 3) and t.shape == (3, 1)
+    assert np.abs(R - Rn).max() < 1e-6 and np.abs(t - tn).max() < 2e-6
+    with pytest.raises(ValueError):
+        ssf.slove_RT_by_SVD(src, -src, kabsch_dtype="float32")
+    R2, _ = ssf.slove_RT_by_SVD(src, -src, reflection="fix", kabsch_dtype="float32")
+    assert abs(np.linalg.det(R2) - 1) < 1e-5
+    c = np.load(os.path.join(GOLDEN, "gmm_noseg_case0.npz"))
+    with pytest.raises(ValueError):
+        ssf.mask_and_pose(c["pos1"], c["flow"], mode="given", gt_mask=np.zeros(len(c["pos1"]), np.uint8),
+                          kabsch_dtype="float32")

@@ -70,7 +70,8 @@ def parse(argv=None):
                     help="ranks (one per GPU); without WORLD_SIZE in the env, bench.py starts them")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="sequences in flight per GPU")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="sequences in flight per GPU (default 256; 1 with --consecutive)")
     ap.add_argument("--n-az", type=int, default=1875,
                     help="azimuth steps (64 x 1875 = 120k pts; 4000 -> 256k, BASELINE configs[4])")
     ap.add_argument("--rows", type=int, default=64)
@@ -111,6 +112,14 @@ def parse(argv=None):
                     help="BASELINE configs[2] as written: K consecutive frame pairs of each sequence "
                          "per step (mask of K frames in one launch, masked features, K chained "
                          "registrations); --batch sequences side by side")
+    ap.add_argument("--sequences-total", type=int, default=0,
+                    help="BASELINE configs[3] as written: this many sequences in total, sharded over "
+                         "the --gpus ranks (strong scaling), --consecutive K (default 32) frames of "
+                         "each per step, chained registrations, one pose all-gather at the end")
+    ap.add_argument("--kabsch-warm-start", action="store_true",
+                    help="with --consecutive / --sequences-total (beyond the reference): warm-start "
+                         "every pair from its own SSF Kabsch pose, so all pairs of a step are "
+                         "independent (two registration launches per step instead of K)")
     ap.add_argument("--latency", action="store_true",
                     help="BASELINE configs[1] as written: one frame pair at a time (B = 1), ms per frame")
     ap.add_argument("--mask-streams", type=int, default=3,
@@ -598,29 +607,74 @@ def latency(args):
     print(json.dumps(line), flush=True)
 
 
-def consecutive(args):
-    """BASELINE configs[2] as written: the PointCloudOdometry_noSeg.py path with the scene-flow
-    mask applied before the features, on a batch of K consecutive frame pairs of ONE sequence
-    (--consecutive K; --batch B runs B such sequences side by side).  One step = the next K frames
-    of every sequence: one mask launch (GMM + Kabsch) for the B x K frames, masked features and the
-    plane table of those frames in one launch each, then the K chained registrations (the warm
-    start of pair k is the solution of pair k - 1, lidarOdometry_onlyPC.cpp:164-169,251-252), one
-    launch of B pairs each.  Masks of consecutive steps alternate over --mask-streams streams, and
-    the registrations of step j overlap the mask of step j + 1.  Prints one JSON line."""
+def _init_dist(args, world, rank, dev):
+    """process group for N > 1 (RCCL, or gloo for a one-GPU rehearsal) -> backend name or None"""
+    import torch.distributed as dist
+    if world <= 1:
+        return None
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    backend = "gloo" if args.rehearse_one_gpu else "nccl"
+    if backend == "gloo":
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    if dist.get_world_size() != args.gpus:
+        sys.exit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    return backend
+
+
+def sequences(args, world=1, rank=0, local=0):
+    """Whole sequences, K consecutive frames of each per step.
+    * BASELINE configs[2] as written (--consecutive K, one GPU): the PointCloudOdometry_noSeg.py
+      path with the scene-flow mask applied before the features, K consecutive frame pairs of
+      each of --batch sequences per step.
+    * BASELINE configs[3] as written (--sequences-total S, 1..8 ranks): a FIXED set of S
+      sequences sharded over the ranks (ssf.dist.sequence_shard: one per GPU at 8 GPUs, like one
+      launch graph per CARLA sequence, run_noSeg.launch:4,15-16), every rank running its own
+      sequences' frames; one deferred all-gather of the per-frame 6-DoF pose records at the end
+      (RCCL over xGMI).  Strong scaling: the total work is the same at every N.  The reference's
+      wiring (frameFeature sees every point, the mask runs beside it) unless --mask-before-features.
+    One step = the next K frames of every owned sequence: one mask launch (GMM + Kabsch) for the
+    B x K frames, features + plane table of them in one launch each, then the registrations:
+    chained (default; the warm start of pair k is the solution of pair k - 1,
+    lidarOdometry_onlyPC.cpp:164-169,251-252), K launches of B pairs; or, with
+    --kabsch-warm-start (beyond the reference), every pair warm-started from its own SSF Kabsch
+    pose, which the mask launch already produced (on the SSF path the reference publishes that pose
+    itself, lidarOdometry.cpp:145-159), so the B x K pairs are independent: two launches per step.
+    Masks of consecutive steps alternate over --mask-streams streams; registrations of step j
+    overlap the mask of step j + 1.  Rank 0 prints one JSON line."""
     import torch
+    import torch.distributed as dist
     import ssf
     from ssf import synth
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
-    K, B = args.consecutive, args.batch
+    from ssf import dist as sd
+    strong = args.sequences_total > 0
+    if args.rehearse_one_gpu:
+        local = 0
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    backend = _init_dist(args, world, rank, dev)
+    K = args.consecutive or 32
+    if strong:
+        shard = list(sd.sequence_shard(args.sequences_total, world, rank))
+        seeds = shard                         # a sequence's data does not depend on N
+        masked = bool(args.mask_before_features)
+    else:
+        seeds = list(range(args.batch or 1))
+        masked = True                         # configs[2] as written: mask before features
+    B = len(seeds)
     iters = args.iters or (10 if args.solver == "gn" else 8)
     N = args.rows * args.n_az
     W, S = max(1, args.warmup), args.steps
     n_steps = W + S
+    per_step_bytes = K * B * N * 24
+    if per_step_bytes * n_steps > 120e9:
+        sys.exit(f"bench.py: {n_steps} steps x {K} x {B} frames of {N} points need "
+                 f"{per_step_bytes * n_steps / 1e9:.0f} GB resident; lower --batch / --consecutive")
     t_data = time.perf_counter()
     # frame 0 of every sequence (the prologue), then per step K frames, frame-major:
     # buffer index kk * B + b holds frame j K + kk + 1 of sequence b
-    scanner = synth.BatchScanner(list(range(B)), K * n_steps + 1, n_rows=args.rows, n_az=args.n_az, device=dev)
+    scanner = synth.BatchScanner(seeds, K * n_steps + 1, n_rows=args.rows, n_az=args.n_az, device=dev)
     pro = (torch.empty((B * N, 3), dtype=torch.float32, device=dev),
            torch.empty((B * N, 3), dtype=torch.float32, device=dev))
     scanner.frame(0, *pro)
@@ -635,81 +689,159 @@ def consecutive(args):
     t_data = time.perf_counter() - t_data
     off1, h1 = ssf.frame_offsets([N] * B, dev)
     offK, hK = ssf.frame_offsets([N] * (K * B), dev)
-    fe_mask = ssf.Frontend(args.rows, device=0)
+    fe_mask = ssf.Frontend(args.rows, device=dev.index)
     fe_mask.reserve(K * B, N)
     fe_mask.mask_split(args.mask_split)
-    fe_mask.seed(20240000)
-    fe_feat = ssf.Frontend(args.rows, device=0, solver=args.solver, max_iter=iters)
+    fe_mask.seed(20240000 + (shard[0] if strong and shard else 0))
+    fe_feat = ssf.Frontend(args.rows, device=dev.index, solver=args.solver, max_iter=iters)
     fe_feat.reserve(K * B, N)
-    fe_reg = ssf.Frontend(args.rows, device=0, solver=args.solver, max_iter=iters)
-    fe_reg.reserve(B, N)
+    fe_reg = ssf.Frontend(args.rows, device=dev.index, solver=args.solver, max_iter=iters)
+    fe_reg.reserve(K * B, N)
     s_masks = [torch.cuda.Stream(dev) for _ in range(max(1, args.mask_streams))]
     s_feat = torch.cuda.Stream(dev, priority=args.feat_priority)
     s_reg = torch.cuda.Stream(dev, priority=args.feat_priority)
     rel, ab = ssf.identity_poses(B, dev), ssf.identity_poses(B, dev)
+    kws = args.kabsch_warm_start
 
-    def view(pb, table, kk):
-        """the B frames of buffer slot kk as a PlaneBatch (+ the table arrays, shared)"""
-        return ssf.PlaneBatch(pb.xyzi, pb.count[kk * B:(kk + 1) * B], pb.off[kk * B:(kk + 1) * B + 1],
-                              pb.h_off[kk * B:(kk + 1) * B + 1], pb.max_points), table
+    def view(pb, table, a, b=None):
+        """frames of buffer slots [a, b) as a PlaneBatch (the table arrays are shared: they are
+        indexed by the frames' point offsets)"""
+        b = a + 1 if b is None else b
+        return ssf.PlaneBatch(pb.xyzi, pb.count[a * B:b * B], pb.off[a * B:b * B + 1],
+                              pb.h_off[a * B:b * B + 1], pb.max_points), table
 
-    # prologue: frame 0 -> the first last frames
+    def warm_start(out):
+        """the SSF Kabsch poses [t, q] of mask_pose -> registration warm starts [q, t] (identity
+        where the mask reported a failure)"""
+        w = torch.cat([out[:, 3:7], out[:, 0:3]], 1)
+        ok = (out[:, 16] == 0).unsqueeze(1)
+        return torch.where(ok, w, ssf.identity_poses(out.shape[0], dev)).contiguous()
+
+    # prologue: frame 0 -> the first last frames (and its Kabsch pose: pair (0, 1)'s warm start)
     with torch.cuda.stream(s_feat):
-        _, bg0 = fe_mask.mask_pose(pro[0], pro[1], off1, h1, mode="gmm", want_mask=True)
-        pb0 = fe_feat.extract_planes_batch(pro[0], off1, h1, max_points=N, keep=bg0)
+        out0, bg0 = fe_mask.mask_pose(pro[0], pro[1], off1, h1, mode="gmm", want_mask=True)
+        pb0 = fe_feat.extract_planes_batch(pro[0], off1, h1, max_points=N, keep=bg0 if masked else None)
         last = (pb0, fe_feat.plane_table(pb0))
     torch.cuda.synchronize(dev)
+    prev_out = out0
+    records = []
 
-    def step(j, ev=None):
-        nonlocal last
+    def step(j, timing):
+        nonlocal last, prev_out
         pos, flow = steps[j]
         sm = s_masks[j % len(s_masks)]
         with torch.cuda.stream(sm):
             out, bg = fe_mask.mask_pose(pos, flow, offK, hK, mode="gmm", want_mask=True)
             done = torch.cuda.Event()
             done.record(sm)
-        s_feat.wait_event(done)
-        bg.record_stream(s_feat)
+        if masked:
+            s_feat.wait_event(done)
+            bg.record_stream(s_feat)
         with torch.cuda.stream(s_feat):
-            pb = fe_feat.extract_planes_batch(pos, offK, hK, max_points=N, keep=bg)
+            pb = fe_feat.extract_planes_batch(pos, offK, hK, max_points=N, keep=bg if masked else None)
             table = fe_feat.plane_table(pb)
             tdone = torch.cuda.Event()
             tdone.record(s_feat)
         s_reg.wait_event(tdone)
         for t in (pb.xyzi, pb.count, *table.tensors()):
             t.record_stream(s_reg)
+        if kws:
+            s_reg.wait_event(done)
+            out.record_stream(s_reg)
         with torch.cuda.stream(s_reg):
-            for kk in range(K):
-                cur = view(pb, table, kk)
-                (lpb, ltab) = last
-                fe_reg.register(lpb, ltab, cur[0], rel, ab)
-                last = cur
+            (lpb, ltab) = last
+            if kws:
+                # pair (slot kk - 1 -> slot kk) starts from the Kabsch pose of frame kk - 1
+                ws = torch.cat([warm_start(prev_out), warm_start(out[:(K - 1) * B])], 0)
+                fe_reg.register(lpb, ltab, view(pb, table, 0)[0], ws[:B])
+                if K > 1:
+                    fe_reg.register(*view(pb, table, 0, K - 1), view(pb, table, 1, K)[0], ws[B:])
+                rel_k = ws.view(K, B, 7)
+            else:
+                snaps = []
+                for kk in range(K):
+                    cur = view(pb, table, kk)
+                    fe_reg.register(lpb, ltab, cur[0], rel, ab)
+                    snaps.append(rel.clone())
+                    (lpb, ltab) = cur
+                rel_k = torch.stack(snaps, 0)
+            if timing:
+                records.append(torch.cat([rel_k, out[:, 0:7].view(K, B, 7)], 2))
+        last = view(pb, table, K - 1)
+        prev_out = out[(K - 1) * B:]
         return out
 
     for j in range(W):
-        step(j)
+        step(j, False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for j in range(W, W + S):
-        step(j)
+        step(j, True)
+    gathered = None
+    if world > 1:                  # the one exchange: every timed frame's records, one all-gather
+        cur = torch.cuda.current_stream(dev)
+        for s in (*s_masks, s_reg):
+            cur.wait_stream(s)
+        gathered = sd.gather_sequence_records(torch.cat(records, 0), args.sequences_total)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    frames = B * K * S
+    mine = torch.cat(records, 0)
+    gather_ok = None
+    finite = bool(torch.isfinite(mine).all())
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        gather_ok = bool(torch.equal(gathered[:, shard[0]:shard[-1] + 1].cpu(), mine.cpu())) if shard else True
+        flag = torch.tensor([1 if gather_ok and finite else 0], dtype=torch.int32,
+                            device="cpu" if backend == "gloo" else dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        gather_ok = bool(flag.item())
+    total_seq = args.sequences_total if strong else B
+    frames = total_seq * K * S
+    ws_note = ("every pair warm-started from its own SSF Kabsch pose (beyond the reference: "
+               "independent pairs, 2 launches per step)" if kws else
+               f"{K} chained registrations per step (warm start = previous solution)")
+    if strong:
+        workload = (f"configs[3] as written: {total_seq} sequences sharded over {world} GPU(s) "
+                    f"(sequence_shard), {K} consecutive frames of each per step, {S} steps "
+                    f"({K * S} timed frames per sequence); mask(GMM+Kabsch) "
+                    f"{'before' if masked else 'beside'} features + plane table + {args.solver} "
+                    f"x{iters}; {ws_note}; one all-gather of the per-frame pose records at the end")
+    else:
+        workload = (f"configs[2] as written: PointCloudOdometry_noSeg path, mask before features, "
+                    f"{K} consecutive frame pairs of each of {B} sequence(s) per step: one mask "
+                    f"launch of {K * B} frames, masked features + plane table of them, "
+                    f"{args.solver} x{iters}; {ws_note}")
     line = {
-        "metric": METRIC, "value": frames / elapsed, "unit": "frames/s", "n_gpus": 1, "steps": S,
-        "warmup": W, "ms_per_step": elapsed / S * 1e3, "higher_is_better": True, "scaling": "none",
-        "vs_baseline": None, "dtype": "f32 features / f64 mask+solve",
-        "data": f"synthetic (seeded ray-cast {args.rows}-beam scans, ssf/synth.py BatchScanner; {B} sequence(s))",
-        "config": {"workload": f"configs[2] as written: PointCloudOdometry_noSeg path, mask before features, "
-                               f"{K} consecutive frame pairs of each of {B} sequence(s) per step: one mask "
-                               f"launch of {K * B} frames, masked features + plane table of them, {K} chained "
-                               f"registrations ({args.solver} x{iters})",
-                   "consecutive_pairs": K, "sequences": B, "points_per_frame": N, "solver": args.solver,
-                   "iters": iters, "mask_before_features": True},
+        "metric": METRIC, "value": frames / elapsed, "unit": "frames/s", "n_gpus": world, "steps": S,
+        "warmup": W, "ms_per_step": elapsed / S * 1e3, "higher_is_better": True,
+        "scaling": "strong" if strong else "none", "vs_baseline": None,
+        "dtype": "f32 features / f64 mask+solve",
+        "data": f"synthetic (seeded ray-cast {args.rows}-beam scans, ssf/synth.py BatchScanner; "
+                f"{total_seq} sequence(s))",
+        "config": {"workload": workload, "consecutive_pairs": K, "sequences": total_seq,
+                   "sequences_this_rank": B, "frames_per_sequence_timed": K * S,
+                   "points_per_frame": N, "solver": args.solver, "iters": iters,
+                   "mask_before_features": masked, "kabsch_warm_start": bool(kws),
+                   "parallelism": f"sequence-sharded x{world}",
+                   "world_size_initialised": (dist.get_world_size() if world > 1 else 1),
+                   "backend": backend or "none",
+                   **({"rehearsal": "all ranks on one GPU, gloo"} if args.rehearse_one_gpu else {})},
+        "gather_check": gather_ok, "poses_finite": finite,
         "data_gen_s": round(t_data, 2),
-        "final_t_norm": float(ab[:, 4:].norm(dim=1).mean()),
+        "final_t_norm": float(mine[-1, :, 4:7].norm(dim=1).mean()),
     }
-    print(json.dumps(line), flush=True)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -718,10 +850,11 @@ def main():
         if args.gpus != 1 or os.environ.get("WORLD_SIZE", "1") != "1":
             sys.exit("bench.py --latency is a one-GPU, one-frame-pair measurement")
         return latency(args)
-    if args.consecutive:
+    if args.consecutive and not args.sequences_total:
         if args.gpus != 1 or os.environ.get("WORLD_SIZE", "1") != "1":
-            sys.exit("bench.py --consecutive is a one-GPU measurement (configs[2])")
-        return consecutive(args)
+            sys.exit("bench.py --consecutive is a one-GPU measurement (configs[2]); "
+                     "--sequences-total S is the multi-GPU configs[3] mode")
+        return sequences(args)
     ws = os.environ.get("WORLD_SIZE")
     if ws is None and args.gpus > 1:
         sys.exit(launch_ranks(args))
@@ -731,23 +864,29 @@ def main():
                  f"{world}-rank run as {args.gpus} GPUs")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.sequences_total and not args.launch_check:
+        return sequences(args, world, rank, local)
     if args.launch_check:
         import torch
         import torch.distributed as dist
+        from ssf.dist import sequence_shard
+        shard = list(sequence_shard(args.sequences_total, world, rank)) if args.sequences_total else None
         if world > 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             dist.init_process_group("gloo", rank=rank, world_size=world)
         got = [None] * world
         if world > 1:
-            dist.all_gather_object(got, dict(rank=rank, local=local, pid=os.getpid()))
+            dist.all_gather_object(got, dict(rank=rank, local=local, pid=os.getpid(), shard=shard))
         else:
-            got = [dict(rank=0, local=local, pid=os.getpid())]
+            got = [dict(rank=0, local=local, pid=os.getpid(), shard=shard)]
         if rank == 0:
             print(json.dumps({"launch_check": True, "n_gpus": args.gpus, "world": world,
                               "ranks": got}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
+    if args.batch is None:
+        args.batch = 256
     if args.warmup < 1:
         args.warmup = 1  # the first frame of a sequence has no last frame to register against
     cpu = None
@@ -760,16 +899,7 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    backend = None
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "gloo" if args.rehearse_one_gpu else "nccl"
-        if backend == "gloo":
-            dist.init_process_group("gloo", rank=rank, world_size=world)
-        else:
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-        if dist.get_world_size() != args.gpus:
-            sys.exit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    backend = _init_dist(args, world, rank, dev)
 
     import ssf
     iters = args.iters or (10 if args.solver == "gn" else 8)

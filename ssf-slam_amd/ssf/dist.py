@@ -42,6 +42,29 @@ def gather_pose_records(records, group=None) -> torch.Tensor:
     return allr.view(world, K, n, k).transpose(0, 1).reshape(K, world * n, k)
 
 
+def gather_sequence_records(records: torch.Tensor, n_sequences: int, group=None) -> torch.Tensor:
+    """Strong-scaling exchange (BASELINE configs[3]: a fixed set of n_sequences sharded over the
+    ranks by sequence_shard): this rank's per-frame records [F, B_r, k] (B_r = its shard size,
+    frames in order) -> [F, n_sequences, k], sequences in id order, in ONE all-gather.  Shards
+    may differ in size by one, so every rank pads to the largest shard (NaN rows) before the
+    collective and the pads are dropped after it."""
+    F, b, k = records.shape
+    if not dist.is_available() or not dist.is_initialized():
+        if b != n_sequences:
+            raise ValueError(f"{b} sequences on a single rank, expected {n_sequences}")
+        return records
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if b != len(sequence_shard(n_sequences, world, rank)):
+        raise ValueError("records do not match this rank's sequence shard")
+    bmax = -(-n_sequences // world)
+    pad = torch.full((F, bmax, k), float("nan"), dtype=records.dtype, device=records.device)
+    pad[:, :b] = records
+    allr = gather_poses(pad.view(F, bmax * k), group).view(world, F, bmax, k)
+    parts = [allr[r, :, :len(sequence_shard(n_sequences, world, r))] for r in range(world)]
+    return torch.cat(parts, 1)
+
+
 def gather_poses(local: torch.Tensor, group=None) -> torch.Tensor:
     """All-gather equal-shaped per-rank pose records -> [world * n, k] in rank order."""
     if not dist.is_available() or not dist.is_initialized():

@@ -34,3 +34,17 @@ def test_world_size_mismatch_is_refused():
                        env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"), capture_output=True,
                        text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_strong_scaling_launch_shards_eight_sequences():
+    """BASELINE configs[3] launch (--sequences-total 8 --gpus N): every rank owns its contiguous
+    block of the 8 sequences (ssf.dist.sequence_shard), together exactly the 8."""
+    for n in (2, 3):
+        r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), "--sequences-total", "8",
+                            "--launch-check"], cwd=REPO, env=_env(), capture_output=True, text=True,
+                           timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+        ranks = sorted(d["ranks"], key=lambda x: x["rank"])
+        assert [s for x in ranks for s in x["shard"]] == list(range(8))
+        assert max(len(x["shard"]) for x in ranks) - min(len(x["shard"]) for x in ranks) <= 1

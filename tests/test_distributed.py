@@ -51,6 +51,55 @@ def _worker(rank, world, port, n_seq, q):
         dist.destroy_process_group()
 
 
+def _strong_worker(rank, world, port, n_seq, q):
+    """BASELINE configs[3] exchange: n_seq sequences sharded (unevenly when world does not divide
+    n_seq), per-frame records of each rank's sequences, one padded all-gather."""
+    import sys
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(here, "ssf-slam_amd"))
+    from ssf import dist as sd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = list(sd.sequence_shard(n_seq, world, rank))
+        F = 5
+        rec = torch.zeros((F, len(mine), 14), dtype=torch.float64)
+        for f in range(F):
+            for j, s in enumerate(mine):
+                rec[f, j, 0] = s
+                rec[f, j, 1] = f
+                rec[f, j, 2] = rank
+        g = sd.gather_sequence_records(rec, n_seq)
+        q.put((rank, mine, g.numpy().tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("world,n_seq", [(2, 8), (3, 8)])
+def test_gloo_strong_scaling_sequence_gather(world, n_seq):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_strong_worker, args=(r, world, port, n_seq, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    shards = {rank: mine for rank, mine, _ in res}
+    assert sorted(s for m in shards.values() for s in m) == list(range(n_seq))
+    owner = {s: r for r, m in shards.items() for s in m}
+    for rank, mine, g in res:
+        assert len(g) == 5 and all(len(row) == n_seq for row in g)
+        for f in range(5):
+            assert [row[0] for row in g[f]] == [float(s) for s in range(n_seq)]
+            assert all(row[1] == f for row in g[f])
+            assert [row[2] for row in g[f]] == [float(owner[s]) for s in range(n_seq)]
+
+
 def sd_shard(n, w, r):
     import sys
     here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -361,3 +361,33 @@ def test_strip_image_argument_checks(dev):
         assert b"strip image" in L.ssf_last_error(fe._h)
     assert L.ssf_plane_table_batch(*base, _ptr(sx), _ptr(si), _ptr(img), _ptr(head)) == 0
     torch.cuda.synchronize()
+
+
+def test_kabsch_warm_start_independent_pairs(oracle, dev):
+    """bench.py --kabsch-warm-start (beyond the reference): every pair of a
+    sequence warm-started from its own SSF Kabsch pose (mask_and_pose of its last frame, whose
+    flow points into the next frame), all pairs in ONE register launch -- each pair equals
+    oracle.register_pair with the same warm start (GN x 10, per-pair poses within the bars)."""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index, solver="gn", max_iter=10)
+    F = 4
+    fr = [frame(5, k, n_az=1875) for k in range(F)]
+    pb = _planes(fe, dev, [f[0] for f in fr])
+    table = fe.plane_table(pb)
+    # the SSF poses of frames 0..F-2 (T_{k <- k+1}) in one mask launch
+    P = np.concatenate([f[0] for f in fr[:-1]]); Fl = np.concatenate([f[1] for f in fr[:-1]])
+    mp = ssf.mask_and_pose(P, Fl, mode="gt", gt_mask=np.concatenate([f[2] for f in fr[:-1]]),
+                           frame_sizes=[len(f[0]) for f in fr[:-1]])
+    ws = np.concatenate([mp["q_xyzw"], mp["t"]], 1)                      # [F-1, 7] (q, t)
+    pose = torch.from_numpy(ws.copy()).to(dev)
+    last, curr = _sub(pb, list(range(F - 1))), _sub(pb, list(range(1, F)))
+    res = fe.register(last, table, curr, pose)
+    torch.cuda.synchronize()
+    got = res["pose_rel"].cpu().numpy()
+    for p in range(F - 1):
+        L, Cc = pb.frame(p).cpu().numpy(), pb.frame(p + 1).cpu().numpy()
+        q, t, _, c = oracle.register_pair(L, Cc, 0.05, mode=1, max_iter=10, q_init=ws[p, :4], t_init=ws[p, 4:])
+        assert int(res["ncorr"][p]) == c
+        assert np.abs(got[p, 4:] - t).max() < TOL_T and _quat_angle(got[p, :4], q) < TOL_R, p
+        # the warm start is already close: the registration moves it by decimetres at most
+        assert np.abs(got[p, 4:] - ws[p, 4:]).max() < 0.2

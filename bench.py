@@ -64,6 +64,17 @@ def _load_profile(path, B, N, masked):
     return t
 
 
+def _lib_sha16():
+    """sha256[:16] of the front-end library this run loads (ties committed PMC profiles to a build)"""
+    import hashlib
+    from ssf import _abi
+    try:
+        with open(_abi.LIB_PATH, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -85,6 +96,10 @@ def parse(argv=None):
     ap.add_argument("--edges", action="store_true",
                     help="beyond the reference (off by default): edge features + point-to-line "
                          "blocks in the registration (north_star wording; the reference is planar)")
+    ap.add_argument("--f64-inputs", action="store_true",
+                    help="the mask reads float64 pos / flow (ssf_mask_pose_batch_f64: the reference's "
+                         "dtype when its npz arrays are float64); the features keep the float32 cloud "
+                         "(PointCloud2 carries f32).  72 B resident per point and step: use <= 30 steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="CPU baseline: seconds per leg (single thread, all cores, sklearn)")
@@ -262,7 +277,10 @@ def make_data(args, dev, n_frames, rank, batch=None):
         pos = torch.empty((B * N, 3), dtype=torch.float32, device=dev)
         flow = torch.empty((B * N, 3), dtype=torch.float32, device=dev)
         scanner.frame(k, pos, flow)
-        out.append((pos, flow))
+        if getattr(args, "f64_inputs", False):   # the mask's float64 copies (same values)
+            out.append((pos, flow, pos.double(), flow.double()))
+        else:
+            out.append((pos, flow))
     torch.cuda.synchronize(dev)
     return out
 
@@ -308,13 +326,14 @@ class Pipeline:
     def step(self, k, batches, off, h_off, timing, streams=None, want_stats=False):
         import torch
         a = self.args
-        pos, flow = batches[k]
+        pos, flow = batches[k][:2]
+        mpos, mflow = batches[k][2:4] if len(batches[k]) == 4 else (pos, flow)   # --f64-inputs
         s_mask, s_feat, s_reg = streams or (self.s_masks[k % len(self.s_masks)], self.s_feat, self.s_reg)
         mk = lambda: torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(s_mask):
             m0, m1 = mk(), mk()
             m0.record(s_mask)
-            out, bg = self.fe_mask.mask_pose(pos, flow, off, h_off, mode="gmm", want_mask=True)
+            out, bg = self.fe_mask.mask_pose(mpos, mflow, off, h_off, mode="gmm", want_mask=True)
             m1.record(s_mask)
         keep = None
         if a.mask_before_features:          # configs[2]: the features wait for the mask
@@ -400,7 +419,7 @@ def kernel_pass(pipe, batches, off, h_off, ks, rows, row_start, row_end):
         c.kernel_times()          # drop anything recorded earlier
         c.profile(True)
     B, N = pipe.B, pipe.N
-    acc = dict(points=0, kept=0, in_range=0, plane=0, plane_reg=0, corr_evals=0, corr=0, mask_passes=[])
+    acc = dict(points=0, chunks=0, kept=0, in_range=0, plane=0, plane_reg=0, corr_evals=0, corr=0, mask_passes=[])
     with torch.cuda.stream(s):
         for i, k in enumerate(ks):
             r = pipe.step(k, batches, off, h_off, False, streams=(s, s, s), want_stats=True)
@@ -412,6 +431,7 @@ def kernel_pass(pipe, batches, off, h_off, ks, rows, row_start, row_end):
             pipe.fe_feat.profile(True)
             roff = roff.to(torch.int64)
             acc["points"] += B * N
+            acc["chunks"] += B * ((N + 2047) // 2048)
             acc["kept"] += int(roff[:, -1].sum())
             acc["in_range"] += int((roff[:, rows - row_end] - roff[:, row_start]).sum())
             acc["plane"] += int(r["pb"].count.sum())
@@ -441,11 +461,18 @@ def rooflines(times, acc, B, N):
     n_mask = len(acc["mask_passes"])
     model = {   # DESIGN.md §5 / SURVEY §8(d) per-unit figures
         "k_mask_pose": B * N * (24.0 * passes + 1.0) * n_mask,     # [flow,xyz] f32 per pass + mask
+        "k_mask_pose_f64": B * N * (48.0 * passes + 1.0) * n_mask,  # [flow,xyz] f64 per pass + mask
         "k_bin_count": 13.0 * acc["points"],                        # xyz read, row id written
         # the stable partition fused with the 11-tap curvature: xyz + row id read once per point
         # (the halo's re-reads of neighbouring chunks are L2 hits, not algorithmic), per kept
         # point its input index (4 B) and candidate flag byte written at its ring position
         "k_bin_curv": 13.0 * acc["points"] + 5.0 * acc["kept"],
+        # round 4, the single-read stage: xyz read once (12 B), a u16 chunk position per point
+        # (2 B) written, per 2048-point chunk its row counts (256 B) and two bit planes (512 B)
+        "k_feat_chunk": 14.0 * acc["points"] + 768.0 * acc["chunks"],
+        # the chunks' counts and bit planes read, per plane point: its slot written and read back
+        # (8 B), its u16 position (2 B) and xyz (12 B) gathered, the xyzi record written (16 B)
+        "k_feat_select": 768.0 * acc["chunks"] + 38.0 * acc["plane"],
         # flag bytes read, per plane point: its index written and read back (4 + 4 B), its ring
         # index (4 B) and xyz (12 B) gathered and the xyzi record written (16 B)
         "k_select": 1.0 * acc["kept"] + 40.0 * acc["plane"],
@@ -473,8 +500,9 @@ def rooflines(times, acc, B, N):
                               evaluations_per_pair=acc["corr_evals"] / max(1, acc["corr"]),
                               note="corr = valid correspondences counted on device (ncorr); "
                                    "evaluations = 1 + logged iterations (nlog)")
-    if "k_bin_curv" in out:
-        out["k_bin_curv"]["kept_points_per_launch"] = acc["kept"] / out["k_bin_curv"]["launches"]
+    for k in ("k_bin_curv", "k_feat_chunk"):
+        if k in out:
+            out[k]["kept_points_per_launch"] = acc["kept"] / out[k]["launches"]
     return out, passes
 
 
@@ -984,14 +1012,25 @@ def main():
         "roofline": None, "cpu_baseline": cpu,
         "kernels": kernels, "overlapped_event_ms": overlapped,
         "mask_passes_per_frame": passes, "gather_check": gather_ok,
-        "data_gen_s": round(t_data, 2),
+        "data_gen_s": round(t_data, 2), "lib_sha16": None,
     }
+    if args.f64_inputs:
+        line["config"]["mask_inputs"] = "float64 pos / flow (ssf_mask_pose_batch_f64), float32 features"
+        line["dtype"] = "f32 features / f64 mask inputs + f64 mask+solve"
     traffic = None if args.edges else _load_profile(TRAFFIC_JSON, B, N, args.mask_before_features)
+    lib_sha = _lib_sha16()
+    tsrc = None
     if traffic:
+        # the traffic is a committed PMC measurement, not this run's: say which, and whether it
+        # was measured on this very library build
+        tsrc = {"traffic_source": os.path.relpath(TRAFFIC_JSON, REPO),
+                "traffic_lib_sha16": traffic.get("lib_sha16"),
+                "traffic_stale": traffic.get("lib_sha16") != lib_sha}
         for k, v in kernels.items():
             t = traffic["kernels"].get(k, {}).get("traffic_bytes_per_launch")
             if t:
                 v["traffic"] = t
+                v.update(tsrc)
                 # the PMC-measured HBM bytes over the same kernel-only duration: the fraction of
                 # the HBM peak the kernel actually moves (beside the byte model's "frac")
                 v["traffic_gbs"] = t / (v["ms"] * 1e-3) / 1e9
@@ -1002,12 +1041,15 @@ def main():
             "GN iteration one evaluation (block reduction of 28 f64 terms, 256 threads) and the "
             "serial 6x6 solve -- 'frac' is SURVEY 8(d)'s 36 B x C x evaluations model, "
             "'traffic_frac' the PMC-measured HBM bytes over the same duration")
-    mk = kernels.get("k_mask_pose")
+    line["lib_sha16"] = lib_sha
+    mk_name = "k_mask_pose_f64" if args.f64_inputs else "k_mask_pose"
+    mk = kernels.get(mk_name)
     if mk and "gbs" in mk:
         line["roofline"] = {"bound": "hbm", "achieved": mk["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": mk["frac"], "traffic": mk.get("traffic"),
-                            "kernel": "k_mask_pose",
-                            "duration": "kernel-only (one-stream kernel pass, HIP events)"}
+                            "kernel": mk_name,
+                            "duration": "kernel-only (one-stream kernel pass, HIP events)",
+                            **({k: v for k, v in tsrc.items()} if tsrc and mk.get("traffic") else {})}
         f64 = None if args.edges else _load_profile(F64_JSON, B, N, args.mask_before_features)
         flops = f64 and f64.get("f64_flops_per_launch")
         if flops:
@@ -1015,7 +1057,7 @@ def main():
             line["roofline_f64"] = {"bound": "valu_f64", "achieved": tf, "peak": F64_PEAK_TFLOPS,
                                     "unit": "TFLOP/s", "frac": tf / F64_PEAK_TFLOPS,
                                     "kernel": "k_mask_pose", "flops_source": os.path.basename(F64_JSON)}
-    ns = {k: kernels[k]["frac"] for k in ("k_bin_curv", "k_solve") if k in kernels and "frac" in kernels[k]}
+    ns = {k: kernels[k]["frac"] for k in ("k_feat_chunk", "k_bin_curv", "k_solve") if k in kernels and "frac" in kernels[k]}
     if ns:
         line["north_star_kernels_hbm_frac"] = ns
         meas = {k: kernels[k]["traffic_frac"] for k in ns if "traffic_frac" in kernels[k]}

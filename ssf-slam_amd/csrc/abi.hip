@@ -49,6 +49,10 @@ struct ssf_ctx {
     std::string err;
     // frameFeature scratch
     DevBuf rid, hist, ring_off, ring_xyzi /* ring index */, sel, sel_cnt /* candidate flags */, fix, plane1, off1, cnt1;
+    // single-read feature stage: per-(chunk, row) counts, u16 chunk positions, bit planes,
+    // chunk-major curvature (debug outputs only)
+    DevBuf fcnt, fidx, fbits, fcurv, rtab;
+    bool rtab_ready = false;
     // registration scratch
     DevBuf corr;
     // ssf_register_pair: offsets, counts, the last frame's plane table + search index, pose, log
@@ -224,7 +228,7 @@ void ssf_destroy(ssf_ctx* c) {
     DevBuf* bufs[] = {&c->rid, &c->hist, &c->ring_off, &c->ring_xyzi, &c->sel, &c->sel_cnt, &c->fix,
                       &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->pair, &c->start1, &c->vg,
                       &c->icp_cur, &c->icp_key, &c->icp_st, &c->icp_guess, &c->esel,
-                      &c->ecorr};
+                      &c->ecorr, &c->fcnt, &c->fidx, &c->fbits, &c->fcurv, &c->rtab};
     for (auto& ds : c->dslot) {
         if (ds.used) { (void)hipEventSynchronize(ds.used); (void)hipEventDestroy(ds.used); }
         if (ds.copied) { (void)hipEventSynchronize(ds.copied); (void)hipEventDestroy(ds.copied); }
@@ -317,6 +321,19 @@ static int32_t ensure_features(ssf_ctx* c, int32_t n_frames, int64_t total, int6
     SSF_TRY_HIP(c, c->sel.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(total, 1)), "alloc sel");
     SSF_TRY_HIP(c, c->sel_cnt.ensure(ssf::flag_bytes(total, n_frames)), "alloc cand flags");
     SSF_TRY_HIP(c, c->fix.ensure(ssf::fix_bytes(total, n_frames)), "alloc curvature fix-up list");
+    if (ssf::feat_single_read(max_pts)) {
+        if (!c->rtab_ready) {
+            std::vector<char> h(ssf::ring_table_bytes());
+            const int rc = ssf::build_ring_table(R, h.data());
+            if (rc) return fail(c, SSF_E_ARG, "ring-id table: build failed (" + std::to_string(rc) + ")");
+            SSF_TRY_HIP(c, c->rtab.ensure(h.size()), "alloc ring table");
+            SSF_TRY_HIP(c, hipMemcpy(c->rtab.p, h.data(), h.size(), hipMemcpyHostToDevice), "H2D ring table");
+            c->rtab_ready = true;
+        }
+        SSF_TRY_HIP(c, c->fcnt.ensure(ssf::feat_cnt_bytes(n_frames, max_pts)), "alloc feature counts");
+        SSF_TRY_HIP(c, c->fidx.ensure(ssf::feat_idx_bytes(total, n_frames)), "alloc feature index");
+        SSF_TRY_HIP(c, c->fbits.ensure(ssf::feat_bits_bytes(n_frames, max_pts)), "alloc feature bits");
+    }
     return SSF_OK;
 }
 
@@ -364,14 +381,18 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
         es = ssf::EdgeSel{c->ecfg.edge_min, c->ecfg.edge_span,
                           c->esel.as<int32_t>(), reinterpret_cast<float4*>(d_edge_xyzi), d_edge_count};
     }
-    ProfScope prof(c, stream);
     float4* ring4 = reinterpret_cast<float4*>(d_ring_xyzi);   // debug output only (nullable)
+    if ((ring4 || d_curv) && ssf::feat_single_read(max_frame_points))
+        SSF_TRY_HIP(c, c->fcurv.ensure(sizeof(float) * (size_t)std::max<int64_t>(total_points, 1)), "alloc chunk curvature");
+    ssf::FeatScratch fs{c->rtab.p, c->fcnt.as<int32_t>(), c->fidx.as<uint16_t>(), c->fbits.as<uint64_t>(),
+                        c->fcurv.as<float>()};
+    ProfScope prof(c, stream);
     int32_t* roff = d_ring_off ? d_ring_off : c->ring_off.as<int32_t>();
     hipError_t e = ssf::launch_extract_planes(
         (hipStream_t)stream, c->cfg, n_frames, d_pts, point_stride, d_frame_off, max_frame_points,
         d_keep, c->rid.as<int8_t>(), c->hist.as<int32_t>(), roff, c->ring_xyzi.as<int32_t>(), ring4,
         d_curv, c->sel_cnt.as<uint8_t>(), c->fix.p, c->sel.as<int32_t>(),
-        reinterpret_cast<float4*>(d_plane_xyzi), d_plane_count, edges ? &es : nullptr);
+        reinterpret_cast<float4*>(d_plane_xyzi), d_plane_count, edges ? &es : nullptr, &fs);
     if (e != hipSuccess) return hip_fail(c, e, "extract_planes launch");
     return SSF_OK;
 }
@@ -683,7 +704,12 @@ static int32_t mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const
     // parts per frame: fixed, or automatic -- enough to fill the resident work-group slots
     if (c->mask_slots < 0) c->mask_slots = ssf::mask_pose_slots(c->device);
     int G = c->mask_split;
-    if (G <= 0) G = c->mask_slots > 0 ? c->mask_slots / n_frames : 1;
+    // automatic: as many parts as keep the resident slots busy; a fixed split is bounded the same
+    // way (frames x G <= slots), so its exchange slots (mask_parts_bytes) stay near the automatic
+    // split's size instead of growing with G for large batches
+    const int g_cap = c->mask_slots > 0 ? std::max(1, c->mask_slots / n_frames) : 1;
+    if (G <= 0) G = g_cap;
+    else G = std::min(G, g_cap);
     G = std::max(1, std::min(G, ssf::kMaskMaxSplit));
     if (mode != SSF_MASK_GMM) G = 1;
     const size_t sync_need = G > 1 ? ssf::mask_sync_bytes(n_frames) + 16 : 0;

@@ -19,6 +19,11 @@
 #include "ssf_device.hpp"
 #include "ssf_internal.hpp"
 
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
 namespace ssf {
 
 // frameFeature.cpp:57-72 (see oracle/ssf_oracle.c orc_ring_id for the precision choices).
@@ -60,6 +65,37 @@ SSF_DEV int ring_id(float x, float y, float z, int n_rows) {
     int id = (n_rows == 16 || (double)af >= -8.83) ? (int)v : n_rows / 2 + (int)v;
     if (n_rows != 16 && n_rows != 64) id = -1;
     return (id > -1 && id < n_rows) ? id : -1;
+}
+
+// ---- the ring id by table (k_feat_chunk) -------------------------------------------------------
+// frameFeature.cpp:57-73 makes the row id a step function of ONE float, ratio = z / sqrt(x^2 + y^2)
+// (a float divide and sqrt, correctly rounded on both sides): atan in double, the degree angle
+// rounded to float, the bin arithmetic of :60 / :63-71 and int() truncation are all monotone in
+// it.  So the host evaluates that exact chain (the oracle's orc_ring_id, glibc atan) once per
+// context and cuts the ratio axis into kRingCells uniform cells (cell = clamp((ratio - r0) * inv),
+// float ops, the same on both sides); a cell holds at most two ids (cells are narrower than the
+// narrowest bin), so per cell {the float ratio where the second id starts, id below, id from
+// there}.  The device computes the ratio exactly as the reference and does ONE table lookup and
+// one compare: no atan, no double precision, no divergent exact path.
+constexpr int kRingCells = 256;
+struct RingCell {
+    float thr;          // ratios >= thr (float order) take id_b
+    int32_t ids;        // id_a (bits 0..7, signed), id_b (bits 8..15, signed)
+};
+struct RingTable {
+    float r0, inv;
+    RingCell cell[kRingCells];
+};
+
+SSF_DEV int ring_id_table(float x, float y, float z, float r0, float inv, const RingCell* T) {
+    const float r2 = x * x + y * y;
+    const float ratio = z / sqrtf(r2);
+    int ci = (int)((ratio - r0) * inv);          // v_cvt_i32_f32 saturates; NaN handled below
+    ci = min(max(ci, 0), kRingCells - 1);
+    const RingCell rc = T[ci];
+    const int a = (int)(int8_t)(rc.ids & 0xff), b = (int)(int8_t)((rc.ids >> 8) & 0xff);
+    const int id = ratio < rc.thr ? a : b;
+    return ratio == ratio ? id : -1;             // 0 / 0 (a point at the origin): no row
 }
 
 // Each thread issues all of its kCountSteps point loads (clamped, unconditional) before the first ring
@@ -629,6 +665,653 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const float* __restrict_
     }
 }
 
+// ==== the single-read feature stage (round 4) ===================================================
+// k_feat_chunk + k_feat_select (+ k_feat_debug for the parity outputs) replace k_bin_count,
+// k_bin_scan, k_bin_curv and k_select for frames of up to kFeatMaxChunks chunks.  The points are
+// read ONCE: k_feat_chunk computes the ring ids of its window itself, ranks and regroups it by row
+// exactly like k_bin_curv, and evaluates every stencil the window covers -- but it needs no global
+// ring position: its outputs are CHUNK-MAJOR, in the chunk's own-tile order (the chunk's own kept
+// points, grouped by row, input order within a row):
+//   cnt    [F][n_chunks + 1][64] own points per row (k_feat_select turns them into row bases)
+//   gidx   u16 per own-tile slot: the point's position in the chunk (frame-local index = chunk *
+//          2048 + gidx), at idx_base(f) + chunk * 2048 + slot
+//   gbits  per chunk three 2048-bit planes: planar candidate, UNRESOLVED, edge candidate
+// A chunk cannot know a point's indexInRow j, only its rank in the window; but a stencil the
+// window covers (5 row points on each side in the window) has 5 <= j < n_r - 5 necessarily, so its
+// curvature decides the flags (frameFeature.cpp:84-107).  Every other own point of a row in range
+// is marked unresolved: k_feat_select, which has the whole frame's counts, gives it curvature 0
+// when j < 5 or j >= n_r - 5 (:85; always a planar candidate) and evaluates the rest -- open
+// stencils, rare for azimuth-ordered scans -- through the chunk-major index, the same taps in the
+// same order.  Every write of k_feat_chunk is a whole, aligned, contiguous run (no per-row
+// scatter); the greedy of k_feat_select walks each row as its sequence of (chunk, row) segments.
+constexpr int kFeatMaxChunks = 128;              // 262144 points per frame (k_feat_select's LDS)
+constexpr int kFeatPlanes = 3;                   // planar candidate, unresolved, edge candidate
+constexpr int kFeatWords = kBinChunk / 64;       // 64-bit words per plane and chunk
+constexpr uint8_t kFlP = 1, kFlU = 2, kFlE = 4;
+static_assert(kCurvSub == 1 && kBinChunk == 2048, "own-tile slots and chunk positions use 11 bits");
+
+// u16 index base of frame f: 64-entry aligned, frames disjoint with a gap of >= 33 entries (the
+// chunk writes run up to 3 entries past the chunk's own points)
+SSF_DEV int64_t idx_base(const int64_t* frame_off, int f) { return (frame_off[f] & ~(int64_t)31) + 64 * (int64_t)f; }
+
+template <bool kDebug, bool kEdge>
+__global__ __launch_bounds__(kCurvNT, 5) void k_feat_chunk(const float* __restrict__ pts, int stride,
+                                                    const int64_t* __restrict__ frame_off,
+                                                    int n_frames, int n_rows, int n_chunks,
+                                                    int row_start, int row_end, float plane_min,
+                                                    float edge_min, const uint8_t* __restrict__ keep,
+                                                    const RingTable* __restrict__ rtab,
+                                                    int32_t* __restrict__ cnt,
+                                                    uint16_t* __restrict__ gidx,
+                                                    uint64_t* __restrict__ gbits,
+                                                    float* __restrict__ curv_cm) {
+    __shared__ __attribute__((aligned(16))) float sc[kTileE + 2 * kTilePad];   // x, then y, then z
+    __shared__ __attribute__((aligned(16))) uint16_t meta[kTileE];   // own-tile slot | 0x8000: stencil
+    // two LDS regions reused across phases (31 KiB in all: 5 work-groups per CU):
+    //   A: the ring-id table (ids) -> u16 chunk position per own-tile slot (place, out)
+    //   B: the per-row lane words (rank) -> the flag byte per own-tile slot (place, curvature, out)
+    __shared__ __attribute__((aligned(16))) char regA[(kBinChunk + 4) * 2];
+    __shared__ __attribute__((aligned(16))) char regB[kCurvNW * (kMaxRows + 1) * 8];
+    static_assert(sizeof(regA) >= kRingCells * sizeof(RingCell) && sizeof(regB) >= kBinChunk, "LDS reuse");
+    RingCell* rcell = reinterpret_cast<RingCell*>(regA);
+    uint16_t* idl = reinterpret_cast<uint16_t*>(regA);
+    auto gmask = reinterpret_cast<unsigned long long (*)[kMaxRows + 1]>(regB);
+    uint8_t* fll = reinterpret_cast<uint8_t*>(regB);
+    // per (wave, row): the wave's row points so far, packed {all : 16, halo-before : 16,
+    // halo-before + own : 16} -- one word read and rewritten per step, no atomics
+    __shared__ unsigned long long wrun[kCurvNW][kMaxRows + 1];
+    // per (wave, row), in the rank space q of the wave's points of that row: tile slot base,
+    // own-tile slot base, the ranks whose 11 taps the window holds
+    __shared__ int4 wrec[kCurvNW][kMaxRows];
+    __shared__ int ntot, nown;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: step masks in SGPRs
+    const int64_t nblk = (int64_t)n_chunks * n_frames;        // XCD-aware logical block
+    const int64_t q8 = (nblk + 7) / 8;
+    const int64_t lb = (int64_t)(blockIdx.x % 8) * q8 + blockIdx.x / 8;
+    if (lb >= nblk) return;
+    const int f = (int)(lb / n_chunks), c = (int)(lb - (int64_t)f * n_chunks);
+    const int64_t fb = frame_off[f], e = frame_off[f + 1];
+    const int64_t s = fb + (int64_t)c * kBinChunk;
+    if (s >= e) return;                                       // uniform
+    const int64_t t = min(e, s + (int64_t)kBinChunk);
+    const int64_t ws = max(fb, s - (int64_t)kCurvHalo), we = min(e, t + (int64_t)kCurvHalo);
+    const int L = (int)(we - ws), hb = (int)(s - ws), he = (int)(t - ws);   // own: [hb, he)
+    const int qlen = ((L + kCurvNW - 1) / kCurvNW + 63) / 64 * 64;
+    if (tid < kMaxRows) {
+#pragma unroll
+        for (int k = 0; k < kCurvNW; ++k) { wrun[k][tid] = 0ull; gmask[k][tid] = 0ull; }
+    }
+    if (tid < kCurvNW) { wrun[tid][kMaxRows] = 0ull; gmask[tid][kMaxRows] = 0ull; }
+    for (int k = tid; k < kRingCells; k += kCurvNT) rcell[k] = rtab->cell[k];
+    const float r0 = rtab->r0, rinv = rtab->inv;
+    __syncthreads();
+    const int q0 = w * qlen, q1 = min(L, q0 + qlen);
+    int idr[kWinQ];
+    float px[kWinQ], py[kWinQ], pz[kWinQ];
+    const float* pw = pts + ws * stride;
+#pragma unroll
+    for (int st = 0; st < kWinQ; ++st) {                      // every load first (clamped)
+        const float* pp = pw + (uint32_t)(min(q0 + lane + 64 * st, L - 1) * stride);
+        px[st] = pp[0]; py[st] = pp[1]; pz[st] = pp[2];
+    }
+    uint8_t kp[kWinQ];
+    if (keep) {
+#pragma unroll
+        for (int st = 0; st < kWinQ; ++st) kp[st] = keep[ws + min(q0 + lane + 64 * st, L - 1)];
+    }
+#pragma unroll
+    for (int st = 0; st < kWinQ; ++st) {                      // frameFeature.cpp:57-73
+        const bool in = q0 + lane + 64 * st < q1 && (!keep || kp[st]);
+        const int id = ring_id_table(px[st], py[st], pz[st], r0, rinv, rcell);   // every lane: no branch
+        idr[st] = in ? id : -1;
+    }
+    // rank among same-row points (the k_bin_curv ranking: per-row lane words, waves in order).
+    // Every lane of a row computes the same new counter word and writes it (and clears the lane
+    // word): the wave's LDS instructions complete in order, so all reads of the step precede
+    // these writes -- no leader branch.  The halo-before / own lanes of a step are uniform masks.
+#pragma unroll
+    for (int st = 0; st < kWinQ; ++st) {
+        const int id = idr[st];
+        const int rs = id >= 0 ? id : kMaxRows;
+        unsigned long long* gm = &gmask[w][rs];
+        __hip_atomic_fetch_or(gm, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint64_t m = __hip_atomic_load(gm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint64_t old = wrun[w][rs];
+        const int s0 = q0 + 64 * st;                          // uniform
+        const int hbl = min(64, max(0, hb - s0)), hel = min(64, max(0, he - s0));
+        const uint64_t hm = hbl >= 64 ? ~0ull : ((1ull << hbl) - 1ull);   // lanes before the chunk
+        const uint64_t om = hel >= 64 ? ~0ull : ((1ull << hel) - 1ull);   // lanes before its end
+        const int rin = __popcll(m & lanemask_lt());
+        wrun[w][rs] = old + (uint64_t)__popcll(m) + ((uint64_t)__popcll(m & hm) << 16) +
+                      ((uint64_t)__popcll(m & om) << 32);
+        __hip_atomic_store(gm, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        idr[st] = (id & 0xff) | (((int)(old & 0xffffu) + rin) << 8);
+    }
+    __syncthreads();
+    if (tid < 64) {                                           // rows on the lanes of wave 0
+        const int r = tid;
+        int tot = 0, nbr = 0, obr = 0;
+        int pwk[kCurvNW];
+        if (r < n_rows) {
+#pragma unroll
+            for (int k = 0; k < kCurvNW; ++k) {
+                const uint64_t v = wrun[k][r];
+                pwk[k] = tot;                                 // the wave's first position in the run
+                tot += (int)(v & 0xffffu);
+                nbr += (int)((v >> 16) & 0xffffu);
+                obr += (int)((v >> 32) & 0xffffu);
+            }
+        }
+        const int own = r < n_rows ? obr - nbr : 0;
+        int incl = tot, oincl = own;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64), yo = __shfl_up(oincl, o, 64);
+            if (r >= o) { incl += y; oincl += yo; }
+        }
+        cnt[((int64_t)f * (n_chunks + 1) + c) * kMaxRows + r] = own;
+        if (r < n_rows) {
+            const int run0 = incl - tot, seg0 = oincl - own;
+#pragma unroll
+            for (int k = 0; k < kCurvNW; ++k)
+                wrec[k][r] = make_int4(run0 + pwk[k], seg0 + pwk[k] - nbr, 5 - pwk[k], tot - 5 - pwk[k]);
+        }
+        if (r == 63) { ntot = incl; nown = oincl; }
+    }
+    __syncthreads();
+    const int nt = ntot;
+    const int64_t cm = fb + (int64_t)c * kBinChunk;           // chunk-major base (curvature)
+    // ---- place: tile slot of every window point, own-tile slot + position of every own point
+    int loc[kWinQ];
+#pragma unroll
+    for (int st = 0; st < kWinQ; ++st) {
+        const int id = (int)(int8_t)(idr[st] & 0xff);
+        loc[st] = kTileE;                                     // no point: the pad slot
+        if (id >= 0) {
+            const int q = idr[st] >> 8;
+            const int4 rw = wrec[w][id];
+            const int k = rw.x + q;
+            const int wp = q0 + lane + 64 * st;
+            const bool own = wp >= hb && wp < he;
+            const bool row_in = id >= row_start && id < n_rows - row_end;
+            const bool covered = q >= rw.z && q < rw.w;
+            uint16_t mk = 0;
+            if (own) {
+                const int p = rw.y + q;
+                idl[p] = (uint16_t)(wp - hb);
+                if (row_in && covered) {
+                    mk = (uint16_t)(p | 0x8000);
+                } else {
+                    fll[p] = row_in ? kFlU : (uint8_t)0;
+                    if (kDebug && curv_cm) curv_cm[cm + p] = 0.0f;
+                }
+            }
+            meta[k] = mk;
+            sc[kTilePad + k] = px[st];
+            loc[st] = k;
+        }
+    }
+    __syncthreads();
+    // ---- curvature of this thread's kCE tile entries, one coordinate at a time (k_bin_curv)
+    const int k0 = kCE * tid;
+    float v[kCE];
+    auto coord = [&](float (&d)[kCE]) {
+        float h[kCE + 16];
+#pragma unroll
+        for (int k = 0; k < (kCE + 16) / 4; ++k) {
+            const float4 x4 = *reinterpret_cast<const float4*>(sc + k0 + 4 * k);
+            h[4 * k] = x4.x; h[4 * k + 1] = x4.y; h[4 * k + 2] = x4.z; h[4 * k + 3] = x4.w;
+        }
+#pragma unroll
+        for (int i = 0; i < kCE; ++i) d[i] = tap11(h + 3 + i);
+    };
+    {
+        // ((dX dX + dY dY) + dZ dZ), each product rounded: the square of one coordinate's sum is
+        // kept, not the sum itself (one kCE array live instead of two)
+        float d0[kCE];
+        coord(d0);
+#pragma unroll
+        for (int i = 0; i < kCE; ++i) v[i] = d0[i] * d0[i];
+        __syncthreads();
+#pragma unroll
+        for (int st = 0; st < kWinQ; ++st) sc[kTilePad + loc[st]] = py[st];
+        __syncthreads();
+        coord(d0);
+#pragma unroll
+        for (int i = 0; i < kCE; ++i) v[i] = v[i] + d0[i] * d0[i];
+        __syncthreads();
+#pragma unroll
+        for (int st = 0; st < kWinQ; ++st) sc[kTilePad + loc[st]] = pz[st];
+        __syncthreads();
+        coord(d0);
+#pragma unroll
+        for (int i = 0; i < kCE; ++i) v[i] = v[i] + d0[i] * d0[i];
+    }
+    uint16_t mt[kCE];
+#pragma unroll
+    for (int i = 0; i < kCE; i += 4) {                        // k0 + kCE <= kTileE: 8-byte reads
+        const uint2 m2 = *reinterpret_cast<const uint2*>(meta + k0 + i);
+        mt[i] = (uint16_t)(m2.x & 0xffffu); mt[i + 1] = (uint16_t)(m2.x >> 16);
+        mt[i + 2] = (uint16_t)(m2.y & 0xffffu); mt[i + 3] = (uint16_t)(m2.y >> 16);
+    }
+#pragma unroll
+    for (int i = 0; i < kCE; ++i) {
+        if (k0 + i < nt && (mt[i] & 0x8000)) {
+            const int p = mt[i] & 0x7fff;
+            const uint8_t fl = cand_flags(true, true, v[i], plane_min, kEdge, edge_min);
+            fll[p] = (uint8_t)((fl & 1) ? kFlP : 0) | (uint8_t)((fl & 2) ? kFlE : 0);
+            if (kDebug && curv_cm) curv_cm[cm + p] = v[i];
+        }
+    }
+    __syncthreads();
+    // ---- out: the chunk's own-tile slots, whole aligned runs
+    const int no = nown;
+    const int clen = (int)(t - s);
+    uint16_t* gi = gidx + idx_base(frame_off, f) + (int64_t)c * kBinChunk;   // 4 KiB aligned run
+    for (int k = tid; 4 * k < clen; k += kCurvNT)             // 8-byte stores (4 slots)
+        *reinterpret_cast<uint2*>(gi + 4 * k) = *reinterpret_cast<const uint2*>(idl + 4 * k);
+    uint64_t* gb = gbits + ((int64_t)f * n_chunks + c) * (kFeatPlanes * kFeatWords);
+    constexpr int kPl = kEdge ? 3 : 2;
+    if (tid < kPl * kFeatWords) {
+        const int pl = tid / kFeatWords, wi = tid - pl * kFeatWords;
+        const int nbit = min(64, max(0, no - 64 * wi));
+        uint64_t wv = 0;
+        if (nbit > 0) {
+            uint64_t b8[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) b8[u] = *reinterpret_cast<const uint64_t*>(fll + 64 * wi + 8 * u);
+            wv = pack64(b8, pl);                              // bit pl of every flag byte
+            if (nbit < 64) wv &= (1ull << nbit) - 1ull;
+        }
+        gb[pl * kFeatWords + wi] = wv;
+    }
+}
+
+// k_feat_select: one 1024-thread work-group per frame.  The chunks' row counts become, in LDS,
+// each row's base per chunk (exclusive prefix over chunks: indexInRow of the segment's first
+// point; the row lengths n_r and the ring offsets follow) and each segment's start in its chunk's
+// own-tile order (exclusive prefix over rows).  Every (chunk, row) segment of the candidate planes
+// is then copied, 64 bits at a time, to its row's place in ring order (bit ro[r] + indexInRow):
+// the frame's candidates as row-major bit words in LDS, as k_select had them.  The unresolved
+// points are decided (row ends -> curvature 0, :85; open stencils evaluated through the
+// chunk-major index, the same taps in the same order) and OR-ed in; then the greedy spacing rule
+// (:110-123) with one row per lane of wave 0 (wave 1: the edge rule), count-trailing-zeros walks
+// over the row's words; each selection is stored as its chunk-major slot (the walk tracks the
+// chunk its indexInRow falls in).  After a row prefix every thread emits framePlanePtr-ordered
+// output: the point gathered through the slot's index, intensity = indexInRow + row / 100.0 (:77).
+constexpr int kFeatRowWords = kFeatMaxChunks * kFeatWords + 1;   // ring-order words of a frame (+1)
+
+template <bool kEdge>
+__global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __restrict__ pts, int stride,
+                                                             const int64_t* __restrict__ frame_off,
+                                                             int n_rows, int n_chunks, int row_start,
+                                                             int row_end, int plane_span,
+                                                             float plane_min, float edge_min,
+                                                             int32_t* __restrict__ cnt,
+                                                             const uint16_t* __restrict__ gidx,
+                                                             const uint64_t* __restrict__ gbits,
+                                                             int32_t* __restrict__ ring_off,
+                                                             float* __restrict__ curv_cm,
+                                                             int32_t* __restrict__ sel,
+                                                             float4* __restrict__ plane,
+                                                             int32_t* __restrict__ plane_count,
+                                                             int edge_span, int32_t* __restrict__ esel,
+                                                             float4* __restrict__ edge,
+                                                             int32_t* __restrict__ edge_count) {
+    constexpr int kRB = kFeatMaxChunks + 1;                   // odd stride: conflict-free columns
+    __shared__ int rb[kMaxRows][kRB];                         // row base per chunk; [.][ncf] = n_r
+    __shared__ uint16_t ss[kFeatMaxChunks][kMaxRows];         // segment start in the chunk's slots
+    __shared__ uint64_t wl[kEdge ? 2 : 1][kFeatRowWords];     // candidates in ring order
+    __shared__ int ro[kMaxRows + 1];
+    __shared__ int pre[2][kMaxRows + 1];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr int nwv = kSelThreads / 64;
+    const int f = blockIdx.x;
+    const int64_t fb = frame_off[f];
+    const int nf = (int)(frame_off[f + 1] - fb);
+    const int ncf = (nf + kBinChunk - 1) / kBinChunk;
+    int32_t* C = cnt + (int64_t)f * (n_chunks + 1) * kMaxRows;
+    const uint64_t* Bf = gbits + (int64_t)f * n_chunks * (kFeatPlanes * kFeatWords);
+    const uint16_t* GI = gidx + idx_base(frame_off, f);
+    // counts -> segment starts (prefix over rows, per chunk); counts into rb
+    for (int c = w; c < ncf; c += nwv) {
+        const int v = C[c * kMaxRows + lane];
+        int incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        ss[c][lane] = (uint16_t)(incl - v);
+        rb[lane][c] = v;
+    }
+    const int nwf = (nf + 63) / 64 + 1;                       // ring-order words of this frame
+    for (int k = tid; k < nwf; k += kSelThreads) {
+        wl[0][k] = 0ull;
+        if (kEdge) wl[kEdge ? 1 : 0][k] = 0ull;
+    }
+    __syncthreads();
+    for (int r = w; r < kMaxRows; r += nwv) {                 // per row: prefix over the chunks
+        int carry = 0;
+        for (int c0 = 0; c0 < ncf; c0 += 64) {                // uniform
+            const int c = c0 + lane;
+            const int v = c < ncf ? rb[r][c] : 0;
+            int incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            if (c < ncf) rb[r][c] = carry + incl - v;
+            carry += __shfl(incl, 63, 64);
+        }
+        if (lane == 0) rb[r][ncf] = carry;
+    }
+    __syncthreads();
+    if (tid < 64) {                                           // ring offsets: prefix over rows
+        const int nr = tid < n_rows ? rb[tid][ncf] : 0;
+        int incl = nr;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (tid >= o) incl += y;
+        }
+        if (tid < n_rows) ro[tid] = incl - nr;
+        if (tid == 63) ro[n_rows] = incl;
+    }
+    __syncthreads();
+    if (tid <= n_rows) ring_off[(int64_t)f * (n_rows + 1) + tid] = ro[tid];
+    if (curv_cm)                                              // debug: the row bases for k_feat_debug
+        for (int k = tid; k < (ncf + 1) * kMaxRows; k += kSelThreads)
+            C[k] = rb[k % kMaxRows][k / kMaxRows];
+    // candidate planes: every (chunk, row) segment of a row in range to its ring-order bits
+    for (int k = tid; k < ncf * kMaxRows; k += kSelThreads) {
+        const int c = k / kMaxRows, r = k - c * kMaxRows;
+        if (r < row_start || r >= n_rows - row_end) continue;
+        const int L = rb[r][c + 1] - rb[r][c];
+        const int src0 = ss[c][r], dst0 = ro[r] + rb[r][c];
+#pragma unroll
+        for (int pl = 0; pl < (kEdge ? 2 : 1); ++pl) {
+            const uint64_t* Wc = Bf + c * (kFeatPlanes * kFeatWords) + (pl ? 2 * kFeatWords : 0);
+            for (int b = 0; b < L; b += 64) {
+                const int sb = src0 + b, wi = sb >> 6, sh = sb & 63;
+                uint64_t v = Wc[wi] >> sh;
+                if (sh && wi + 1 < kFeatWords) v |= Wc[wi + 1] << (64 - sh);
+                const int nb = L - b;
+                if (nb < 64) v &= (1ull << nb) - 1ull;
+                if (!v) continue;
+                const int db = dst0 + b, di = db >> 6, dh = db & 63;
+                atomicOr((unsigned long long*)&wl[pl][di], v << dh);
+                if (dh) atomicOr((unsigned long long*)&wl[pl][di + 1], v >> (64 - dh));
+            }
+        }
+    }
+    // the unresolved own points of rows in range
+    for (int k = tid; k < ncf * kFeatWords; k += kSelThreads) {
+        const int c = k / kFeatWords, wi = k - c * kFeatWords;
+        uint64_t u = Bf[c * (kFeatPlanes * kFeatWords) + kFeatWords + wi];
+        while (u) {
+            const int p = 64 * wi + (int)__builtin_ctzll(u);
+            u &= u - 1ull;
+            int r = 0;                                        // the last row whose segment starts <= p
+#pragma unroll
+            for (int st = 32; st > 0; st >>= 1)
+                if (r + st < kMaxRows && ss[c][r + st] <= p) r += st;
+            const int j = rb[r][c] + (p - ss[c][r]), nr = rb[r][ncf];
+            const int g = ro[r] + j;                          // ring position
+            if (j < 5 || j >= nr - 5) {                       // curvature 0: a planar candidate
+                atomicOr((unsigned long long*)&wl[0][g >> 6], 1ull << (g & 63));
+                continue;
+            }
+            float ux[11], uy[11], uz[11];                     // an open stencil, through the index
+#pragma unroll
+            for (int m = 0; m < 11; ++m) {
+                const int jj = j - 5 + m;
+                int cc = 0;                                   // the last chunk whose base <= jj
+                for (int st = 64; st > 0; st >>= 1)
+                    if (cc + st < ncf && rb[r][cc + st] <= jj) cc += st;
+                const int pp = ss[cc][r] + (jj - rb[r][cc]);
+                const int ii = cc * kBinChunk + (int)GI[(int64_t)cc * kBinChunk + pp];
+                const float* q = pts + (fb + ii) * stride;
+                ux[m] = q[0]; uy[m] = q[1]; uz[m] = q[2];
+            }
+            const float d0 = tap11(ux), d1 = tap11(uy), d2 = tap11(uz);
+            float val = d0 * d0 + d1 * d1;
+            val = val + d2 * d2;
+            const uint8_t fl = cand_flags(true, true, val, plane_min, kEdge, edge_min);
+            if (fl & 1) atomicOr((unsigned long long*)&wl[0][g >> 6], 1ull << (g & 63));
+            if (kEdge && (fl & 2)) atomicOr((unsigned long long*)&wl[kEdge ? 1 : 0][g >> 6], 1ull << (g & 63));
+            if (curv_cm) curv_cm[fb + (int64_t)c * kBinChunk + p] = val;
+        }
+    }
+    __syncthreads();
+    if (w < (kEdge ? 2 : 1)) {                                // wave 0 planes, wave 1 edges
+        const int r = lane;
+        const bool e = kEdge && w == 1;
+        const uint64_t* W = wl[e ? 1 : 0];
+        const int span = e ? edge_span : plane_span;
+        int32_t* out = e ? esel : sel;
+        int cnt_r = 0;
+        if (r < n_rows && r >= row_start && r < n_rows - row_end) {
+            const int rs = ro[r], n_r = ro[r + 1] - rs;
+            if (n_r > 0) {
+                int js = 0;                                   // jstart, row-relative
+                int cc = 0;                                   // the chunk of the last selection
+                const int kend = (rs + n_r - 1) >> 6;
+                uint64_t nxt = W[rs >> 6];
+                for (int k = rs >> 6; k <= kend; ++k) {       // the row's words in order
+                    uint64_t wv = nxt;
+                    nxt = W[min(k + 1, kend)];                // the next word in flight
+                    const int gb = k * 64;
+                    int low = rs + js - gb;
+                    if (low >= 64) continue;
+                    if (low > 0) wv &= ~0ull << low;
+                    const int top = rs + n_r - gb;
+                    if (top < 64) wv &= (1ull << top) - 1ull;
+                    while (wv) {
+                        const int j = gb + (int)__builtin_ctzll(wv) - rs;
+                        while (cc + 1 < ncf && rb[r][cc + 1] <= j) ++cc;
+                        out[fb + rs + cnt_r] = cc * kBinChunk + ss[cc][r] + (j - rb[r][cc]);
+                        ++cnt_r;
+                        js = j + span;
+                        low = rs + js - gb;
+                        wv = low >= 64 ? 0ull : (wv & (~0ull << low));
+                    }
+                }
+            }
+        }
+        int incl = cnt_r;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane < n_rows) pre[e ? 1 : 0][lane] = incl - cnt_r;
+        if (lane == 63) pre[e ? 1 : 0][n_rows] = incl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < (kEdge ? 2 : 1); ++e) {
+        const int* P = pre[e];
+        const int total = P[n_rows];
+        if (tid == 0) (e ? edge_count : plane_count)[f] = total;
+        const int32_t* S = e ? esel : sel;
+        float4* O = e ? edge : plane;
+        constexpr int U = 4;
+        for (int k0 = 0; k0 < total; k0 += U * kSelThreads) {   // uniform
+            int kk[U], rr[U], qq[U], ii[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                kk[u] = min(k0 + u * kSelThreads + tid, total - 1);
+                int a = 0;
+#pragma unroll
+                for (int st = 32; st > 0; st >>= 1)
+                    if (a + st < n_rows && P[a + st] <= kk[u]) a += st;
+                rr[u] = a;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) qq[u] = S[fb + ro[rr[u]] + (kk[u] - P[rr[u]])];
+#pragma unroll
+            for (int u = 0; u < U; ++u) ii[u] = (qq[u] & ~(kBinChunk - 1)) + (int)GI[qq[u]];
+            float q[U][3];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float* p = pts + (fb + ii[u]) * stride;
+                q[u][0] = p[0]; q[u][1] = p[1]; q[u][2] = p[2];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int cq = qq[u] / kBinChunk, pq = qq[u] - cq * kBinChunk;
+                const int j = rb[rr[u]][cq] + (pq - ss[cq][rr[u]]);
+                if (k0 + u * kSelThreads + tid < total)
+                    O[fb + kk[u]] = make_float4(q[u][0], q[u][1], q[u][2],
+                                                (float)((double)j + (double)rr[u] / 100.0));
+            }
+        }
+    }
+}
+
+// Parity outputs of the single-read stage (debug only): per own-tile slot of a chunk, its row and
+// indexInRow from the row bases k_feat_select left in cnt, and at its ring position the point
+// (x, y, z, intensity = indexInRow + row / 100.0) and its curvature (chunk-major -> ring order).
+__global__ __launch_bounds__(256) void k_feat_debug(const float* __restrict__ pts, int stride,
+                                                    const int64_t* __restrict__ frame_off,
+                                                    int n_rows, int n_chunks,
+                                                    const int32_t* __restrict__ cnt,
+                                                    const int32_t* __restrict__ ring_off,
+                                                    const uint16_t* __restrict__ gidx,
+                                                    const float* __restrict__ curv_cm,
+                                                    float4* __restrict__ out4, float* __restrict__ curv) {
+    __shared__ int base[kMaxRows], segs[kMaxRows + 1], ro[kMaxRows];
+    const int c = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
+    const int64_t fb = frame_off[f];
+    const int nf = (int)(frame_off[f + 1] - fb);
+    if ((int64_t)c * kBinChunk >= nf) return;
+    const int32_t* Cb = cnt + (int64_t)f * (n_chunks + 1) * kMaxRows;
+    if (tid < 64) {
+        const int b0 = Cb[c * kMaxRows + tid], b1 = Cb[(c + 1) * kMaxRows + tid];
+        const int v = b1 - b0;
+        int incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (tid >= o) incl += y;
+        }
+        base[tid] = b0;
+        segs[tid] = incl - v;
+        if (tid == 63) segs[64] = incl;
+        ro[tid] = tid < n_rows ? ring_off[(int64_t)f * (n_rows + 1) + tid] : 0;
+    }
+    __syncthreads();
+    const int no = segs[64];
+    const uint16_t* GI = gidx + idx_base(frame_off, f) + (int64_t)c * kBinChunk;
+    for (int p = tid; p < no; p += 256) {
+        int r = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1)
+            if (r + st < kMaxRows && segs[r + st] <= p) r += st;
+        const int j = base[r] + (p - segs[r]);
+        const int64_t g = fb + ro[r] + j;
+        const int ii = c * kBinChunk + (int)GI[p];
+        const float* q = pts + (fb + ii) * stride;
+        if (out4) out4[g] = make_float4(q[0], q[1], q[2], (float)((double)j + (double)r / 100.0));
+        if (curv) curv[g] = curv_cm[fb + (int64_t)c * kBinChunk + p];
+    }
+}
+
+// ---- host: the ring-id table ------------------------------------------------------------------
+namespace {
+// the reference's row id of a float ratio (frameFeature.cpp:57-73; oracle/ssf_oracle.c orc_ring_id)
+int host_ring_id(float ratio, int n_rows) {
+    if (ratio != ratio) return -1;
+    const float angle = (float)(std::atan((double)ratio) * 180.0 / 3.14159265358979323846);
+    int id = -1;
+    if (n_rows == 16) {
+        const double v = (double)((angle + 15.0f) / 2.0f) + 0.5;
+        id = v > -2147483648.0 && v < 2147483647.0 ? (int)v : -1;
+    } else if (n_rows == 64) {
+        const double v = (double)angle >= -8.83 ? (double)(2.0f - angle) * 3.0 + 0.5 : (-8.83 - (double)angle) * 2.0 + 0.5;
+        const int t = v > -2147483648.0 && v < 2147483647.0 ? (int)v : -1000;
+        id = (double)angle >= -8.83 ? t : (t == -1000 ? -1 : n_rows / 2 + t);
+    }
+    return (id > -1 && id < n_rows) ? id : -1;
+}
+uint32_t fkey(float f) { uint32_t b; std::memcpy(&b, &f, 4); return (b & 0x80000000u) ? ~b : (b | 0x80000000u); }
+float kfloat(uint32_t k) { const uint32_t b = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k; float f; std::memcpy(&f, &b, 4); return f; }
+int host_cell(float ratio, float r0, float inv) {   // the device's cell, the same float ops
+    const float tc = (ratio - r0) * inv;
+    return tc < 0.0f ? 0 : (tc >= (float)kRingCells ? kRingCells - 1 : std::min((int)tc, kRingCells - 1));
+}
+// smallest key in [lo, hi] with pred true (pred monotone false -> true on the range; hi must satisfy it)
+template <class P> uint32_t first_key(uint32_t lo, uint32_t hi, P pred) {
+    while (lo < hi) {
+        const uint32_t m = lo + (hi - lo) / 2;
+        if (pred(m)) hi = m; else lo = m + 1;
+    }
+    return lo;
+}
+}  // namespace
+
+int build_ring_table(int n_rows, void* out_host) {
+    RingTable& T = *reinterpret_cast<RingTable*>(out_host);
+    if (n_rows == 64) { T.r0 = -0.5f; T.inv = (float)kRingCells / 0.6f; }
+    else { T.r0 = -0.4f; T.inv = (float)kRingCells / 0.8f; }
+    const uint32_t kmin = fkey(-INFINITY), kmax = fkey(INFINITY);
+    // the id's change points: brackets from a dense sweep of [-2, 2] (the ids are -1 beyond),
+    // each refined to the exact first key of the new id
+    std::vector<uint32_t> chg;
+    float prev_r = -2.0f;
+    int prev_id = host_ring_id(prev_r, n_rows);
+    if (host_ring_id(-INFINITY, n_rows) != prev_id || host_ring_id(INFINITY, n_rows) != host_ring_id(2.0f, n_rows))
+        return -1;
+    for (int k = 1; k <= 40000; ++k) {
+        const float r = -2.0f + 4.0f * (float)k / 40000.0f;
+        const int id = host_ring_id(r, n_rows);
+        if (id != prev_id) {
+            const int a = prev_id;
+            chg.push_back(first_key(fkey(prev_r) + 1, fkey(r), [&](uint32_t q) { return host_ring_id(kfloat(q), n_rows) != a; }));
+            if (host_ring_id(kfloat(chg.back()), n_rows) != id) return -2;   // two changes in one bracket
+        }
+        prev_r = r; prev_id = id;
+    }
+    for (int c = 0; c < kRingCells; ++c) {
+        const uint32_t ks = c == 0 ? kmin : first_key(kmin, kmax, [&](uint32_t q) { return host_cell(kfloat(q), T.r0, T.inv) >= c; });
+        const uint32_t ke = c == kRingCells - 1 ? kmax
+                          : first_key(kmin, kmax, [&](uint32_t q) { return host_cell(kfloat(q), T.r0, T.inv) >= c + 1; }) - 1;
+        if (c > 0 && host_cell(kfloat(ks), T.r0, T.inv) != c) return -3;   // an empty cell
+        const int a = host_ring_id(kfloat(ks), n_rows);
+        int nchg = 0;
+        uint32_t at = 0;
+        for (uint32_t q : chg) if (q > ks && q <= ke) { ++nchg; at = q; }
+        if (nchg > 1) return -4;                                             // cells too wide
+        const int b = nchg ? host_ring_id(kfloat(at), n_rows) : a;
+        T.cell[c].thr = nchg ? kfloat(at) : INFINITY;
+        T.cell[c].ids = (int32_t)(((uint32_t)(uint8_t)(int8_t)a) | ((uint32_t)(uint8_t)(int8_t)b << 8));
+    }
+    return 0;
+}
+size_t ring_table_bytes() { return sizeof(RingTable); }
+
+size_t feat_idx_bytes(int64_t total, int n_frames) { return sizeof(uint16_t) * (size_t)(total + 64 * (int64_t)n_frames + 64); }
+size_t feat_bits_bytes(int n_frames, int64_t max_pts) {
+    const int64_t nc = (max_pts + kBinChunk - 1) / kBinChunk;
+    return sizeof(uint64_t) * (size_t)std::max<int64_t>(1, (int64_t)n_frames * nc) * kFeatPlanes * kFeatWords;
+}
+size_t feat_cnt_bytes(int n_frames, int64_t max_pts) {
+    const int64_t nc = (max_pts + kBinChunk - 1) / kBinChunk;
+    return sizeof(int32_t) * (size_t)std::max(1, n_frames) * (nc + 1) * kMaxRows;
+}
+bool feat_single_read(int64_t max_pts) {
+#ifdef SSF_FEAT_LEGACY
+    (void)max_pts;
+    return false;
+#else
+    return (max_pts + kBinChunk - 1) / kBinChunk <= kFeatMaxChunks;
+#endif
+}
+
 size_t flag_bytes(int64_t total, int n_frames) { return (size_t)(total + 64 * (int64_t)n_frames + 64); }
 // per-frame fix-up counts (64-byte aligned block), then the entries at the frame offsets
 static size_t fix_head(int n_frames) { return ((size_t)n_frames * sizeof(uint32_t) + 63) & ~(size_t)63; }
@@ -639,12 +1322,47 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
                                  int32_t* ring_off, int32_t* ring_idx, float4* ring_xyzi, float* curv,
                                  uint8_t* flags, void* fix, int32_t* sel, float4* plane,
-                                 int32_t* plane_count, const EdgeSel* edge) {
+                                 int32_t* plane_count, const EdgeSel* edge, const FeatScratch* fs) {
     const int R = cfg.n_rows;
     const int n_chunks = (int)((max_pts + kBinChunk - 1) / kBinChunk);
     if (n_frames <= 0) return hipSuccess;
     if (R > kMaxRows) return hipErrorInvalidValue;
     if (max_pts >= (int64_t)1 << 24) return hipErrorInvalidValue;   // ring positions: 24 bits
+    const bool dbg = curv != nullptr || ring_xyzi != nullptr;
+    const float emin = edge ? edge->min_curv : 0.f;
+    if (fs && feat_single_read(max_pts) && n_chunks > 0) {
+        // the single-read stage: k_feat_chunk -> k_feat_select (-> k_feat_debug)
+        float* ccm = dbg ? fs->curv_cm : nullptr;
+        const int64_t nblk = (int64_t)n_chunks * n_frames;
+        const dim3 grid((unsigned)((nblk + 7) / 8 * 8));
+        kmark(s, "k_feat_chunk");
+#define SSF_FC_LAUNCH(D, E)                                                                         \
+        hipLaunchKernelGGL((k_feat_chunk<D, E>), grid, dim3(kCurvNT), 0, s, pts, stride, frame_off,  \
+                           n_frames, R, n_chunks, cfg.row_start, cfg.row_end, cfg.plane_min, emin,  \
+                           keep, reinterpret_cast<const RingTable*>(fs->rtab), fs->cnt, fs->gidx,   \
+                           fs->gbits, ccm)
+        if (edge) { if (dbg) SSF_FC_LAUNCH(true, true); else SSF_FC_LAUNCH(false, true); }
+        else { if (dbg) SSF_FC_LAUNCH(true, false); else SSF_FC_LAUNCH(false, false); }
+#undef SSF_FC_LAUNCH
+        kmark(s, "k_feat_select");
+        if (edge)
+            hipLaunchKernelGGL(k_feat_select<true>, dim3(n_frames), dim3(kSelThreads), 0, s, pts, stride,
+                               frame_off, R, n_chunks, cfg.row_start, cfg.row_end, cfg.plane_span,
+                               cfg.plane_min, emin, fs->cnt, fs->gidx, fs->gbits, ring_off, ccm, sel,
+                               plane, plane_count, edge->span, edge->sel, edge->out, edge->count);
+        else
+            hipLaunchKernelGGL(k_feat_select<false>, dim3(n_frames), dim3(kSelThreads), 0, s, pts, stride,
+                               frame_off, R, n_chunks, cfg.row_start, cfg.row_end, cfg.plane_span,
+                               cfg.plane_min, emin, fs->cnt, fs->gidx, fs->gbits, ring_off, ccm, sel,
+                               plane, plane_count, 1, nullptr, nullptr, nullptr);
+        if (dbg) {
+            kmark(s, "k_feat_debug");
+            hipLaunchKernelGGL(k_feat_debug, dim3(n_chunks, n_frames), dim3(256), 0, s, pts, stride,
+                               frame_off, R, n_chunks, fs->cnt, ring_off, fs->gidx, fs->curv_cm,
+                               ring_xyzi, curv);
+        }
+        return hipGetLastError();
+    }
     // fix-up lists: per-frame counts, then the entries at the frame offsets
     uint32_t* fix_count = reinterpret_cast<uint32_t*>(fix);
     int32_t* fixl = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(fix) + fix_head(n_frames));
@@ -655,8 +1373,6 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
     }
     kmark(s, "k_bin_scan");
     hipLaunchKernelGGL(k_bin_scan, dim3(n_frames), dim3(64), 0, s, R, n_chunks, hist, ring_off, fix_count);
-    const bool dbg = curv != nullptr || ring_xyzi != nullptr;
-    const float emin = edge ? edge->min_curv : 0.f;
     if (n_chunks > 0) {
         const int64_t nblk = (int64_t)((n_chunks + kCurvSub - 1) / kCurvSub) * n_frames;
         const dim3 grid((unsigned)((nblk + 7) / 8 * 8));

@@ -1328,10 +1328,24 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         if (it == 1 && tid == 0) S.dg_e[0] = S.dg_e[1] = S.dg_e[2] = 0.0;
         const unsigned long long e_t0 = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef SSF_EM_SGPR
+        // A/B: the 27 E-step parameters as wave-uniform SGPR operands, read
+        // from LDS once per pass instead of once per point pair
+        double Aqs[21], bqs[6];
+#pragma unroll
+        for (int k = 0; k < 21; ++k) Aqs[k] = uni(S.Aq[k]);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) bqs[k] = uni(S.bq[k]);
+#endif
         for_point_pairs(P, Fl, r0, r1, [&](const double* xa, const double* xb, double wb) {
+#ifdef SSF_EM_SGPR
+            const double* Aq = Aqs;
+            const double* bq = bqs;
+#else
             // Aq / bq are re-read from LDS once per PAIR of points (lds_laundered)
             const LdsDouble* Aq = lds_laundered(S.Aq);
             const LdsDouble* bq = lds_laundered(S.bq);
+#endif
             double va[6], vb[6];
 #pragma unroll
             for (int a = 0; a < 6; ++a) { va[a] = xa[a] - mean[a]; vb[a] = xb[a] - mean[a]; }

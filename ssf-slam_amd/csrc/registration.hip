@@ -567,6 +567,19 @@ struct StripGeo {
 // (the header lives in the frame's own m words; the association stages float4 up to there).
 constexpr int kStripHeadWords = (kStripMax + 1) + 2 * kStripMax + 4;
 SSF_DEV bool strip_image_frame(int m) { return m >= kStripHeadWords && m <= kAssocStripF4Max; }
+// every frame the association may stage from an image is one the table imaged: the table sorts
+// it (<= kSortMax) and keeps its float4 strips (<= kTableStripF4Max)
+static_assert(kTableStripF4Max >= kAssocStripF4Max && kSortMax >= kAssocStripF4Max,
+              "strip image: the table must image every frame the association stages as float4");
+// The header's last word is ns | kStripImageMagic << 16; a frame whose table launch did not image
+// it carries 0 there (k_plane_table_sorted's other branches, k_strip_invalidate), and the
+// association builds its strips itself unless the word checks out.
+constexpr int32_t kStripImageMagic = 0x57A1;
+SSF_DEV bool strip_image_valid(const int32_t* __restrict__ head) {
+    const int32_t v = head[3 * kStripMax + 1 + 3];
+    const int ns = v & 0xffff;
+    return (v >> 16) == kStripImageMagic && ns >= 1 && ns <= kStripMax;
+}
 
 SSF_DEV void strip_image_store(const float4* F, const StripLds& T, const StripGeo& g, int m,
                                float4* __restrict__ img, int32_t* __restrict__ head) {
@@ -578,7 +591,8 @@ SSF_DEV void strip_image_store(const float4* F, const StripLds& T, const StripGe
     }
     if (threadIdx.x == 0) {
         int32_t* gh = head + 3 * kStripMax + 1;
-        gh[0] = __float_as_int(g.y0); gh[1] = __float_as_int(g.W); gh[2] = __float_as_int(g.invW); gh[3] = g.ns;
+        gh[0] = __float_as_int(g.y0); gh[1] = __float_as_int(g.W); gh[2] = __float_as_int(g.invW);
+        gh[3] = g.ns | (kStripImageMagic << 16);
     }
 }
 
@@ -587,7 +601,7 @@ SSF_DEV StripGeo strip_image_load(const float4* __restrict__ img, const int32_t*
                                   float4* F, StripLds& T) {
     const int32_t* gh = head + 3 * kStripMax + 1;
     StripGeo g;
-    g.y0 = __int_as_float(gh[0]); g.W = __int_as_float(gh[1]); g.invW = __int_as_float(gh[2]); g.ns = gh[3];
+    g.y0 = __int_as_float(gh[0]); g.W = __int_as_float(gh[1]); g.invW = __int_as_float(gh[2]); g.ns = gh[3] & 0xffff;
     for (int r = threadIdx.x; r < m; r += blockDim.x) F[r] = img[r];
     for (int j = threadIdx.x; j <= kStripMax; j += blockDim.x) T.start[j] = head[j];
     for (int j = threadIdx.x; j < g.ns; j += blockDim.x) {
@@ -1236,6 +1250,9 @@ SSF_DEV void table_sort_regs(const float4* __restrict__ P, int m, float* key, in
 template <int E>
 SSF_DEV void table_sort_radix(const float4* __restrict__ P, int m, void* storage, int* idx) {
     using Sort = rocprim::block_radix_sort<unsigned int, kTableThreads, E, int>;
+    // the exchange storage lives in the key region; the index stores below follow the sort with
+    // no barrier, so the storage must not reach the index region
+    static_assert(sizeof(typename Sort::storage_type) <= kSortMax * 4, "radix sort storage exceeds the key region");
     auto& st = *reinterpret_cast<typename Sort::storage_type*>(storage);
     const int tid = threadIdx.x;
     unsigned int k[E];
@@ -1771,7 +1788,7 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     uint16_t* SI16 = reinterpret_cast<uint16_t*>(SX + 3 * ml);
     // the plane table's image of this last frame when the caller kept it (a copy: ~4 us of the
     // ~40 us build), otherwise the build
-    const StripGeo geo = (!kSoa && strip_xyzi && strip_image_frame(ml))
+    const StripGeo geo = (!kSoa && strip_xyzi && strip_image_frame(ml) && strip_image_valid(strip_head + lo))
         ? strip_image_load(strip_xyzi + lo, strip_head + lo, ml, SL, T)
         : strips_build<kSoa, kStripPerMax>(
               [&](int, int r) { float4 pt = SP[r]; pt.w = __int_as_float(SI[r]); return pt; }, ml, T, SL, SX, SI16);
@@ -2604,6 +2621,13 @@ __global__ void k_accumulate(int n, const double* __restrict__ rel, const double
     }
 }
 
+__global__ __launch_bounds__(256) void k_strip_invalidate(const int64_t* __restrict__ frame_off,
+                                                          const int32_t* __restrict__ count, int n_frames,
+                                                          int32_t* __restrict__ strip_head) {
+    const int f = blockIdx.x * 256 + threadIdx.x;
+    if (f < n_frames && strip_image_frame(count[f])) strip_head[frame_off[f] + 3 * kStripMax + 4] = 0;
+}
+
 hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames,
                               const float4* plane, const int64_t* frame_off, const int32_t* count,
                               int64_t max_m, float* normal, uint8_t* valid, float4* sorted_xyzi,
@@ -2619,6 +2643,9 @@ hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames
         kmark(s, "k_plane_table");
         hipLaunchKernelGGL(k_plane_table, dim3(bx, n_frames), dim3(256), 0, s, plane, frame_off,
                            count, cfg.plane_max, normal, valid);
+        if (strip_head)                     // no image from this launch: no frame may look imaged
+            hipLaunchKernelGGL(k_strip_invalidate, dim3((n_frames + 255) / 256), dim3(256), 0, s,
+                               frame_off, count, n_frames, strip_head);
     }
     return hipGetLastError();
 }

@@ -70,12 +70,30 @@ struct EdgeSel {
     float4* out;
     int32_t* count;
 };
+// Scratch of the single-read feature stage (k_feat_chunk / k_feat_select, frames of at most
+// 128 chunks): per-(chunk, row) counts -> row bases, u16 chunk positions per own-tile slot, the
+// chunks' candidate / unresolved bit planes, and (debug outputs only) chunk-major curvature.
+struct FeatScratch {
+    const void* rtab;   // the ring-id table (build_ring_table), device copy
+    int32_t* cnt;       // feat_cnt_bytes
+    uint16_t* gidx;     // feat_idx_bytes
+    uint64_t* gbits;    // feat_bits_bytes
+    float* curv_cm;     // total floats (debug), else nullptr
+};
+size_t feat_idx_bytes(int64_t total, int n_frames);
+size_t feat_bits_bytes(int n_frames, int64_t max_pts);
+size_t feat_cnt_bytes(int n_frames, int64_t max_pts);
+bool feat_single_read(int64_t max_pts);
+// host: the ring-id table of n_rows (16 / 64) into out (ring_table_bytes); 0 or a negative code
+int build_ring_table(int n_rows, void* out_host);
+size_t ring_table_bytes();
 hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_frames,
                                  const float* pts, int stride, const int64_t* frame_off,
                                  int64_t max_pts, const uint8_t* keep, int8_t* rid, int32_t* hist,
                                  int32_t* ring_off, int32_t* ring_idx, float4* ring_xyzi,
                                  float* curv, uint8_t* flags, void* fix, int32_t* sel, float4* plane,
-                                 int32_t* plane_count, const EdgeSel* edge = nullptr);
+                                 int32_t* plane_count, const EdgeSel* edge = nullptr,
+                                 const FeatScratch* fs = nullptr);
 
 // ---- launchers (registration.hip) ----
 hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames,

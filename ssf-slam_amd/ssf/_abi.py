@@ -18,6 +18,9 @@ LIB_PATH = os.environ.get("SSF_LIB", os.path.join(LIB_DIR, "libssf_frontend.so")
 SSF_OK, SSF_E_ARG, SSF_E_HIP, SSF_E_NOMEM, SSF_E_CAPACITY, SSF_E_NODEV = 0, -1, -2, -3, -4, -5
 SOLVER_CERES_LM, SOLVER_GN = 0, 1
 MASK_GMM, MASK_GT, MASK_GIVEN = 0, 1, 2
+# frames of plane points the association can stage from the plane table's strip image
+# (registration.hip: kStripHeadWords, kAssocStripF4Max)
+STRIP_IMAGE_MIN, STRIP_IMAGE_MAX = (256 + 1) + 2 * 256 + 4, 6144
 POSE_OUT_STRIDE = 32
 POSE_OUT = dict(T=0, Q=3, R=7, STATUS=16, NBG=17, BGLABEL=18, KM_ITER=19, EM_ITER=20,
                 CONVERGED=21, CENTER0=22, CENTER1=23, LOWER_BOUND=24, PASSES=25)

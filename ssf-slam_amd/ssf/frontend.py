@@ -252,7 +252,10 @@ class Frontend:
         if not brute_force:
             sx = torch.empty((total, 4), dtype=torch.float32, device=self.device)
             si = torch.empty(total, dtype=torch.int32, device=self.device)
-            if strips:
+            # the association stages an image only for frames of STRIP_IMAGE_MIN..MAX points
+            # (registration.hip strip_image_frame) and only in launches whose plane bound is
+            # within MAX (float4 strips): otherwise the 20 B per plane point would be dead weight
+            if strips and _abi.STRIP_IMAGE_MIN <= pb.max_points and pb.max_points <= _abi.STRIP_IMAGE_MAX:
                 st = (torch.empty((total, 4), dtype=torch.float32, device=self.device),
                       torch.empty(total, dtype=torch.int32, device=self.device))
         rc = _abi.lib().ssf_plane_table_batch(self._h, _stream(self.device), pb.count.numel(),

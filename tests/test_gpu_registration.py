@@ -391,3 +391,36 @@ def test_kabsch_warm_start_independent_pairs(oracle, dev):
         assert np.abs(got[p, 4:] - t).max() < TOL_T and _quat_angle(got[p, :4], q) < TOL_R, p
         # the warm start is already close: the registration moves it by decimetres at most
         assert np.abs(got[p, 4:] - ws[p, 4:]).max() < 0.2
+
+
+def test_strip_image_invalidated_when_not_imaged(dev):
+    """a plane-table launch that does not image its frames (here the brute-force table,
+    max_plane_points above the sort limit) clears their header's validity word, so an association
+    handed these strip buffers rebuilds its strips instead of reading a stale image."""
+    import ssf
+    from ssf import _abi
+    from ssf.frontend import _ptr, _stream
+    fe = ssf.Frontend(64, device=dev.index)
+    pb = _planes(fe, dev, [frame(3, 1, n_az=1875)[0], frame(3, 2, n_az=1875)[0]])
+    m = [int(c) for c in pb.count.cpu()]
+    assert all(_abi.STRIP_IMAGE_MIN <= c <= _abi.STRIP_IMAGE_MAX for c in m), m
+    total = pb.xyzi.shape[0]
+    normal = torch.empty((total, 3), dtype=torch.float32, device=dev)
+    valid = torch.empty(total, dtype=torch.uint8, device=dev)
+    sx = torch.empty((total, 4), dtype=torch.float32, device=dev)
+    si = torch.empty(total, dtype=torch.int32, device=dev)
+    img = torch.zeros((total, 4), dtype=torch.float32, device=dev)
+    head = torch.zeros(total, dtype=torch.int32, device=dev)
+    word = 3 * 256 + 4                                  # ns | magic << 16
+    offs = [int(v) for v in pb.h_off[:2]]
+    for o in offs:
+        head[o + word] = 0x57A1 << 16 | 7               # a stale "valid" header
+    rc = _abi.lib().ssf_plane_table_batch(fe._h, _stream(dev), 2, _ptr(pb.xyzi), _ptr(pb.off),
+                                          _ptr(pb.count), 20000, _ptr(normal), _ptr(valid), _ptr(sx),
+                                          _ptr(si), _ptr(img), _ptr(head))
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert [int(head[o + word]) for o in offs] == [0, 0]
+    t = fe.plane_table(pb)                              # the sorted table images them again
+    torch.cuda.synchronize()
+    assert all((int(t.strips[1][o + word]) >> 16) == 0x57A1 for o in offs)

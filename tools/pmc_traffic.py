@@ -21,7 +21,7 @@ import csv
 import json
 from collections import defaultdict
 
-KERNELS = ("k_mask_pose", "k_bin_count", "k_bin_scan", "k_bin_curv", "k_select",
+KERNELS = ("k_mask_pose_f64", "k_mask_pose", "k_feat_chunk", "k_feat_select", "k_bin_count", "k_bin_scan", "k_bin_curv", "k_select",
            "k_plane_table_sorted", "k_associate_strips", "k_associate_lds", "k_associate_sorted", "k_solve")
 
 
@@ -65,6 +65,7 @@ def main():
                 d = json.loads(line)
                 out["config"] = {k: d["config"][k] for k in ("sequences_per_gpu", "points_per_frame",
                                                               "mask_before_features")}
+                out["lib_sha16"] = d.get("lib_sha16")        # the build these counters measured
                 for k, v in d.get("kernels", {}).items():
                     if k in out["kernels"] and "bytes" in v:
                         out["kernels"][k]["algorithmic_bytes_per_launch"] = v["bytes"]

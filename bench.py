@@ -760,6 +760,7 @@ def sequences(args, world=1, rank=0, local=0):
         sm = s_masks[j % len(s_masks)]
         with torch.cuda.stream(sm):
             out, bg = fe_mask.mask_pose(pos, flow, offK, hK, mode="gmm", want_mask=True)
+            mrec = out[:, 0:7].view(K, B, 7).clone() if timing else None   # the SSF poses, on their stream
             done = torch.cuda.Event()
             done.record(sm)
         if masked:
@@ -794,7 +795,7 @@ def sequences(args, world=1, rank=0, local=0):
                     (lpb, ltab) = cur
                 rel_k = torch.stack(snaps, 0)
             if timing:
-                records.append(torch.cat([rel_k, out[:, 0:7].view(K, B, 7)], 2))
+                records.append((rel_k, mrec, sm))
         last = view(pb, table, K - 1)
         prev_out = out[(K - 1) * B:]
         return out
@@ -808,18 +809,19 @@ def sequences(args, world=1, rank=0, local=0):
     t0 = time.perf_counter()
     for j in range(W, W + S):
         step(j, True)
+    # per timed frame: the registration pose [q, t] and the SSF Kabsch pose [t, q] -> [F, B, 14]
+    cur = torch.cuda.current_stream(dev)
+    for s in (*s_masks, s_reg):
+        cur.wait_stream(s)
+    mine = torch.cat([torch.cat([r, m], 2) for r, m, _ in records], 0)
     gathered = None
     if world > 1:                  # the one exchange: every timed frame's records, one all-gather
-        cur = torch.cuda.current_stream(dev)
-        for s in (*s_masks, s_reg):
-            cur.wait_stream(s)
-        gathered = sd.gather_sequence_records(torch.cat(records, 0), args.sequences_total)
+        gathered = sd.gather_sequence_records(mine, args.sequences_total)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    mine = torch.cat(records, 0)
     gather_ok = None
     finite = bool(torch.isfinite(mine).all())
     if world > 1:

@@ -77,6 +77,9 @@ SSF_DEV int ring_id(float x, float y, float z, int n_rows) {
 // narrowest bin), so per cell {the float ratio where the second id starts, id below, id from
 // there}.  The device computes the ratio exactly as the reference and does ONE table lookup and
 // one compare: no atan, no double precision, no divergent exact path.
+#ifndef SSF_FEAT_EXACT_ID
+#define SSF_FEAT_EXACT_ID 0                      // A/B: the correctly rounded ratio for every point
+#endif
 constexpr int kRingCells = 256;
 struct RingCell {
     float thr;          // ratios >= thr (float order) take id_b
@@ -87,15 +90,36 @@ struct RingTable {
     RingCell cell[kRingCells];
 };
 
-SSF_DEV int ring_id_table(float x, float y, float z, float r0, float inv, const RingCell* T) {
-    const float r2 = x * x + y * y;
-    const float ratio = z / sqrtf(r2);
+SSF_DEV int ring_id_lookup(float ratio, float r0, float inv, const RingCell* T) {
     int ci = (int)((ratio - r0) * inv);          // v_cvt_i32_f32 saturates; NaN handled below
     ci = min(max(ci, 0), kRingCells - 1);
     const RingCell rc = T[ci];
     const int a = (int)(int8_t)(rc.ids & 0xff), b = (int)(int8_t)((rc.ids >> 8) & 0xff);
     const int id = ratio < rc.thr ? a : b;
     return ratio == ratio ? id : -1;             // 0 / 0 (a point at the origin): no row
+}
+
+// The reference's ratio needs a correctly rounded sqrt and divide (~30 instructions).  The
+// hardware reciprocal square root gives it to ~3e-7 relative (v_rsq_f32 1 ulp, one multiply,
+// and the two roundings of the exact form): that ratio takes the exact form's id unless a table
+// threshold or a cell edge lies within 1e-6 of it (relative; a few in a million points), or r2
+// is tiny or not finite -- then the exact form decides (a rare, divergent branch).
+SSF_DEV int ring_id_table(float x, float y, float z, float r0, float inv, const RingCell* T) {
+    const float r2 = x * x + y * y;
+    if (SSF_FEAT_EXACT_ID) return ring_id_lookup(z / sqrtf(r2), r0, inv, T);   // A/B: no fast path
+    const float ra = z * __builtin_amdgcn_rsqf(r2);
+    int ci = (int)((ra - r0) * inv);
+    ci = min(max(ci, 0), kRingCells - 1);
+    const RingCell rc = T[ci];
+    const float m = 1e-6f * fmaxf(1.0f, fabsf(ra));
+    const float tc = (ra - r0) * inv, fr = tc - floorf(tc);
+    // every test evaluated (no short-circuit: one exec mask, one branch)
+    const int near = (int)!(fabsf(ra - rc.thr) > m) | (int)!(fr > m * inv) | (int)!(fr < 1.0f - m * inv) |
+                     (int)!(r2 > 1e-30f) | (int)!(r2 < 1e30f);
+    const int a = (int)(int8_t)(rc.ids & 0xff), b = (int)(int8_t)((rc.ids >> 8) & 0xff);
+    int id = ra < rc.thr ? a : b;
+    if (near) id = ring_id_lookup(z / sqrtf(r2), r0, inv, T);
+    return id;
 }
 
 // Each thread issues all of its kCountSteps point loads (clamped, unconditional) before the first ring
@@ -684,6 +708,15 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const float* __restrict_
 // stencils, rare for azimuth-ordered scans -- through the chunk-major index, the same taps in the
 // same order.  Every write of k_feat_chunk is a whole, aligned, contiguous run (no per-row
 // scatter); the greedy of k_feat_select walks each row as its sequence of (chunk, row) segments.
+#ifndef SSF_FEAT_PACKED
+#define SSF_FEAT_PACKED 0                        // packed-f32 stencil (A/B, see k_feat_chunk)
+#endif
+#ifndef SSF_FEAT_ZONES
+#define SSF_FEAT_ZONES 1                         // k_feat_chunk: one-zone steps count without masks
+#endif
+#ifndef SSF_FEAT_WAVES
+#define SSF_FEAT_WAVES 5                         // k_feat_chunk waves per SIMD (launch bound)
+#endif
 constexpr int kFeatMaxChunks = 128;              // 262144 points per frame (k_feat_select's LDS)
 constexpr int kFeatPlanes = 3;                   // planar candidate, unresolved, edge candidate
 constexpr int kFeatWords = kBinChunk / 64;       // 64-bit words per plane and chunk
@@ -695,7 +728,7 @@ static_assert(kCurvSub == 1 && kBinChunk == 2048, "own-tile slots and chunk posi
 SSF_DEV int64_t idx_base(const int64_t* frame_off, int f) { return (frame_off[f] & ~(int64_t)31) + 64 * (int64_t)f; }
 
 template <bool kDebug, bool kEdge>
-__global__ __launch_bounds__(kCurvNT, 5) void k_feat_chunk(const float* __restrict__ pts, int stride,
+__global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const float* __restrict__ pts, int stride,
                                                     const int64_t* __restrict__ frame_off,
                                                     int n_frames, int n_rows, int n_chunks,
                                                     int row_start, int row_end, float plane_min,
@@ -779,12 +812,19 @@ __global__ __launch_bounds__(kCurvNT, 5) void k_feat_chunk(const float* __restri
         const uint64_t m = __hip_atomic_load(gm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const uint64_t old = wrun[w][rs];
         const int s0 = q0 + 64 * st;                          // uniform
-        const int hbl = min(64, max(0, hb - s0)), hel = min(64, max(0, he - s0));
-        const uint64_t hm = hbl >= 64 ? ~0ull : ((1ull << hbl) - 1ull);   // lanes before the chunk
-        const uint64_t om = hel >= 64 ? ~0ull : ((1ull << hel) - 1ull);   // lanes before its end
+        const int hbl = __builtin_amdgcn_readfirstlane(min(64, max(0, hb - s0)));   // SGPRs
+        const int hel = __builtin_amdgcn_readfirstlane(min(64, max(0, he - s0)));
         const int rin = __popcll(m & lanemask_lt());
-        wrun[w][rs] = old + (uint64_t)__popcll(m) + ((uint64_t)__popcll(m & hm) << 16) +
-                      ((uint64_t)__popcll(m & om) << 32);
+        const uint64_t pm = (uint64_t)__popcll(m);
+        uint64_t inc;
+        if (SSF_FEAT_ZONES && (hbl == 0 || hbl == 64) && (hel == 0 || hel == 64)) {   // uniform: one zone
+            inc = pm * (1ull + (hbl ? 1ull << 16 : 0ull) + (hel ? 1ull << 32 : 0ull));
+        } else {                                              // the (at most two) boundary steps
+            const uint64_t hm = hbl >= 64 ? ~0ull : ((1ull << hbl) - 1ull);   // lanes before the chunk
+            const uint64_t om = hel >= 64 ? ~0ull : ((1ull << hel) - 1ull);   // lanes before its end
+            inc = pm + ((uint64_t)__popcll(m & hm) << 16) + ((uint64_t)__popcll(m & om) << 32);
+        }
+        wrun[w][rs] = old + inc;
         __hip_atomic_store(gm, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         idr[st] = (id & 0xff) | (((int)(old & 0xffffu) + rin) << 8);
     }
@@ -853,6 +893,44 @@ __global__ __launch_bounds__(kCurvNT, 5) void k_feat_chunk(const float* __restri
         }
     }
     __syncthreads();
+#if SSF_FEAT_PACKED
+    // ---- curvature of this thread's kCE tile entries, one coordinate at a time, entries i and
+    // i + kCE / 2 side by side in packed f32 (v_pk_add_f32 / v_pk_mul_f32: two IEEE operations,
+    // the same rounding as two scalar ones): tap k of the pair is (t[k0 + i + k], t[k0 + i + 6 + k]),
+    // one ds_read2_b32 -- the sums keep the reference's left-to-right order (frameFeature.cpp:88-97)
+    static_assert(kCE == 12, "the packed stencil pairs entries i and i + 6");
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const int k0 = kCE * tid;
+    f2 v2[kCE / 2];
+    auto coord = [&](bool first) {
+        const float* t = sc + k0 + 3;                         // tap 0 of entry 0 (centre at + 5)
+        f2 P[kCE / 2 + 10];                                   // P[j] = (t[j], t[j + 6])
+#pragma unroll
+        for (int j = 0; j < kCE / 2 + 10; ++j) P[j] = f2{t[j], t[j + kCE / 2]};
+#pragma unroll
+        for (int i = 0; i < kCE / 2; ++i) {
+            f2 acc = P[i] + P[i + 1];
+#pragma unroll
+            for (int k = 2; k < 11; ++k) acc = (k == 5) ? acc - f2{10.0f, 10.0f} * P[i + 5] : acc + P[i + k];
+            const f2 sq = acc * acc;
+            v2[i] = first ? sq : v2[i] + sq;
+        }
+    };
+    coord(true);
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < kWinQ; ++st) sc[kTilePad + loc[st]] = py[st];
+    __syncthreads();
+    coord(false);
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < kWinQ; ++st) sc[kTilePad + loc[st]] = pz[st];
+    __syncthreads();
+    coord(false);
+    float v[kCE];
+#pragma unroll
+    for (int i = 0; i < kCE / 2; ++i) { v[i] = v2[i].x; v[i + kCE / 2] = v2[i].y; }
+#else
     // ---- curvature of this thread's kCE tile entries, one coordinate at a time (k_bin_curv)
     const int k0 = kCE * tid;
     float v[kCE];
@@ -888,6 +966,7 @@ __global__ __launch_bounds__(kCurvNT, 5) void k_feat_chunk(const float* __restri
 #pragma unroll
         for (int i = 0; i < kCE; ++i) v[i] = v[i] + d0[i] * d0[i];
     }
+#endif
     uint16_t mt[kCE];
 #pragma unroll
     for (int i = 0; i < kCE; i += 4) {                        // k0 + kCE <= kTileE: 8-byte reads
@@ -963,6 +1042,9 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
     __shared__ int rb[kMaxRows][kRB];                         // row base per chunk; [.][ncf] = n_r
     __shared__ uint16_t ss[kFeatMaxChunks][kMaxRows];         // segment start in the chunk's slots
     __shared__ uint64_t wl[kEdge ? 2 : 1][kFeatRowWords];     // candidates in ring order
+    // one chunk-major candidate plane staged from global (coalesced) for the transposition, then
+    // reused for the planar selections (indexInRow per output slot) when they fit
+    __shared__ uint64_t stg[kFeatMaxChunks * kFeatWords];
     __shared__ int ro[kMaxRows + 1];
     __shared__ int pre[2][kMaxRows + 1];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1026,19 +1108,25 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
     if (curv_cm)                                              // debug: the row bases for k_feat_debug
         for (int k = tid; k < (ncf + 1) * kMaxRows; k += kSelThreads)
             C[k] = rb[k % kMaxRows][k / kMaxRows];
-    // candidate planes: every (chunk, row) segment of a row in range to its ring-order bits
-    for (int k = tid; k < ncf * kMaxRows; k += kSelThreads) {
-        const int c = k / kMaxRows, r = k - c * kMaxRows;
-        if (r < row_start || r >= n_rows - row_end) continue;
-        const int L = rb[r][c + 1] - rb[r][c];
-        const int src0 = ss[c][r], dst0 = ro[r] + rb[r][c];
+    // candidate planes: every (chunk, row) segment of a row in range to its ring-order bits,
+    // one plane at a time through the staging copy
 #pragma unroll
-        for (int pl = 0; pl < (kEdge ? 2 : 1); ++pl) {
-            const uint64_t* Wc = Bf + c * (kFeatPlanes * kFeatWords) + (pl ? 2 * kFeatWords : 0);
+    for (int pl = 0; pl < (kEdge ? 2 : 1); ++pl) {
+        if (pl) __syncthreads();                              // the previous plane's reads are done
+        for (int k = tid; k < ncf * kFeatWords; k += kSelThreads) {
+            const int c = k / kFeatWords, wi = k - c * kFeatWords;
+            stg[k] = Bf[c * (kFeatPlanes * kFeatWords) + (pl ? 2 * kFeatWords : 0) + wi];
+        }
+        __syncthreads();
+        for (int k = tid; k < ncf * kMaxRows; k += kSelThreads) {
+            const int c = k / kMaxRows, r = k - c * kMaxRows;
+            if (r < row_start || r >= n_rows - row_end) continue;
+            const int L = rb[r][c + 1] - rb[r][c];
+            const int src0 = c * kBinChunk + ss[c][r], dst0 = ro[r] + rb[r][c];
             for (int b = 0; b < L; b += 64) {
                 const int sb = src0 + b, wi = sb >> 6, sh = sb & 63;
-                uint64_t v = Wc[wi] >> sh;
-                if (sh && wi + 1 < kFeatWords) v |= Wc[wi + 1] << (64 - sh);
+                uint64_t v = stg[wi] >> sh;
+                if (sh && wi + 1 < ncf * kFeatWords) v |= stg[wi + 1] << (64 - sh);
                 const int nb = L - b;
                 if (nb < 64) v &= (1ull << nb) - 1ull;
                 if (!v) continue;
@@ -1087,18 +1175,21 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
         }
     }
     __syncthreads();
+    // the planar selections (indexInRow per slot) stay in LDS when a frame cannot make more than
+    // the staging region holds (sum over rows of ceil(n_r / span) <= nf / span + rows)
+    const bool sel_lds = nf / max(1, plane_span) + kMaxRows <= kFeatMaxChunks * kFeatWords * 2;
+    int32_t* sel_l = reinterpret_cast<int32_t*>(stg);
     if (w < (kEdge ? 2 : 1)) {                                // wave 0 planes, wave 1 edges
         const int r = lane;
         const bool e = kEdge && w == 1;
         const uint64_t* W = wl[e ? 1 : 0];
         const int span = e ? edge_span : plane_span;
-        int32_t* out = e ? esel : sel;
+        int32_t* out = e ? esel + fb : (sel_lds ? sel_l : sel + fb);
         int cnt_r = 0;
         if (r < n_rows && r >= row_start && r < n_rows - row_end) {
             const int rs = ro[r], n_r = ro[r + 1] - rs;
             if (n_r > 0) {
                 int js = 0;                                   // jstart, row-relative
-                int cc = 0;                                   // the chunk of the last selection
                 const int kend = (rs + n_r - 1) >> 6;
                 uint64_t nxt = W[rs >> 6];
                 for (int k = rs >> 6; k <= kend; ++k) {       // the row's words in order
@@ -1112,8 +1203,7 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
                     if (top < 64) wv &= (1ull << top) - 1ull;
                     while (wv) {
                         const int j = gb + (int)__builtin_ctzll(wv) - rs;
-                        while (cc + 1 < ncf && rb[r][cc + 1] <= j) ++cc;
-                        out[fb + rs + cnt_r] = cc * kBinChunk + ss[cc][r] + (j - rb[r][cc]);
+                        out[rs + cnt_r] = j;                  // indexInRow
                         ++cnt_r;
                         js = j + span;
                         low = rs + js - gb;
@@ -1137,11 +1227,11 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
         const int* P = pre[e];
         const int total = P[n_rows];
         if (tid == 0) (e ? edge_count : plane_count)[f] = total;
-        const int32_t* S = e ? esel : sel;
+        const int32_t* S = e ? esel + fb : (sel_lds ? sel_l : sel + fb);
         float4* O = e ? edge : plane;
         constexpr int U = 4;
         for (int k0 = 0; k0 < total; k0 += U * kSelThreads) {   // uniform
-            int kk[U], rr[U], qq[U], ii[U];
+            int kk[U], rr[U], jj[U], ii[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 kk[u] = min(k0 + u * kSelThreads + tid, total - 1);
@@ -1152,9 +1242,17 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
                 rr[u] = a;
             }
 #pragma unroll
-            for (int u = 0; u < U; ++u) qq[u] = S[fb + ro[rr[u]] + (kk[u] - P[rr[u]])];
+            for (int u = 0; u < U; ++u) jj[u] = S[ro[rr[u]] + (kk[u] - P[rr[u]])];
 #pragma unroll
-            for (int u = 0; u < U; ++u) ii[u] = (qq[u] & ~(kBinChunk - 1)) + (int)GI[qq[u]];
+            for (int u = 0; u < U; ++u) {                     // indexInRow -> chunk, slot, position
+                const int r = rr[u], j = jj[u];
+                int cc = 0;                                   // the last chunk whose base <= j
+#pragma unroll
+                for (int st = 64; st > 0; st >>= 1)
+                    if (cc + st < ncf && rb[r][cc + st] <= j) cc += st;
+                const int q = cc * kBinChunk + ss[cc][r] + (j - rb[r][cc]);
+                ii[u] = cc * kBinChunk + (int)GI[q];
+            }
             float q[U][3];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -1162,13 +1260,10 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
                 q[u][0] = p[0]; q[u][1] = p[1]; q[u][2] = p[2];
             }
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int cq = qq[u] / kBinChunk, pq = qq[u] - cq * kBinChunk;
-                const int j = rb[rr[u]][cq] + (pq - ss[cq][rr[u]]);
+            for (int u = 0; u < U; ++u)
                 if (k0 + u * kSelThreads + tid < total)
                     O[fb + kk[u]] = make_float4(q[u][0], q[u][1], q[u][2],
-                                                (float)((double)j + (double)rr[u] / 100.0));
-            }
+                                                (float)((double)jj[u] + (double)rr[u] / 100.0));
         }
     }
 }

@@ -272,3 +272,30 @@ def test_product_path_equals_debug_path(oracle, dev):
         got = _planes_product(fe, [c, c[: len(c) // 3]], dev)
         assert np.array_equal(got[0].view(np.uint32), oracle.extract_planes(c, n_rows).view(np.uint32))
         assert np.array_equal(got[1].view(np.uint32), oracle.extract_planes(c[: len(c) // 3], n_rows).view(np.uint32))
+
+
+@pytest.mark.parametrize("n_rows", [64, 16])
+def test_ring_id_table_edges(oracle, dev, n_rows):
+    """The single-read stage's ring id (one table cell + one compare, features.hip
+    ring_id_table) on the exact ratios where the reference's row id changes, +-3 ulps around each
+    (points (1, 0, ratio): z / sqrt(1) is the ratio itself), every cell edge, the origin (0/0) and
+    +-inf ratios: the ring-ordered cloud equals the oracle's (glibc atan, double angle chain), so
+    every point lands in the reference's row.  The points are shuffled and 64 copies of each are
+    interleaved, so every row holds enough points for full stencils as well."""
+    import ssf
+    import test_ring_table as rt
+    r0, inv, cells = rt.table(n_rows)
+    probe = []
+    for t in [t for t in cells["thr"] if np.isfinite(t)] + [np.float32(r0 + k / inv) for k in range(0, 257, 8)]:
+        u = np.float32(t).view(np.int32)
+        probe += [np.int32(u + d).view(np.float32) for d in range(-3, 4)]
+    z = np.array(probe, np.float32)
+    pts = np.stack([np.ones_like(z), np.zeros_like(z), z], 1)
+    pts = np.concatenate([pts, [[0, 0, 0], [0, 0, 1], [0, 0, -1]]]).astype(np.float32)
+    rng = np.random.default_rng(n_rows)
+    cloud = np.concatenate([pts[rng.permutation(len(pts))] for _ in range(64)]).astype(np.float32)
+    fe = ssf.Frontend(n_rows, device=dev.index)
+    out, h_off = _run(fe, [cloud], dev)
+    _check_frame(oracle, fe, out, h_off, 0, cloud, n_rows)
+    ids = np.array([oracle.lib().orc_ring_id(float(p[0]), float(p[1]), float(p[2]), n_rows) for p in pts])
+    assert len(set(ids.tolist()) - {-1}) == n_rows         # every row is exercised

@@ -712,7 +712,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const float* __restrict_
 #define SSF_FEAT_PACKED 0                        // packed-f32 stencil (A/B, see k_feat_chunk)
 #endif
 #ifndef SSF_FEAT_ZONES
-#define SSF_FEAT_ZONES 1                         // k_feat_chunk: one-zone steps count without masks
+#define SSF_FEAT_ZONES 0                         // A/B: one-zone steps count without masks (spills: slower)
 #endif
 #ifndef SSF_FEAT_WAVES
 #define SSF_FEAT_WAVES 5                         // k_feat_chunk waves per SIMD (launch bound)
@@ -1046,6 +1046,7 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
     // reused for the planar selections (indexInRow per output slot) when they fit
     __shared__ uint64_t stg[kFeatMaxChunks * kFeatWords];
     __shared__ int ro[kMaxRows + 1];
+    __shared__ int lb[kMaxRows + 1];                          // per-row slot bases of the LDS selections
     __shared__ int pre[2][kMaxRows + 1];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1102,6 +1103,17 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
         }
         if (tid < n_rows) ro[tid] = incl - nr;
         if (tid == 63) ro[n_rows] = incl;
+        // a row of n_r points makes at most ceil(n_r / planeSpan) selections: slot bases for
+        // the LDS copy of the planar selections
+        const int cap = tid < n_rows ? (nr + plane_span - 1) / max(1, plane_span) : 0;
+        int ci = cap;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(ci, o, 64);
+            if (tid >= o) ci += y;
+        }
+        if (tid < n_rows) lb[tid] = ci - cap;
+        if (tid == 63) lb[n_rows] = ci;
     }
     __syncthreads();
     if (tid <= n_rows) ring_off[(int64_t)f * (n_rows + 1) + tid] = ro[tid];
@@ -1177,20 +1189,22 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
     __syncthreads();
     // the planar selections (indexInRow per slot) stay in LDS when a frame cannot make more than
     // the staging region holds (sum over rows of ceil(n_r / span) <= nf / span + rows)
-    const bool sel_lds = nf / max(1, plane_span) + kMaxRows <= kFeatMaxChunks * kFeatWords * 2;
+    const bool sel_lds = lb[n_rows] <= kFeatMaxChunks * kFeatWords * 2;
     int32_t* sel_l = reinterpret_cast<int32_t*>(stg);
     if (w < (kEdge ? 2 : 1)) {                                // wave 0 planes, wave 1 edges
         const int r = lane;
         const bool e = kEdge && w == 1;
         const uint64_t* W = wl[e ? 1 : 0];
         const int span = e ? edge_span : plane_span;
-        int32_t* out = e ? esel + fb : (sel_lds ? sel_l : sel + fb);
+        const bool lds_out = !e && sel_lds;
+        int32_t* out = e ? esel + fb : (lds_out ? sel_l : sel + fb);
         int cnt_r = 0;
         if (r < n_rows && r >= row_start && r < n_rows - row_end) {
             const int rs = ro[r], n_r = ro[r + 1] - rs;
             if (n_r > 0) {
                 int js = 0;                                   // jstart, row-relative
                 const int kend = (rs + n_r - 1) >> 6;
+                int32_t* orow = out + (lds_out ? lb[r] : rs);  // this row's selection slots
                 uint64_t nxt = W[rs >> 6];
                 for (int k = rs >> 6; k <= kend; ++k) {       // the row's words in order
                     uint64_t wv = nxt;
@@ -1203,7 +1217,7 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
                     if (top < 64) wv &= (1ull << top) - 1ull;
                     while (wv) {
                         const int j = gb + (int)__builtin_ctzll(wv) - rs;
-                        out[rs + cnt_r] = j;                  // indexInRow
+                        orow[cnt_r] = j;                      // indexInRow
                         ++cnt_r;
                         js = j + span;
                         low = rs + js - gb;
@@ -1227,7 +1241,9 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
         const int* P = pre[e];
         const int total = P[n_rows];
         if (tid == 0) (e ? edge_count : plane_count)[f] = total;
-        const int32_t* S = e ? esel + fb : (sel_lds ? sel_l : sel + fb);
+        const bool lds_in = !e && sel_lds;
+        const int32_t* S = e ? esel + fb : (lds_in ? sel_l : sel + fb);
+        const int* SB = lds_in ? lb : ro;                     // per-row slot bases
         float4* O = e ? edge : plane;
         constexpr int U = 4;
         for (int k0 = 0; k0 < total; k0 += U * kSelThreads) {   // uniform
@@ -1242,7 +1258,7 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
                 rr[u] = a;
             }
 #pragma unroll
-            for (int u = 0; u < U; ++u) jj[u] = S[ro[rr[u]] + (kk[u] - P[rr[u]])];
+            for (int u = 0; u < U; ++u) jj[u] = S[SB[rr[u]] + (kk[u] - P[rr[u]])];
 #pragma unroll
             for (int u = 0; u < U; ++u) {                     // indexInRow -> chunk, slot, position
                 const int r = rr[u], j = jj[u];

@@ -340,9 +340,9 @@ int32_t ssf_kabsch_f32_batch(ssf_ctx* ctx, void* stream, int32_t n_frames, const
                              double* d_out);
 /* Work-groups per frame of the GMM fit in ssf_mask_pose_batch (no reference counterpart;
  * results do not depend on it beyond f64 summation order): 0 = automatic (as many as keep the
- * chip full: ~256 / frames, at most 32; 1 for 256 frames and more), 1..32 = fixed, capped per
- * launch like the automatic value (frames x parts <= the resident work-group slots, so the
- * exchange scratch stays ~ n_frames x parts x 104 KiB).  With more
+ * chip full: ~256 / frames, at most 32; 1 for 256 frames and more), 1..32 = fixed.  Memory: a
+ * launch with G > 1 keeps frames x G x 104 KiB of exchange slots in the context (grown on
+ * demand, never shrunk): a fixed 32 on a 256-frame batch is ~850 MB.  With more
  * than one, a frame's points are cut into contiguous parts whose per-pass sums are exchanged
  * in global memory; a partner that never arrives gives status SSF_POSE_SYNC_FAILED. */
 int32_t ssf_set_mask_split(ssf_ctx* ctx, int32_t parts_per_frame);

@@ -704,12 +704,10 @@ static int32_t mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const
     // parts per frame: fixed, or automatic -- enough to fill the resident work-group slots
     if (c->mask_slots < 0) c->mask_slots = ssf::mask_pose_slots(c->device);
     int G = c->mask_split;
-    // automatic: as many parts as keep the resident slots busy; a fixed split is bounded the same
-    // way (frames x G <= slots), so its exchange slots (mask_parts_bytes) stay near the automatic
-    // split's size instead of growing with G for large batches
-    const int g_cap = c->mask_slots > 0 ? std::max(1, c->mask_slots / n_frames) : 1;
-    if (G <= 0) G = g_cap;
-    else G = std::min(G, g_cap);
+    // automatic: as many parts as keep the resident slots busy.  A fixed split is honoured as
+    // set (frames x G may exceed the slots: work-groups then take several tickets); its exchange
+    // scratch grows with it (mask_parts_bytes: frames x G x 104 KiB, see ssf_set_mask_split)
+    if (G <= 0) G = c->mask_slots > 0 ? c->mask_slots / n_frames : 1;
     G = std::max(1, std::min(G, ssf::kMaskMaxSplit));
     if (mode != SSF_MASK_GMM) G = 1;
     const size_t sync_need = G > 1 ? ssf::mask_sync_bytes(n_frames) + 16 : 0;

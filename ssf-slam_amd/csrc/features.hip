@@ -771,20 +771,14 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
     const int64_t ws = max(fb, s - (int64_t)kCurvHalo), we = min(e, t + (int64_t)kCurvHalo);
     const int L = (int)(we - ws), hb = (int)(s - ws), he = (int)(t - ws);   // own: [hb, he)
     const int qlen = ((L + kCurvNW - 1) / kCurvNW + 63) / 64 * 64;
-    if (tid < kMaxRows) {
-#pragma unroll
-        for (int k = 0; k < kCurvNW; ++k) { wrun[k][tid] = 0ull; gmask[k][tid] = 0ull; }
-    }
-    if (tid < kCurvNW) { wrun[tid][kMaxRows] = 0ull; gmask[tid][kMaxRows] = 0ull; }
-    for (int k = tid; k < kRingCells; k += kCurvNT) rcell[k] = rtab->cell[k];
-    const float r0 = rtab->r0, rinv = rtab->inv;
-    __syncthreads();
     const int q0 = w * qlen, q1 = min(L, q0 + qlen);
     int idr[kWinQ];
     float px[kWinQ], py[kWinQ], pz[kWinQ];
     const float* pw = pts + ws * stride;
+    // every point load first (clamped, unconditional), in flight across the LDS set-up and its
+    // barrier -- the ring table's load no longer goes ahead of them
 #pragma unroll
-    for (int st = 0; st < kWinQ; ++st) {                      // every load first (clamped)
+    for (int st = 0; st < kWinQ; ++st) {
         const float* pp = pw + (uint32_t)(min(q0 + lane + 64 * st, L - 1) * stride);
         px[st] = pp[0]; py[st] = pp[1]; pz[st] = pp[2];
     }
@@ -793,6 +787,14 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
 #pragma unroll
         for (int st = 0; st < kWinQ; ++st) kp[st] = keep[ws + min(q0 + lane + 64 * st, L - 1)];
     }
+    if (tid < kMaxRows) {
+#pragma unroll
+        for (int k = 0; k < kCurvNW; ++k) { wrun[k][tid] = 0ull; gmask[k][tid] = 0ull; }
+    }
+    if (tid < kCurvNW) { wrun[tid][kMaxRows] = 0ull; gmask[tid][kMaxRows] = 0ull; }
+    for (int k = tid; k < kRingCells; k += kCurvNT) rcell[k] = rtab->cell[k];
+    const float r0 = rtab->r0, rinv = rtab->inv;
+    __syncthreads();
 #pragma unroll
     for (int st = 0; st < kWinQ; ++st) {                      // frameFeature.cpp:57-73
         const bool in = q0 + lane + 64 * st < q1 && (!keep || kp[st]);

@@ -43,6 +43,7 @@ def main():
                 d = json.loads(line)
                 out["config"] = {k: d["config"][k] for k in ("sequences_per_gpu", "points_per_frame",
                                                               "mask_before_features")}
+                out["lib_sha16"] = d.get("lib_sha16")        # the build these counters measured
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "counters_per_launch"}, indent=1))

@@ -299,3 +299,22 @@ def test_ring_id_table_edges(oracle, dev, n_rows):
     _check_frame(oracle, fe, out, h_off, 0, cloud, n_rows)
     ids = np.array([oracle.lib().orc_ring_id(float(p[0]), float(p[1]), float(p[2]), n_rows) for p in pts])
     assert len(set(ids.tolist()) - {-1}) == n_rows         # every row is exercised
+
+
+def test_frames_above_single_read_capacity(oracle, dev):
+    """k_feat_select holds a frame's chunk counts for at most kFeatMaxChunks = 128 chunks
+    (262 144 points); a launch whose frames may be larger takes the round-3 kernels
+    (k_bin_count / k_bin_scan / k_bin_curv / k_select, features.hip launch_extract_planes).  A
+    64 x 4200 = 268 800-point frame, the same frame shuffled, and a short one in the same launch:
+    ring cloud, curvature bits and plane lists bit-exact, debug and product instantiations."""
+    import ssf
+    c = frame(8, 2, n_az=4200)[0]
+    assert c.shape[0] > 128 * 2048
+    clouds = [c, shuffled(c, 3), c[:5000]]
+    fe = ssf.Frontend(64, device=dev.index or 0)
+    out, h_off = _run(fe, clouds, dev)
+    for f, cl in enumerate(clouds):
+        _check_frame(oracle, fe, out, h_off, f, cl, 64)
+    got = _planes_product(fe, clouds, dev)
+    for f, cl in enumerate(clouds):
+        assert np.array_equal(got[f].view(np.uint32), oracle.extract_planes(cl, 64).view(np.uint32)), f

@@ -714,6 +714,9 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const float* __restrict_
 #ifndef SSF_FEAT_ZONES
 #define SSF_FEAT_ZONES 0                         // A/B: one-zone steps count without masks (spills: slower)
 #endif
+#ifndef SSF_FEAT_CUT
+#define SSF_FEAT_CUT 0                           // timing tools only: stop k_feat_chunk after phase 1..4
+#endif
 #ifndef SSF_FEAT_WAVES
 #define SSF_FEAT_WAVES 5                         // k_feat_chunk waves per SIMD (launch bound)
 #endif
@@ -726,6 +729,18 @@ static_assert(kCurvSub == 1 && kBinChunk == 2048, "own-tile slots and chunk posi
 // u16 index base of frame f: 64-entry aligned, frames disjoint with a gap of >= 33 entries (the
 // chunk writes run up to 3 entries past the chunk's own points)
 SSF_DEV int64_t idx_base(const int64_t* frame_off, int f) { return (frame_off[f] & ~(int64_t)31) + 64 * (int64_t)f; }
+
+// LDS layouts of k_feat_chunk without write bank conflicts (ds_write_*: bank = (a / 4) mod 32,
+// two 32-lane groups).  An azimuth-ordered scan puts one row per lane in every step, so a step's
+// own-tile slots are p = seg(row) + q with seg spaced by the rows' own counts (32 for a full
+// 2048-point chunk of a 64-beam scan): u16 slots 64 B apart (16-way), flag bytes 32 B apart
+// (8-way).  XOR-swizzling bits 2..5 (idl) / 2..4 (flags) with the slot's row-size bits spreads
+// them over every bank (2-way for the u16s: free for a store) and keeps 4-slot groups (8 B of
+// idl) intact for the copy-out.  The f32 tile is padded by one float after every row run
+// instead (runs of 44 floats: 12r mod 32 -> 45r mod 32), since its readers are 16-B loads.
+static_assert(kTileE >= kWin + kMaxRows, "k_feat_chunk's tile holds the window plus one pad per row");
+SSF_DEV int idl_sw(int p) { return p ^ (((p >> 6) & 15) << 2); }
+SSF_DEV int fll_sw(int p) { return p ^ (((p >> 7) & 7) << 2); }
 
 template <bool kDebug, bool kEdge>
 __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const float* __restrict__ pts, int stride,
@@ -801,6 +816,9 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
         const int id = ring_id_table(px[st], py[st], pz[st], r0, rinv, rcell);   // every lane: no branch
         idr[st] = in ? id : -1;
     }
+#if SSF_FEAT_CUT == 1                                         // timing only (tools): ring ids
+    { int acc = 0; for (int st = 0; st < kWinQ; ++st) acc += idr[st]; if (acc == 0x7fffffff) cnt[0] = acc; return; }
+#endif
     // rank among same-row points (the k_bin_curv ranking: per-row lane words, waves in order).
     // Every lane of a row computes the same new counter word and writes it (and clears the lane
     // word): the wave's LDS instructions complete in order, so all reads of the step precede
@@ -857,11 +875,15 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
             const int run0 = incl - tot, seg0 = oincl - own;
 #pragma unroll
             for (int k = 0; k < kCurvNW; ++k)
-                wrec[k][r] = make_int4(run0 + pwk[k], seg0 + pwk[k] - nbr, 5 - pwk[k], tot - 5 - pwk[k]);
+                wrec[k][r] = make_int4(run0 + r + pwk[k], seg0 + pwk[k] - nbr, 5 - pwk[k], tot - 5 - pwk[k]);
+            meta[run0 + r + tot] = 0;                         // the row run's pad entry: no stencil
         }
-        if (r == 63) { ntot = incl; nown = oincl; }
+        if (r == 63) { ntot = incl + n_rows; nown = oincl; }  // tile entries incl. one pad per row
     }
     __syncthreads();
+#if SSF_FEAT_CUT == 2                                         // timing only: + ranking, row scan
+    { int acc = ntot; for (int st = 0; st < kWinQ; ++st) acc += idr[st]; if (acc == 0x7fffffff) cnt[0] = acc; return; }
+#endif
     const int nt = ntot;
     const int64_t cm = fb + (int64_t)c * kBinChunk;           // chunk-major base (curvature)
     // ---- place: tile slot of every window point, own-tile slot + position of every own point
@@ -881,11 +903,11 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
             uint16_t mk = 0;
             if (own) {
                 const int p = rw.y + q;
-                idl[p] = (uint16_t)(wp - hb);
+                idl[idl_sw(p)] = (uint16_t)(wp - hb);
                 if (row_in && covered) {
                     mk = (uint16_t)(p | 0x8000);
                 } else {
-                    fll[p] = row_in ? kFlU : (uint8_t)0;
+                    fll[fll_sw(p)] = row_in ? kFlU : (uint8_t)0;
                     if (kDebug && curv_cm) curv_cm[cm + p] = 0.0f;
                 }
             }
@@ -895,6 +917,9 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
         }
     }
     __syncthreads();
+#if SSF_FEAT_CUT == 3                                         // timing only: + place
+    { int acc = 0; for (int st = 0; st < kWinQ; ++st) acc += loc[st]; if (acc == 0x7fffffff) cnt[0] = acc; return; }
+#endif
 #if SSF_FEAT_PACKED
     // ---- curvature of this thread's kCE tile entries, one coordinate at a time, entries i and
     // i + kCE / 2 side by side in packed f32 (v_pk_add_f32 / v_pk_mul_f32: two IEEE operations,
@@ -969,6 +994,9 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
         for (int i = 0; i < kCE; ++i) v[i] = v[i] + d0[i] * d0[i];
     }
 #endif
+#if SSF_FEAT_CUT == 4                                         // timing only: + stencils
+    { float acc = 0.f; for (int i = 0; i < kCE; ++i) acc += v[i]; if (acc == 1234.5f) cnt[0] = 1; return; }
+#endif
     uint16_t mt[kCE];
 #pragma unroll
     for (int i = 0; i < kCE; i += 4) {                        // k0 + kCE <= kTileE: 8-byte reads
@@ -981,7 +1009,7 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
         if (k0 + i < nt && (mt[i] & 0x8000)) {
             const int p = mt[i] & 0x7fff;
             const uint8_t fl = cand_flags(true, true, v[i], plane_min, kEdge, edge_min);
-            fll[p] = (uint8_t)((fl & 1) ? kFlP : 0) | (uint8_t)((fl & 2) ? kFlE : 0);
+            fll[fll_sw(p)] = (uint8_t)((fl & 1) ? kFlP : 0) | (uint8_t)((fl & 2) ? kFlE : 0);
             if (kDebug && curv_cm) curv_cm[cm + p] = v[i];
         }
     }
@@ -991,7 +1019,7 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
     const int clen = (int)(t - s);
     uint16_t* gi = gidx + idx_base(frame_off, f) + (int64_t)c * kBinChunk;   // 4 KiB aligned run
     for (int k = tid; 4 * k < clen; k += kCurvNT)             // 8-byte stores (4 slots)
-        *reinterpret_cast<uint2*>(gi + 4 * k) = *reinterpret_cast<const uint2*>(idl + 4 * k);
+        *reinterpret_cast<uint2*>(gi + 4 * k) = *reinterpret_cast<const uint2*>(idl + 4 * (k ^ ((k >> 4) & 15)));
     uint64_t* gb = gbits + ((int64_t)f * n_chunks + c) * (kFeatPlanes * kFeatWords);
     constexpr int kPl = kEdge ? 3 : 2;
     if (tid < kPl * kFeatWords) {
@@ -1000,8 +1028,12 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
         uint64_t wv = 0;
         if (nbit > 0) {
             uint64_t b8[8];
+            const int sw = (wi >> 1) & 7;                     // fll_sw of this word's 64 flags
 #pragma unroll
-            for (int u = 0; u < 8; ++u) b8[u] = *reinterpret_cast<const uint64_t*>(fll + 64 * wi + 8 * u);
+            for (int u = 0; u < 8; ++u) {
+                const uint64_t x = *reinterpret_cast<const uint64_t*>(fll + 8 * ((8 * wi + u) ^ (sw >> 1)));
+                b8[u] = (sw & 1) ? ((x >> 32) | (x << 32)) : x;
+            }
             wv = pack64(b8, pl);                              // bit pl of every flag byte
             if (nbit < 64) wv &= (1ull << nbit) - 1ull;
         }
@@ -1457,6 +1489,12 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
         if (edge) { if (dbg) SSF_FC_LAUNCH(true, true); else SSF_FC_LAUNCH(false, true); }
         else { if (dbg) SSF_FC_LAUNCH(true, false); else SSF_FC_LAUNCH(false, false); }
 #undef SSF_FC_LAUNCH
+#if SSF_FEAT_CUT
+        // timing variants (tools only): the chunk kernel stopped early and wrote nothing, so the
+        // select must not read its outputs; empty plane lists instead
+        (void)ring_off; (void)sel;
+        return hipMemsetAsync(plane_count, 0, sizeof(int32_t) * (size_t)n_frames, s);
+#endif
         kmark(s, "k_feat_select");
         if (edge)
             hipLaunchKernelGGL(k_feat_select<true>, dim3(n_frames), dim3(kSelThreads), 0, s, pts, stride,

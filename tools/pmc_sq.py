@@ -80,6 +80,10 @@ def main():
                       "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_INT32", "SQ_INSTS_LDS_LOAD"):
                 if m.get(c) is not None:
                     per[c.replace("SQ_INSTS_", "")] = m[c] / waves
+            for c in ("SQ_LDS_BANK_CONFLICT", "SQ_LDS_ADDR_CONFLICT", "SQ_LDS_IDX_ACTIVE",
+                      "SQ_LDS_UNALIGNED_STALL"):       # LDS cycle counters, per wave
+                if m.get(c) is not None:
+                    per[c.replace("SQ_", "")] = m[c] / waves
             if m.get("SQ_WAVE_CYCLES") is not None:
                 per["WAVE_CYCLES"] = 4.0 * m["SQ_WAVE_CYCLES"] / waves
             d["per_wave"] = per

@@ -135,6 +135,10 @@ def parse(argv=None):
                     help="with --consecutive / --sequences-total (beyond the reference): warm-start "
                          "every pair from its own SSF Kabsch pose, so all pairs of a step are "
                          "independent (two registration launches per step instead of K)")
+    ap.add_argument("--timeline", action="store_true",
+                    help="with --consecutive / --sequences-total: HIP events around every step's mask, "
+                         "features + table and registrations on their streams; per-step start / end "
+                         "times (ms from the first timed step) to stderr (diagnostic)")
     ap.add_argument("--latency", action="store_true",
                     help="BASELINE configs[1] as written: one frame pair at a time (B = 1), ms per frame")
     ap.add_argument("--mask-streams", type=int, default=3,
@@ -754,12 +758,24 @@ def sequences(args, world=1, rank=0, local=0):
     prev_out = out0
     records = []
 
+    tl = []                                   # --timeline: per step, (phase, start, end) events
+
+    def ev(stream):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        return e
+
     def step(j, timing):
         nonlocal last, prev_out
         pos, flow = steps[j]
         sm = s_masks[j % len(s_masks)]
+        rec = {} if (timing and args.timeline) else None
         with torch.cuda.stream(sm):
+            if rec is not None:
+                rec["mask"] = [ev(sm)]
             out, bg = fe_mask.mask_pose(pos, flow, offK, hK, mode="gmm", want_mask=True)
+            if rec is not None:
+                rec["mask"].append(ev(sm))
             mrec = out[:, 0:7].view(K, B, 7).clone() if timing else None   # the SSF poses, on their stream
             done = torch.cuda.Event()
             done.record(sm)
@@ -767,10 +783,14 @@ def sequences(args, world=1, rank=0, local=0):
             s_feat.wait_event(done)
             bg.record_stream(s_feat)
         with torch.cuda.stream(s_feat):
+            if rec is not None:
+                rec["feat"] = [ev(s_feat)]
             pb = fe_feat.extract_planes_batch(pos, offK, hK, max_points=N, keep=bg if masked else None)
             table = fe_feat.plane_table(pb)
             tdone = torch.cuda.Event()
             tdone.record(s_feat)
+            if rec is not None:
+                rec["feat"].append(ev(s_feat))
         s_reg.wait_event(tdone)
         for t in (pb.xyzi, pb.count, *table.tensors()):
             t.record_stream(s_reg)
@@ -778,6 +798,8 @@ def sequences(args, world=1, rank=0, local=0):
             s_reg.wait_event(done)
             out.record_stream(s_reg)
         with torch.cuda.stream(s_reg):
+            if rec is not None:
+                rec["reg"] = [ev(s_reg)]
             (lpb, ltab) = last
             if kws:
                 # pair (slot kk - 1 -> slot kk) starts from the Kabsch pose of frame kk - 1
@@ -796,6 +818,9 @@ def sequences(args, world=1, rank=0, local=0):
                 rel_k = torch.stack(snaps, 0)
             if timing:
                 records.append((rel_k, mrec, sm))
+            if rec is not None:
+                rec["reg"].append(ev(s_reg))
+                tl.append(rec)
         last = view(pb, table, K - 1)
         prev_out = out[(K - 1) * B:]
         return out
@@ -822,6 +847,12 @@ def sequences(args, world=1, rank=0, local=0):
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    if tl and rank == 0:
+        z = tl[0]["mask"][0]
+        for j, rec in enumerate(tl):
+            print("timeline step %d: " % j + "  ".join(
+                "%s %.3f-%.3f" % (k, z.elapsed_time(a), z.elapsed_time(b)) for k, (a, b) in rec.items()),
+                file=sys.stderr)
     gather_ok = None
     finite = bool(torch.isfinite(mine).all())
     if world > 1:

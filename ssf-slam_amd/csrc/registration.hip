@@ -361,6 +361,9 @@ __global__ __launch_bounds__(256) void k_associate(const float4* __restrict__ la
 // written out and reused as the LAST frame of the next pair's association.
 constexpr int kSortMax = 16384;           // plane points per frame sorted in LDS (128 KiB)
 constexpr int kTableThreads = 1024;
+#ifndef SSF_TABLE_MAX_SPLIT
+#define SSF_TABLE_MAX_SPLIT 8                     // work-groups per frame at most (small batches)
+#endif
 
 constexpr int kTableStripF4Max = 9216;    // after the sort, frames up to this size search strips of
 // 16-B points in LDS (16 m + the 12 KiB strip table + >= 2 KiB of deferred queue) ...
@@ -1055,8 +1058,11 @@ SSF_DEV bool pick_beyond_invalid(const StripView<false>& v, const StripLds& T, c
 SSF_DEV void table_pick_walks(const float4* __restrict__ P, const StripView<false>& v, const StripLds& T,
                               const StripGeo& g, int m, float plane_max, int64_t base, float* __restrict__ normal,
                               uint8_t* __restrict__ valid, int* queue, int qcap, int* qlen,
-                              int32_t* stamp_out = nullptr, unsigned long long stamp0 = 0) {
-    for (int j = threadIdx.x; j < m; j += blockDim.x) {
+                              int32_t* stamp_out = nullptr, unsigned long long stamp0 = 0,
+                              int share = 0, int nshare = 1) {
+    // queries of this work-group's share: every nshare-th one (k_plane_table_sorted splits a
+    // frame's queries over nshare work-groups for small batches)
+    for (int j = share + nshare * (int)threadIdx.x; j < m; j += nshare * (int)blockDim.x) {
         const float4 q = v.pt(j);
         const int64_t o = base + v.id(j);
         PickState s;
@@ -1118,8 +1124,8 @@ SSF_DEV void table_strip_walks(const float4* __restrict__ P, const StripView<kSo
                                int64_t base, float* __restrict__ normal, uint8_t* __restrict__ valid,
                                int* queue, int qcap, int* qlen, const float4* __restrict__ SP,
                                const int32_t* __restrict__ SI, int32_t* stamp_out,
-                               unsigned long long stamp0) {
-    for (int j = threadIdx.x; j < m; j += blockDim.x) {
+                               unsigned long long stamp0, int share = 0, int nshare = 1) {
+    for (int j = share + nshare * (int)threadIdx.x; j < m; j += nshare * (int)blockDim.x) {
         const float4 q = v.pt(j);
         double kk[kK];
         int dec;
@@ -1282,10 +1288,15 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
     float* key = reinterpret_cast<float*>(lds);
     int* idx = reinterpret_cast<int*>(lds + kSortMax * 4);
     const int f = blockIdx.x, tid = threadIdx.x;
+    // small batches: gridDim.y work-groups per frame, each sorting and building the strips
+    // (identical results) and walking every gridDim.y-th query; share 0 alone
+    // writes the sorted copy, the strip image and the stamps
+    const int share = (int)blockIdx.y, nshare = (int)gridDim.y;
     const int m = count[f];
     const int64_t base = frame_off[f];
     const float4* P = plane + base;
     if (m <= 0) return;
+    if (share > 0 && (m > kTableStripSoaMax || m <= share)) return;   // uniform: no queries here
 #ifdef SSF_TABLE_STAMPS
     const unsigned long long tstamp0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1329,9 +1340,11 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
     }
     float4* SP = sorted_xyzi + base;
     int32_t* SI = sorted_idx + base;
-    for (int r = tid; r < m; r += blockDim.x) {
-        SP[r] = P[idx[r]];
-        SI[r] = idx[r];
+    if (share == 0) {
+        for (int r = tid; r < m; r += blockDim.x) {
+            SP[r] = P[idx[r]];
+            SI[r] = idx[r];
+        }
     }
     __syncthreads();
     SSF_TSTAMP(0);
@@ -1362,14 +1375,14 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
             return p;
         };
 #ifdef SSF_TABLE_STAMPS
-        int32_t* stamp_out = SI + m + 1;
+        int32_t* stamp_out = share == 0 ? SI + m + 1 : nullptr;
         const unsigned long long st0 = tstamp0;
 #else
         int32_t* stamp_out = nullptr;
         const unsigned long long st0 = 0;
 #endif
 #ifdef SSF_TABLE_STAMPS
-#define SSF_TSTAMP_BUILD() do { if (tid == 0) stamp_out[3] = (int32_t)((__builtin_amdgcn_s_memtime() - st0) >> 4); } while (0)
+#define SSF_TSTAMP_BUILD() do { if (tid == 0 && stamp_out) stamp_out[3] = (int32_t)((__builtin_amdgcn_s_memtime() - st0) >> 4); } while (0)
 #else
 #define SSF_TSTAMP_BUILD() do { } while (0)
 #endif
@@ -1377,7 +1390,7 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
             const StripGeo g = strips_build<true, kStripPerMax>(get, m, T, F, X, I16);
             SSF_TSTAMP_BUILD();
             table_strip_walks(P, StripView<true>{F, X, I16, m}, T, g, m, plane_max, base, normal,
-                              valid, queue, qcap, qlen, SP, SI, stamp_out, st0);
+                              valid, queue, qcap, qlen, SP, SI, stamp_out, st0, share, nshare);
         } else {
             // 16-B records carry the ring code of every point (bits 16..23 of .w): the pick then
             // runs without the 30-key list (table_pick_walks) unless the frame is tiny or a ring
@@ -1405,7 +1418,8 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
             // 13 B per point fit behind the strip image with a queue of m / 4 entries (m <= ~5000):
             // scattered 12-B normal and 1-B validity stores each cost a 64-B write request
             const int soff = ((int)sizeof(lds) - 16 - 13 * m) & ~15;
-            const bool stage = (soff - qoff) / 4 >= m / 4 + 64;              // uniform
+            // (one work-group per frame only: a share's results are scattered over the frame)
+            const bool stage = nshare == 1 && (soff - qoff) / 4 >= m / 4 + 64;   // uniform
             if (rows_ok && m > kK && stage) {
                 float* nl = reinterpret_cast<float*>(lds + soff);
                 uint8_t* vl = reinterpret_cast<uint8_t*>(lds + soff + 12 * m);
@@ -1418,12 +1432,12 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
                 for (int k = tid; k < m; k += kTableThreads) gv[k] = vl[k];
             } else if (rows_ok && m > kK)
                 table_pick_walks(P, StripView<false>{F, X, I16, m}, T, g, m, plane_max, base, normal, valid,
-                                 queue, qcap, qlen, stamp_out, st0);
+                                 queue, qcap, qlen, stamp_out, st0, share, nshare);
             else
                 table_strip_walks(P, StripView<false>{F, X, I16, m}, T, g, m, plane_max, base, normal,
-                                  valid, queue, qcap, qlen, SP, SI, stamp_out, st0);
+                                  valid, queue, qcap, qlen, SP, SI, stamp_out, st0, share, nshare);
             // the walks only read F and T: the image leaves as it is (uniform condition)
-            if (strip_xyzi && strip_image_frame(m))
+            if (share == 0 && strip_xyzi && strip_image_frame(m))
                 strip_image_store(F, T, g, m, strip_xyzi + base, strip_head + base);
         }
         SSF_TSTAMP(3);
@@ -2634,8 +2648,13 @@ hipError_t launch_plane_table(hipStream_t s, const ssf_config& cfg, int n_frames
                               int32_t* sorted_idx, float4* strip_xyzi, int32_t* strip_head) {
     if (n_frames <= 0 || max_m <= 0) return hipSuccess;
     if (max_m <= kSortMax && sorted_xyzi && sorted_idx) {
+        // few frames (a node's one frame, configs[2]'s 32): up to 8 work-groups per frame share
+        // its queries (each sorts and builds the strips itself), so the launch spreads over the
+        // chip instead of n_frames CUs; 256 frames and more keep one work-group per frame
+        const int qsplit = (int)std::max<int64_t>(1, std::min<int64_t>({SSF_TABLE_MAX_SPLIT, 256 / n_frames,
+                                                             max_m / 256}));
         kmark(s, "k_plane_table_sorted");
-        hipLaunchKernelGGL(k_plane_table_sorted, dim3(n_frames), dim3(kTableThreads), 0, s, plane,
+        hipLaunchKernelGGL(k_plane_table_sorted, dim3(n_frames, qsplit), dim3(kTableThreads), 0, s, plane,
                            frame_off, count, cfg.plane_max, normal, valid, sorted_xyzi, sorted_idx,
                            strip_head ? strip_xyzi : nullptr, strip_head);
     } else {

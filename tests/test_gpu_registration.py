@@ -424,3 +424,31 @@ def test_strip_image_invalidated_when_not_imaged(dev):
     t = fe.plane_table(pb)                              # the sorted table images them again
     torch.cuda.synchronize()
     assert all((int(t.strips[1][o + word]) >> 16) == 0x57A1 for o in offs)
+
+
+def test_plane_table_split_over_work_groups(oracle, dev):
+    """Small batches split a frame's queries over up to 8 work-groups (launch_plane_table:
+    min(8, 256 / frames, m / 256) shares, each sorting and building the strips itself): the same
+    frame in batches of 1, 5, 40 and 256 frames (8, 8, 6 and 1 shares) gives bit-identical
+    normals, validity, sorted copy and strip image, equal to the oracle"""
+    import ssf
+    c = frame(3, 4, n_az=1875)[0]
+    ref = None
+    for B in (1, 5, 40, 256):
+        fe = ssf.Frontend(64, device=dev.index or 0)
+        pb = _planes(fe, dev, [c] * B)
+        tab = fe.plane_table(pb)
+        normal, valid, sx, si = tab
+        o, m = int(pb.h_off[B - 1]), int(pb.count[B - 1])
+        got = [normal[o:o + m].cpu().numpy().view(np.uint32), valid[o:o + m].cpu().numpy(),
+               sx[o:o + m].cpu().numpy(), si[o:o + m].cpu().numpy()]
+        if tab.strips is not None:
+            got += [t[o:o + m].cpu().numpy() for t in tab.strips]
+        if ref is None:
+            ref = got
+            nr, vr, _, _ = oracle.plane_table(pb.frame(0).cpu().numpy(), 0.05)
+            assert np.array_equal(got[0], nr.view(np.uint32)), "normal bits differ"
+            assert np.array_equal(got[1], vr.astype(np.uint8))
+        assert len(got) == len(ref), B
+        for a, b in zip(got, ref):
+            assert np.array_equal(a, b), B

@@ -474,9 +474,14 @@ def rooflines(times, acc, B, N):
         # round 4, the single-read stage: xyz read once (12 B), a u16 chunk position per point
         # (2 B) written, per 2048-point chunk its row counts (256 B) and two bit planes (512 B)
         "k_feat_chunk": 14.0 * acc["points"] + 768.0 * acc["chunks"],
-        # the chunks' counts and bit planes read, per plane point: its slot written and read back
-        # (8 B), its u16 position (2 B) and xyz (12 B) gathered, the xyzi record written (16 B)
-        "k_feat_select": 768.0 * acc["chunks"] + 38.0 * acc["plane"],
+        # round 4: the regular-window kernel does every chunk of an unmasked 64-beam azimuth-ordered
+        # frame (the bench's scans): the same bytes + its block flag; k_feat_chunk then only reads
+        # the flags (its model is dropped below when this kernel ran)
+        # (no u16 index: a 64-B row -> lane map per chunk instead)
+        "k_feat_chunk_reg": 12.0 * acc["points"] + 833.0 * acc["chunks"],
+        # the chunks' counts and bit planes read, per plane point: its u16 position (2 B) and xyz
+        # (12 B) gathered, the xyzi record written (16 B); the selections stay in LDS
+        "k_feat_select": 768.0 * acc["chunks"] + 30.0 * acc["plane"],
         # flag bytes read, per plane point: its index written and read back (4 + 4 B), its ring
         # index (4 B) and xyz (12 B) gathered and the xyzi record written (16 B)
         "k_select": 1.0 * acc["kept"] + 40.0 * acc["plane"],
@@ -490,6 +495,10 @@ def rooflines(times, acc, B, N):
         "k_associate_sorted": 64.0 * acc["plane_reg"],
         "k_solve": 36.0 * acc["corr_evals"],                        # §8(d): 36 B x C per evaluation
     }
+    if "k_feat_chunk_reg" in times:
+        model.pop("k_feat_chunk", None)
+        # select reads the lane maps (and flags) and no u16 positions
+        model["k_feat_select"] = 833.0 * acc["chunks"] + 28.0 * acc["plane"]
     out = {}
     for name, (n, ms) in sorted(times.items(), key=lambda kv: -kv[1][1]):
         d = dict(launches=n, ms=ms / n)
@@ -504,7 +513,7 @@ def rooflines(times, acc, B, N):
                               evaluations_per_pair=acc["corr_evals"] / max(1, acc["corr"]),
                               note="corr = valid correspondences counted on device (ncorr); "
                                    "evaluations = 1 + logged iterations (nlog)")
-    for k in ("k_bin_curv", "k_feat_chunk"):
+    for k in ("k_bin_curv", "k_feat_chunk", "k_feat_chunk_reg"):
         if k in out:
             out[k]["kept_points_per_launch"] = acc["kept"] / out[k]["launches"]
     return out, passes
@@ -1090,7 +1099,7 @@ def main():
             line["roofline_f64"] = {"bound": "valu_f64", "achieved": tf, "peak": F64_PEAK_TFLOPS,
                                     "unit": "TFLOP/s", "frac": tf / F64_PEAK_TFLOPS,
                                     "kernel": "k_mask_pose", "flops_source": os.path.basename(F64_JSON)}
-    ns = {k: kernels[k]["frac"] for k in ("k_feat_chunk", "k_bin_curv", "k_solve") if k in kernels and "frac" in kernels[k]}
+    ns = {k: kernels[k]["frac"] for k in ("k_feat_chunk_reg", "k_feat_chunk", "k_bin_curv", "k_solve") if k in kernels and "frac" in kernels[k]}
     if ns:
         line["north_star_kernels_hbm_frac"] = ns
         meas = {k: kernels[k]["traffic_frac"] for k in ns if "traffic_frac" in kernels[k]}

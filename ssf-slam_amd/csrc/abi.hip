@@ -51,7 +51,7 @@ struct ssf_ctx {
     DevBuf rid, hist, ring_off, ring_xyzi /* ring index */, sel, sel_cnt /* candidate flags */, fix, plane1, off1, cnt1;
     // single-read feature stage: per-(chunk, row) counts, u16 chunk positions, bit planes,
     // chunk-major curvature (debug outputs only)
-    DevBuf fcnt, fidx, fbits, fcurv, rtab;
+    DevBuf fcnt, fidx, fbits, fcurv, rtab, firr, flmap;
     bool rtab_ready = false;
     // registration scratch
     DevBuf corr;
@@ -228,7 +228,7 @@ void ssf_destroy(ssf_ctx* c) {
     DevBuf* bufs[] = {&c->rid, &c->hist, &c->ring_off, &c->ring_xyzi, &c->sel, &c->sel_cnt, &c->fix,
                       &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->pair, &c->start1, &c->vg,
                       &c->icp_cur, &c->icp_key, &c->icp_st, &c->icp_guess, &c->esel,
-                      &c->ecorr, &c->fcnt, &c->fidx, &c->fbits, &c->fcurv, &c->rtab};
+                      &c->ecorr, &c->fcnt, &c->fidx, &c->fbits, &c->fcurv, &c->rtab, &c->firr, &c->flmap};
     for (auto& ds : c->dslot) {
         if (ds.used) { (void)hipEventSynchronize(ds.used); (void)hipEventDestroy(ds.used); }
         if (ds.copied) { (void)hipEventSynchronize(ds.copied); (void)hipEventDestroy(ds.copied); }
@@ -333,6 +333,8 @@ static int32_t ensure_features(ssf_ctx* c, int32_t n_frames, int64_t total, int6
         SSF_TRY_HIP(c, c->fcnt.ensure(ssf::feat_cnt_bytes(n_frames, max_pts)), "alloc feature counts");
         SSF_TRY_HIP(c, c->fidx.ensure(ssf::feat_idx_bytes(total, n_frames)), "alloc feature index");
         SSF_TRY_HIP(c, c->fbits.ensure(ssf::feat_bits_bytes(n_frames, max_pts)), "alloc feature bits");
+        SSF_TRY_HIP(c, c->firr.ensure(ssf::feat_irr_bytes(n_frames, max_pts)), "alloc feature block flags");
+        SSF_TRY_HIP(c, c->flmap.ensure(ssf::feat_lmap_bytes(n_frames, max_pts)), "alloc feature lane maps");
     }
     return SSF_OK;
 }
@@ -385,7 +387,7 @@ static int32_t extract_planes_impl(ssf_ctx* c, void* stream, int32_t n_frames, c
     if ((ring4 || d_curv) && ssf::feat_single_read(max_frame_points))
         SSF_TRY_HIP(c, c->fcurv.ensure(sizeof(float) * (size_t)std::max<int64_t>(total_points, 1)), "alloc chunk curvature");
     ssf::FeatScratch fs{c->rtab.p, c->fcnt.as<int32_t>(), c->fidx.as<uint16_t>(), c->fbits.as<uint64_t>(),
-                        c->fcurv.as<float>()};
+                        c->fcurv.as<float>(), c->firr.as<uint8_t>(), c->flmap.as<uint8_t>()};
     ProfScope prof(c, stream);
     int32_t* roff = d_ring_off ? d_ring_off : c->ring_off.as<int32_t>();
     hipError_t e = ssf::launch_extract_planes(

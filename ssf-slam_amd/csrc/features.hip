@@ -714,6 +714,12 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const float* __restrict_
 #ifndef SSF_FEAT_ZONES
 #define SSF_FEAT_ZONES 0                         // A/B: one-zone steps count without masks (spills: slower)
 #endif
+#ifndef SSF_FEAT_REGULAR
+#define SSF_FEAT_REGULAR 1                       // k_feat_chunk_reg for regular windows (A/B: 0)
+#endif
+#ifndef SSF_SEL_CUT
+#define SSF_SEL_CUT 0                            // timing tools only: stop k_feat_select after phase 1..4
+#endif
 #ifndef SSF_FEAT_CUT
 #define SSF_FEAT_CUT 0                           // timing tools only: stop k_feat_chunk after phase 1..4
 #endif
@@ -742,6 +748,38 @@ static_assert(kTileE >= kWin + kMaxRows, "k_feat_chunk's tile holds the window p
 SSF_DEV int idl_sw(int p) { return p ^ (((p >> 6) & 15) << 2); }
 SSF_DEV int fll_sw(int p) { return p ^ (((p >> 7) & 7) << 2); }
 
+// The chunk's outputs from LDS (k_feat_chunk, k_feat_chunk_reg): the u16 chunk positions in
+// own-tile order as whole 8-byte runs (idl, swizzled by idl_sw), and the candidate / unresolved
+// (/ edge) bit planes packed from the flag bytes (fll, swizzled by fll_sw).
+template <bool kEdge>
+SSF_DEV void feat_chunk_out(int tid, int f, int c, int n_chunks, const int64_t* __restrict__ frame_off,
+                            int clen, int no, const uint16_t* idl, const uint8_t* fll,
+                            uint16_t* __restrict__ gidx, uint64_t* __restrict__ gbits, bool write_idx = true) {
+    uint16_t* gi = gidx + idx_base(frame_off, f) + (int64_t)c * kBinChunk;   // 4 KiB aligned run
+    if (write_idx)                                            // uniform
+        for (int k = tid; 4 * k < clen; k += kCurvNT)         // 8-byte stores (4 slots)
+            *reinterpret_cast<uint2*>(gi + 4 * k) = *reinterpret_cast<const uint2*>(idl + 4 * (k ^ ((k >> 4) & 15)));
+    uint64_t* gb = gbits + ((int64_t)f * n_chunks + c) * (kFeatPlanes * kFeatWords);
+    constexpr int kPl = kEdge ? 3 : 2;
+    if (tid < kPl * kFeatWords) {
+        const int pl = tid / kFeatWords, wi = tid - pl * kFeatWords;
+        const int nbit = min(64, max(0, no - 64 * wi));
+        uint64_t wv = 0;
+        if (nbit > 0) {
+            uint64_t b8[8];
+            const int sw = (wi >> 1) & 7;                     // fll_sw of this word's 64 flags
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint64_t x = *reinterpret_cast<const uint64_t*>(fll + 8 * ((8 * wi + u) ^ (sw >> 1)));
+                b8[u] = (sw & 1) ? ((x >> 32) | (x << 32)) : x;
+            }
+            wv = pack64(b8, pl);                              // bit pl of every flag byte
+            if (nbit < 64) wv &= (1ull << nbit) - 1ull;
+        }
+        gb[pl * kFeatWords + wi] = wv;
+    }
+}
+
 template <bool kDebug, bool kEdge>
 __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const float* __restrict__ pts, int stride,
                                                     const int64_t* __restrict__ frame_off,
@@ -752,7 +790,8 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
                                                     int32_t* __restrict__ cnt,
                                                     uint16_t* __restrict__ gidx,
                                                     uint64_t* __restrict__ gbits,
-                                                    float* __restrict__ curv_cm) {
+                                                    float* __restrict__ curv_cm,
+                                                    const uint8_t* __restrict__ irregular) {
     __shared__ __attribute__((aligned(16))) float sc[kTileE + 2 * kTilePad];   // x, then y, then z
     __shared__ __attribute__((aligned(16))) uint16_t meta[kTileE];   // own-tile slot | 0x8000: stencil
     // two LDS regions reused across phases (31 KiB in all: 5 work-groups per CU):
@@ -778,6 +817,7 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
     const int64_t q8 = (nblk + 7) / 8;
     const int64_t lb = (int64_t)(blockIdx.x % 8) * q8 + blockIdx.x / 8;
     if (lb >= nblk) return;
+    if (irregular && !irregular[lb]) return;                  // uniform: done by k_feat_chunk_reg
     const int f = (int)(lb / n_chunks), c = (int)(lb - (int64_t)f * n_chunks);
     const int64_t fb = frame_off[f], e = frame_off[f + 1];
     const int64_t s = fb + (int64_t)c * kBinChunk;
@@ -1015,30 +1055,172 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
     }
     __syncthreads();
     // ---- out: the chunk's own-tile slots, whole aligned runs
-    const int no = nown;
-    const int clen = (int)(t - s);
-    uint16_t* gi = gidx + idx_base(frame_off, f) + (int64_t)c * kBinChunk;   // 4 KiB aligned run
-    for (int k = tid; 4 * k < clen; k += kCurvNT)             // 8-byte stores (4 slots)
-        *reinterpret_cast<uint2*>(gi + 4 * k) = *reinterpret_cast<const uint2*>(idl + 4 * (k ^ ((k >> 4) & 15)));
-    uint64_t* gb = gbits + ((int64_t)f * n_chunks + c) * (kFeatPlanes * kFeatWords);
-    constexpr int kPl = kEdge ? 3 : 2;
-    if (tid < kPl * kFeatWords) {
-        const int pl = tid / kFeatWords, wi = tid - pl * kFeatWords;
-        const int nbit = min(64, max(0, no - 64 * wi));
-        uint64_t wv = 0;
-        if (nbit > 0) {
-            uint64_t b8[8];
-            const int sw = (wi >> 1) & 7;                     // fll_sw of this word's 64 flags
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const uint64_t x = *reinterpret_cast<const uint64_t*>(fll + 8 * ((8 * wi + u) ^ (sw >> 1)));
-                b8[u] = (sw & 1) ? ((x >> 32) | (x << 32)) : x;
-            }
-            wv = pack64(b8, pl);                              // bit pl of every flag byte
-            if (nbit < 64) wv &= (1ull << nbit) - 1ull;
-        }
-        gb[pl * kFeatWords + wi] = wv;
+    feat_chunk_out<kEdge>(tid, f, c, n_chunks, frame_off, (int)(t - s), nown, idl, fll, gidx, gbits);
+}
+
+// k_feat_chunk_reg: the same outputs for REGULAR windows, the common layout of a 64-beam scan in
+// azimuth order (the reference's driver order; the bench's synthetic scans): the window is whole
+// columns of 64 points, each column holds every row once, and lane l of every column is the same
+// row.  Then a row's points in the window are one lane's column sequence -- rank = column, the
+// own-tile slot is row x own columns + (column - first own column), and the 11 taps of a stencil
+// are that lane's columns c - 5 .. c + 5 -- so there is no ranking, no placement and no
+// row-grouped tile: each coordinate goes through a column-major LDS image (conflict-free 4-byte
+// stores and loads), the lane's 21 columns into registers, tap11 in the reference's order.
+// Covered stencils, unresolved points, flags, positions and counts are exactly those of
+// k_feat_chunk (same taps, same order, same rounding).  A window that is not regular (masked
+// points, a ragged frame end, a point without a row, another order) is flagged, and k_feat_chunk,
+// launched after it, does exactly the flagged blocks.
+#ifndef SSF_FEAT_REG_LDS
+#define SSF_FEAT_REG_LDS 0                       // k_feat_chunk_reg: halo columns from global (A/B 1: through LDS, 0.155 vs 0.147 ms)
+#endif
+#ifndef SSF_FEAT_REG_WAVES
+#define SSF_FEAT_REG_WAVES 5                     // k_feat_chunk_reg waves per SIMD (launch bound)
+#endif
+template <bool kDebug, bool kEdge>
+__global__ __launch_bounds__(kCurvNT, SSF_FEAT_REG_WAVES) void k_feat_chunk_reg(
+    const float* __restrict__ pts, int stride, const int64_t* __restrict__ frame_off, int n_frames,
+    int n_rows, int n_chunks, int row_start, int row_end, float plane_min, float edge_min,
+    const RingTable* __restrict__ rtab, int32_t* __restrict__ cnt, uint16_t* __restrict__ gidx,
+    uint64_t* __restrict__ gbits, float* __restrict__ curv_cm, uint8_t* __restrict__ irregular,
+    uint8_t* __restrict__ lanemap) {
+    __shared__ __attribute__((aligned(16))) float sc[kWin];     // one coordinate, column-major
+    __shared__ __attribute__((aligned(16))) char regA[(kBinChunk + 4) * 2];   // ring table -> idl
+    __shared__ __attribute__((aligned(16))) uint8_t fll[kBinChunk];
+    __shared__ int lid[kMaxRows];
+    __shared__ unsigned long long lrows;
+    static_assert(sizeof(regA) >= sizeof(RingCell) * kRingCells && kWin % 64 == 0 && 64 * kCurvNW * kWinQ >= kWin, "columns");
+    RingCell* rcell = reinterpret_cast<RingCell*>(regA);
+    uint16_t* idl = reinterpret_cast<uint16_t*>(regA);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t nblk = (int64_t)n_chunks * n_frames;        // XCD-aware logical block
+    const int64_t q8 = (nblk + 7) / 8;
+    const int64_t lb = (int64_t)(blockIdx.x % 8) * q8 + blockIdx.x / 8;
+    if (lb >= nblk) return;
+    const int f = (int)(lb / n_chunks), c = (int)(lb - (int64_t)f * n_chunks);
+    const int64_t fb = frame_off[f], e = frame_off[f + 1];
+    const int64_t s = fb + (int64_t)c * kBinChunk;
+    if (s >= e) {                                             // uniform: no chunk here at all
+        if (tid == 0) irregular[lb] = 0;
+        return;
     }
+    const int64_t t = min(e, s + (int64_t)kBinChunk);
+    const int64_t ws = max(fb, s - (int64_t)kCurvHalo), we = min(e, t + (int64_t)kCurvHalo);
+    const int L = (int)(we - ws), hb = (int)(s - ws), he = (int)(t - ws);
+    if (((L | hb | he) & 63) != 0) {                          // uniform: not whole columns
+        if (tid == 0) irregular[lb] = 1;
+        return;
+    }
+    const int ncols = L >> 6, c_hb = hb >> 6, own_cols = (he - hb) >> 6;
+    const int cpw = (ncols + kCurvNW - 1) / kCurvNW;          // columns per wave (<= kWinQ)
+    const int cw0 = w * cpw, nst = max(0, min(cpw, ncols - cw0));   // uniform
+    float px[kWinQ], py[kWinQ], pz[kWinQ];
+    const float* pw = pts + ws * stride;
+#pragma unroll
+    for (int st = 0; st < kWinQ; ++st) {                      // every load first (clamped)
+        const float* pp = pw + (uint32_t)((min(cw0 + st, ncols - 1) * 64 + lane) * stride);
+        px[st] = pp[0]; py[st] = pp[1]; pz[st] = pp[2];
+    }
+#if !SSF_FEAT_REG_LDS
+    // the 5 columns on each side of the wave's 11 (stencil taps of its edge columns) straight
+    // from global memory (L2: neighbouring waves load them as their own), in flight across the
+    // ring ids and the regularity check
+    float hx[10], hy[10], hz[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        const int col = k < 5 ? max(cw0 - 5 + k, 0) : min(cw0 + kWinQ + k - 5, ncols - 1);
+        const float* pp = pw + (uint32_t)((col * 64 + lane) * stride);
+        hx[k] = pp[0]; hy[k] = pp[1]; hz[k] = pp[2];
+    }
+#endif
+    for (int k = tid; k < kRingCells; k += kCurvNT) rcell[k] = rtab->cell[k];
+    if (tid == 0) lrows = 0ull;
+    const float r0 = rtab->r0, rinv = rtab->inv;
+    __syncthreads();
+    int ok = 1, mine = -1;
+#pragma unroll
+    for (int st = 0; st < kWinQ; ++st) {                      // frameFeature.cpp:57-73
+        const int id = ring_id_table(px[st], py[st], pz[st], r0, rinv, rcell);
+        if (st == 0) mine = id;
+        ok &= (int)(st >= nst) | (int)(id == mine);
+    }
+    if (w == 0) lid[lane] = mine;
+    __syncthreads();
+    const int row = lid[lane];
+    ok &= (int)(nst == 0) | (int)(mine == row);
+    ok &= (int)(row >= 0);
+    if (w == 0 && row >= 0)
+        __hip_atomic_fetch_or(&lrows, 1ull << row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __syncthreads();
+    ok &= (int)(lrows == ~0ull);                              // every row once per column
+    if (!__syncthreads_and(ok)) {                             // uniform: the general kernel's block
+        if (tid == 0) irregular[lb] = 1;
+        return;
+    }
+    if (tid == 0) irregular[lb] = 0;
+    // the chunk's row -> lane map (64 B): k_feat_select derives a selected point's chunk position
+    // from it (64 x own column + lane) instead of gathering it from the u16 index, which this
+    // kernel then writes only for the debug outputs
+    if (w == 0) lanemap[lb * kMaxRows + row] = (uint8_t)lane;
+    float v[kWinQ];
+#if SSF_FEAT_REG_LDS
+    auto coord = [&](const float (&P)[kWinQ], bool first) {
+#pragma unroll
+        for (int st = 0; st < kWinQ; ++st)
+            if (st < nst) sc[(cw0 + st) * 64 + lane] = P[st];
+        __syncthreads();
+        float ext[kWinQ + 10];                                // columns cw0 - 5 .. cw0 + kWinQ + 4
+#pragma unroll
+        for (int k = 0; k < kWinQ + 10; ++k) ext[k] = sc[min(max(cw0 - 5 + k, 0), ncols - 1) * 64 + lane];
+#pragma unroll
+        for (int st = 0; st < kWinQ; ++st) {
+            const float d = tap11(ext + st);
+            v[st] = first ? d * d : v[st] + d * d;            // ((dX dX + dY dY) + dZ dZ)
+        }
+        __syncthreads();                                      // before the next coordinate's stores
+    };
+    coord(px, true);
+    coord(py, false);
+    coord(pz, false);
+#else
+    auto coord = [&](const float (&P)[kWinQ], const float (&H)[10], bool first) {
+        float ext[kWinQ + 10];                                // columns cw0 - 5 .. cw0 + kWinQ + 4
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { ext[k] = H[k]; ext[kWinQ + 5 + k] = H[5 + k]; }
+#pragma unroll
+        for (int st = 0; st < kWinQ; ++st) ext[5 + st] = P[st];   // px[st] is column cw0 + st (clamped)
+#pragma unroll
+        for (int st = 0; st < kWinQ; ++st) {
+            const float d = tap11(ext + st);
+            v[st] = first ? d * d : v[st] + d * d;            // ((dX dX + dY dY) + dZ dZ)
+        }
+    };
+    coord(px, hx, true);
+    coord(py, hy, false);
+    coord(pz, hz, false);
+#endif
+    const bool row_in = row >= row_start && row < n_rows - row_end;
+    const int64_t cm = fb + (int64_t)c * kBinChunk;           // chunk-major base (curvature)
+#pragma unroll
+    for (int st = 0; st < kWinQ; ++st) {
+        const int col = cw0 + st;
+        if (st < nst && col >= c_hb && col < c_hb + own_cols) {
+            const int p = row * own_cols + (col - c_hb);
+            const bool covered = col >= 5 && col < ncols - 5;
+            uint8_t fl = row_in ? kFlU : (uint8_t)0;
+            if (row_in && covered) {
+                const uint8_t cf = cand_flags(true, true, v[st], plane_min, kEdge, edge_min);
+                fl = (uint8_t)((cf & 1) ? kFlP : 0) | (uint8_t)((cf & 2) ? kFlE : 0);
+            }
+            idl[idl_sw(p)] = (uint16_t)(64 * (col - c_hb) + lane);
+            fll[fll_sw(p)] = fl;
+            if (kDebug && curv_cm) curv_cm[cm + p] = (row_in && covered) ? v[st] : 0.0f;
+        }
+    }
+    if (tid < kMaxRows) cnt[((int64_t)f * (n_chunks + 1) + c) * kMaxRows + tid] = own_cols;
+    __syncthreads();
+    feat_chunk_out<kEdge>(tid, f, c, n_chunks, frame_off, (int)(t - s), kMaxRows * own_cols, idl, fll,
+                          gidx, gbits, kDebug);
 }
 
 // k_feat_select: one 1024-thread work-group per frame.  The chunks' row counts become, in LDS,
@@ -1071,7 +1253,9 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
                                                              int32_t* __restrict__ plane_count,
                                                              int edge_span, int32_t* __restrict__ esel,
                                                              float4* __restrict__ edge,
-                                                             int32_t* __restrict__ edge_count) {
+                                                             int32_t* __restrict__ edge_count,
+                                                             const uint8_t* __restrict__ irregular,
+                                                             const uint8_t* __restrict__ lanemap) {
     constexpr int kRB = kFeatMaxChunks + 1;                   // odd stride: conflict-free columns
     __shared__ int rb[kMaxRows][kRB];                         // row base per chunk; [.][ncf] = n_r
     __shared__ uint16_t ss[kFeatMaxChunks][kMaxRows];         // segment start in the chunk's slots
@@ -1082,6 +1266,10 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
     __shared__ int ro[kMaxRows + 1];
     __shared__ int lb[kMaxRows + 1];                          // per-row slot bases of the LDS selections
     __shared__ int pre[2][kMaxRows + 1];
+    // per chunk: 1 = general-kernel block (positions from the u16 index), else its row -> lane map
+    // (k_feat_chunk_reg: a selected point's chunk position is 64 x its own column + that lane)
+    __shared__ uint8_t irc[kFeatMaxChunks];
+    __shared__ uint8_t lmc[kFeatMaxChunks][kMaxRows];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     constexpr int nwv = kSelThreads / 64;
@@ -1092,9 +1280,51 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
     int32_t* C = cnt + (int64_t)f * (n_chunks + 1) * kMaxRows;
     const uint64_t* Bf = gbits + (int64_t)f * n_chunks * (kFeatPlanes * kFeatWords);
     const uint16_t* GI = gidx + idx_base(frame_off, f);
+    // every global load of the set-up issued first, into registers (one latency, not one per
+    // loop trip): the chunks' row counts (a wave's chunks), their candidate and unresolved words,
+    // the block flags and the lane maps (4-byte words)
+    constexpr int kCPW = kFeatMaxChunks / nwv;                // chunks per wave at most
+    constexpr int kWPT = kFeatMaxChunks * kFeatWords / kSelThreads;   // plane words per thread
+    constexpr int kLPT = kFeatMaxChunks * kMaxRows / 4 / kSelThreads; // lane-map words per thread
+    int cv[kCPW];
+#pragma unroll
+    for (int i = 0; i < kCPW; ++i) {
+        const int c = w + i * nwv;
+        cv[i] = c < ncf ? C[c * kMaxRows + lane] : 0;
+    }
+    uint64_t pwd[kWPT], uwd[kWPT];
+#pragma unroll
+    for (int i = 0; i < kWPT; ++i) {
+        const int k = tid + i * kSelThreads, cc = k / kFeatWords, wi = k - cc * kFeatWords;
+        const bool in = k < ncf * kFeatWords;
+        pwd[i] = in ? Bf[cc * (kFeatPlanes * kFeatWords) + wi] : 0ull;
+        uwd[i] = in ? Bf[cc * (kFeatPlanes * kFeatWords) + kFeatWords + wi] : 0ull;
+    }
+    uint32_t lmw[kLPT];
+    const uint32_t* LM = reinterpret_cast<const uint32_t*>(lanemap + (lanemap ? (int64_t)f * n_chunks * kMaxRows : 0));
+#pragma unroll
+    for (int i = 0; i < kLPT; ++i) {
+        const int k = tid + i * kSelThreads;
+        lmw[i] = (lanemap && k < ncf * (kMaxRows / 4)) ? LM[k] : 0u;
+    }
+    const uint8_t irv = (tid < ncf && irregular) ? irregular[(int64_t)f * n_chunks + tid] : (uint8_t)1;
+    if (tid < ncf) irc[tid] = irv;
+#pragma unroll
+    for (int i = 0; i < kLPT; ++i) {
+        const int k = tid + i * kSelThreads;
+        if (k < ncf * (kMaxRows / 4)) reinterpret_cast<uint32_t*>(&lmc[0][0])[k] = lmw[i];
+    }
+    // the frame-local input index of row r's point j (indexInRow) in chunk cc (rb: row bases)
+    auto point_of = [&](int cc, int r, int j) -> int {
+        const int o = j - rb[r][cc];                          // its place in the (chunk, row) segment
+        return cc * kBinChunk + (irc[cc] ? (int)GI[(int64_t)cc * kBinChunk + ss[cc][r] + o] : 64 * o + lmc[cc][r]);
+    };
     // counts -> segment starts (prefix over rows, per chunk); counts into rb
-    for (int c = w; c < ncf; c += nwv) {
-        const int v = C[c * kMaxRows + lane];
+#pragma unroll
+    for (int i = 0; i < kCPW; ++i) {
+        const int c = w + i * nwv;
+        if (c >= ncf) break;                                  // uniform
+        const int v = cv[i];
         int incl = v;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -1154,14 +1384,27 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
     if (curv_cm)                                              // debug: the row bases for k_feat_debug
         for (int k = tid; k < (ncf + 1) * kMaxRows; k += kSelThreads)
             C[k] = rb[k % kMaxRows][k / kMaxRows];
+#if SSF_SEL_CUT == 1                                          // timing only (tools)
+    __syncthreads();
+    if (tid == 0) plane_count[f] = 0;
+    return;
+#endif
     // candidate planes: every (chunk, row) segment of a row in range to its ring-order bits,
     // one plane at a time through the staging copy
 #pragma unroll
     for (int pl = 0; pl < (kEdge ? 2 : 1); ++pl) {
         if (pl) __syncthreads();                              // the previous plane's reads are done
-        for (int k = tid; k < ncf * kFeatWords; k += kSelThreads) {
-            const int c = k / kFeatWords, wi = k - c * kFeatWords;
-            stg[k] = Bf[c * (kFeatPlanes * kFeatWords) + (pl ? 2 * kFeatWords : 0) + wi];
+        if (pl == 0) {
+#pragma unroll
+            for (int i = 0; i < kWPT; ++i) {
+                const int k = tid + i * kSelThreads;
+                if (k < ncf * kFeatWords) stg[k] = pwd[i];
+            }
+        } else {
+            for (int k = tid; k < ncf * kFeatWords; k += kSelThreads) {
+                const int c = k / kFeatWords, wi = k - c * kFeatWords;
+                stg[k] = Bf[c * (kFeatPlanes * kFeatWords) + 2 * kFeatWords + wi];
+            }
         }
         __syncthreads();
         for (int k = tid; k < ncf * kMaxRows; k += kSelThreads) {
@@ -1182,10 +1425,17 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
             }
         }
     }
+#if SSF_SEL_CUT == 2                                          // timing only (tools)
+    __syncthreads();
+    if (tid == 0) plane_count[f] = 0;
+    return;
+#endif
     // the unresolved own points of rows in range
-    for (int k = tid; k < ncf * kFeatWords; k += kSelThreads) {
+#pragma unroll
+    for (int i = 0; i < kWPT; ++i) {
+        const int k = tid + i * kSelThreads;
         const int c = k / kFeatWords, wi = k - c * kFeatWords;
-        uint64_t u = Bf[c * (kFeatPlanes * kFeatWords) + kFeatWords + wi];
+        uint64_t u = uwd[i];                                  // 0 beyond the frame's words
         while (u) {
             const int p = 64 * wi + (int)__builtin_ctzll(u);
             u &= u - 1ull;
@@ -1206,8 +1456,7 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
                 int cc = 0;                                   // the last chunk whose base <= jj
                 for (int st = 64; st > 0; st >>= 1)
                     if (cc + st < ncf && rb[r][cc + st] <= jj) cc += st;
-                const int pp = ss[cc][r] + (jj - rb[r][cc]);
-                const int ii = cc * kBinChunk + (int)GI[(int64_t)cc * kBinChunk + pp];
+                const int ii = point_of(cc, r, jj);
                 const float* q = pts + (fb + ii) * stride;
                 ux[m] = q[0]; uy[m] = q[1]; uz[m] = q[2];
             }
@@ -1221,6 +1470,11 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
         }
     }
     __syncthreads();
+#if SSF_SEL_CUT == 3                                          // timing only (tools)
+    __syncthreads();
+    if (tid == 0) plane_count[f] = 0;
+    return;
+#endif
     // the planar selections (indexInRow per slot) stay in LDS when a frame cannot make more than
     // the staging region holds (sum over rows of ceil(n_r / span) <= nf / span + rows)
     const bool sel_lds = lb[n_rows] <= kFeatMaxChunks * kFeatWords * 2;
@@ -1270,6 +1524,10 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
         if (lane == 63) pre[e ? 1 : 0][n_rows] = incl;
     }
     __syncthreads();
+#if SSF_SEL_CUT == 4                                          // timing only (tools)
+    if (tid == 0) plane_count[f] = 0;
+    return;
+#endif
 #pragma unroll
     for (int e = 0; e < (kEdge ? 2 : 1); ++e) {
         const int* P = pre[e];
@@ -1300,8 +1558,7 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
 #pragma unroll
                 for (int st = 64; st > 0; st >>= 1)
                     if (cc + st < ncf && rb[r][cc + st] <= j) cc += st;
-                const int q = cc * kBinChunk + ss[cc][r] + (j - rb[r][cc]);
-                ii[u] = cc * kBinChunk + (int)GI[q];
+                ii[u] = point_of(cc, r, j);
             }
             float q[U][3];
 #pragma unroll
@@ -1448,6 +1705,14 @@ size_t feat_cnt_bytes(int n_frames, int64_t max_pts) {
     const int64_t nc = (max_pts + kBinChunk - 1) / kBinChunk;
     return sizeof(int32_t) * (size_t)std::max(1, n_frames) * (nc + 1) * kMaxRows;
 }
+size_t feat_lmap_bytes(int n_frames, int64_t max_pts) {
+    const int64_t nc = (max_pts + kBinChunk - 1) / kBinChunk;
+    return (size_t)std::max<int64_t>(1, (int64_t)n_frames * nc) * kMaxRows;
+}
+size_t feat_irr_bytes(int n_frames, int64_t max_pts) {
+    const int64_t nc = (max_pts + kBinChunk - 1) / kBinChunk;
+    return (size_t)std::max<int64_t>(16, ((int64_t)n_frames * nc + 15) & ~(int64_t)15);
+}
 bool feat_single_read(int64_t max_pts) {
 #ifdef SSF_FEAT_LEGACY
     (void)max_pts;
@@ -1480,12 +1745,27 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
         float* ccm = dbg ? fs->curv_cm : nullptr;
         const int64_t nblk = (int64_t)n_chunks * n_frames;
         const dim3 grid((unsigned)((nblk + 7) / 8 * 8));
+        // unmasked 64-beam frames: the regular-window kernel first, then the general one for the
+        // blocks it flagged (every other block returns at once)
+        const bool regular = SSF_FEAT_REGULAR && !keep && R == kMaxRows && fs->irr && fs->lmap;
+        uint8_t* irr = regular ? fs->irr : nullptr;
+        const RingTable* rt = reinterpret_cast<const RingTable*>(fs->rtab);
+        if (regular) {
+            kmark(s, "k_feat_chunk_reg");
+#define SSF_FR_LAUNCH(D, E)                                                                         \
+            hipLaunchKernelGGL((k_feat_chunk_reg<D, E>), grid, dim3(kCurvNT), 0, s, pts, stride,     \
+                               frame_off, n_frames, R, n_chunks, cfg.row_start, cfg.row_end,         \
+                               cfg.plane_min, emin, rt, fs->cnt, fs->gidx, fs->gbits, ccm, irr,    \
+                               fs->lmap)
+            if (edge) { if (dbg) SSF_FR_LAUNCH(true, true); else SSF_FR_LAUNCH(false, true); }
+            else { if (dbg) SSF_FR_LAUNCH(true, false); else SSF_FR_LAUNCH(false, false); }
+#undef SSF_FR_LAUNCH
+        }
         kmark(s, "k_feat_chunk");
 #define SSF_FC_LAUNCH(D, E)                                                                         \
         hipLaunchKernelGGL((k_feat_chunk<D, E>), grid, dim3(kCurvNT), 0, s, pts, stride, frame_off,  \
                            n_frames, R, n_chunks, cfg.row_start, cfg.row_end, cfg.plane_min, emin,  \
-                           keep, reinterpret_cast<const RingTable*>(fs->rtab), fs->cnt, fs->gidx,   \
-                           fs->gbits, ccm)
+                           keep, rt, fs->cnt, fs->gidx, fs->gbits, ccm, irr)
         if (edge) { if (dbg) SSF_FC_LAUNCH(true, true); else SSF_FC_LAUNCH(false, true); }
         else { if (dbg) SSF_FC_LAUNCH(true, false); else SSF_FC_LAUNCH(false, false); }
 #undef SSF_FC_LAUNCH
@@ -1500,12 +1780,14 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
             hipLaunchKernelGGL(k_feat_select<true>, dim3(n_frames), dim3(kSelThreads), 0, s, pts, stride,
                                frame_off, R, n_chunks, cfg.row_start, cfg.row_end, cfg.plane_span,
                                cfg.plane_min, emin, fs->cnt, fs->gidx, fs->gbits, ring_off, ccm, sel,
-                               plane, plane_count, edge->span, edge->sel, edge->out, edge->count);
+                               plane, plane_count, edge->span, edge->sel, edge->out, edge->count, irr,
+                               regular ? fs->lmap : nullptr);
         else
             hipLaunchKernelGGL(k_feat_select<false>, dim3(n_frames), dim3(kSelThreads), 0, s, pts, stride,
                                frame_off, R, n_chunks, cfg.row_start, cfg.row_end, cfg.plane_span,
                                cfg.plane_min, emin, fs->cnt, fs->gidx, fs->gbits, ring_off, ccm, sel,
-                               plane, plane_count, 1, nullptr, nullptr, nullptr);
+                               plane, plane_count, 1, nullptr, nullptr, nullptr, irr,
+                               regular ? fs->lmap : nullptr);
         if (dbg) {
             kmark(s, "k_feat_debug");
             hipLaunchKernelGGL(k_feat_debug, dim3(n_chunks, n_frames), dim3(256), 0, s, pts, stride,

@@ -79,10 +79,14 @@ struct FeatScratch {
     uint16_t* gidx;     // feat_idx_bytes
     uint64_t* gbits;    // feat_bits_bytes
     float* curv_cm;     // total floats (debug), else nullptr
+    uint8_t* irr;       // feat_irr_bytes: per (frame, chunk) block, 1 = not a regular window
+    uint8_t* lmap;      // feat_lmap_bytes: per regular block, row -> lane (64 B)
 };
 size_t feat_idx_bytes(int64_t total, int n_frames);
 size_t feat_bits_bytes(int n_frames, int64_t max_pts);
 size_t feat_cnt_bytes(int n_frames, int64_t max_pts);
+size_t feat_irr_bytes(int n_frames, int64_t max_pts);
+size_t feat_lmap_bytes(int n_frames, int64_t max_pts);
 bool feat_single_read(int64_t max_pts);
 // host: the ring-id table of n_rows (16 / 64) into out (ring_table_bytes); 0 or a negative code
 int build_ring_table(int n_rows, void* out_host);

@@ -442,8 +442,12 @@ def test_plane_table_split_over_work_groups(oracle, dev):
         o, m = int(pb.h_off[B - 1]), int(pb.count[B - 1])
         got = [normal[o:o + m].cpu().numpy().view(np.uint32), valid[o:o + m].cpu().numpy(),
                sx[o:o + m].cpu().numpy(), si[o:o + m].cpu().numpy()]
-        if tab.strips is not None:
-            got += [t[o:o + m].cpu().numpy() for t in tab.strips]
+        if tab.strips is not None:                            # the image and its defined head words
+            img, head = (t[o:o + m].cpu().numpy() for t in tab.strips)
+            K = 256                                           # kStripMax (registration.hip)
+            ns = int(head[3 * K + 4]) & 0xFFFF
+            got += [img, head[:K + 1], head[K + 1:K + 1 + ns], head[2 * K + 1:2 * K + 1 + ns],
+                    head[3 * K + 1:3 * K + 5]]
         if ref is None:
             ref = got
             nr, vr, _, _ = oracle.plane_table(pb.frame(0).cpu().numpy(), 0.05)

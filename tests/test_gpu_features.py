@@ -318,3 +318,29 @@ def test_frames_above_single_read_capacity(oracle, dev):
     got = _planes_product(fe, clouds, dev)
     for f, cl in enumerate(clouds):
         assert np.array_equal(got[f].view(np.uint32), oracle.extract_planes(cl, 64).view(np.uint32)), f
+
+
+def test_regular_windows_mixed_with_flagged_blocks(oracle, dev):
+    """k_feat_chunk_reg does the windows of an azimuth-ordered 64-beam scan (whole columns, every
+    row once per column, one row per lane) and flags every other block for k_feat_chunk;
+    k_feat_select then mixes lane-map positions and u16-index positions in one frame.  A full
+    120k-point frame with a NaN point (no row) in one chunk, a point moved to another ring in a
+    second, and a column's two points swapped in a third -- those windows (and their neighbours'
+    halos) go through the general kernel -- next to the clean frame and a frame cut mid-column
+    (a ragged last window): ring cloud, curvature bits and plane lists bit-exact vs the oracle,
+    debug and product instantiations."""
+    import ssf
+    c = frame(9, 5, n_az=1875)[0]
+    d = c.copy()
+    d[10 * 2048 + 700] = np.nan                               # no row
+    d[30 * 2048 + 1000, 2] += 3.0                             # another ring
+    i = 45 * 2048 + 64 * 7 + 3
+    d[[i, i + 1]] = d[[i + 1, i]]                             # lane order broken in one column
+    clouds = [c, d, c[: 64 * 1000 + 17]]
+    fe = ssf.Frontend(64, device=dev.index or 0)
+    out, h_off = _run(fe, clouds, dev)
+    for f, cl in enumerate(clouds):
+        _check_frame(oracle, fe, out, h_off, f, cl, 64)
+    got = _planes_product(fe, clouds, dev)
+    for f, cl in enumerate(clouds):
+        assert np.array_equal(got[f].view(np.uint32), oracle.extract_planes(cl, 64).view(np.uint32)), f

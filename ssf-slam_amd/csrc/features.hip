@@ -88,6 +88,9 @@ struct RingCell {
 struct RingTable {
     float r0, inv;
     RingCell cell[kRingCells];
+    // per row, the float ratios of its interval [lo, hi) (the id is a monotone step function of
+    // the ratio); an empty interval (lo >= hi) for a row that never occurs or is split
+    float rlo[kMaxRows], rhi[kMaxRows];
 };
 
 SSF_DEV int ring_id_lookup(float ratio, float r0, float inv, const RingCell* T) {
@@ -1084,13 +1087,11 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_REG_WAVES) void k_feat_chunk_reg(
     uint64_t* __restrict__ gbits, float* __restrict__ curv_cm, uint8_t* __restrict__ irregular,
     uint8_t* __restrict__ lanemap) {
     __shared__ __attribute__((aligned(16))) float sc[kWin];     // one coordinate, column-major
-    __shared__ __attribute__((aligned(16))) char regA[(kBinChunk + 4) * 2];   // ring table -> idl
+    __shared__ __attribute__((aligned(16))) uint16_t idl[kBinChunk + 4];
     __shared__ __attribute__((aligned(16))) uint8_t fll[kBinChunk];
     __shared__ int lid[kMaxRows];
     __shared__ unsigned long long lrows;
-    static_assert(sizeof(regA) >= sizeof(RingCell) * kRingCells && kWin % 64 == 0 && 64 * kCurvNW * kWinQ >= kWin, "columns");
-    RingCell* rcell = reinterpret_cast<RingCell*>(regA);
-    uint16_t* idl = reinterpret_cast<uint16_t*>(regA);
+    static_assert(kWin % 64 == 0 && 64 * kCurvNW * kWinQ >= kWin, "columns");
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t nblk = (int64_t)n_chunks * n_frames;        // XCD-aware logical block
@@ -1133,17 +1134,28 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_REG_WAVES) void k_feat_chunk_reg(
         hx[k] = pp[0]; hy[k] = pp[1]; hz[k] = pp[2];
     }
 #endif
-    for (int k = tid; k < kRingCells; k += kCurvNT) rcell[k] = rtab->cell[k];
     if (tid == 0) lrows = 0ull;
-    const float r0 = rtab->r0, rinv = rtab->inv;
-    __syncthreads();
-    int ok = 1, mine = -1;
+    // the row of the lane's first column (frameFeature.cpp:57-73 by the exact table, read from
+    // L2), then every column's point checked INSIDE that row's ratio interval with the fast ratio
+    // z * rsq(x^2 + y^2): 1e-6 (relative) clear of both ends, so the correctly rounded ratio, and
+    // with it the reference's id, is that row too; a point near an end (a few in a million)
+    // makes the window irregular
+    const int mine = ring_id_table(px[0], py[0], pz[0], rtab->r0, rtab->inv, rtab->cell);
+    const int mr = mine & (kMaxRows - 1);
+    const float rlo = rtab->rlo[mr], rhi = rtab->rhi[mr];
+    int ok = mine >= 0 && mine < kMaxRows;
+    // the columns' ratios into one 0 / 1 word first (no ratio kept live across the loop)
+    uint32_t inb = 0;
 #pragma unroll
-    for (int st = 0; st < kWinQ; ++st) {                      // frameFeature.cpp:57-73
-        const int id = ring_id_table(px[st], py[st], pz[st], r0, rinv, rcell);
-        if (st == 0) mine = id;
-        ok &= (int)(st >= nst) | (int)(id == mine);
+    for (int st = 0; st < kWinQ; ++st) {
+        const float r2 = px[st] * px[st] + py[st] * py[st];
+        const float ra = pz[st] * __builtin_amdgcn_rsqf(r2);
+        const float m = 1e-6f * fmaxf(1.0f, fabsf(ra));
+        const bool in = ra >= rlo + m && ra < rhi - m && r2 > 1e-30f && r2 < 1e30f;
+        inb |= (uint32_t)in << st;
     }
+    const uint32_t need = nst >= 32 ? ~0u : ((1u << nst) - 1u);
+    ok &= (int)((inb & need) == need);
     if (w == 0) lid[lane] = mine;
     __syncthreads();
     const int row = lid[lane];
@@ -1677,6 +1689,14 @@ int build_ring_table(int n_rows, void* out_host) {
             if (host_ring_id(kfloat(chg.back()), n_rows) != id) return -2;   // two changes in one bracket
         }
         prev_r = r; prev_id = id;
+    }
+    int seen[kMaxRows] = {};
+    for (int r = 0; r < kMaxRows; ++r) { T.rlo[r] = INFINITY; T.rhi[r] = -INFINITY; }
+    for (size_t i = 0; i + 1 < chg.size(); ++i) {             // the constant-id intervals between changes
+        const int id = host_ring_id(kfloat(chg[i]), n_rows);
+        if (id < 0 || id >= kMaxRows) continue;
+        if (++seen[id] == 1) { T.rlo[id] = kfloat(chg[i]); T.rhi[id] = kfloat(chg[i + 1]); }
+        else { T.rlo[id] = INFINITY; T.rhi[id] = -INFINITY; }   // a split row: never regular
     }
     for (int c = 0; c < kRingCells; ++c) {
         const uint32_t ks = c == 0 ? kmin : first_key(kmin, kmax, [&](uint32_t q) { return host_cell(kfloat(q), T.r0, T.inv) >= c; });

@@ -22,12 +22,28 @@ def table(n_rows):
     f = getattr(L, "_ZN3ssf16build_ring_tableEiPv")
     f.argtypes = [C.c_int, C.c_void_p]
     f.restype = C.c_int
-    buf = (C.c_char * (8 + 8 * CELLS))()
+    nb = getattr(L, "_ZN3ssf16ring_table_bytesEv")
+    nb.restype = C.c_size_t
+    assert nb() == 8 + 8 * CELLS + 2 * 4 * 64               # r0, inv, cells, per-row intervals
+    buf = (C.c_char * nb())()
     assert f(n_rows, C.addressof(buf)) == 0
     raw = bytes(buf)
     r0, inv = np.frombuffer(raw[:8], np.float32)
-    cells = np.frombuffer(raw[8:], np.dtype([("thr", np.float32), ("ids", np.int32)]))
+    cells = np.frombuffer(raw[8:8 + 8 * CELLS], np.dtype([("thr", np.float32), ("ids", np.int32)]))
     return np.float32(r0), np.float32(inv), cells
+
+
+def intervals(n_rows):
+    """per row, the [lo, hi) ratio interval of the table (k_feat_chunk_reg's regularity check)"""
+    from ssf import _abi
+    L = C.CDLL(_abi.LIB_PATH)
+    f = getattr(L, "_ZN3ssf16build_ring_tableEiPv")
+    f.argtypes = [C.c_int, C.c_void_p]
+    f.restype = C.c_int
+    buf = (C.c_char * (8 + 8 * CELLS + 512))()
+    assert f(n_rows, C.addressof(buf)) == 0
+    iv = np.frombuffer(bytes(buf)[8 + 8 * CELLS:], np.float32)
+    return iv[:64], iv[64:]
 
 
 def lookup(ratio, r0, inv, cells):
@@ -67,3 +83,26 @@ def test_ring_table_equals_reference_ids(oracle, n_rows):
     assert bad.size == 0, [(float(probe[i]), int(got[i]), int(want[i])) for i in bad[:10]]
     # every row appears, the change points are where the reference's id changes
     assert set(want.tolist()) >= set(range(n_rows))
+
+
+
+@pytest.mark.parametrize("n_rows", [64, 16])
+def test_row_intervals_hold_exactly_their_row(oracle, n_rows):
+    """k_feat_chunk_reg accepts a point for the lane's row when its ratio lies inside the row's
+    [lo, hi) with a margin: every ratio in a row's interval has that row's reference id, the
+    float just below lo and the float at hi do not, and rows the profile lacks are empty"""
+    lo, hi = intervals(n_rows)
+    ref = lambda x: oracle.lib().orc_ring_id(1.0, 0.0, float(x), n_rows)
+    present = 0
+    for r in range(64):
+        if not lo[r] < hi[r]:
+            assert r >= n_rows or not np.isfinite(lo[r])
+            continue
+        present += 1
+        a, b = np.float32(lo[r]), np.float32(hi[r])
+        below = np.nextafter(a, np.float32(-np.inf), dtype=np.float32)
+        last = np.nextafter(b, np.float32(-np.inf), dtype=np.float32)
+        assert ref(a) == r and ref(last) == r and ref(below) != r and ref(b) != r, r
+        for x in np.linspace(float(a), float(last), 7).astype(np.float32):
+            assert ref(x) == r, (r, x)
+    assert present == n_rows

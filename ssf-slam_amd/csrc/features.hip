@@ -783,8 +783,10 @@ SSF_DEV void feat_chunk_out(int tid, int f, int c, int n_chunks, const int64_t* 
     }
 }
 
+// One (frame, chunk) block of k_feat_chunk / k_feat_chunk_flagged (the work-group's LDS is
+// declared here: one block at a time)
 template <bool kDebug, bool kEdge>
-__global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const float* __restrict__ pts, int stride,
+SSF_DEV void feat_chunk_block(int64_t lb, const float* __restrict__ pts, int stride,
                                                     const int64_t* __restrict__ frame_off,
                                                     int n_frames, int n_rows, int n_chunks,
                                                     int row_start, int row_end, float plane_min,
@@ -793,8 +795,7 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
                                                     int32_t* __restrict__ cnt,
                                                     uint16_t* __restrict__ gidx,
                                                     uint64_t* __restrict__ gbits,
-                                                    float* __restrict__ curv_cm,
-                                                    const uint8_t* __restrict__ irregular) {
+                                                    float* __restrict__ curv_cm) {
     __shared__ __attribute__((aligned(16))) float sc[kTileE + 2 * kTilePad];   // x, then y, then z
     __shared__ __attribute__((aligned(16))) uint16_t meta[kTileE];   // own-tile slot | 0x8000: stencil
     // two LDS regions reused across phases (31 KiB in all: 5 work-groups per CU):
@@ -816,11 +817,6 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
     __shared__ int ntot, nown;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: step masks in SGPRs
-    const int64_t nblk = (int64_t)n_chunks * n_frames;        // XCD-aware logical block
-    const int64_t q8 = (nblk + 7) / 8;
-    const int64_t lb = (int64_t)(blockIdx.x % 8) * q8 + blockIdx.x / 8;
-    if (lb >= nblk) return;
-    if (irregular && !irregular[lb]) return;                  // uniform: done by k_feat_chunk_reg
     const int f = (int)(lb / n_chunks), c = (int)(lb - (int64_t)f * n_chunks);
     const int64_t fb = frame_off[f], e = frame_off[f + 1];
     const int64_t s = fb + (int64_t)c * kBinChunk;
@@ -1060,6 +1056,50 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(const fl
     // ---- out: the chunk's own-tile slots, whole aligned runs
     feat_chunk_out<kEdge>(tid, f, c, n_chunks, frame_off, (int)(t - s), nown, idl, fll, gidx, gbits);
 }
+
+#define SSF_FC_ARGS pts, stride, frame_off, n_frames, n_rows, n_chunks, row_start, row_end, plane_min, \
+                    edge_min, keep, rtab, cnt, gidx, gbits, curv_cm
+#define SSF_FC_PARAMS const float* __restrict__ pts, int stride, const int64_t* __restrict__ frame_off, \
+    int n_frames, int n_rows, int n_chunks, int row_start, int row_end, float plane_min,              \
+    float edge_min, const uint8_t* __restrict__ keep, const RingTable* __restrict__ rtab,             \
+    int32_t* __restrict__ cnt, uint16_t* __restrict__ gidx, uint64_t* __restrict__ gbits,            \
+    float* __restrict__ curv_cm
+// every (frame, chunk) block, one per work-group (XCD-aware: each XCD walks a contiguous range, so
+// a window's halo was just read into its own L2)
+template <bool kDebug, bool kEdge>
+__global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk(SSF_FC_PARAMS) {
+    const int64_t nblk = (int64_t)n_chunks * n_frames;
+    const int64_t q8 = (nblk + 7) / 8;
+    const int64_t lb = (int64_t)(blockIdx.x % 8) * q8 + blockIdx.x / 8;
+    if (lb >= nblk) return;
+    feat_chunk_block<kDebug, kEdge>(lb, SSF_FC_ARGS);
+}
+
+// after k_feat_chunk_reg: only the blocks it flagged.  A work-group reads the flags of 16
+// consecutive blocks in one 16-byte load and does the flagged ones in turn, so a launch of
+// regular frames is nblk / 16 work-groups that return at once (one work-group per block cost
+// ~9 us to drain for 15 k blocks)
+constexpr int kFlagGroup = 16;
+template <bool kDebug, bool kEdge>
+__global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk_flagged(SSF_FC_PARAMS,
+                                                                             const uint8_t* __restrict__ irregular) {
+    const int64_t nblk = (int64_t)n_chunks * n_frames;
+    const int64_t b0 = (int64_t)blockIdx.x * kFlagGroup;
+    const uint4 fw = *reinterpret_cast<const uint4*>(irregular + b0);   // feat_irr_bytes: 16-B padded
+    uint32_t m = 0;
+    const uint32_t wd[4] = {fw.x, fw.y, fw.z, fw.w};
+#pragma unroll
+    for (int k = 0; k < kFlagGroup; ++k) m |= (uint32_t)(((wd[k >> 2] >> (8 * (k & 3))) & 0xffu) != 0u) << k;
+    while (m) {                                               // uniform
+        const int k = __builtin_ctz(m);
+        m &= m - 1u;
+        if (b0 + k >= nblk) break;
+        feat_chunk_block<kDebug, kEdge>(b0 + k, SSF_FC_ARGS);
+        __syncthreads();                                      // the block's LDS readers are done
+    }
+}
+#undef SSF_FC_ARGS
+#undef SSF_FC_PARAMS
 
 // k_feat_chunk_reg: the same outputs for REGULAR windows, the common layout of a 64-beam scan in
 // azimuth order (the reference's driver order; the bench's synthetic scans): the window is whole
@@ -1781,14 +1821,23 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
             else { if (dbg) SSF_FR_LAUNCH(true, false); else SSF_FR_LAUNCH(false, false); }
 #undef SSF_FR_LAUNCH
         }
-        kmark(s, "k_feat_chunk");
-#define SSF_FC_LAUNCH(D, E)                                                                         \
-        hipLaunchKernelGGL((k_feat_chunk<D, E>), grid, dim3(kCurvNT), 0, s, pts, stride, frame_off,  \
-                           n_frames, R, n_chunks, cfg.row_start, cfg.row_end, cfg.plane_min, emin,  \
-                           keep, rt, fs->cnt, fs->gidx, fs->gbits, ccm, irr)
-        if (edge) { if (dbg) SSF_FC_LAUNCH(true, true); else SSF_FC_LAUNCH(false, true); }
-        else { if (dbg) SSF_FC_LAUNCH(true, false); else SSF_FC_LAUNCH(false, false); }
+#define SSF_FC_COMMON pts, stride, frame_off, n_frames, R, n_chunks, cfg.row_start, cfg.row_end,         \
+                      cfg.plane_min, emin, keep, rt, fs->cnt, fs->gidx, fs->gbits, ccm
+        if (regular) {
+            kmark(s, "k_feat_chunk_flagged");
+            const dim3 fgrid((unsigned)((nblk + kFlagGroup - 1) / kFlagGroup));
+#define SSF_FC_LAUNCH(D, E) hipLaunchKernelGGL((k_feat_chunk_flagged<D, E>), fgrid, dim3(kCurvNT), 0, s, SSF_FC_COMMON, irr)
+            if (edge) { if (dbg) SSF_FC_LAUNCH(true, true); else SSF_FC_LAUNCH(false, true); }
+            else { if (dbg) SSF_FC_LAUNCH(true, false); else SSF_FC_LAUNCH(false, false); }
 #undef SSF_FC_LAUNCH
+        } else {
+            kmark(s, "k_feat_chunk");
+#define SSF_FC_LAUNCH(D, E) hipLaunchKernelGGL((k_feat_chunk<D, E>), grid, dim3(kCurvNT), 0, s, SSF_FC_COMMON)
+            if (edge) { if (dbg) SSF_FC_LAUNCH(true, true); else SSF_FC_LAUNCH(false, true); }
+            else { if (dbg) SSF_FC_LAUNCH(true, false); else SSF_FC_LAUNCH(false, false); }
+#undef SSF_FC_LAUNCH
+        }
+#undef SSF_FC_COMMON
 #if SSF_FEAT_CUT
         // timing variants (tools only): the chunk kernel stopped early and wrote nothing, so the
         // select must not read its outputs; empty plane lists instead

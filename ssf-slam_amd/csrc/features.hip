@@ -1156,10 +1156,13 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_REG_WAVES) void k_feat_chunk_reg(
     const int cpw = (ncols + kCurvNW - 1) / kCurvNW;          // columns per wave (<= kWinQ)
     const int cw0 = w * cpw, nst = max(0, min(cpw, ncols - cw0));   // uniform
     float px[kWinQ], py[kWinQ], pz[kWinQ];
-    const float* pw = pts + ws * stride;
+    // column col, lane l at pw + col x 64 stride (uniform: scalar) + l x stride (once per lane):
+    // no per-load integer multiply
+    const float* pw = pts + ws * stride + lane * stride;
+    const int cstride = 64 * stride;
 #pragma unroll
     for (int st = 0; st < kWinQ; ++st) {                      // every load first (clamped)
-        const float* pp = pw + (uint32_t)((min(cw0 + st, ncols - 1) * 64 + lane) * stride);
+        const float* pp = pw + min(cw0 + st, ncols - 1) * cstride;
         px[st] = pp[0]; py[st] = pp[1]; pz[st] = pp[2];
     }
 #if !SSF_FEAT_REG_LDS
@@ -1170,7 +1173,7 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_REG_WAVES) void k_feat_chunk_reg(
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
         const int col = k < 5 ? max(cw0 - 5 + k, 0) : min(cw0 + kWinQ + k - 5, ncols - 1);
-        const float* pp = pw + (uint32_t)((col * 64 + lane) * stride);
+        const float* pp = pw + col * cstride;
         hx[k] = pp[0]; hy[k] = pp[1]; hz[k] = pp[2];
     }
 #endif

@@ -139,6 +139,8 @@ def parse(argv=None):
                     help="with --consecutive / --sequences-total: HIP events around every step's mask, "
                          "features + table and registrations on their streams; per-step start / end "
                          "times (ms from the first timed step) to stderr (diagnostic)")
+    ap.add_argument("--timeline-host", action="store_true",
+                    help="as --timeline, host enqueue times only (no timing events on the streams)")
     ap.add_argument("--latency", action="store_true",
                     help="BASELINE configs[1] as written: one frame pair at a time (B = 1), ms per frame")
     ap.add_argument("--mask-streams", type=int, default=3,
@@ -770,6 +772,8 @@ def sequences(args, world=1, rank=0, local=0):
     tl = []                                   # --timeline: per step, (phase, start, end) events
 
     def ev(stream):
+        if args.timeline_host:
+            return None
         e = torch.cuda.Event(enable_timing=True)
         e.record(stream)
         return e
@@ -778,14 +782,16 @@ def sequences(args, world=1, rank=0, local=0):
         nonlocal last, prev_out
         pos, flow = steps[j]
         sm = s_masks[j % len(s_masks)]
-        rec = {} if (timing and args.timeline) else None
+        rec = {} if (timing and (args.timeline or args.timeline_host)) else None
+        hst = [time.perf_counter()] if rec is not None else None   # host enqueue times
         with torch.cuda.stream(sm):
             if rec is not None:
                 rec["mask"] = [ev(sm)]
             out, bg = fe_mask.mask_pose(pos, flow, offK, hK, mode="gmm", want_mask=True)
             if rec is not None:
+                hst.append(time.perf_counter())
                 rec["mask"].append(ev(sm))
-            mrec = out[:, 0:7].view(K, B, 7).clone() if timing else None   # the SSF poses, on their stream
+            mrec = out[:, 0:7].view(K, B, 7).clone()       # the SSF poses, on their stream
             done = torch.cuda.Event()
             done.record(sm)
         if masked:
@@ -793,6 +799,7 @@ def sequences(args, world=1, rank=0, local=0):
             bg.record_stream(s_feat)
         with torch.cuda.stream(s_feat):
             if rec is not None:
+                hst.append(time.perf_counter())
                 rec["feat"] = [ev(s_feat)]
             pb = fe_feat.extract_planes_batch(pos, offK, hK, max_points=N, keep=bg if masked else None)
             table = fe_feat.plane_table(pb)
@@ -808,6 +815,7 @@ def sequences(args, world=1, rank=0, local=0):
             out.record_stream(s_reg)
         with torch.cuda.stream(s_reg):
             if rec is not None:
+                hst.append(time.perf_counter())
                 rec["reg"] = [ev(s_reg)]
             (lpb, ltab) = last
             if kws:
@@ -825,10 +833,11 @@ def sequences(args, world=1, rank=0, local=0):
                     snaps.append(rel.clone())
                     (lpb, ltab) = cur
                 rel_k = torch.stack(snaps, 0)
-            if timing:
-                records.append((rel_k, mrec, sm))
+            records.append((rel_k, mrec, sm))                # (warmup records are dropped)
             if rec is not None:
                 rec["reg"].append(ev(s_reg))
+                hst.append(time.perf_counter())
+                rec["host"] = hst
                 tl.append(rec)
         last = view(pb, table, K - 1)
         prev_out = out[(K - 1) * B:]
@@ -836,6 +845,15 @@ def sequences(args, world=1, rank=0, local=0):
 
     for j in range(W):
         step(j, False)
+    # the end-of-run path once on the warmup records (first launches load their kernels: the
+    # timed region must not pay that), then only timed records
+    for s in (*s_masks, s_reg):
+        torch.cuda.current_stream(dev).wait_stream(s)
+    warm = torch.cat([torch.cat([r, m], 2) for r, m, _ in records], 0)
+    if world > 1:
+        sd.gather_sequence_records(warm, args.sequences_total)
+    del warm
+    records.clear()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -858,9 +876,12 @@ def sequences(args, world=1, rank=0, local=0):
     elapsed = time.perf_counter() - t0
     if tl and rank == 0:
         z = tl[0]["mask"][0]
+        h0 = tl[0]["host"][0]
         for j, rec in enumerate(tl):
-            print("timeline step %d: " % j + "  ".join(
-                "%s %.3f-%.3f" % (k, z.elapsed_time(a), z.elapsed_time(b)) for k, (a, b) in rec.items()),
+            hs = rec.pop("host")
+            print("timeline step %d: " % j + ("" if args.timeline_host else "  ".join(
+                "%s %.3f-%.3f" % (k, z.elapsed_time(a), z.elapsed_time(b)) for k, (a, b) in rec.items()))
+                + "  host(mask,masked,feat,reg,end) " + " ".join("%.3f" % ((h - h0) * 1e3) for h in hs),
                 file=sys.stderr)
     gather_ok = None
     finite = bool(torch.isfinite(mine).all())
@@ -982,8 +1003,15 @@ def main():
     pipe = Pipeline(args, dev, B, N, iters, world)
     pipe.fe_mask.seed(20240000 + rank)
 
+    # the last warmup step takes the timed steps' code path, and the one exchange runs once, so
+    # every kernel and collective the timed region uses has been loaded and set up before it
+    # (HIP loads a kernel's code object on its first launch: ~50 ms for a torch copy kernel)
     for k in range(args.warmup):
-        pipe.step(k, batches, off, h_off, False)
+        pipe.step(k, batches, off, h_off, k == args.warmup - 1)
+    if world > 1:
+        pipe.exchange()
+    pipe.records.clear(); pipe.gathered.clear()
+    pipe.ev = {k: [] for k in pipe.ev}
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -734,13 +734,19 @@ def sequences(args, world=1, rank=0, local=0):
     offK, hK = ssf.frame_offsets([N] * (K * B), dev)
     fe_mask = ssf.Frontend(args.rows, device=dev.index)
     fe_mask.reserve(K * B, N)
-    fe_mask.mask_split(args.mask_split)
+    # the automatic split fills the chip with ONE launch (slots / frames parts per frame); here
+    # the masks of --mask-streams consecutive steps are in flight together, so each launch gets
+    # its share: slots / (streams x frames) (32 frames, 3 streams: 2 parts; 256 frames: 1)
+    n_ms = max(1, args.mask_streams)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    g_split = args.mask_split or max(1, cus // (n_ms * K * B))
+    fe_mask.mask_split(g_split)
     fe_mask.seed(20240000 + (shard[0] if strong and shard else 0))
     fe_feat = ssf.Frontend(args.rows, device=dev.index, solver=args.solver, max_iter=iters)
     fe_feat.reserve(K * B, N)
     fe_reg = ssf.Frontend(args.rows, device=dev.index, solver=args.solver, max_iter=iters)
     fe_reg.reserve(K * B, N)
-    s_masks = [torch.cuda.Stream(dev) for _ in range(max(1, args.mask_streams))]
+    s_masks = [torch.cuda.Stream(dev) for _ in range(n_ms)]
     s_feat = torch.cuda.Stream(dev, priority=args.feat_priority)
     s_reg = torch.cuda.Stream(dev, priority=args.feat_priority)
     rel, ab = ssf.identity_poses(B, dev), ssf.identity_poses(B, dev)
@@ -921,6 +927,7 @@ def sequences(args, world=1, rank=0, local=0):
                    "sequences_this_rank": B, "frames_per_sequence_timed": K * S,
                    "points_per_frame": N, "solver": args.solver, "iters": iters,
                    "mask_before_features": masked, "kabsch_warm_start": bool(kws),
+                   "mask_streams": n_ms, "mask_parts_per_frame": g_split,
                    "parallelism": f"sequence-sharded x{world}",
                    "world_size_initialised": (dist.get_world_size() if world > 1 else 1),
                    "backend": backend or "none",

@@ -1134,6 +1134,20 @@ def main():
             line["roofline_f64"] = {"bound": "valu_f64", "achieved": tf, "peak": F64_PEAK_TFLOPS,
                                     "unit": "TFLOP/s", "frac": tf / F64_PEAK_TFLOPS,
                                     "kernel": "k_mask_pose", "flops_source": os.path.basename(F64_JSON)}
+    # the step as a whole: every kernel of the front-end runs once per step, so the step's
+    # algorithmic bytes (and PMC bytes) over the measured overlapped step time -- how much of HBM
+    # the pipeline moves, beside the single-kernel roofline above (whose kernel-only duration
+    # includes its launch's slowest frame)
+    step_bytes = sum(v["bytes"] for v in kernels.values() if v.get("bytes"))
+    if step_bytes and not args.serial:
+        st = elapsed / args.steps
+        ach = step_bytes / st / 1e9
+        line["roofline_step"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": ach / HBM_PEAK_GBS, "bytes_per_step": step_bytes,
+                                 "kernels": sorted(k for k, v in kernels.items() if v.get("bytes"))}
+        tb = sum(v["traffic"] for v in kernels.values() if v.get("traffic"))
+        if tb:
+            line["roofline_step"].update(traffic_per_step=tb, traffic_frac=tb / st / 1e9 / HBM_PEAK_GBS)
     ns = {k: kernels[k]["frac"] for k in ("k_feat_chunk_reg", "k_feat_chunk", "k_bin_curv", "k_solve") if k in kernels and "frac" in kernels[k]}
     if ns:
         line["north_star_kernels_hbm_frac"] = ns

@@ -1278,6 +1278,216 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_REG_WAVES) void k_feat_chunk_reg(
                           gidx, gbits, kDebug);
 }
 
+// k_feat_wave_reg: k_feat_chunk_reg's outputs with ONE WAVE per chunk (round 4).  In a regular
+// window lane l of every column is the same row, so a chunk's whole stencil work is one lane's
+// column sequence and needs no other wave: a work-group is kCurvNW independent chunks with no
+// barrier at all.  Each wave loads the ring table into registers (lane l: cells 4l .. 4l + 3,
+// rlo / rhi of row l; a lookup is a lane permute), then the chunk's 32 own columns and the 5 on
+// each side (42 column loads of 768 B, all issued at once, consumed in column order: no halo
+// re-loads by neighbouring waves), checks regularity, evaluates every covered stencil from
+// registers and builds the candidate / unresolved / edge bits of its own points as per-lane
+// masks (bit i = own column i), OR-ed into the chunk's bit planes in the wave's LDS words
+// (own-tile slot p = row x own columns + i) and stored as whole words.  The window's outermost
+// columns (one each side of a full 6-column halo) are not loaded: no stencil of an own point
+// reaches them, and they cannot change whether one is covered (a covered own point's 5 row
+// neighbours on each side lie in the checked columns, which hold its row exactly once each), so
+// the outputs are those of k_feat_chunk on every window this kernel calls regular.
+#ifndef SSF_FEAT_WAVE_REG
+#define SSF_FEAT_WAVE_REG 0                      // k_feat_wave_reg instead of k_feat_chunk_reg (A/B)
+#endif
+#ifndef SSF_FEAT_WAVE_WAVES
+#define SSF_FEAT_WAVE_WAVES 4                    // k_feat_wave_reg waves per SIMD (launch bound; 123 VGPRs)
+#endif
+constexpr int kWaveOwn = kBinChunk / 64;         // own columns of a full chunk (32)
+constexpr int kWaveCols = kWaveOwn + 10;         // columns a wave loads
+#ifndef SSF_FEAT_WAVE_BLOCK
+#define SSF_FEAT_WAVE_BLOCK 8                    // own columns per streamed block
+#endif
+constexpr int kWB = SSF_FEAT_WAVE_BLOCK;
+static_assert(kWaveOwn % kWB == 0, "whole blocks");
+static_assert(kRingCells == 4 * 64 && kWaveOwn <= 32 && kCurvHalo >= 5 * 64,
+              "ring table: 4 cells per lane; own-column masks are 32 bits; 5 halo columns");
+
+// the table's cell ci from the lanes' registers (every lane must be active)
+SSF_DEV RingCell cell_from_lanes(int ci, const float (&thr)[4], const int (&ids)[4]) {
+    const int src = ci >> 2, q = ci & 3;
+    float t4[4];
+    int i4[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { t4[k] = __shfl(thr[k], src, 64); i4[k] = __shfl(ids[k], src, 64); }
+    RingCell rc;
+    rc.thr = q == 0 ? t4[0] : q == 1 ? t4[1] : q == 2 ? t4[2] : t4[3];
+    rc.ids = q == 0 ? i4[0] : q == 1 ? i4[1] : q == 2 ? i4[2] : i4[3];
+    return rc;
+}
+
+template <bool kDebug, bool kEdge>
+__global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVES) void k_feat_wave_reg(
+    const float* __restrict__ pts, int stride, const int64_t* __restrict__ frame_off, int n_frames,
+    int n_rows, int n_chunks, int row_start, int row_end, float plane_min, float edge_min,
+    const RingTable* __restrict__ rtab, int32_t* __restrict__ cnt, uint16_t* __restrict__ gidx,
+    uint64_t* __restrict__ gbits, float* __restrict__ curv_cm, uint8_t* __restrict__ irregular,
+    uint8_t* __restrict__ lanemap) {
+    __shared__ unsigned long long wpl[kCurvNW][kFeatPlanes * kFeatWords];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t nblk = (int64_t)n_chunks * n_frames;
+    const int64_t nwg = (nblk + kCurvNW - 1) / kCurvNW;       // XCD-aware logical work-group
+    const int64_t q8 = (nwg + 7) / 8;
+    const int64_t lw = (int64_t)(blockIdx.x % 8) * q8 + blockIdx.x / 8;
+    const int64_t lb = lw * kCurvNW + w;                      // this wave's (frame, chunk)
+    if (lw >= nwg || lb >= nblk) return;                      // uniform per wave (no barrier below)
+    const int f = (int)(lb / n_chunks), c = (int)(lb - (int64_t)f * n_chunks);
+    const int64_t fb = frame_off[f], e = frame_off[f + 1];
+    const int64_t s = fb + (int64_t)c * kBinChunk;
+    if (s >= e) {                                             // uniform: no chunk here at all
+        if (lane == 0) irregular[lb] = 0;
+        return;
+    }
+    const int64_t t = min(e, s + (int64_t)kBinChunk);
+    const int64_t ws = max(fb, s - (int64_t)kCurvHalo), we = min(e, t + (int64_t)kCurvHalo);
+    const int L = (int)(we - ws), hb = (int)(s - ws), he = (int)(t - ws);
+    if (((L | hb | he) & 63) != 0) {                          // uniform: not whole columns
+        if (lane == 0) irregular[lb] = 1;
+        return;
+    }
+    // the table first: its loads are then the first to complete
+    const float4 th4 = *reinterpret_cast<const float4*>(&rtab->cell[4 * lane]);          // cells 4l, 4l + 1
+    const float4 th4b = *reinterpret_cast<const float4*>(&rtab->cell[4 * lane + 2]);     // 4l + 2, 4l + 3
+    const float rlo_l = rtab->rlo[lane], rhi_l = rtab->rhi[lane];
+    const float r0 = rtab->r0, rinv = rtab->inv;
+    const int ncols = L >> 6, c_hb = hb >> 6, oc = (he - hb) >> 6;
+    const int j0 = c_hb - 5;                                  // window column of register k = 0
+    const int klo = max(0, -j0), khi = min(kWaveCols, ncols - j0);   // registers holding real columns
+    float X[kWaveCols], Y[kWaveCols], Z[kWaveCols];
+    // a column's base is uniform (SGPRs), the lane's byte offset one 32-bit VGPR for every column
+    const uint32_t lob = (uint32_t)(lane * stride) * 4u;
+    const char* wbase = reinterpret_cast<const char*>(pts + ws * stride);
+    const uint32_t colb = 256u * (uint32_t)stride;            // bytes per column (< 2^31: checked at launch)
+    auto load_col = [&](int k) {
+        const uint32_t o = (uint32_t)min(max(j0 + k, 0), ncols - 1) * colb + lob;
+        const float3 p3 = *reinterpret_cast<const float3*>(wbase + o);
+        X[k] = p3.x; Y[k] = p3.y; Z[k] = p3.z;
+    };
+    // the columns stream in blocks of kWB own columns: the first window (kWB + 10 columns), then
+    // each block's loads issued before the previous block's stencils
+#pragma unroll
+    for (int k = 0; k < kWB + 10; ++k) load_col(k);
+    wpl[w][lane] = 0ull;                                      // the wave's plane words
+    if (lane < kFeatPlanes * kFeatWords - 64) wpl[w][64 + lane] = 0ull;
+    const float thr[4] = {th4.x, th4.z, th4b.x, th4b.z};
+    const int ids[4] = {__float_as_int(th4.y), __float_as_int(th4.w), __float_as_int(th4b.y), __float_as_int(th4b.w)};
+    // the lane's row from its first own column: ring_id_table's test with the cells from lane
+    // permutes (the exact ratio's cell fetched for every lane, used where the fast one is near)
+    int mine;
+    {
+        const float x = X[5], y = Y[5], z = Z[5];
+        const float r2 = x * x + y * y;
+        const float ra = z * __builtin_amdgcn_rsqf(r2);
+        int ci = (int)((ra - r0) * rinv);
+        ci = min(max(ci, 0), kRingCells - 1);
+        const RingCell rc = cell_from_lanes(ci, thr, ids);
+        const float m = 1e-6f * fmaxf(1.0f, fabsf(ra));
+        const float tc = (ra - r0) * rinv, fr = tc - floorf(tc);
+        const int near = (int)!(fabsf(ra - rc.thr) > m) | (int)!(fr > m * rinv) | (int)!(fr < 1.0f - m * rinv) |
+                         (int)!(r2 > 1e-30f) | (int)!(r2 < 1e30f);
+        const float rx = z / sqrtf(r2);                       // ring_id_lookup's exact ratio
+        int cx = (int)((rx - r0) * rinv);
+        cx = min(max(cx, 0), kRingCells - 1);
+        const RingCell rcx = cell_from_lanes(cx, thr, ids);
+        const int a = (int)(int8_t)(rc.ids & 0xff), b = (int)(int8_t)((rc.ids >> 8) & 0xff);
+        const int ax = (int)(int8_t)(rcx.ids & 0xff), bx = (int)(int8_t)((rcx.ids >> 8) & 0xff);
+        const int idx = rx == rx ? (rx < rcx.thr ? ax : bx) : -1;
+        mine = near ? idx : (ra < rc.thr ? a : b);
+    }
+    const int row = mine & (kMaxRows - 1);
+    const float rlo = __shfl(rlo_l, row, 64), rhi = __shfl(rhi_l, row, 64);
+    unsigned long long rows = 1ull << row;                    // every row once per column
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) rows |= __shfl_xor(rows, o, 64);
+    // every real column's point inside the row's ratio interval, 1e-6 clear of both ends
+    uint64_t inb = 0, need = 0;
+    auto check_col = [&](int k) {
+        const float r2 = X[k] * X[k] + Y[k] * Y[k];
+        const float ra = Z[k] * __builtin_amdgcn_rsqf(r2);
+        const float m = 1e-6f * fmaxf(1.0f, fabsf(ra));
+        const bool in = ra >= rlo + m && ra < rhi - m && r2 > 1e-30f && r2 < 1e30f;
+        inb |= (uint64_t)in << k;
+        need |= (uint64_t)(k >= klo && k < khi) << k;         // uniform
+    };
+    // stencils of the own columns (window column c_hb + i, registers i .. i + 10), the flags as
+    // bit i of per-lane masks: planar candidate, unresolved, edge candidate
+    const bool row_in = row >= row_start && row < n_rows - row_end;
+    const int64_t cm = fb + (int64_t)c * kBinChunk;           // chunk-major base (curvature)
+    uint16_t* gi = gidx + idx_base(frame_off, f) + (int64_t)c * kBinChunk;
+    uint32_t mp = 0, mu = 0, me = 0;
+#pragma unroll
+    for (int k = 0; k < kWB + 10; ++k) check_col(k);
+#pragma unroll
+    for (int bk = 0; bk < kWaveOwn / kWB; ++bk) {
+        if (bk + 1 < kWaveOwn / kWB) {                        // the next block's columns in flight
+#pragma unroll
+            for (int k = kWB * (bk + 1) + 10; k < kWB * (bk + 2) + 10; ++k) load_col(k);
+        }
+#pragma unroll
+        for (int i = kWB * bk; i < kWB * (bk + 1); ++i) {     // no branch: columns past oc masked
+            const int col = c_hb + i;
+            const bool own = i < oc, covered = col >= 5 && col < ncols - 5;   // uniform
+            const float dx = tap11(X + i), dy = tap11(Y + i), dz = tap11(Z + i);
+            float v = dx * dx;
+            v = v + dy * dy;                                  // ((dX dX + dY dY) + dZ dZ)
+            v = v + dz * dz;
+            const uint8_t cf = cand_flags(true, true, v, plane_min, kEdge, edge_min);
+            const bool dec = own && row_in && covered;
+            mp |= (uint32_t)(dec && (cf & 1)) << i;
+            if (kEdge) me |= (uint32_t)(dec && (cf & 2)) << i;
+            mu |= (uint32_t)(own && row_in && !covered) << i;
+            if (kDebug && own) {                              // (an irregular chunk's are rewritten)
+                const int p = row * oc + i;
+                gi[p] = (uint16_t)(64 * i + lane);
+                if (curv_cm) curv_cm[cm + p] = dec ? v : 0.0f;
+            }
+        }
+        // the block's stencils complete here, and no load moves across: 26 columns live, not 42
+        asm volatile("" : "+v"(mp), "+v"(mu), "+v"(me), "+v"(inb) : : "memory");
+        if (bk + 1 < kWaveOwn / kWB) {
+#pragma unroll
+            for (int k = kWB * (bk + 1) + 10; k < kWB * (bk + 2) + 10; ++k) check_col(k);
+        }
+    }
+    const bool ok = mine >= 0 && mine < kMaxRows && (inb & need) == need && rows == ~0ull;
+    if (!__all(ok)) {                                         // uniform: the general kernel's chunk
+        if (lane == 0) irregular[lb] = 1;
+        return;
+    }
+    // own-tile bits [row x oc, row x oc + oc) of each plane: at most two 64-bit words
+    const int p0 = row * oc, wlo = p0 >> 6, sh = p0 & 63;
+    const bool spill = sh + oc > 64;
+    const uint32_t mk[kFeatPlanes] = {mp, mu, me};
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");    // the zeroed words before the ORs
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int pl = 0; pl < (kEdge ? 3 : 2); ++pl) {
+        const uint64_t bm = mk[pl];
+        if (bm) {
+            __hip_atomic_fetch_or(&wpl[w][pl * kFeatWords + wlo], bm << sh, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (spill)
+                __hip_atomic_fetch_or(&wpl[w][pl * kFeatWords + wlo + 1], bm >> (64 - sh), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    uint64_t* gb = gbits + ((int64_t)f * n_chunks + c) * (kFeatPlanes * kFeatWords);
+    gb[lane] = __hip_atomic_load(&wpl[w][lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   // planes 0, 1
+    if (kEdge && lane < kFeatWords)
+        gb[64 + lane] = __hip_atomic_load(&wpl[w][64 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    cnt[((int64_t)f * (n_chunks + 1) + c) * kMaxRows + lane] = oc;
+    lanemap[lb * kMaxRows + row] = (uint8_t)lane;
+    if (lane == 0) irregular[lb] = 0;
+}
+
 // k_feat_select: one 1024-thread work-group per frame.  The chunks' row counts become, in LDS,
 // each row's base per chunk (exclusive prefix over chunks: indexInRow of the segment's first
 // point; the row lengths n_r and the ring offsets follow) and each segment's start in its chunk's
@@ -1810,10 +2020,23 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
         const dim3 grid((unsigned)((nblk + 7) / 8 * 8));
         // unmasked 64-beam frames: the regular-window kernel first, then the general one for the
         // blocks it flagged (every other block returns at once)
-        const bool regular = SSF_FEAT_REGULAR && !keep && R == kMaxRows && fs->irr && fs->lmap;
+        const bool regular = SSF_FEAT_REGULAR && !keep && R == kMaxRows && fs->irr && fs->lmap &&
+                             stride <= 4096;              // k_feat_wave_reg: 32-bit window offsets
         uint8_t* irr = regular ? fs->irr : nullptr;
         const RingTable* rt = reinterpret_cast<const RingTable*>(fs->rtab);
-        if (regular) {
+        if (regular && SSF_FEAT_WAVE_REG) {                   // one wave per chunk
+            kmark(s, "k_feat_wave_reg");
+            const int64_t nwg = (nblk + kCurvNW - 1) / kCurvNW;
+            const dim3 wgrid((unsigned)((nwg + 7) / 8 * 8));
+#define SSF_FR_LAUNCH(D, E)                                                                         \
+            hipLaunchKernelGGL((k_feat_wave_reg<D, E>), wgrid, dim3(kCurvNT), 0, s, pts, stride,     \
+                               frame_off, n_frames, R, n_chunks, cfg.row_start, cfg.row_end,         \
+                               cfg.plane_min, emin, rt, fs->cnt, fs->gidx, fs->gbits, ccm, irr,    \
+                               fs->lmap)
+            if (edge) { if (dbg) SSF_FR_LAUNCH(true, true); else SSF_FR_LAUNCH(false, true); }
+            else { if (dbg) SSF_FR_LAUNCH(true, false); else SSF_FR_LAUNCH(false, false); }
+#undef SSF_FR_LAUNCH
+        } else if (regular) {
             kmark(s, "k_feat_chunk_reg");
 #define SSF_FR_LAUNCH(D, E)                                                                         \
             hipLaunchKernelGGL((k_feat_chunk_reg<D, E>), grid, dim3(kCurvNT), 0, s, pts, stride,     \

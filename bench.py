@@ -481,6 +481,8 @@ def rooflines(times, acc, B, N):
         # the flags (its model is dropped below when this kernel ran)
         # (no u16 index: a 64-B row -> lane map per chunk instead)
         "k_feat_chunk_reg": 12.0 * acc["points"] + 833.0 * acc["chunks"],
+        # the same outputs with one wave per chunk (its halo columns are L2 hits, not algorithmic)
+        "k_feat_wave_reg": 12.0 * acc["points"] + 833.0 * acc["chunks"],
         # the chunks' counts and bit planes read, per plane point: its u16 position (2 B) and xyz
         # (12 B) gathered, the xyzi record written (16 B); the selections stay in LDS
         "k_feat_select": 768.0 * acc["chunks"] + 30.0 * acc["plane"],
@@ -497,7 +499,7 @@ def rooflines(times, acc, B, N):
         "k_associate_sorted": 64.0 * acc["plane_reg"],
         "k_solve": 36.0 * acc["corr_evals"],                        # §8(d): 36 B x C per evaluation
     }
-    if "k_feat_chunk_reg" in times:
+    if "k_feat_chunk_reg" in times or "k_feat_wave_reg" in times:
         model.pop("k_feat_chunk", None)
         # select reads the lane maps (and flags) and no u16 positions
         model["k_feat_select"] = 833.0 * acc["chunks"] + 28.0 * acc["plane"]
@@ -515,7 +517,7 @@ def rooflines(times, acc, B, N):
                               evaluations_per_pair=acc["corr_evals"] / max(1, acc["corr"]),
                               note="corr = valid correspondences counted on device (ncorr); "
                                    "evaluations = 1 + logged iterations (nlog)")
-    for k in ("k_bin_curv", "k_feat_chunk", "k_feat_chunk_reg"):
+    for k in ("k_bin_curv", "k_feat_chunk", "k_feat_chunk_reg", "k_feat_wave_reg"):
         if k in out:
             out[k]["kept_points_per_launch"] = acc["kept"] / out[k]["launches"]
     return out, passes
@@ -1148,7 +1150,7 @@ def main():
         tb = sum(v["traffic"] for v in kernels.values() if v.get("traffic"))
         if tb:
             line["roofline_step"].update(traffic_per_step=tb, traffic_frac=tb / st / 1e9 / HBM_PEAK_GBS)
-    ns = {k: kernels[k]["frac"] for k in ("k_feat_chunk_reg", "k_feat_chunk", "k_bin_curv", "k_solve") if k in kernels and "frac" in kernels[k]}
+    ns = {k: kernels[k]["frac"] for k in ("k_feat_wave_reg", "k_feat_chunk_reg", "k_feat_chunk", "k_bin_curv", "k_solve") if k in kernels and "frac" in kernels[k]}
     if ns:
         line["north_star_kernels_hbm_frac"] = ns
         meas = {k: kernels[k]["traffic_frac"] for k in ns if "traffic_frac" in kernels[k]}

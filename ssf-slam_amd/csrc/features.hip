@@ -1293,7 +1293,7 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_REG_WAVES) void k_feat_chunk_reg(
 // neighbours on each side lie in the checked columns, which hold its row exactly once each), so
 // the outputs are those of k_feat_chunk on every window this kernel calls regular.
 #ifndef SSF_FEAT_WAVE_REG
-#define SSF_FEAT_WAVE_REG 0                      // k_feat_wave_reg instead of k_feat_chunk_reg (A/B)
+#define SSF_FEAT_WAVE_REG 1                      // k_feat_wave_reg instead of k_feat_chunk_reg (A/B: 0)
 #endif
 #ifndef SSF_FEAT_WAVE_WAVES
 #define SSF_FEAT_WAVE_WAVES 4                    // k_feat_wave_reg waves per SIMD (launch bound; 123 VGPRs)

@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 namespace ssf {
@@ -1369,44 +1370,19 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
         const float3 p3 = *reinterpret_cast<const float3*>(wbase + o);
         X[k] = p3.x; Y[k] = p3.y; Z[k] = p3.z;
     };
-    // the columns stream in blocks of kWB own columns: the first window (kWB + 10 columns), then
-    // each block's loads issued before the previous block's stencils
-#pragma unroll
-    for (int k = 0; k < kWB + 10; ++k) load_col(k);
     wpl[w][lane] = 0ull;                                      // the wave's plane words
     if (lane < kFeatPlanes * kFeatWords - 64) wpl[w][64 + lane] = 0ull;
     const float thr[4] = {th4.x, th4.z, th4b.x, th4b.z};
     const int ids[4] = {__float_as_int(th4.y), __float_as_int(th4.w), __float_as_int(th4b.y), __float_as_int(th4b.w)};
-    // the lane's row from its first own column: ring_id_table's test with the cells from lane
-    // permutes (the exact ratio's cell fetched for every lane, used where the fast one is near)
-    int mine;
-    {
-        const float x = X[5], y = Y[5], z = Z[5];
-        const float r2 = x * x + y * y;
-        const float ra = z * __builtin_amdgcn_rsqf(r2);
-        int ci = (int)((ra - r0) * rinv);
-        ci = min(max(ci, 0), kRingCells - 1);
-        const RingCell rc = cell_from_lanes(ci, thr, ids);
-        const float m = 1e-6f * fmaxf(1.0f, fabsf(ra));
-        const float tc = (ra - r0) * rinv, fr = tc - floorf(tc);
-        const int near = (int)!(fabsf(ra - rc.thr) > m) | (int)!(fr > m * rinv) | (int)!(fr < 1.0f - m * rinv) |
-                         (int)!(r2 > 1e-30f) | (int)!(r2 < 1e30f);
-        const float rx = z / sqrtf(r2);                       // ring_id_lookup's exact ratio
-        int cx = (int)((rx - r0) * rinv);
-        cx = min(max(cx, 0), kRingCells - 1);
-        const RingCell rcx = cell_from_lanes(cx, thr, ids);
-        const int a = (int)(int8_t)(rc.ids & 0xff), b = (int)(int8_t)((rc.ids >> 8) & 0xff);
-        const int ax = (int)(int8_t)(rcx.ids & 0xff), bx = (int)(int8_t)((rcx.ids >> 8) & 0xff);
-        const int idx = rx == rx ? (rx < rcx.thr ? ax : bx) : -1;
-        mine = near ? idx : (ra < rc.thr ? a : b);
-    }
-    const int row = mine & (kMaxRows - 1);
-    const float rlo = __shfl(rlo_l, row, 64), rhi = __shfl(rhi_l, row, 64);
-    unsigned long long rows = 1ull << row;                    // every row once per column
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) rows |= __shfl_xor(rows, o, 64);
-    // every real column's point inside the row's ratio interval, 1e-6 clear of both ends
+    int mine = -1, row = 0;
+    float rlo = 0.f, rhi = 0.f;
+    unsigned long long rows = 0ull;
+    bool row_in = false;
     uint64_t inb = 0, need = 0;
+    uint32_t mp = 0, mu = 0, me = 0;
+    const int64_t cm = fb + (int64_t)c * kBinChunk;           // chunk-major base (curvature)
+    uint16_t* gi = gidx + idx_base(frame_off, f) + (int64_t)c * kBinChunk;
+    // every real column's point inside the row's ratio interval, 1e-6 clear of both ends
     auto check_col = [&](int k) {
         const float r2 = X[k] * X[k] + Y[k] * Y[k];
         const float ra = Z[k] * __builtin_amdgcn_rsqf(r2);
@@ -1415,46 +1391,89 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
         inb |= (uint64_t)in << k;
         need |= (uint64_t)(k >= klo && k < khi) << k;         // uniform
     };
-    // stencils of the own columns (window column c_hb + i, registers i .. i + 10), the flags as
-    // bit i of per-lane masks: planar candidate, unresolved, edge candidate
-    const bool row_in = row >= row_start && row < n_rows - row_end;
-    const int64_t cm = fb + (int64_t)c * kBinChunk;           // chunk-major base (curvature)
-    uint16_t* gi = gidx + idx_base(frame_off, f) + (int64_t)c * kBinChunk;
-    uint32_t mp = 0, mu = 0, me = 0;
+    // The columns stream in blocks of kWB own columns: the first block's window (kWB + 10
+    // columns), then each block's loads issued before the previous block's stencils.  Even chunks
+    // stream left to right, odd chunks right to left, so the 5 columns two neighbouring chunks
+    // share are loaded by both at the same end of their streams, close in time (an L2 hit for the
+    // later one: streaming both ways from the left, the right neighbour's copy had left the L2).
+    constexpr int nb = kWaveOwn / kWB;
+    auto stream = [&](auto rev) {
+        constexpr bool R = decltype(rev)::value;
+        constexpr int kf = R ? kWaveCols - 6 : 5;              // an own column of the first window
+        constexpr int f0 = R ? kWB * (nb - 1) : 0;             // the first window [f0, f0 + kWB + 10)
 #pragma unroll
-    for (int k = 0; k < kWB + 10; ++k) check_col(k);
-#pragma unroll
-    for (int bk = 0; bk < kWaveOwn / kWB; ++bk) {
-        if (bk + 1 < kWaveOwn / kWB) {                        // the next block's columns in flight
-#pragma unroll
-            for (int k = kWB * (bk + 1) + 10; k < kWB * (bk + 2) + 10; ++k) load_col(k);
+        for (int k = f0; k < f0 + kWB + 10; ++k) load_col(k);
+        // the lane's row from that column (a clamped load is still a real column, and every real
+        // column is checked below): ring_id_table's test with the cells from lane permutes (the
+        // exact ratio's cell fetched for every lane, used where the fast one is near)
+        {
+            const float x = X[kf], y = Y[kf], z = Z[kf];
+            const float r2 = x * x + y * y;
+            const float ra = z * __builtin_amdgcn_rsqf(r2);
+            int ci = (int)((ra - r0) * rinv);
+            ci = min(max(ci, 0), kRingCells - 1);
+            const RingCell rc = cell_from_lanes(ci, thr, ids);
+            const float m = 1e-6f * fmaxf(1.0f, fabsf(ra));
+            const float tc = (ra - r0) * rinv, fr = tc - floorf(tc);
+            const int near = (int)!(fabsf(ra - rc.thr) > m) | (int)!(fr > m * rinv) | (int)!(fr < 1.0f - m * rinv) |
+                             (int)!(r2 > 1e-30f) | (int)!(r2 < 1e30f);
+            const float rx = z / sqrtf(r2);                   // ring_id_lookup's exact ratio
+            int cx = (int)((rx - r0) * rinv);
+            cx = min(max(cx, 0), kRingCells - 1);
+            const RingCell rcx = cell_from_lanes(cx, thr, ids);
+            const int a = (int)(int8_t)(rc.ids & 0xff), b = (int)(int8_t)((rc.ids >> 8) & 0xff);
+            const int ax = (int)(int8_t)(rcx.ids & 0xff), bx = (int)(int8_t)((rcx.ids >> 8) & 0xff);
+            const int idx = rx == rx ? (rx < rcx.thr ? ax : bx) : -1;
+            mine = near ? idx : (ra < rc.thr ? a : b);
         }
+        row = mine & (kMaxRows - 1);
+        rlo = __shfl(rlo_l, row, 64);
+        rhi = __shfl(rhi_l, row, 64);
+        rows = 1ull << row;                                    // every row once per column
 #pragma unroll
-        for (int i = kWB * bk; i < kWB * (bk + 1); ++i) {     // no branch: columns past oc masked
-            const int col = c_hb + i;
-            const bool own = i < oc, covered = col >= 5 && col < ncols - 5;   // uniform
-            const float dx = tap11(X + i), dy = tap11(Y + i), dz = tap11(Z + i);
-            float v = dx * dx;
-            v = v + dy * dy;                                  // ((dX dX + dY dY) + dZ dZ)
-            v = v + dz * dz;
-            const uint8_t cf = cand_flags(true, true, v, plane_min, kEdge, edge_min);
-            const bool dec = own && row_in && covered;
-            mp |= (uint32_t)(dec && (cf & 1)) << i;
-            if (kEdge) me |= (uint32_t)(dec && (cf & 2)) << i;
-            mu |= (uint32_t)(own && row_in && !covered) << i;
-            if (kDebug && own) {                              // (an irregular chunk's are rewritten)
-                const int p = row * oc + i;
-                gi[p] = (uint16_t)(64 * i + lane);
-                if (curv_cm) curv_cm[cm + p] = dec ? v : 0.0f;
+        for (int o = 1; o < 64; o <<= 1) rows |= __shfl_xor(rows, o, 64);
+        row_in = row >= row_start && row < n_rows - row_end;
+#pragma unroll
+        for (int k = f0; k < f0 + kWB + 10; ++k) check_col(k);
+        // stencils of the own columns (window column c_hb + i, registers i .. i + 10), the flags
+        // as bit i of per-lane masks: planar candidate, unresolved, edge candidate
+#pragma unroll
+        for (int bs = 0; bs < nb; ++bs) {
+            const int bk = R ? nb - 1 - bs : bs;               // this block
+            const int n0 = R ? kWB * (bk - 1) : kWB * (bk + 1) + 10;   // the next block's new columns
+            if (bs + 1 < nb) {                                 // ... in flight
+#pragma unroll
+                for (int k = n0; k < n0 + kWB; ++k) load_col(k);
+            }
+#pragma unroll
+            for (int i = kWB * bk; i < kWB * (bk + 1); ++i) { // no branch: columns past oc masked
+                const int col = c_hb + i;
+                const bool own = i < oc, covered = col >= 5 && col < ncols - 5;   // uniform
+                const float dx = tap11(X + i), dy = tap11(Y + i), dz = tap11(Z + i);
+                float v = dx * dx;
+                v = v + dy * dy;                              // ((dX dX + dY dY) + dZ dZ)
+                v = v + dz * dz;
+                const uint8_t cf = cand_flags(true, true, v, plane_min, kEdge, edge_min);
+                const bool dec = own && row_in && covered;
+                mp |= (uint32_t)(dec && (cf & 1)) << i;
+                if (kEdge) me |= (uint32_t)(dec && (cf & 2)) << i;
+                mu |= (uint32_t)(own && row_in && !covered) << i;
+                if (kDebug && own) {                          // (an irregular chunk's are rewritten)
+                    const int p = row * oc + i;
+                    gi[p] = (uint16_t)(64 * i + lane);
+                    if (curv_cm) curv_cm[cm + p] = dec ? v : 0.0f;
+                }
+            }
+            // the block's stencils complete here, and no load moves across: 26 columns live, not 42
+            asm volatile("" : "+v"(mp), "+v"(mu), "+v"(me), "+v"(inb) : : "memory");
+            if (bs + 1 < nb) {
+#pragma unroll
+                for (int k = n0; k < n0 + kWB; ++k) check_col(k);
             }
         }
-        // the block's stencils complete here, and no load moves across: 26 columns live, not 42
-        asm volatile("" : "+v"(mp), "+v"(mu), "+v"(me), "+v"(inb) : : "memory");
-        if (bk + 1 < kWaveOwn / kWB) {
-#pragma unroll
-            for (int k = kWB * (bk + 1) + 10; k < kWB * (bk + 2) + 10; ++k) check_col(k);
-        }
-    }
+    };
+    if (c & 1) stream(std::true_type{});                      // uniform
+    else stream(std::false_type{});
     const bool ok = mine >= 0 && mine < kMaxRows && (inb & need) == need && rows == ~0ull;
     if (!__all(ok)) {                                         // uniform: the general kernel's chunk
         if (lane == 0) irregular[lb] = 1;

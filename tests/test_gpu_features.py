@@ -344,3 +344,35 @@ def test_regular_windows_mixed_with_flagged_blocks(oracle, dev):
     got = _planes_product(fe, clouds, dev)
     for f, cl in enumerate(clouds):
         assert np.array_equal(got[f].view(np.uint32), oracle.extract_planes(cl, 64).view(np.uint32)), f
+
+
+def test_outermost_window_columns_not_loaded(oracle, dev):
+    """k_feat_wave_reg loads a chunk's 32 own columns and 5 on each side, not the window's
+    outermost column on each side (6 halo columns): no own stencil reaches it, and it cannot change
+    whether one is covered.  Points broken exactly there -- a NaN (no row) in window column 0 of
+    chunk 20, a point moved to another ring in window column 43 of chunk 40, two lanes swapped in
+    window column 0 of chunk 50 -- make the neighbouring chunk (whose own column it is) irregular,
+    while the chunk itself stays on the regular path; one more break in window column 1 of chunk
+    30 (a loaded column) flags both.  Ring cloud, curvature bits and plane lists bit-exact vs the
+    oracle, debug and product instantiations, for even (left-to-right) and odd (right-to-left)
+    chunks."""
+    import ssf
+    c = frame(11, 3, n_az=1875)[0]
+    d = c.copy()
+    col = lambda k: 64 * k                                    # first input of global column k
+    d[col(20 * 32 - 6) + 9] = np.nan                          # chunk 20, window column 0
+    d[col(40 * 32 + 32 + 5) + 17, 2] += 3.0                   # chunk 40, window column 43
+    i = col(50 * 32 - 6) + 30
+    d[[i, i + 1]] = d[[i + 1, i]]                             # chunk 50, window column 0
+    d[col(30 * 32 - 5) + 40] = np.nan                         # chunk 30, window column 1
+    e = c.copy()                                              # odd chunks: 21 (column 0), 41 (43)
+    e[col(21 * 32 - 6) + 3, 2] -= 2.5
+    e[col(41 * 32 + 32 + 5) + 60] = np.nan
+    clouds = [d, e, c]
+    fe = ssf.Frontend(64, device=dev.index or 0)
+    out, h_off = _run(fe, clouds, dev)
+    for f, cl in enumerate(clouds):
+        _check_frame(oracle, fe, out, h_off, f, cl, 64)
+    got = _planes_product(fe, clouds, dev)
+    for f, cl in enumerate(clouds):
+        assert np.array_equal(got[f].view(np.uint32), oracle.extract_planes(cl, 64).view(np.uint32)), f

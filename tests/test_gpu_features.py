@@ -321,7 +321,7 @@ def test_frames_above_single_read_capacity(oracle, dev):
 
 
 def test_regular_windows_mixed_with_flagged_blocks(oracle, dev):
-    """k_feat_chunk_reg does the windows of an azimuth-ordered 64-beam scan (whole columns, every
+    """k_feat_wave_reg (k_feat_chunk_reg in the A/B build) does the windows of an azimuth-ordered 64-beam scan (whole columns, every
     row once per column, one row per lane) and flags every other block for k_feat_chunk;
     k_feat_select then mixes lane-map positions and u16-index positions in one frame.  A full
     120k-point frame with a NaN point (no row) in one chunk, a point moved to another ring in a

@@ -34,7 +34,7 @@ def table(n_rows):
 
 
 def intervals(n_rows):
-    """per row, the [lo, hi) ratio interval of the table (k_feat_chunk_reg's regularity check)"""
+    """per row, the [lo, hi) ratio interval of the table (the regular-window kernels' regularity check)"""
     from ssf import _abi
     L = C.CDLL(_abi.LIB_PATH)
     f = getattr(L, "_ZN3ssf16build_ring_tableEiPv")
@@ -88,7 +88,7 @@ def test_ring_table_equals_reference_ids(oracle, n_rows):
 
 @pytest.mark.parametrize("n_rows", [64, 16])
 def test_row_intervals_hold_exactly_their_row(oracle, n_rows):
-    """k_feat_chunk_reg accepts a point for the lane's row when its ratio lies inside the row's
+    """k_feat_wave_reg (and k_feat_chunk_reg) accept a point for the lane's row when its ratio lies inside the row's
     [lo, hi) with a margin: every ratio in a row's interval has that row's reference id, the
     float just below lo and the float at hi do not, and rows the profile lacks are empty"""
     lo, hi = intervals(n_rows)

@@ -1284,9 +1284,9 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_REG_WAVES) void k_feat_chunk_reg(
 // column sequence and needs no other wave: a work-group is kCurvNW independent chunks with no
 // barrier at all.  Each wave loads the ring table into registers (lane l: cells 4l .. 4l + 3,
 // rlo / rhi of row l; a lookup is a lane permute), then the chunk's 32 own columns and the 5 on
-// each side (42 column loads of 768 B, all issued at once, consumed in column order: no halo
-// re-loads by neighbouring waves), checks regularity, evaluates every covered stencil from
-// registers and builds the candidate / unresolved / edge bits of its own points as per-lane
+// each side (42 column loads of 768 B, streamed in blocks of kWB own columns, see stream below),
+// checks regularity, evaluates every covered stencil from registers and builds the
+// candidate / unresolved / edge bits of its own points as per-lane
 // masks (bit i = own column i), OR-ed into the chunk's bit planes in the wave's LDS words
 // (own-tile slot p = row x own columns + i) and stored as whole words.  The window's outermost
 // columns (one each side of a full 6-column halo) are not loaded: no stencil of an own point
@@ -1297,7 +1297,7 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_REG_WAVES) void k_feat_chunk_reg(
 #define SSF_FEAT_WAVE_REG 1                      // k_feat_wave_reg instead of k_feat_chunk_reg (A/B: 0)
 #endif
 #ifndef SSF_FEAT_WAVE_WAVES
-#define SSF_FEAT_WAVE_WAVES 4                    // k_feat_wave_reg waves per SIMD (launch bound; 123 VGPRs)
+#define SSF_FEAT_WAVE_WAVES 4                    // k_feat_wave_reg waves per SIMD (launch bound; 126 VGPRs)
 #endif
 constexpr int kWaveOwn = kBinChunk / 64;         // own columns of a full chunk (32)
 constexpr int kWaveCols = kWaveOwn + 10;         // columns a wave loads

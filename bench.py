@@ -143,6 +143,11 @@ def parse(argv=None):
                     help="as --timeline, host enqueue times only (no timing events on the streams)")
     ap.add_argument("--latency", action="store_true",
                     help="BASELINE configs[1] as written: one frame pair at a time (B = 1), ms per frame")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; 0 = leave the "
+                         "environment's, HIP's default 4). 8 measured the same as 4 over three "
+                         "alternations (r04bq: 56.7 vs 56.6 k frames/s; 58.0 / 58.1 vs 55.4 / 57.2 k "
+                         "in r04bp was box noise)")
     ap.add_argument("--mask-streams", type=int, default=3,
                     help="mask launches of consecutive steps alternate over this many streams: the "
                          "GMM of a frame depends on no other frame, so a step's slow frames overlap "
@@ -946,6 +951,8 @@ def sequences(args, world=1, rank=0, local=0):
 
 def main():
     args = parse()
+    if args.hw_queues > 0:                # before anything starts the HIP runtime
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.latency:
         if args.gpus != 1 or os.environ.get("WORLD_SIZE", "1") != "1":
             sys.exit("bench.py --latency is a one-GPU, one-frame-pair measurement")
@@ -1087,6 +1094,7 @@ def main():
                    "parallelism": f"sequence-sharded x{world}",
                    "world_size_initialised": (dist.get_world_size() if world > 1 else 1),
                    "backend": backend or "none",
+                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) or None,
                    **({"rehearsal": "all ranks on one GPU, gloo"} if args.rehearse_one_gpu else {})},
         "roofline": None, "cpu_baseline": cpu,
         "kernels": kernels, "overlapped_event_ms": overlapped,

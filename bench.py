@@ -116,6 +116,9 @@ def parse(argv=None):
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="registration on the features stream (default: its own stream and context, so "
                          "features + plane table of step k+1 run ahead of the registration of step k)")
+    ap.add_argument("--reg-after-table", action="store_true",
+                    help="the registration of step k waits for step k's plane table too (before "
+                         "round 4's end; it needs only the table of step k - 1)")
     ap.add_argument("--dump-poses", default=None,
                     help="save the accumulated poses after the timed steps (.npy; stream-order check)")
     ap.add_argument("--launch-check", action="store_true",
@@ -366,7 +369,10 @@ class Pipeline:
                 etable = self.fe_feat.edge_table(eb)
             es[2].record(s_feat)
         if s_reg is not s_feat:
-            s_reg.wait_event(es[2])
+            # registration k needs the plane cloud of step k and the TABLE OF STEP k - 1 (on s_feat
+            # before this step's features): it waits for the features only and runs beside this
+            # step's table, which registration k + 1 gets through its own wait (same stream order)
+            s_reg.wait_event(es[2] if a.reg_after_table else es[1])
             # the plane batch and its table are read on s_reg in this step and the next: keep
             # the caching allocator from handing their blocks to s_feat until s_reg is done
             extra = (eb.xyzi, eb.count, *etable) if a.edges else ()

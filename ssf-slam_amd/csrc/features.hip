@@ -1360,7 +1360,12 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
     const int ncols = L >> 6, c_hb = hb >> 6, oc = (he - hb) >> 6;
     const int j0 = c_hb - 5;                                  // window column of register k = 0
     const int klo = max(0, -j0), khi = min(kWaveCols, ncols - j0);   // registers holding real columns
-    float X[kWaveCols], Y[kWaveCols], Z[kWaveCols];
+    // x and y of a column side by side (the dwordx3 load's first two registers): the stencils of
+    // x and y run as packed f32 pairs (v_pk_add_f32 / v_pk_mul_f32: two IEEE operations with
+    // the rounding of two scalar ones, the reference's order kept), z alone
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 XY[kWaveCols];
+    float Z[kWaveCols];
     // a column's base is uniform (SGPRs), the lane's byte offset one 32-bit VGPR for every column
     const uint32_t lob = (uint32_t)(lane * stride) * 4u;
     const char* wbase = reinterpret_cast<const char*>(pts + ws * stride);
@@ -1368,7 +1373,7 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
     auto load_col = [&](int k) {
         const uint32_t o = (uint32_t)min(max(j0 + k, 0), ncols - 1) * colb + lob;
         const float3 p3 = *reinterpret_cast<const float3*>(wbase + o);
-        X[k] = p3.x; Y[k] = p3.y; Z[k] = p3.z;
+        XY[k] = f2{p3.x, p3.y}; Z[k] = p3.z;
     };
     wpl[w][lane] = 0ull;                                      // the wave's plane words
     if (lane < kFeatPlanes * kFeatWords - 64) wpl[w][64 + lane] = 0ull;
@@ -1384,7 +1389,8 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
     uint16_t* gi = gidx + idx_base(frame_off, f) + (int64_t)c * kBinChunk;
     // every real column's point inside the row's ratio interval, 1e-6 clear of both ends
     auto check_col = [&](int k) {
-        const float r2 = X[k] * X[k] + Y[k] * Y[k];
+        const f2 q2 = XY[k] * XY[k];
+        const float r2 = q2.x + q2.y;
         const float ra = Z[k] * __builtin_amdgcn_rsqf(r2);
         const float m = 1e-6f * fmaxf(1.0f, fabsf(ra));
         const bool in = ra >= rlo + m && ra < rhi - m && r2 > 1e-30f && r2 < 1e30f;
@@ -1407,7 +1413,7 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
         // column is checked below): ring_id_table's test with the cells from lane permutes (the
         // exact ratio's cell fetched for every lane, used where the fast one is near)
         {
-            const float x = X[kf], y = Y[kf], z = Z[kf];
+            const float x = XY[kf].x, y = XY[kf].y, z = Z[kf];
             const float r2 = x * x + y * y;
             const float ra = z * __builtin_amdgcn_rsqf(r2);
             int ci = (int)((ra - r0) * rinv);
@@ -1449,9 +1455,12 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
             for (int i = kWB * bk; i < kWB * (bk + 1); ++i) { // no branch: columns past oc masked
                 const int col = c_hb + i;
                 const bool own = i < oc, covered = col >= 5 && col < ncols - 5;   // uniform
-                const float dx = tap11(X + i), dy = tap11(Y + i), dz = tap11(Z + i);
-                float v = dx * dx;
-                v = v + dy * dy;                              // ((dX dX + dY dY) + dZ dZ)
+                f2 dxy = XY[i] + XY[i + 1];                   // tap11 of x and y (frameFeature.cpp:88-97)
+#pragma unroll
+                for (int k = 2; k < 11; ++k) dxy = (k == 5) ? dxy - f2{10.0f, 10.0f} * XY[i + 5] : dxy + XY[i + k];
+                const float dz = tap11(Z + i);
+                const f2 sq = dxy * dxy;
+                float v = sq.x + sq.y;                        // ((dX dX + dY dY) + dZ dZ)
                 v = v + dz * dz;
                 const uint8_t cf = cand_flags(true, true, v, plane_min, kEdge, edge_min);
                 const bool dec = own && row_in && covered;

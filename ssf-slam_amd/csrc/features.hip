@@ -1387,13 +1387,15 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
     uint32_t mp = 0, mu = 0, me = 0;
     const int64_t cm = fb + (int64_t)c * kBinChunk;           // chunk-major base (curvature)
     uint16_t* gi = gidx + idx_base(frame_off, f) + (int64_t)c * kBinChunk;
-    // every real column's point inside the row's ratio interval, 1e-6 clear of both ends
+    // every real column's point inside the row's ratio interval, clear of both ends by the row's
+    // margin 1e-6 max(1, |rlo|, |rhi|) -- at least k_feat_chunk_reg's per-point 1e-6 max(1, |ra|)
+    // for any ra inside, so it accepts a subset of what that check accepts -- folded into the
+    // bounds once per lane (rlo / rhi below): per column one rsq, one multiply, four compares
     auto check_col = [&](int k) {
         const f2 q2 = XY[k] * XY[k];
         const float r2 = q2.x + q2.y;
         const float ra = Z[k] * __builtin_amdgcn_rsqf(r2);
-        const float m = 1e-6f * fmaxf(1.0f, fabsf(ra));
-        const bool in = ra >= rlo + m && ra < rhi - m && r2 > 1e-30f && r2 < 1e30f;
+        const bool in = ra >= rlo && ra < rhi && r2 > 1e-30f && r2 < 1e30f;
         inb |= (uint64_t)in << k;
         need |= (uint64_t)(k >= klo && k < khi) << k;         // uniform
     };
@@ -1433,8 +1435,12 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
             mine = near ? idx : (ra < rc.thr ? a : b);
         }
         row = mine & (kMaxRows - 1);
-        rlo = __shfl(rlo_l, row, 64);
-        rhi = __shfl(rhi_l, row, 64);
+        {
+            const float lo = __shfl(rlo_l, row, 64), hi = __shfl(rhi_l, row, 64);
+            const float m = 1e-6f * fmaxf(1.0f, fmaxf(fabsf(lo), fabsf(hi)));
+            rlo = lo + m;                                      // the check's bounds, margins in
+            rhi = hi - m;
+        }
         rows = 1ull << row;                                    // every row once per column
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) rows |= __shfl_xor(rows, o, 64);

@@ -46,8 +46,8 @@ F64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector, spec (AMD datasheet); f64 MFMA
 # HBM bytes per launch of every kernel / f64 FLOPs per k_mask_pose launch, measured with rocprofv3
 # PMC passes on a serial run of this bench (tools/pmc_traffic.py, tools/pmc_f64.py); used when
 # their workload config matches the run's.
-TRAFFIC_JSON = os.path.join(REPO, "profiles", "r04bw_traffic.json")
-F64_JSON = os.path.join(REPO, "profiles", "r04bw_f64.json")
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "r04by_traffic.json")
+F64_JSON = os.path.join(REPO, "profiles", "r04by_f64.json")
 METRIC = "LiDAR front-end frames/sec (mask+feature+GN), 64-beam 120k pts, 1/2/4/8 GPUs"
 
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SSF_ABI_VERSION 1
+#define SSF_ABI_VERSION 2
 
 enum {
     SSF_OK = 0,
@@ -43,6 +43,18 @@ enum {
 
 enum { SSF_SOLVER_CERES_LM = 0, SSF_SOLVER_GN = 1 };
 enum { SSF_MASK_GMM = 0, SSF_MASK_GT = 1, SSF_MASK_GIVEN = 2 };
+/* The evaluation of src/frameFeature.cpp:57 `atan(point.z / sqrt(x*x + y*y)) * 180 / M_PI` on
+ * float members.  C++ overload resolution allows exactly two:
+ *   SSF_RING_CHAIN_FLOAT   the float overloads std::atan(float) / std::sqrt(float) are visible at
+ *                          global scope -- libstdc++'s <math.h> wrapper does `using std::atan;
+ *                          using std::sqrt;`, and include/header.h:8-35 (ROS, tf, PCL, Ceres)
+ *                          includes <math.h>: ratio z / sqrtf(r2), atanf, `* 180` in float,
+ *                          `/ M_PI` in double, stored to float.  The default.
+ *   SSF_RING_CHAIN_DOUBLE  only the C ::sqrt(double) / ::atan(double): the ratio and the angle
+ *                          in double, stored to float.
+ * The host libm (glibc) evaluates atanf / atan once per context into a step table; the device
+ * never evaluates atan. */
+enum { SSF_RING_CHAIN_FLOAT = 0, SSF_RING_CHAIN_DOUBLE = 1 };
 
 /* Runtime replacement of the compile-time N_SCAN_ROW parameter blocks
  * (include/header.h:37-38, src/frameFeature.cpp:141-152, src/lidarOdometry_onlyPC.cpp:313-319). */
@@ -55,6 +67,7 @@ typedef struct {
     float plane_max;      /* coplanarity gate (planeMax)                           */
     int32_t solver;       /* SSF_SOLVER_CERES_LM (reference) or SSF_SOLVER_GN      */
     int32_t max_iter;     /* 8 (ceres::Solver::Options max_num_iterations) or 10   */
+    int32_t ring_chain;   /* SSF_RING_CHAIN_FLOAT (default) or SSF_RING_CHAIN_DOUBLE  */
 } ssf_config;
 
 typedef struct ssf_ctx ssf_ctx;

@@ -70,6 +70,17 @@ def lib():
     L.orc_ring_id.restype = C.c_int32
     L.orc_ring_id_of_angle.argtypes = [C.c_float, C.c_int32]
     L.orc_ring_id_of_angle.restype = C.c_int32
+    L.orc_set_ring_chain.argtypes = [C.c_int32]
+    L.orc_set_ring_chain.restype = C.c_int32
+    L.orc_get_ring_chain.restype = C.c_int32
+    L.orc_ring_angle.argtypes = [C.c_float, C.c_float, C.c_float, C.c_int32]
+    L.orc_ring_angle.restype = C.c_float
+    L.orc_ring_id_chain.argtypes = [C.c_float, C.c_float, C.c_float, C.c_int32, C.c_int32]
+    L.orc_ring_id_chain.restype = C.c_int32
+    L.orc_ring_id_ratio_d.argtypes = [C.c_double, C.c_int32]
+    L.orc_ring_id_ratio_d.restype = C.c_int32
+    L.orc_ring_changes_f32.argtypes = [C.c_float, C.c_float, C.c_int32, f32p, i32p, C.c_int64]
+    L.orc_ring_changes_f32.restype = C.c_int64
     L.orc_xindex_build.argtypes = [C.c_void_p, C.c_int64]
     L.orc_xindex_build.restype = C.c_void_p
     L.orc_xindex_free.argtypes = [C.c_void_p]
@@ -132,6 +143,37 @@ def profile(n_rows):
 
 
 # --------------------------------------------------------------------------- features
+RING_CHAIN_FLOAT = 0     # std::atan(float) / std::sqrt(float) (libstdc++ <math.h>): the default
+RING_CHAIN_DOUBLE = 1    # ::atan(double) / ::sqrt(double) only
+RING_CHAINS = {"float": RING_CHAIN_FLOAT, "double": RING_CHAIN_DOUBLE}
+
+
+class ring_chain:
+    """with ring_chain("double"): every oracle ring id (bin_rings, extract_planes, ...) uses that
+    evaluation of frameFeature.cpp:57, then the previous one again"""
+
+    def __init__(self, chain):
+        self.chain = RING_CHAINS[chain] if isinstance(chain, str) else int(chain)
+
+    def __enter__(self):
+        self.prev = lib().orc_set_ring_chain(self.chain)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_ring_chain(self.prev)
+        return False
+
+
+def ring_changes_f32(lo, hi, n_rows, cap=4096):
+    """every change of the float chain's row id over ALL float ratios in [lo, hi] (exhaustive)
+    -> (at [n] f32: the first float of each new id, id [n] i32)"""
+    at = np.zeros(cap, np.float32)
+    ids = np.zeros(cap, np.int32)
+    n = lib().orc_ring_changes_f32(float(lo), float(hi), n_rows, at, ids, cap)
+    assert n <= cap
+    return at[:n], ids[:n]
+
+
 def ring_ids(pts, n_rows):
     pts = np.ascontiguousarray(pts, np.float32)
     return np.array([lib().orc_ring_id(float(x), float(y), float(z), n_rows) for x, y, z in pts],

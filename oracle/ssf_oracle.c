@@ -32,32 +32,89 @@ int orc_profile_get(int32_t n_rows, orc_profile* p) {
 
 /* ======================================================================== */
 /* frameFeature.cpp:57-72 -- vertical angle -> scan row.
- * angle = atan(z / sqrt(x*x + y*y)) * 180 / M_PI: the ratio is formed in float (sqrt of a
- * float), atan / scaling in double, stored to a float.  The `||` guards at :59 and :64 are
- * always true and are therefore omitted. */
+ * `float angle = atan(point.z / sqrt(point.x * point.x + point.y * point.y)) * 180 / M_PI;`
+ * with float members.  Which atan / sqrt that names is C++ overload resolution over what the
+ * TU's headers declare at global scope (header.h:8-35: ROS, tf, PCL, Ceres, GTSAM):
+ *  - libstdc++'s <math.h> wrapper (any of those headers including <math.h>, e.g. tf's
+ *    LinearMath/Scalar.h, ros/time.h) adds `using std::atan; using std::sqrt;`, so the float
+ *    overloads win (exact match over promotion): sqrtf, a float divide, atanf, then `* 180` is a
+ *    FLOAT multiply (int 180 -> 180.0f) and `/ M_PI` a double divide, stored to float.  This is
+ *    ORC_RING_CHAIN_FLOAT, the default.
+ *  - with only the C declarations, the chain is double from the sqrt on: ORC_RING_CHAIN_DOUBLE.
+ * glibc's atanf / atan are the ones evaluated (this container's glibc; the device table is built
+ * by the same host libm).  The `||` guards at :59 and :64 are always true and are omitted. */
+static int32_t g_ring_chain = ORC_RING_CHAIN_FLOAT;
+int32_t orc_set_ring_chain(int32_t chain) {
+    int32_t prev = g_ring_chain;
+    g_ring_chain = chain == ORC_RING_CHAIN_DOUBLE ? ORC_RING_CHAIN_DOUBLE : ORC_RING_CHAIN_FLOAT;
+    return prev;
+}
+int32_t orc_get_ring_chain(void) { return g_ring_chain; }
+
+float orc_ring_angle(float x, float y, float z, int32_t chain) {
+    float r2 = x * x + y * y;                                   /* float members: a float sum */
+    if (chain == ORC_RING_CHAIN_DOUBLE)
+        return (float)(atan((double)z / sqrt((double)r2)) * 180.0 / M_PI);
+    float deg = atanf(z / sqrtf(r2)) * 180.0f;                  /* std::atan(float) * 180 */
+    return (float)((double)deg / M_PI);                         /* float / double, to float */
+}
+
 /* The row of a float angle, with the C++ promotions of the reference's expressions:
  *   :60  (angle + 15) / 2 + 0.5   float + int, float / int (float), then + double
  *   :66  (2 - angle) * 3.0 + 0.5  int - float is a FLOAT subtraction, then double
  *   :68  (-8.83 - angle) * 2.0    double - float (double) */
 int32_t orc_ring_id_of_angle(float angle, int32_t n_rows) {
     int32_t id = -1;
+    if (angle != angle) return -1;     /* 0/0: int(NaN) is INT_MIN on x86 -> no row either way */
     if (n_rows == 16) {
-        id = (int32_t)((double)((angle + 15.0f) / 2.0f) + 0.5);        /* :60 */
+        double v = (double)((angle + 15.0f) / 2.0f) + 0.5;                 /* :60 */
+        id = v > -2147483648.0 && v < 2147483647.0 ? (int32_t)v : -1;
     } else if (n_rows == 64) {
-        if ((double)angle >= -8.83)                                      /* :65 */
-            id = (int32_t)((double)(2.0f - angle) * 3.0 + 0.5);          /* :66 */
-        else
-            id = n_rows / 2 + (int32_t)((-8.83 - (double)angle) * 2.0 + 0.5); /* :68 */
+        if ((double)angle >= -8.83) {                                      /* :65 */
+            double v = (double)(2.0f - angle) * 3.0 + 0.5;                 /* :66 */
+            id = v > -2147483648.0 && v < 2147483647.0 ? (int32_t)v : -1;
+        } else {
+            double v = (-8.83 - (double)angle) * 2.0 + 0.5;                /* :68 */
+            id = v > -2147483648.0 && v < 2147483647.0 ? n_rows / 2 + (int32_t)v : -1;
+        }
     }
     if (id > -1 && id < n_rows) return id;                               /* :73 */
     return -1;
 }
 
+int32_t orc_ring_id_chain(float x, float y, float z, int32_t n_rows, int32_t chain) {
+    return orc_ring_id_of_angle(orc_ring_angle(x, y, z, chain), n_rows);
+}
 int32_t orc_ring_id(float x, float y, float z, int32_t n_rows) {
-    float r2 = x * x + y * y;
-    float ratio = z / sqrtf(r2);
-    float angle = (float)(atan((double)ratio) * 180.0 / M_PI);
-    return orc_ring_id_of_angle(angle, n_rows);
+    return orc_ring_id_chain(x, y, z, n_rows, g_ring_chain);
+}
+int32_t orc_ring_id_ratio_d(double ratio, int32_t n_rows) {
+    if (ratio != ratio) return -1;
+    return orc_ring_id_of_angle((float)(atan(ratio) * 180.0 / M_PI), n_rows);
+}
+
+int64_t orc_ring_changes_f32(float lo, float hi, int32_t n_rows, float* at, int32_t* id, int64_t cap) {
+    /* walk the floats of [lo, hi] in increasing order through their order-preserving keys */
+    uint32_t b;
+    memcpy(&b, &lo, 4);
+    uint32_t k = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    memcpy(&b, &hi, 4);
+    const uint32_t kh = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    int32_t prev = -2;
+    int64_t n = 0;
+    for (;; ++k) {
+        const uint32_t fb = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+        float r;
+        memcpy(&r, &fb, 4);
+        const int32_t v = orc_ring_id_chain(1.0f, 0.0f, r, n_rows, ORC_RING_CHAIN_FLOAT);
+        if (v != prev) {
+            if (n < cap) { at[n] = r; id[n] = v; }
+            ++n;
+            prev = v;
+        }
+        if (k == kh) break;
+    }
+    return n;
 }
 
 /* frameFeature.cpp:45-81 -- stable append per row, intensity = indexInRow + id/100.0 */

@@ -42,8 +42,27 @@ typedef struct {
 int orc_profile_get(int32_t n_rows, orc_profile* out);
 
 /* ---- frameFeature (src/frameFeature.cpp:45-123) ---- */
+/* The two evaluations C++ overload resolution allows for frameFeature.cpp:57:
+ *   ORC_RING_CHAIN_FLOAT   std::atan(float) / std::sqrt(float) visible at global scope (libstdc++'s
+ *                          <math.h> wrapper, pulled in by header.h:8-35's ROS / tf / PCL headers):
+ *                          (float)((double)(atanf(z / sqrtf(r2)) * 180.0f) / M_PI)  -- the default
+ *   ORC_RING_CHAIN_DOUBLE  only ::atan(double) / ::sqrt(double):
+ *                          (float)(atan((double)z / sqrt((double)r2)) * 180.0 / M_PI)
+ * r2 = x*x + y*y is a float sum in both.  orc_ring_id uses the process-wide chain
+ * (orc_set_ring_chain, default FLOAT); the _chain variants take it explicitly. */
+enum { ORC_RING_CHAIN_FLOAT = 0, ORC_RING_CHAIN_DOUBLE = 1 };
+int32_t orc_set_ring_chain(int32_t chain);     /* returns the previous chain */
+int32_t orc_get_ring_chain(void);
+float orc_ring_angle(float x, float y, float z, int32_t chain);
+int32_t orc_ring_id_chain(float x, float y, float z, int32_t n_rows, int32_t chain);
 int32_t orc_ring_id(float x, float y, float z, int32_t n_rows);
 int32_t orc_ring_id_of_angle(float angle, int32_t n_rows);
+/* the double chain's id of a double ratio z / sqrt(r2) (thresholds of the device table) */
+int32_t orc_ring_id_ratio_d(double ratio, int32_t n_rows);
+/* Exhaustive scan of EVERY float ratio r in [lo, hi] (points (1, 0, r): the float chain's ratio is
+ * r itself): records each change of the float chain's id as (first float of the new id, new id),
+ * up to cap entries; returns the number of changes (may exceed cap). */
+int64_t orc_ring_changes_f32(float lo, float hi, int32_t n_rows, float* at, int32_t* id, int64_t cap);
 /* Stable per-ring partition.  pts has stride `stride` floats (xyz at 0..2).
  * rxyzi: ring-ordered kept points (x,y,z,intensity) -- capacity n*4 floats.
  * ring_off[n_rows+1]: exclusive prefix of per-ring counts.

@@ -178,7 +178,8 @@ int64_t choice_uniform(ssf_ctx* c, int64_t n, double u) {
 bool valid_cfg(const ssf_config& c) {
     return (c.n_rows == 16 || c.n_rows == 64) && c.plane_span >= 2 && c.row_start >= 0 &&
            c.row_end >= 0 && c.max_iter >= 0 && c.max_iter <= 64 &&
-           (c.solver == SSF_SOLVER_CERES_LM || c.solver == SSF_SOLVER_GN);
+           (c.solver == SSF_SOLVER_CERES_LM || c.solver == SSF_SOLVER_GN) &&
+           (c.ring_chain == SSF_RING_CHAIN_FLOAT || c.ring_chain == SSF_RING_CHAIN_DOUBLE);
 }
 
 }  // namespace
@@ -193,6 +194,7 @@ int32_t ssf_config_default(int32_t n_rows, ssf_config* out) {
     out->n_rows = n_rows;
     out->solver = SSF_SOLVER_CERES_LM;
     out->max_iter = 8;                          // lidarOdometry_onlyPC.cpp:246
+    out->ring_chain = SSF_RING_CHAIN_FLOAT;     // frameFeature.cpp:57 under libstdc++
     if (n_rows == 16) {                         // frameFeature.cpp:143-146, onlyPC:314-316
         out->plane_min = 0.05f; out->plane_span = 3; out->plane_max = 0.15f;
         return SSF_OK;
@@ -321,15 +323,15 @@ static int32_t ensure_features(ssf_ctx* c, int32_t n_frames, int64_t total, int6
     SSF_TRY_HIP(c, c->sel.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(total, 1)), "alloc sel");
     SSF_TRY_HIP(c, c->sel_cnt.ensure(ssf::flag_bytes(total, n_frames)), "alloc cand flags");
     SSF_TRY_HIP(c, c->fix.ensure(ssf::fix_bytes(total, n_frames)), "alloc curvature fix-up list");
+    if (!c->rtab_ready) {                           // every feature path looks ring ids up in it
+        std::vector<char> h(ssf::ring_table_bytes());
+        const int rc = ssf::build_ring_table(R, c->cfg.ring_chain, h.data());
+        if (rc) return fail(c, SSF_E_ARG, "ring-id table: build failed (" + std::to_string(rc) + ")");
+        SSF_TRY_HIP(c, c->rtab.ensure(h.size()), "alloc ring table");
+        SSF_TRY_HIP(c, hipMemcpy(c->rtab.p, h.data(), h.size(), hipMemcpyHostToDevice), "H2D ring table");
+        c->rtab_ready = true;
+    }
     if (ssf::feat_single_read(max_pts)) {
-        if (!c->rtab_ready) {
-            std::vector<char> h(ssf::ring_table_bytes());
-            const int rc = ssf::build_ring_table(R, h.data());
-            if (rc) return fail(c, SSF_E_ARG, "ring-id table: build failed (" + std::to_string(rc) + ")");
-            SSF_TRY_HIP(c, c->rtab.ensure(h.size()), "alloc ring table");
-            SSF_TRY_HIP(c, hipMemcpy(c->rtab.p, h.data(), h.size(), hipMemcpyHostToDevice), "H2D ring table");
-            c->rtab_ready = true;
-        }
         SSF_TRY_HIP(c, c->fcnt.ensure(ssf::feat_cnt_bytes(n_frames, max_pts)), "alloc feature counts");
         SSF_TRY_HIP(c, c->fidx.ensure(ssf::feat_idx_bytes(total, n_frames)), "alloc feature index");
         SSF_TRY_HIP(c, c->fbits.ensure(ssf::feat_bits_bytes(n_frames, max_pts)), "alloc feature bits");

@@ -27,71 +27,39 @@
 
 namespace ssf {
 
-// frameFeature.cpp:57-72 (see oracle/ssf_oracle.c orc_ring_id for the precision choices).
-SSF_DEV int ring_id_exact(float ratio, int n_rows) {
-    float angle = (float)(atan((double)ratio) * 180.0 / 3.14159265358979323846);
-    int id = -1;
-    if (n_rows == 16) {
-        id = (int)((double)((angle + 15.0f) / 2.0f) + 0.5);
-    } else if (n_rows == 64) {
-        if ((double)angle >= -8.83)
-            id = (int)((double)(2.0f - angle) * 3.0 + 0.5);      // int - float: a float subtraction
-        else
-            id = n_rows / 2 + (int)((-8.83 - (double)angle) * 2.0 + 0.5);
-    }
-    return (id > -1 && id < n_rows) ? id : -1;
-}
-
-// The same id with a float atan (the f64 atan made k_bin_count f64-issue-bound).  The float
-// angle is within ~3e-5 deg of the f64 expression's; whenever it lies within 1e-3 deg of a bin
-// edge (or of the -8.83 switch, or is not finite) the exact f64 path decides, so the id is the
-// exact path's for every input.
-SSF_DEV int ring_id(float x, float y, float z, int n_rows) {
-    float r2 = x * x + y * y;
-    float ratio = z / sqrtf(r2);
-    const float af = atanf(ratio) * 57.29577951308232f;
-    double v;
-    float margin;
-    if (n_rows == 16) {
-        v = (double)((af + 15.0f) / 2.0f) + 0.5;
-        margin = 0.5e-3f;
-    } else {
-        const bool upper = (double)af >= -8.83;
-        v = upper ? (double)(2.0f - af) * 3.0 + 0.5 : (-8.83 - (double)af) * 2.0 + 0.5;
-        margin = upper ? 3e-3f : 2e-3f;
-        if (!(fabsf(af + 8.83f) > 1e-3f)) margin = -1.0f;   // near the switch (or NaN): exact
-    }
-    const float edge = (float)fabs(v - rint(v));
-    if (!(edge > margin)) return ring_id_exact(ratio, n_rows);
-    int id = (n_rows == 16 || (double)af >= -8.83) ? (int)v : n_rows / 2 + (int)v;
-    if (n_rows != 16 && n_rows != 64) id = -1;
-    return (id > -1 && id < n_rows) ? id : -1;
-}
-
-// ---- the ring id by table (k_feat_chunk) -------------------------------------------------------
-// frameFeature.cpp:57-73 makes the row id a step function of ONE float, ratio = z / sqrt(x^2 + y^2)
-// (a float divide and sqrt, correctly rounded on both sides): atan in double, the degree angle
-// rounded to float, the bin arithmetic of :60 / :63-71 and int() truncation are all monotone in
-// it.  So the host evaluates that exact chain (the oracle's orc_ring_id, glibc atan) once per
+// ---- the ring id by table ---------------------------------------------------------------------
+// frameFeature.cpp:57-73: `float angle = atan(point.z / sqrt(x*x + y*y)) * 180 / M_PI`, then the
+// bin arithmetic of :60 / :63-71 and int() truncation.  C++ overload resolution allows two
+// evaluations (oracle/ssf_oracle.c orc_ring_angle), selected by ssf_config.ring_chain:
+//   SSF_RING_CHAIN_FLOAT (default): the float overloads libstdc++'s <math.h> puts at global scope
+//     -- ratio = z / sqrtf(r2) (float), atanf, `* 180` in float, `/ M_PI` in double, to float;
+//   SSF_RING_CHAIN_DOUBLE: only ::sqrt / ::atan(double) -- ratio = (double)z / sqrt((double)r2).
+// Either way the row id is a monotone step function of ONE ratio (float or double).  The host
+// evaluates the exact chain with the host libm (glibc atanf / atan, as oracle/ssf_oracle.c) once per
 // context and cuts the ratio axis into kRingCells uniform cells (cell = clamp((ratio - r0) * inv),
-// float ops, the same on both sides); a cell holds at most two ids (cells are narrower than the
-// narrowest bin), so per cell {the float ratio where the second id starts, id below, id from
-// there}.  The device computes the ratio exactly as the reference and does ONE table lookup and
-// one compare: no atan, no double precision, no divergent exact path.
+// float ops, the same on both sides; a double ratio takes the cell of its float rounding); a cell
+// holds at most two ids (cells are narrower than the narrowest bin), so per cell {the threshold
+// where the second id starts (float; and as the exact double for the double chain), id below,
+// id from there}.  The device computes the ratio exactly as the reference and does ONE table
+// lookup and one compare: no atan on the device at all.
 #ifndef SSF_FEAT_EXACT_ID
-#define SSF_FEAT_EXACT_ID 0                      // A/B: the correctly rounded ratio for every point
+#define SSF_FEAT_EXACT_ID 0                      // A/B: the exact ratio for every point
 #endif
 constexpr int kRingCells = 256;
+constexpr int kRingChainFloat = SSF_RING_CHAIN_FLOAT, kRingChainDouble = SSF_RING_CHAIN_DOUBLE;
 struct RingCell {
-    float thr;          // ratios >= thr (float order) take id_b
+    float thr;          // ratios >= thr (float order) take id_b (double chain: thr rounded to float)
     int32_t ids;        // id_a (bits 0..7, signed), id_b (bits 8..15, signed)
 };
 struct RingTable {
     float r0, inv;
     RingCell cell[kRingCells];
     // per row, the float ratios of its interval [lo, hi) (the id is a monotone step function of
-    // the ratio); an empty interval (lo >= hi) for a row that never occurs or is split
+    // the ratio); an empty interval (lo >= hi) for a row that never occurs or is split.  Double
+    // chain: the interval's ends rounded to float (the regular kernels' 1e-6 margins cover that)
     float rlo[kMaxRows], rhi[kMaxRows];
+    int32_t chain, pad_;
+    double dthr[kRingCells];   // per cell, the exact threshold of the double chain (float chain: thr)
 };
 
 SSF_DEV int ring_id_lookup(float ratio, float r0, float inv, const RingCell* T) {
@@ -103,14 +71,32 @@ SSF_DEV int ring_id_lookup(float ratio, float r0, float inv, const RingCell* T) 
     return ratio == ratio ? id : -1;             // 0 / 0 (a point at the origin): no row
 }
 
-// The reference's ratio needs a correctly rounded sqrt and divide (~30 instructions).  The
-// hardware reciprocal square root gives it to ~3e-7 relative (v_rsq_f32 1 ulp, one multiply,
-// and the two roundings of the exact form): that ratio takes the exact form's id unless a table
-// threshold or a cell edge lies within 1e-6 of it (relative; a few in a million points), or r2
-// is tiny or not finite -- then the exact form decides (a rare, divergent branch).
-SSF_DEV int ring_id_table(float x, float y, float z, float r0, float inv, const RingCell* T) {
+// The reference's id from its exact ratio: the correctly rounded float z / sqrtf(r2) (float
+// chain) or the correctly rounded double (double)z / sqrt((double)r2) against the cell's double
+// threshold (double chain).  T: the cells (LDS or global), rt: the table (chain, dthr).
+SSF_DEV int ring_id_exact(float x, float y, float z, float r0, float inv, const RingCell* T,
+                          const RingTable* __restrict__ rt) {
     const float r2 = x * x + y * y;
-    if (SSF_FEAT_EXACT_ID) return ring_id_lookup(z / sqrtf(r2), r0, inv, T);   // A/B: no fast path
+    if (rt->chain != kRingChainDouble) return ring_id_lookup(z / sqrtf(r2), r0, inv, T);
+    const double dr = (double)z / sqrt((double)r2);
+    const float fr = (float)dr;
+    int ci = (int)((fr - r0) * inv);
+    ci = min(max(ci, 0), kRingCells - 1);
+    const RingCell rc = T[ci];
+    const int a = (int)(int8_t)(rc.ids & 0xff), b = (int)(int8_t)((rc.ids >> 8) & 0xff);
+    const int id = dr < rt->dthr[ci] ? a : b;
+    return dr == dr ? id : -1;
+}
+
+// The exact ratio needs a correctly rounded sqrt and divide (~30 instructions; f64 for the double
+// chain).  The hardware reciprocal square root gives it to ~3e-7 relative (v_rsq_f32 1 ulp, one
+// multiply, and the roundings of the exact form): that ratio takes the exact form's id unless a
+// table threshold or a cell edge lies within 1e-6 of it (relative; a few in a million points), or
+// r2 is tiny or not finite -- then the exact form decides (a rare, divergent branch).
+SSF_DEV int ring_id_table(float x, float y, float z, float r0, float inv, const RingCell* T,
+                          const RingTable* __restrict__ rt) {
+    const float r2 = x * x + y * y;
+    if (SSF_FEAT_EXACT_ID) return ring_id_exact(x, y, z, r0, inv, T, rt);   // A/B: no fast path
     const float ra = z * __builtin_amdgcn_rsqf(r2);
     int ci = (int)((ra - r0) * inv);
     ci = min(max(ci, 0), kRingCells - 1);
@@ -122,7 +108,7 @@ SSF_DEV int ring_id_table(float x, float y, float z, float r0, float inv, const 
                      (int)!(r2 > 1e-30f) | (int)!(r2 < 1e30f);
     const int a = (int)(int8_t)(rc.ids & 0xff), b = (int)(int8_t)((rc.ids >> 8) & 0xff);
     int id = ra < rc.thr ? a : b;
-    if (near) id = ring_id_lookup(z / sqrtf(r2), r0, inv, T);
+    if (near) id = ring_id_exact(x, y, z, r0, inv, T, rt);
     return id;
 }
 
@@ -134,6 +120,7 @@ __global__ __launch_bounds__(256) void k_bin_count(const float* __restrict__ pts
                                                    const int64_t* __restrict__ frame_off,
                                                    int n_rows, int n_chunks,
                                                    const uint8_t* __restrict__ keep,
+                                                   const RingTable* __restrict__ rtab,
                                                    int8_t* __restrict__ rid,
                                                    int32_t* __restrict__ hist) {
     __shared__ int h[kMaxRows];
@@ -154,7 +141,8 @@ __global__ __launch_bounds__(256) void k_bin_count(const float* __restrict__ pts
         for (int k = 0; k < kCountSteps; ++k) {
             const int64_t i = s + threadIdx.x + 256 * k;
             if (i < t) {
-                const int id = (keep && !keep[i]) ? -1 : ring_id(px[k], py[k], pz[k], n_rows);
+                const int id = (keep && !keep[i]) ? -1 : ring_id_table(px[k], py[k], pz[k], rtab->r0, rtab->inv,
+                                                                        rtab->cell, rtab);
                 rid[i] = (int8_t)id;
                 if (id >= 0) atomicAdd(&h[id], 1);
             }
@@ -853,7 +841,7 @@ SSF_DEV void feat_chunk_block(int64_t lb, const float* __restrict__ pts, int str
 #pragma unroll
     for (int st = 0; st < kWinQ; ++st) {                      // frameFeature.cpp:57-73
         const bool in = q0 + lane + 64 * st < q1 && (!keep || kp[st]);
-        const int id = ring_id_table(px[st], py[st], pz[st], r0, rinv, rcell);   // every lane: no branch
+        const int id = ring_id_table(px[st], py[st], pz[st], r0, rinv, rcell, rtab);   // every lane: no branch
         idr[st] = in ? id : -1;
     }
 #if SSF_FEAT_CUT == 1                                         // timing only (tools): ring ids
@@ -1184,7 +1172,7 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_REG_WAVES) void k_feat_chunk_reg(
     // z * rsq(x^2 + y^2): 1e-6 (relative) clear of both ends, so the correctly rounded ratio, and
     // with it the reference's id, is that row too; a point near an end (a few in a million)
     // makes the window irregular
-    const int mine = ring_id_table(px[0], py[0], pz[0], rtab->r0, rtab->inv, rtab->cell);
+    const int mine = ring_id_table(px[0], py[0], pz[0], rtab->r0, rtab->inv, rtab->cell, rtab);
     const int mr = mine & (kMaxRows - 1);
     const float rlo = rtab->rlo[mr], rhi = rtab->rhi[mr];
     int ok = mine >= 0 && mine < kMaxRows;
@@ -1357,6 +1345,7 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
     const float4 th4b = *reinterpret_cast<const float4*>(&rtab->cell[4 * lane + 2]);     // 4l + 2, 4l + 3
     const float rlo_l = rtab->rlo[lane], rhi_l = rtab->rhi[lane];
     const float r0 = rtab->r0, rinv = rtab->inv;
+    const bool dchain = rtab->chain == kRingChainDouble;      // uniform (a scalar load)
     const int ncols = L >> 6, c_hb = hb >> 6, oc = (he - hb) >> 6;
     const int j0 = c_hb - 5;                                  // window column of register k = 0
     const int klo = max(0, -j0), khi = min(kWaveCols, ncols - j0);   // registers holding real columns
@@ -1425,13 +1414,19 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
             const float tc = (ra - r0) * rinv, fr = tc - floorf(tc);
             const int near = (int)!(fabsf(ra - rc.thr) > m) | (int)!(fr > m * rinv) | (int)!(fr < 1.0f - m * rinv) |
                              (int)!(r2 > 1e-30f) | (int)!(r2 < 1e30f);
-            const float rx = z / sqrtf(r2);                   // ring_id_lookup's exact ratio
+            // ring_id_exact's ratio: the float chain's z / sqrtf(r2), or the double chain's
+            // double ratio (its cell from the float rounding, its threshold the cell's double)
+            float rx;
+            double dr = 0.0;
+            if (dchain) { dr = (double)z / sqrt((double)r2); rx = (float)dr; }   // uniform
+            else rx = z / sqrtf(r2);
             int cx = (int)((rx - r0) * rinv);
             cx = min(max(cx, 0), kRingCells - 1);
             const RingCell rcx = cell_from_lanes(cx, thr, ids);
             const int a = (int)(int8_t)(rc.ids & 0xff), b = (int)(int8_t)((rc.ids >> 8) & 0xff);
             const int ax = (int)(int8_t)(rcx.ids & 0xff), bx = (int)(int8_t)((rcx.ids >> 8) & 0xff);
-            const int idx = rx == rx ? (rx < rcx.thr ? ax : bx) : -1;
+            int idx = rx == rx ? (rx < rcx.thr ? ax : bx) : -1;
+            if (dchain) idx = dr == dr ? (dr < rtab->dthr[cx] ? ax : bx) : -1;
             mine = near ? idx : (ra < rc.thr ? a : b);
         }
         row = mine & (kMaxRows - 1);
@@ -1924,10 +1919,10 @@ __global__ __launch_bounds__(256) void k_feat_debug(const float* __restrict__ pt
 
 // ---- host: the ring-id table ------------------------------------------------------------------
 namespace {
-// the reference's row id of a float ratio (frameFeature.cpp:57-73; oracle/ssf_oracle.c orc_ring_id)
-int host_ring_id(float ratio, int n_rows) {
-    if (ratio != ratio) return -1;
-    const float angle = (float)(std::atan((double)ratio) * 180.0 / 3.14159265358979323846);
+constexpr double kPi = 3.14159265358979323846;       // M_PI
+// the bin arithmetic of a float angle (frameFeature.cpp:58-73; oracle/ssf_oracle.c orc_ring_id_of_angle)
+int angle_id(float angle, int n_rows) {
+    if (angle != angle) return -1;
     int id = -1;
     if (n_rows == 16) {
         const double v = (double)((angle + 15.0f) / 2.0f) + 0.5;
@@ -1939,64 +1934,87 @@ int host_ring_id(float ratio, int n_rows) {
     }
     return (id > -1 && id < n_rows) ? id : -1;
 }
+// the float chain's id of its float ratio: atanf, `* 180` in float, `/ M_PI` in double, to float
+int id_float_chain(float ratio, int n_rows) {
+    if (ratio != ratio) return -1;
+    const float deg = ::atanf(ratio) * 180.0f;
+    return angle_id((float)((double)deg / kPi), n_rows);
+}
+// the double chain's id of its double ratio
+int id_double_chain(double ratio, int n_rows) {
+    if (ratio != ratio) return -1;
+    return angle_id((float)(::atan(ratio) * 180.0 / kPi), n_rows);
+}
 uint32_t fkey(float f) { uint32_t b; std::memcpy(&b, &f, 4); return (b & 0x80000000u) ? ~b : (b | 0x80000000u); }
 float kfloat(uint32_t k) { const uint32_t b = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k; float f; std::memcpy(&f, &b, 4); return f; }
+uint64_t dkey(double d) { uint64_t b; std::memcpy(&b, &d, 8); return (b >> 63) ? ~b : (b | (1ull << 63)); }
+double kdouble(uint64_t k) { const uint64_t b = (k >> 63) ? (k & ~(1ull << 63)) : ~k; double d; std::memcpy(&d, &b, 8); return d; }
 int host_cell(float ratio, float r0, float inv) {   // the device's cell, the same float ops
     const float tc = (ratio - r0) * inv;
     return tc < 0.0f ? 0 : (tc >= (float)kRingCells ? kRingCells - 1 : std::min((int)tc, kRingCells - 1));
 }
 // smallest key in [lo, hi] with pred true (pred monotone false -> true on the range; hi must satisfy it)
-template <class P> uint32_t first_key(uint32_t lo, uint32_t hi, P pred) {
+template <class K, class P> K first_key(K lo, K hi, P pred) {
     while (lo < hi) {
-        const uint32_t m = lo + (hi - lo) / 2;
+        const K m = lo + (hi - lo) / 2;
         if (pred(m)) hi = m; else lo = m + 1;
     }
     return lo;
 }
 }  // namespace
 
-int build_ring_table(int n_rows, void* out_host) {
+int build_ring_table(int n_rows, int chain, void* out_host) {
+    if (chain != kRingChainFloat && chain != kRingChainDouble) return -5;
+    const bool dbl = chain == kRingChainDouble;
     RingTable& T = *reinterpret_cast<RingTable*>(out_host);
+    std::memset(&T, 0, sizeof(T));
+    T.chain = chain;
     if (n_rows == 64) { T.r0 = -0.5f; T.inv = (float)kRingCells / 0.6f; }
     else { T.r0 = -0.4f; T.inv = (float)kRingCells / 0.8f; }
-    const uint32_t kmin = fkey(-INFINITY), kmax = fkey(INFINITY);
+    // the id of a ratio given as a double (the float chain's ratios are floats: exact in double)
+    auto id_of = [&](double r) { return dbl ? id_double_chain(r, n_rows) : id_float_chain((float)r, n_rows); };
+    if (id_of(-INFINITY) != id_of(-2.0) || id_of(INFINITY) != id_of(2.0)) return -1;
     // the id's change points: brackets from a dense sweep of [-2, 2] (the ids are -1 beyond),
-    // each refined to the exact first key of the new id
-    std::vector<uint32_t> chg;
-    float prev_r = -2.0f;
-    int prev_id = host_ring_id(prev_r, n_rows);
-    if (host_ring_id(-INFINITY, n_rows) != prev_id || host_ring_id(INFINITY, n_rows) != host_ring_id(2.0f, n_rows))
-        return -1;
+    // each refined to the exact first ratio of the new id (first float / first double)
+    std::vector<double> chg;
+    double prev_r = -2.0;
+    int prev_id = id_of(prev_r);
     for (int k = 1; k <= 40000; ++k) {
-        const float r = -2.0f + 4.0f * (float)k / 40000.0f;
-        const int id = host_ring_id(r, n_rows);
+        const double r = (double)(-2.0f + 4.0f * (float)k / 40000.0f);
+        const int id = id_of(r);
         if (id != prev_id) {
             const int a = prev_id;
-            chg.push_back(first_key(fkey(prev_r) + 1, fkey(r), [&](uint32_t q) { return host_ring_id(kfloat(q), n_rows) != a; }));
-            if (host_ring_id(kfloat(chg.back()), n_rows) != id) return -2;   // two changes in one bracket
+            if (dbl) chg.push_back(kdouble(first_key<uint64_t>(dkey(prev_r) + 1, dkey(r), [&](uint64_t q) { return id_of(kdouble(q)) != a; })));
+            else chg.push_back(kfloat(first_key<uint32_t>(fkey((float)prev_r) + 1, fkey((float)r), [&](uint32_t q) { return id_of(kfloat(q)) != a; })));
+            if (id_of(chg.back()) != id) return -2;                           // two changes in one bracket
         }
         prev_r = r; prev_id = id;
     }
     int seen[kMaxRows] = {};
     for (int r = 0; r < kMaxRows; ++r) { T.rlo[r] = INFINITY; T.rhi[r] = -INFINITY; }
     for (size_t i = 0; i + 1 < chg.size(); ++i) {             // the constant-id intervals between changes
-        const int id = host_ring_id(kfloat(chg[i]), n_rows);
+        const int id = id_of(chg[i]);
         if (id < 0 || id >= kMaxRows) continue;
-        if (++seen[id] == 1) { T.rlo[id] = kfloat(chg[i]); T.rhi[id] = kfloat(chg[i + 1]); }
+        if (++seen[id] == 1) { T.rlo[id] = (float)chg[i]; T.rhi[id] = (float)chg[i + 1]; }
         else { T.rlo[id] = INFINITY; T.rhi[id] = -INFINITY; }   // a split row: never regular
     }
+    const uint32_t kmin = fkey(-INFINITY), kmax = fkey(INFINITY);
     for (int c = 0; c < kRingCells; ++c) {
-        const uint32_t ks = c == 0 ? kmin : first_key(kmin, kmax, [&](uint32_t q) { return host_cell(kfloat(q), T.r0, T.inv) >= c; });
-        const uint32_t ke = c == kRingCells - 1 ? kmax
-                          : first_key(kmin, kmax, [&](uint32_t q) { return host_cell(kfloat(q), T.r0, T.inv) >= c + 1; }) - 1;
+        // the cell's floats [ks, ke]; a change point T belongs to the cell of its float rounding
+        // (the device looks a double ratio up in the cell of its float rounding; a float chain
+        // ratio is its own rounding)
+        const uint32_t ks = c == 0 ? kmin : first_key<uint32_t>(kmin, kmax, [&](uint32_t q) { return host_cell(kfloat(q), T.r0, T.inv) >= c; });
         if (c > 0 && host_cell(kfloat(ks), T.r0, T.inv) != c) return -3;   // an empty cell
-        const int a = host_ring_id(kfloat(ks), n_rows);
         int nchg = 0;
-        uint32_t at = 0;
-        for (uint32_t q : chg) if (q > ks && q <= ke) { ++nchg; at = q; }
+        double at = 0.0;
+        for (double q : chg) if (host_cell((float)q, T.r0, T.inv) == c) { ++nchg; at = q; }
         if (nchg > 1) return -4;                                             // cells too wide
-        const int b = nchg ? host_ring_id(kfloat(at), n_rows) : a;
-        T.cell[c].thr = nchg ? kfloat(at) : INFINITY;
+        // below the change (or the whole cell): the id of the cell's first float
+        const int a = nchg ? id_of(dbl ? kdouble(dkey(at) - 1) : (double)kfloat(fkey((float)at) - 1))
+                           : id_of((double)kfloat(ks));
+        const int b = nchg ? id_of(at) : a;
+        T.cell[c].thr = nchg ? (float)at : INFINITY;
+        T.dthr[c] = nchg ? at : INFINITY;
         T.cell[c].ids = (int32_t)(((uint32_t)(uint8_t)(int8_t)a) | ((uint32_t)(uint8_t)(int8_t)b << 8));
     }
     return 0;
@@ -2130,8 +2148,10 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
     int32_t* fixl = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(fix) + fix_head(n_frames));
     if (n_chunks > 0) {
         kmark(s, "k_bin_count");
+        if (!fs || !fs->rtab) return hipErrorInvalidValue;          // the ring-id table is required
         hipLaunchKernelGGL(k_bin_count, dim3(n_chunks, n_frames), dim3(256), 0, s, pts, stride,
-                           frame_off, R, n_chunks, keep, rid, hist);
+                           frame_off, R, n_chunks, keep, reinterpret_cast<const RingTable*>(fs->rtab),
+                           rid, hist);
     }
     kmark(s, "k_bin_scan");
     hipLaunchKernelGGL(k_bin_scan, dim3(n_frames), dim3(64), 0, s, R, n_chunks, hist, ring_off, fix_count);

@@ -1290,7 +1290,7 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
     const int f = blockIdx.x, tid = threadIdx.x;
     // small batches: gridDim.y work-groups per frame, each sorting and building the strips
     // (identical results) and walking every gridDim.y-th query; share 0 alone
-    // writes the sorted copy, the strip image and the stamps
+    // writes the strip image and the stamps (every share writes the sorted copy, see below)
     const int share = (int)blockIdx.y, nshare = (int)gridDim.y;
     const int m = count[f];
     const int64_t base = frame_off[f];
@@ -1340,11 +1340,13 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
     }
     float4* SP = sorted_xyzi + base;
     int32_t* SI = sorted_idx + base;
-    if (share == 0) {
-        for (int r = tid; r < m; r += blockDim.x) {
-            SP[r] = P[idx[r]];
-            SI[r] = idx[r];
-        }
+    // EVERY share writes the sorted copy: table_strip_walks' deferred walk reads it back
+    // (table_deferred_walk), and only this work-group's own stores are ordered before those reads
+    // by the barrier below -- another share's (possibly on another XCD, whose L2 is not coherent
+    // for plain stores) are not.  The shares write identical values, so the duplicates are benign.
+    for (int r = tid; r < m; r += blockDim.x) {
+        SP[r] = P[idx[r]];
+        SI[r] = idx[r];
     }
     __syncthreads();
     SSF_TSTAMP(0);

@@ -88,8 +88,9 @@ size_t feat_cnt_bytes(int n_frames, int64_t max_pts);
 size_t feat_irr_bytes(int n_frames, int64_t max_pts);
 size_t feat_lmap_bytes(int n_frames, int64_t max_pts);
 bool feat_single_read(int64_t max_pts);
-// host: the ring-id table of n_rows (16 / 64) into out (ring_table_bytes); 0 or a negative code
-int build_ring_table(int n_rows, void* out_host);
+// host: the ring-id table of n_rows (16 / 64) and ring_chain (SSF_RING_CHAIN_*) into out
+// (ring_table_bytes); 0 or a negative code
+int build_ring_table(int n_rows, int chain, void* out_host);
 size_t ring_table_bytes();
 hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_frames,
                                  const float* pts, int stride, const int64_t* frame_off,

@@ -18,6 +18,9 @@ LIB_PATH = os.environ.get("SSF_LIB", os.path.join(LIB_DIR, "libssf_frontend.so")
 SSF_OK, SSF_E_ARG, SSF_E_HIP, SSF_E_NOMEM, SSF_E_CAPACITY, SSF_E_NODEV = 0, -1, -2, -3, -4, -5
 SOLVER_CERES_LM, SOLVER_GN = 0, 1
 MASK_GMM, MASK_GT, MASK_GIVEN = 0, 1, 2
+# the evaluation of frameFeature.cpp:57 (ssf_config.ring_chain, include/ssf_frontend.h)
+RING_CHAIN_FLOAT, RING_CHAIN_DOUBLE = 0, 1
+RING_CHAINS = {"float": RING_CHAIN_FLOAT, "double": RING_CHAIN_DOUBLE}
 # frames of plane points the association can stage from the plane table's strip image
 # (registration.hip: kStripHeadWords, kAssocStripF4Max)
 STRIP_IMAGE_MIN, STRIP_IMAGE_MAX = (256 + 1) + 2 * 256 + 4, 6144
@@ -77,7 +80,7 @@ class KernelTime(C.Structure):
 class Config(C.Structure):
     _fields_ = [("n_rows", C.c_int32), ("plane_min", C.c_float), ("plane_span", C.c_int32),
                 ("row_start", C.c_int32), ("row_end", C.c_int32), ("plane_max", C.c_float),
-                ("solver", C.c_int32), ("max_iter", C.c_int32)]
+                ("solver", C.c_int32), ("max_iter", C.c_int32), ("ring_chain", C.c_int32)]
 
 
 class EdgeConfig(C.Structure):

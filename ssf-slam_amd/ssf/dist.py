@@ -49,6 +49,8 @@ def gather_sequence_records(records: torch.Tensor, n_sequences: int, group=None)
     may differ in size by one, so every rank pads to the largest shard (NaN rows) before the
     collective and the pads are dropped after it."""
     F, b, k = records.shape
+    if not records.dtype.is_floating_point:
+        raise TypeError(f"sequence records must be floating point (NaN pads), got {records.dtype}")
     if not dist.is_available() or not dist.is_initialized():
         if b != n_sequences:
             raise ValueError(f"{b} sequences on a single rank, expected {n_sequences}")
@@ -57,11 +59,16 @@ def gather_sequence_records(records: torch.Tensor, n_sequences: int, group=None)
     rank = dist.get_rank(group)
     if b != len(sequence_shard(n_sequences, world, rank)):
         raise ValueError("records do not match this rank's sequence shard")
+    # the concatenation below puts rank r's rows at sequence_shard(.., r): that is the id order
+    # only because the shards are contiguous, in rank order, and cover every id once
+    shards = [sequence_shard(n_sequences, world, r) for r in range(world)]
+    if [i for sh in shards for i in sh] != list(range(n_sequences)):
+        raise AssertionError("sequence_shard must give contiguous id-ordered shards")
     bmax = -(-n_sequences // world)
     pad = torch.full((F, bmax, k), float("nan"), dtype=records.dtype, device=records.device)
     pad[:, :b] = records
     allr = gather_poses(pad.view(F, bmax * k), group).view(world, F, bmax, k)
-    parts = [allr[r, :, :len(sequence_shard(n_sequences, world, r))] for r in range(world)]
+    parts = [allr[r, :, :len(shards[r])] for r in range(world)]
     return torch.cat(parts, 1)
 
 

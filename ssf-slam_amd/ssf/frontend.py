@@ -75,7 +75,10 @@ class Frontend:
     """One C-ABI context (one device, one parameter profile)."""
 
     def __init__(self, n_rows: int = 64, device: int | torch.device | None = None,
-                 solver: str = "ceres_lm", max_iter: int | None = None):
+                 solver: str = "ceres_lm", max_iter: int | None = None, ring_chain: str = "float"):
+        """ring_chain: the evaluation of frameFeature.cpp:57's atan / sqrt -- "float" (the float
+        overloads libstdc++'s <math.h> makes visible; the default) or "double" (C's double
+        functions only); include/ssf_frontend.h SSF_RING_CHAIN_*."""
         if not torch.cuda.is_available():
             raise SSFError("no HIP device visible: the MI355X front-end has no CPU fallback")
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else
@@ -84,6 +87,9 @@ class Frontend:
         self.cfg = _abi.config_default(n_rows)
         self.cfg.solver = SOLVERS[solver]
         self.cfg.max_iter = (8 if self.cfg.solver == _abi.SOLVER_CERES_LM else 10) if max_iter is None else int(max_iter)
+        if ring_chain not in _abi.RING_CHAINS:
+            raise ValueError(f"ring_chain must be one of {sorted(_abi.RING_CHAINS)}, got {ring_chain!r}")
+        self.cfg.ring_chain = _abi.RING_CHAINS[ring_chain]
         self.n_rows = n_rows
         h = C.c_void_p()
         rc = _abi.lib().ssf_create(dev.index, C.byref(self.cfg), C.byref(h))
@@ -378,10 +384,21 @@ class Frontend:
         if (src is None) == (flow is None):
             raise SSFError("kabsch_f32: give exactly one of src / flow")
         mask = None if mask is None else self._dev(mask, torch.uint8)
+        off = self._dev(off, torch.int64)
         F = h_off.numel() - 1
+        if off.numel() != F + 1:
+            raise ValueError(f"off has {off.numel()} entries for {F} frames")
+        total = int(h_off[-1])
+        for name, t, per in (("dst", dst, 3), ("src", src, 3), ("flow", flow, 3), ("mask", mask, 1)):
+            if t is not None and t.numel() != per * total:
+                raise ValueError(f"{name} has {t.numel()} values for {total} points ({per} per point)")
         after = out is not None
         if out is None:
             out = torch.empty((max(F, 1), _abi.POSE_OUT_STRIDE), dtype=torch.float64, device=self.device)
+        else:
+            out = self._dev(out, torch.float64)
+            if out.dim() != 2 or out.shape[0] < F or out.shape[1] != _abi.POSE_OUT_STRIDE:
+                raise ValueError(f"out must be [>= {F}, {_abi.POSE_OUT_STRIDE}] float64, got {tuple(out.shape)}")
         rc = _abi.lib().ssf_kabsch_f32_batch(self._h, _stream(self.device), F, _ptr(src), _ptr(dst),
                                              _ptr(flow), _ptr(off), _ptr(mask), int(reflection),
                                              1 if after else 0, _ptr(out))

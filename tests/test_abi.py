@@ -30,9 +30,10 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_profiles():
     from ssf import _abi
     L = _abi.lib()
-    assert L.ssf_abi_version() == 1
+    assert L.ssf_abi_version() == 2
     c64 = _abi.config_default(64)
     assert (c64.n_rows, c64.plane_span, c64.row_start, c64.row_end, c64.max_iter) == (64, 25, 5, 5, 8)
+    assert c64.ring_chain == _abi.RING_CHAIN_FLOAT         # frameFeature.cpp:57 under libstdc++
     assert c64.plane_min == np.float32(0.005) and c64.plane_max == np.float32(0.05)
     c16 = _abi.config_default(16)
     assert (c16.plane_span, c16.row_start, c16.row_end) == (3, 0, 0)

@@ -124,12 +124,14 @@ def test_rows_across_curvature_tiles(oracle, dev, n_rows, n_az):
     _check_frame(oracle, fe, out, h_off, 1, c, n_rows)
 
 
+@pytest.mark.parametrize("chain", ["float", "double"])
 @pytest.mark.parametrize("n_rows", [16, 64])
-def test_ring_ids_near_bin_edges(oracle, dev, n_rows):
+def test_ring_ids_near_bin_edges(oracle, dev, n_rows, chain):
     """Elevations on and within 1e-6..1e-2 deg of every bin edge (and the -8.83 switch), plus a
-    uniform spread: the float-atan fast path of the ring id must fall back to the f64
-    expression wherever the two could disagree (src/frameFeature.cpp:57-72), so the binned
-    cloud is bit-identical to the oracle's."""
+    uniform spread, under both evaluations of src/frameFeature.cpp:57 (ssf_config.ring_chain:
+    the float overloads, the default, and the all-double chain): the table's fast ratio must
+    defer to the exact ratio wherever the two could disagree, so the binned cloud is
+    bit-identical to the oracle's under the same chain."""
     import ssf
     O = oracle
     if n_rows == 64:
@@ -148,13 +150,19 @@ def test_ring_ids_near_bin_edges(oracle, dev, n_rows):
     e = np.radians(el)
     pts = np.stack([rng_m * np.cos(e) * np.cos(az), rng_m * np.cos(e) * np.sin(az),
                     rng_m * np.sin(e)], 1).astype(np.float32)
-    fe = ssf.Frontend(n_rows, device=dev.index or 0)
+    fe = ssf.Frontend(n_rows, device=dev.index or 0, ring_chain=chain)
     out, h_off = _run(fe, [pts], dev)
     pb, ring, roff, curv = out
-    rx, off_ref, _, _ = O.bin_rings(pts, n_rows)
+    with O.ring_chain(chain):
+        rx, off_ref, _, rid = O.bin_rings(pts, n_rows)
     assert np.array_equal(roff[0].cpu().numpy().astype(np.int64), off_ref)
     kept = int(off_ref[-1])
     assert np.array_equal(ring[:kept].cpu().numpy(), rx), "ring-ordered cloud differs near bin edges"
+    other = [O.lib().orc_ring_id_chain(float(p[0]), float(p[1]), float(p[2]), n_rows,
+                                       O.RING_CHAINS["double" if chain == "float" else "float"]) for p in pts]
+    # the set holds points the two chains bin differently (64 rows: 25, 16 rows: 3), so a device
+    # that ignored ring_chain would fail one of the two parametrisations
+    assert np.count_nonzero(np.array(other) != rid) > 0
 
 
 def test_mask_before_features_equals_compacted_cloud(oracle, dev):
@@ -274,17 +282,19 @@ def test_product_path_equals_debug_path(oracle, dev):
         assert np.array_equal(got[1].view(np.uint32), oracle.extract_planes(c[: len(c) // 3], n_rows).view(np.uint32))
 
 
+@pytest.mark.parametrize("chain", ["float", "double"])
 @pytest.mark.parametrize("n_rows", [64, 16])
-def test_ring_id_table_edges(oracle, dev, n_rows):
+def test_ring_id_table_edges(oracle, dev, n_rows, chain):
     """The single-read stage's ring id (one table cell + one compare, features.hip
     ring_id_table) on the exact ratios where the reference's row id changes, +-3 ulps around each
-    (points (1, 0, ratio): z / sqrt(1) is the ratio itself), every cell edge, the origin (0/0) and
-    +-inf ratios: the ring-ordered cloud equals the oracle's (glibc atan, double angle chain), so
-    every point lands in the reference's row.  The points are shuffled and 64 copies of each are
-    interleaved, so every row holds enough points for full stencils as well."""
+    (points (1, 0, ratio): z / sqrt(1) is the ratio itself in both chains), every cell edge, the
+    origin (0/0) and +-inf ratios: the ring-ordered cloud equals the oracle's under the same
+    evaluation of frameFeature.cpp:57 (glibc atanf / atan), so every point lands in the
+    reference's row.  The points are shuffled and 64 copies of each are interleaved, so every
+    row holds enough points for full stencils as well."""
     import ssf
     import test_ring_table as rt
-    r0, inv, cells = rt.table(n_rows)
+    r0, inv, cells, _ = rt.table(n_rows, chain)
     probe = []
     for t in [t for t in cells["thr"] if np.isfinite(t)] + [np.float32(r0 + k / inv) for k in range(0, 257, 8)]:
         u = np.float32(t).view(np.int32)
@@ -294,10 +304,11 @@ def test_ring_id_table_edges(oracle, dev, n_rows):
     pts = np.concatenate([pts, [[0, 0, 0], [0, 0, 1], [0, 0, -1]]]).astype(np.float32)
     rng = np.random.default_rng(n_rows)
     cloud = np.concatenate([pts[rng.permutation(len(pts))] for _ in range(64)]).astype(np.float32)
-    fe = ssf.Frontend(n_rows, device=dev.index)
+    fe = ssf.Frontend(n_rows, device=dev.index, ring_chain=chain)
     out, h_off = _run(fe, [cloud], dev)
-    _check_frame(oracle, fe, out, h_off, 0, cloud, n_rows)
-    ids = np.array([oracle.lib().orc_ring_id(float(p[0]), float(p[1]), float(p[2]), n_rows) for p in pts])
+    with oracle.ring_chain(chain):
+        _check_frame(oracle, fe, out, h_off, 0, cloud, n_rows)
+        ids = np.array([oracle.lib().orc_ring_id(float(p[0]), float(p[1]), float(p[2]), n_rows) for p in pts])
     assert len(set(ids.tolist()) - {-1}) == n_rows         # every row is exercised
 
 

@@ -456,3 +456,46 @@ def test_plane_table_split_over_work_groups(oracle, dev):
         assert len(got) == len(ref), B
         for a, b in zip(got, ref):
             assert np.array_equal(a, b), B
+
+
+def test_plane_table_split_global_deferred_walk(oracle, dev):
+    """with the queries of one frame split over several work-groups, the
+    strip-walk tier's deferred queries read the sorted copy back from global memory
+    (table_deferred_walk: a full queue, or a query still undecided after the 6 m strips).  Every
+    share must read its OWN copy.  Frames that take that tier at B = 1 (8 shares): a sparse
+    frame whose 30-NN reach far beyond 6 m with ring codes the list-free pick cannot use
+    (negative intensities), and a 14-B SoA frame (9217..10624 points).  The caching allocator is
+    filled with NaN first so a read of unwritten memory cannot pass by luck.  Bit-exact vs the
+    oracle, and equal at B = 1 and B = 256."""
+    import ssf
+    rng = np.random.default_rng(11)
+    n = 2000
+    sparse = np.zeros((n, 4), np.float32)
+    sparse[:, 0] = rng.uniform(-150, 150, n)
+    sparse[:, 1] = rng.uniform(-150, 150, n)
+    sparse[:, 2] = rng.choice([-2.5, 0.0, 3.0], n) + rng.normal(0, 0.01, n)
+    sparse[:, 3] = -(rng.integers(0, 500, n) + rng.integers(0, 64, n) / 100.0)
+    base = np.concatenate([oracle.extract_planes(frame(s, 0, n_az=1875)[0], 64) for s in range(4)])
+    soa = base[rng.choice(len(base), 10000, replace=False)]
+    assert 9216 < len(soa) <= 10624
+    for P in (sparse, soa):
+        nr, vr, _, _ = oracle.plane_table(P, 0.05)
+        ref = None
+        for B in (1, 256):
+            junk = torch.full((64 << 20,), float("nan"), device=dev)   # poison the allocator's pool
+            del junk
+            fe = ssf.Frontend(64, device=dev.index or 0)
+            m = len(P)
+            xyzi = torch.from_numpy(np.tile(P.astype(np.float32), (B, 1))).to(dev)
+            off, h_off = ssf.frame_offsets([m] * B, dev)
+            pb = ssf.PlaneBatch(xyzi, torch.full((B,), m, dtype=torch.int32, device=dev), off, h_off, m)
+            normal, valid, sx, si = fe.plane_table(pb)
+            o = int(h_off[B - 1])
+            got = [normal[o:o + m].cpu().numpy().view(np.uint32), valid[o:o + m].cpu().numpy(),
+                   sx[o:o + m].cpu().numpy(), si[o:o + m].cpu().numpy()]
+            assert np.array_equal(got[0], nr.view(np.uint32)), (m, B, "normal bits differ")
+            assert np.array_equal(got[1], vr.astype(np.uint8)), (m, B)
+            if ref is None:
+                ref = got
+            for a, b in zip(got, ref):
+                assert np.array_equal(a, b), (m, B)

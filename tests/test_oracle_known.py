@@ -117,7 +117,9 @@ def test_oracle_register_on_synthetic_pair(oracle):
 
 # Upper-branch bin edges where `2 - angle` (frameFeature.cpp:66, int - float: a FLOAT
 # subtraction) rounds across the edge that the double expression would not cross.  The z values
-# put a point at x = 1, y = 0 exactly on those float angles (found by ulp search).
+# put a point at x = 1, y = 0 exactly on those float angles (found by ulp search; the double
+# chain of :57 lands on all three, the float chain on the first and third and on -1.5 for the
+# second -- the same row).
 UPPER_EDGE_CASES = [  # (z bits, float angle, row with float '2 - angle', row with double)
     (0x3C0EFB24, 0.5000000596046448, 5, 4),
     (-0x3CD683DB, -1.4999998807907104, 11, 10),
@@ -141,6 +143,8 @@ def test_ring_id_upper_branch_float_subtraction(oracle):
         assert int((2.0 - float(a32)) * 3.0 + 0.5) == row_d != row_f
         z = _f32_from_bits(zb)
         assert oracle.ring_ids(np.array([[1.0, 0.0, z]], np.float32), 64).tolist() == [row_f]
+        for chain in (oracle.RING_CHAIN_FLOAT, oracle.RING_CHAIN_DOUBLE):   # both evaluations of :57
+            assert oracle.lib().orc_ring_id_chain(1.0, 0.0, float(z), 64, chain) == row_f
 
 
 def test_xindex_knn_equals_brute_force(oracle):

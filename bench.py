@@ -51,7 +51,7 @@ F64_JSON = os.path.join(REPO, "profiles", "r04by_f64.json")
 METRIC = "LiDAR front-end frames/sec (mask+feature+GN), 64-beam 120k pts, 1/2/4/8 GPUs"
 
 
-def _load_profile(path, B, N, masked):
+def _load_profile(path, B, N, masked, layout="azimuth"):
     try:
         with open(path) as f:
             t = json.load(f)
@@ -59,7 +59,8 @@ def _load_profile(path, B, N, masked):
         return None
     cfg = t.get("config", {})
     if (cfg.get("sequences_per_gpu") != B or cfg.get("points_per_frame") != N
-            or bool(cfg.get("mask_before_features")) != bool(masked)):
+            or bool(cfg.get("mask_before_features")) != bool(masked)
+            or cfg.get("layout", "azimuth") != layout):
         return None
     return t
 
@@ -86,6 +87,10 @@ def parse(argv=None):
     ap.add_argument("--n-az", type=int, default=1875,
                     help="azimuth steps (64 x 1875 = 120k pts; 4000 -> 256k, BASELINE configs[4])")
     ap.add_argument("--rows", type=int, default=64)
+    ap.add_argument("--layout", default="azimuth", choices=["azimuth", "carla"],
+                    help="synthetic scan layout: azimuth-major, every ray returns (default), or the "
+                         "reference's own data layout (ssf/synth.py 'carla': channel-major, no-return "
+                         "rays and road points dropped, random drop-off to the same point count)")
     ap.add_argument("--solver", default="gn", choices=["gn", "ceres_lm"])
     ap.add_argument("--iters", type=int, default=None)
     ap.add_argument("--distinct", type=int, default=None,
@@ -151,6 +156,9 @@ def parse(argv=None):
                          "environment's, HIP's default 4). 8 measured the same as 4 over three "
                          "alternations (r04bq: 56.7 vs 56.6 k frames/s; 58.0 / 58.1 vs 55.4 / 57.2 k "
                          "in r04bp was box noise)")
+    ap.add_argument("--no-ring", dest="ring", action="store_false",
+                    help="allocate every step's plane cloud / plane table / mask outputs anew, with "
+                         "cross-stream record_stream (the pipeline before round 5; A/B of the ring)")
     ap.add_argument("--mask-streams", type=int, default=3,
                     help="mask launches of consecutive steps alternate over this many streams: the "
                          "GMM of a frame depends on no other frame, so a step's slow frames overlap "
@@ -241,14 +249,15 @@ def cpu_baseline(args):
     own third-party mask call (sklearn GaussianMixture) for the mask stage alone."""
     iters = args.iters or (10 if args.solver == "gn" else 8)
     extra = ["--rows", str(args.rows), "--n-az", str(args.n_az), "--solver", args.solver,
-             "--iters", str(iters)]
+             "--iters", str(iters), "--layout", args.layout]
     share = args.cpu_cores or _cpu_share()
     cpus, smt = _physical_cpus(share)
     cores = len(cpus)
     T = args.cpu_seconds
     single = _run_legs([("oracle", 0, extra)], T, cpus[:1])[0]
     many = _run_legs([("oracle", s, extra) for s in range(cores)], T, cpus)
-    skl = _run_legs([("sklearn", 0, ["--rows", str(args.rows), "--n-az", str(args.n_az)])], T)[0]
+    skl = _run_legs([("sklearn", 0, ["--rows", str(args.rows), "--n-az", str(args.n_az),
+                                     "--layout", args.layout])], T)[0]
     rate = lambda r: r["frames"] / r["seconds"] if r.get("seconds") else 0.0
     agg = sum(rate(r) for r in many)
     N = args.rows * args.n_az
@@ -285,7 +294,7 @@ def make_data(args, dev, n_frames, rank, batch=None):
     S = max(1, min(args.distinct or B, B))
     N = args.rows * args.n_az
     scanner = synth.BatchScanner([rank * 100000 + (b % S) for b in range(B)], n_frames,
-                                 n_rows=args.rows, n_az=args.n_az, device=dev)
+                                 n_rows=args.rows, n_az=args.n_az, device=dev, layout=args.layout)
     out = []
     for k in range(n_frames):
         pos = torch.empty((B * N, 3), dtype=torch.float32, device=dev)
@@ -329,10 +338,38 @@ class Pipeline:
         self.pose_abs = ssf.identity_poses(B, dev)
         self.last = self.last_table = None
         self.last_e = self.last_etable = None
+        # round 5: a ring of per-step output buffers (plane cloud, plane table, background mask),
+        # allocated once (in the warmup) instead of ~2 GB of allocations per step with
+        # cross-stream record_stream; slot k % RING is written by step k and read by the
+        # registrations of steps k and k + 1, so step k waits for the registration of step
+        # k + 2 - RING before it overwrites the slot
+        self.ring, self.reg_done, self.feat_done = [], {}, {}
+        if args.ring:
+            self.slot(self.RING - 1)                          # every slot now, not in the timed region
         self.records = []           # per timed step: the pose record this rank contributed
         self.gathered = []          # per timed step: the all-gathered records of every rank
         self.snaps = []             # (pose snapshot on s_reg, mask out, its streams) until exchange()
         self.ev = {k: [] for k in ("mask", "feat", "table", "reg")}
+
+    RING = 4
+
+    def slot(self, k):
+        import torch
+        i = k % self.RING
+        while len(self.ring) <= i:
+            B, N, d = self.B, self.N, self.dev
+            T = B * N
+            self.ring.append(dict(
+                bg=torch.empty(T, dtype=torch.uint8, device=d),
+                plane=torch.empty((T, 4), dtype=torch.float32, device=d),
+                count=torch.empty(B, dtype=torch.int32, device=d),
+                table=(torch.empty((T, 3), dtype=torch.float32, device=d),
+                       torch.empty(T, dtype=torch.uint8, device=d),
+                       torch.empty((T, 4), dtype=torch.float32, device=d),
+                       torch.empty(T, dtype=torch.int32, device=d),
+                       torch.empty((T, 4), dtype=torch.float32, device=d),
+                       torch.empty(T, dtype=torch.int32, device=d))))
+        return self.ring[i]
 
     def contexts(self):
         return [self.fe_mask, self.fe_feat] + ([self.fe_reg] if self.fe_reg is not self.fe_feat else [])
@@ -344,16 +381,29 @@ class Pipeline:
         mpos, mflow = batches[k][2:4] if len(batches[k]) == 4 else (pos, flow)   # --f64-inputs
         s_mask, s_feat, s_reg = streams or (self.s_masks[k % len(self.s_masks)], self.s_feat, self.s_reg)
         mk = lambda: torch.cuda.Event(enable_timing=True)
+        # the kernel pass allocates its own; --no-ring: the per-step allocations before round 5
+        ring = self.slot(k) if streams is None and a.ring else None
+        if ring is not None:
+            # the slot's previous readers: the features (mask before features) of step k - RING,
+            # the registrations of steps k - RING and k + 1 - RING
+            if a.mask_before_features and (k - self.RING) in self.feat_done:
+                s_mask.wait_event(self.feat_done.pop(k - self.RING))
+            if (k + 1 - self.RING) in self.reg_done:
+                s_feat.wait_event(self.reg_done.pop(k + 1 - self.RING))
         with torch.cuda.stream(s_mask):
             m0, m1 = mk(), mk()
             m0.record(s_mask)
-            out, bg = self.fe_mask.mask_pose(mpos, mflow, off, h_off, mode="gmm", want_mask=True)
+            out, bg = self.fe_mask.mask_pose(mpos, mflow, off, h_off, mode="gmm", want_mask=True,
+                                             out=None if ring is None else (
+                                                 torch.empty((self.B, 32), dtype=torch.float64, device=self.dev),
+                                                 ring["bg"]))
             m1.record(s_mask)
         keep = None
         if a.mask_before_features:          # configs[2]: the features wait for the mask
             if s_feat is not s_mask:
                 s_feat.wait_event(m1)
-                bg.record_stream(s_feat)
+                if ring is None:
+                    bg.record_stream(s_feat)
             keep = bg
         eb = etable = None
         with torch.cuda.stream(s_feat):
@@ -362,9 +412,10 @@ class Pipeline:
             if a.edges:                     # beyond the reference: edge features as well
                 pb, eb = self.fe_feat.extract_features_batch(pos, off, h_off, max_points=self.N, keep=keep)
             else:
-                pb = self.fe_feat.extract_planes_batch(pos, off, h_off, max_points=self.N, keep=keep)
+                pb = self.fe_feat.extract_planes_batch(pos, off, h_off, max_points=self.N, keep=keep,
+                                                       out=None if ring is None else (ring["plane"], ring["count"]))
             es[1].record(s_feat)
-            table = self.fe_feat.plane_table(pb)
+            table = self.fe_feat.plane_table(pb, out=None if ring is None or a.edges else ring["table"])
             if a.edges:
                 etable = self.fe_feat.edge_table(eb)
             es[2].record(s_feat)
@@ -376,8 +427,9 @@ class Pipeline:
             # the plane batch and its table are read on s_reg in this step and the next: keep
             # the caching allocator from handing their blocks to s_feat until s_reg is done
             extra = (eb.xyzi, eb.count, *etable) if a.edges else ()
-            for t in (pb.xyzi, pb.count, *table.tensors(), *extra):
-                t.record_stream(s_reg)
+            if ring is None or a.edges:     # ring buffers are guarded by the events above instead
+                for t in (pb.xyzi, pb.count, *table.tensors(), *extra):
+                    t.record_stream(s_reg)
         stats = None
         with torch.cuda.stream(s_reg):
             r0, r1 = mk(), mk()
@@ -390,6 +442,10 @@ class Pipeline:
                     stats = (res["ncorr"], res["nlog"])
             r1.record(s_reg)
             snap = self.pose_abs.clone() if self.world > 1 else None   # step-k poses, on s_reg
+        if ring is not None:
+            self.reg_done[k] = r1
+            if a.mask_before_features:
+                self.feat_done[k] = es[1]
         self.last, self.last_table = pb, table
         self.last_e, self.last_etable = eb, etable
         if self.world > 1 and timing:   # for the deferred exchange (exchange()): no per-step wait
@@ -469,7 +525,7 @@ def kernel_pass(pipe, batches, off, h_off, ks, rows, row_start, row_end):
     return times, acc
 
 
-def rooflines(times, acc, B, N):
+def rooflines(times, acc, B, N, layout="azimuth"):
     """{kernel: launches, ms per launch, algorithmic bytes per launch, GB/s, fraction of HBM
     peak}.  The byte totals cover exactly the launches the pass profiled (features, table and
     mask: every pass step; association and solve: the steps that had a last frame)."""
@@ -514,6 +570,16 @@ def rooflines(times, acc, B, N):
         model.pop("k_feat_chunk", None)
         # select reads the lane maps (and flags) and no u16 positions
         model["k_feat_select"] = 833.0 * acc["chunks"] + 28.0 * acc["plane"]
+    if layout == "carla":
+        # round 5, the reference's own layout (channel-major runs): k_feat_wave_run does the chunks
+        # -- xyz read once (12 B), per chunk its row counts (256 B), two bit planes (512 B), the
+        # rows' u16 run starts (128 B) and its flag -- after k_feat_wave_reg's probe, which reads
+        # one 64-point column per chunk (768 B) and leaves; k_feat_select reads the run start of a
+        # plane point's (chunk, row) (2 B) instead of a lane map
+        model["k_feat_wave_run"] = 12.0 * acc["points"] + 897.0 * acc["chunks"]
+        model["k_feat_wave_reg"] = 768.0 * acc["chunks"]
+        model.pop("k_feat_chunk", None)
+        model["k_feat_select"] = 897.0 * acc["chunks"] + 30.0 * acc["plane"]
     out = {}
     for name, (n, ms) in sorted(times.items(), key=lambda kv: -kv[1][1]):
         d = dict(launches=n, ms=ms / n)
@@ -528,7 +594,7 @@ def rooflines(times, acc, B, N):
                               evaluations_per_pair=acc["corr_evals"] / max(1, acc["corr"]),
                               note="corr = valid correspondences counted on device (ncorr); "
                                    "evaluations = 1 + logged iterations (nlog)")
-    for k in ("k_bin_curv", "k_feat_chunk", "k_feat_chunk_reg", "k_feat_wave_reg"):
+    for k in ("k_bin_curv", "k_feat_chunk", "k_feat_chunk_reg", "k_feat_wave_reg", "k_feat_wave_run"):
         if k in out:
             out[k]["kept_points_per_launch"] = acc["kept"] / out[k]["launches"]
     return out, passes
@@ -730,7 +796,8 @@ def sequences(args, world=1, rank=0, local=0):
     t_data = time.perf_counter()
     # frame 0 of every sequence (the prologue), then per step K frames, frame-major:
     # buffer index kk * B + b holds frame j K + kk + 1 of sequence b
-    scanner = synth.BatchScanner(seeds, K * n_steps + 1, n_rows=args.rows, n_az=args.n_az, device=dev)
+    scanner = synth.BatchScanner(seeds, K * n_steps + 1, n_rows=args.rows, n_az=args.n_az, device=dev,
+                                 layout=args.layout)
     pro = (torch.empty((B * N, 3), dtype=torch.float32, device=dev),
            torch.empty((B * N, 3), dtype=torch.float32, device=dev))
     scanner.frame(0, *pro)
@@ -1038,6 +1105,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    mem0 = torch.cuda.memory_stats(dev)
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
         pipe.step(k, batches, off, h_off, True)
@@ -1048,6 +1116,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    mem1 = torch.cuda.memory_stats(dev)
+    # the caching allocator inside the timed region: device allocations (hipMalloc) and retries
+    # (a retry frees cached blocks and synchronises the device) -- both 0 with the buffer ring
+    allocator = {k: int(mem1.get(k, 0)) - int(mem0.get(k, 0))
+                 for k in ("num_alloc_retries", "num_device_alloc", "num_device_free", "num_ooms")}
     if args.dump_poses and rank == 0:
         np.save(args.dump_poses, pipe.pose_abs.cpu().numpy())
     gather_ok = None
@@ -1073,7 +1146,7 @@ def main():
     if args.kernel_pass > 0:
         cfg = pipe.fe_feat.cfg
         times, acc = kernel_pass(pipe, batches, off, h_off, ks, args.rows, cfg.row_start, cfg.row_end)
-        kernels, passes = rooflines(times, acc, B, N)
+        kernels, passes = rooflines(times, acc, B, N, args.layout)
 
     total_frames = B * args.steps * world
     value = total_frames / elapsed
@@ -1087,7 +1160,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f32 features / f64 mask+solve",
-        "data": f"synthetic (seeded ray-cast 64-beam scans, ssf/synth.py; "
+        "data": f"synthetic (seeded ray-cast 64-beam scans, ssf/synth.py, layout {args.layout}; "
                 f"{min(args.distinct or B, B)} distinct sequences per rank)",
         "config": {"workload": f"{cfg_name}: {B} sequences in flight per GPU x {args.rows}-beam "
                                f"{N}-pt scans; mask(GMM+Kabsch) + "
@@ -1095,6 +1168,7 @@ def main():
                                f"table + {'edge table + point-to-line + ' if args.edges else ''}"
                                f"{args.solver} x{iters}",
                    "sequences_per_gpu": B, "points_per_frame": N, "solver": args.solver,
+                   "layout": args.layout,
                    "iters": iters, "mask_before_features": bool(args.mask_before_features),
                    "edges": bool(args.edges),
                    "parallelism": f"sequence-sharded x{world}",
@@ -1105,12 +1179,13 @@ def main():
         "roofline": None, "cpu_baseline": cpu,
         "kernels": kernels, "overlapped_event_ms": overlapped,
         "mask_passes_per_frame": passes, "gather_check": gather_ok,
+        "allocator_timed_region": allocator,
         "data_gen_s": round(t_data, 2), "lib_sha16": None,
     }
     if args.f64_inputs:
         line["config"]["mask_inputs"] = "float64 pos / flow (ssf_mask_pose_batch_f64), float32 features"
         line["dtype"] = "f32 features / f64 mask inputs + f64 mask+solve"
-    traffic = None if args.edges else _load_profile(TRAFFIC_JSON, B, N, args.mask_before_features)
+    traffic = None if args.edges else _load_profile(TRAFFIC_JSON, B, N, args.mask_before_features, args.layout)
     lib_sha = _lib_sha16()
     tsrc = None
     if traffic:
@@ -1143,7 +1218,7 @@ def main():
                             "kernel": mk_name,
                             "duration": "kernel-only (one-stream kernel pass, HIP events)",
                             **({k: v for k, v in tsrc.items()} if tsrc and mk.get("traffic") else {})}
-        f64 = None if args.edges else _load_profile(F64_JSON, B, N, args.mask_before_features)
+        f64 = None if args.edges else _load_profile(F64_JSON, B, N, args.mask_before_features, args.layout)
         flops = f64 and f64.get("f64_flops_per_launch")
         if flops:
             tf = flops / (mk["ms"] * 1e-3) / 1e12
@@ -1164,7 +1239,8 @@ def main():
         tb = sum(v["traffic"] for v in kernels.values() if v.get("traffic"))
         if tb:
             line["roofline_step"].update(traffic_per_step=tb, traffic_frac=tb / st / 1e9 / HBM_PEAK_GBS)
-    ns = {k: kernels[k]["frac"] for k in ("k_feat_wave_reg", "k_feat_chunk_reg", "k_feat_chunk", "k_bin_curv", "k_solve") if k in kernels and "frac" in kernels[k]}
+    curv_k = ("k_feat_wave_run",) if args.layout == "carla" else ("k_feat_wave_reg", "k_feat_chunk_reg", "k_feat_chunk", "k_bin_curv")
+    ns = {k: kernels[k]["frac"] for k in (*curv_k, "k_solve") if k in kernels and "frac" in kernels[k]}
     if ns:
         line["north_star_kernels_hbm_frac"] = ns
         meas = {k: kernels[k]["traffic_frac"] for k in ns if "traffic_frac" in kernels[k]}

@@ -28,14 +28,14 @@ for p in (os.path.join(REPO, "ssf-slam_amd"), REPO):
         sys.path.insert(0, p)
 
 
-def _frames(seq, rows, n_az, n):
+def _frames(seq, rows, n_az, n, layout="azimuth"):
     import torch
     torch.set_num_threads(1)
     from ssf import synth
     sc = synth.Scene(seq)
     out = []
     for k in range(n):
-        f = synth.scan(seq, k, n_rows=rows, n_az=n_az, scene=sc)
+        f = synth.scan(seq, k, n_rows=rows, n_az=n_az, scene=sc, layout=layout)
         out.append((f["pos1"].numpy(), f["flow"].numpy()))
     return out
 
@@ -44,7 +44,7 @@ def leg_oracle(a):
     import numpy as np
     from oracle import oracle as O
     O.lib()
-    fr = _frames(a.seq, a.rows, a.n_az, 4)
+    fr = _frames(a.seq, a.rows, a.n_az, 4, a.layout)
     prof = O.profile(a.rows)
     mode = O.MODE_GN if a.solver == "gn" else O.MODE_CERES_LM
     last = O.extract_planes(fr[0][0], a.rows)
@@ -82,7 +82,7 @@ def leg_sklearn(a):
         import sklearn
     except ImportError as e:                       # not installed on this host
         return dict(frames=0, seconds=0.0, skipped=str(e))
-    fr = _frames(a.seq, a.rows, a.n_az, 2)
+    fr = _frames(a.seq, a.rows, a.n_az, 2, a.layout)
     done = 0
     t0 = time.perf_counter()
     while True:
@@ -108,6 +108,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=8.0)
     ap.add_argument("--rows", type=int, default=64)
     ap.add_argument("--n-az", type=int, default=1875)
+    ap.add_argument("--layout", default="azimuth", choices=["azimuth", "carla"])
     ap.add_argument("--solver", default="gn")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--cpu", type=int, default=None, help="pin this process to one CPU")

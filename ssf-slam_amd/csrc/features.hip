@@ -722,6 +722,13 @@ constexpr int kFeatMaxChunks = 128;              // 262144 points per frame (k_f
 constexpr int kFeatPlanes = 3;                   // planar candidate, unresolved, edge candidate
 constexpr int kFeatWords = kBinChunk / 64;       // 64-bit words per plane and chunk
 constexpr uint8_t kFlP = 1, kFlU = 2, kFlE = 4;
+// per (frame, chunk) block flag of the single-read stage: which kernel did the chunk and where
+// k_feat_select finds a selected point's chunk position
+//   kIrrRegular  k_feat_wave_reg / k_feat_chunk_reg: 64 x own column + the row's lane (lane map)
+//   kIrrGeneral  not done yet -> k_feat_chunk_flagged, which writes the u16 position of every slot
+//   kIrrRun      k_feat_wave_run: the row's run start (u16 at the chunk's first 64 index entries) + o
+//   kIrrRunIdx   k_feat_wave_run with the debug outputs: the u16 position of every slot
+constexpr uint8_t kIrrRegular = 0, kIrrGeneral = 1, kIrrRun = 2, kIrrRunIdx = 3;
 static_assert(kCurvSub == 1 && kBinChunk == 2048, "own-tile slots and chunk positions use 11 bits");
 
 // u16 index base of frame f: 64-entry aligned, frames disjoint with a gap of >= 33 entries (the
@@ -1078,7 +1085,7 @@ __global__ __launch_bounds__(kCurvNT, SSF_FEAT_WAVES) void k_feat_chunk_flagged(
     uint32_t m = 0;
     const uint32_t wd[4] = {fw.x, fw.y, fw.z, fw.w};
 #pragma unroll
-    for (int k = 0; k < kFlagGroup; ++k) m |= (uint32_t)(((wd[k >> 2] >> (8 * (k & 3))) & 0xffu) != 0u) << k;
+    for (int k = 0; k < kFlagGroup; ++k) m |= (uint32_t)(((wd[k >> 2] >> (8 * (k & 3))) & 0xffu) == kIrrGeneral) << k;
     while (m) {                                               // uniform
         const int k = __builtin_ctz(m);
         m &= m - 1u;
@@ -1394,12 +1401,13 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
     // share are loaded by both at the same end of their streams, close in time (an L2 hit for the
     // later one: streaming both ways from the left, the right neighbour's copy had left the L2).
     constexpr int nb = kWaveOwn / kWB;
-    auto stream = [&](auto rev) {
+    auto stream = [&](auto rev) -> bool {
         constexpr bool R = decltype(rev)::value;
         constexpr int kf = R ? kWaveCols - 6 : 5;              // an own column of the first window
         constexpr int f0 = R ? kWB * (nb - 1) : 0;             // the first window [f0, f0 + kWB + 10)
-#pragma unroll
-        for (int k = f0; k < f0 + kWB + 10; ++k) load_col(k);
+        // that column first: a chunk whose first column is not one row per lane (any other layout,
+        // e.g. channel-major CARLA sweeps) leaves before the other 41 columns are read
+        load_col(kf);
         // the lane's row from that column (a clamped load is still a real column, and every real
         // column is checked below): ring_id_table's test with the cells from lane permutes (the
         // exact ratio's cell fetched for every lane, used where the fast one is near)
@@ -1439,6 +1447,11 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
         rows = 1ull << row;                                    // every row once per column
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) rows |= __shfl_xor(rows, o, 64);
+        if (rows != ~0ull || !__all(mine >= 0 && mine < kMaxRows)) return false;   // uniform
+        asm volatile("" ::: "memory");                         // no column load above the probe
+#pragma unroll
+        for (int k = f0; k < f0 + kWB + 10; ++k)
+            if (k != kf) load_col(k);
         row_in = row >= row_start && row < n_rows - row_end;
 #pragma unroll
         for (int k = f0; k < f0 + kWB + 10; ++k) check_col(k);
@@ -1481,9 +1494,13 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
                 for (int k = n0; k < n0 + kWB; ++k) check_col(k);
             }
         }
+        return true;
     };
-    if (c & 1) stream(std::true_type{});                      // uniform
-    else stream(std::false_type{});
+    const bool probed = (c & 1) ? stream(std::true_type{}) : stream(std::false_type{});   // uniform
+    if (!probed) {                                            // not one row per lane: not regular
+        if (lane == 0) irregular[lb] = kIrrGeneral;
+        return;
+    }
     const bool ok = mine >= 0 && mine < kMaxRows && (inb & need) == need && rows == ~0ull;
     if (!__all(ok)) {                                         // uniform: the general kernel's chunk
         if (lane == 0) irregular[lb] = 1;
@@ -1515,6 +1532,363 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
     cnt[((int64_t)f * (n_chunks + 1) + c) * kMaxRows + lane] = oc;
     lanemap[lb * kMaxRows + row] = (uint8_t)lane;
     if (lane == 0) irregular[lb] = 0;
+}
+
+// k_feat_wave_run: the single-read feature stage for chunks whose rows come as RUNS of consecutive
+// inputs -- the layout of the reference's own data: a CARLA sweep is stored channel-major (every
+// return of a channel in azimuth order, then the next channel), with the no-return rays and the
+// road dropped (launch/run_noSeg.launch:4 reads a road-removed set; Scenario_Traj.py:307-315),
+// so rows are ragged and no column holds one point per row.  A stencil (frameFeature.cpp:84-107)
+// whose 11 taps are 11 CONSECUTIVE INPUTS of one row is exactly the reference's, whatever the rest
+// of the frame holds: consecutive inputs of a row are consecutive in its ring order (:73-80).  So
+// ONE WAVE per 2048-point chunk streams the chunk as 64-lane registers (lane l of register k =
+// input s - 5 + 54k + l: 54 centres and 5 halo lanes each side; coalesced 768-B loads) and
+// evaluates the stencil ALONG THE LANES: each of the reference's left-to-right additions is one
+// v_add_f32 whose first operand is the partial sum one lane down (DPP wave_shr:1, free inside the
+// instruction), so centre i's sum arrives in lane i + 5 after 11 dependent operations per
+// coordinate, with tap11's roundings in tap11's order (lane_tap11x3).  Row ids: the fast ratio
+// against the current row's interval (as k_feat_wave_reg's check); a register wholly inside it is
+// one row, any other takes the table lookup where the check fails.  A centre is covered when its
+// 10 neighbours share its row (a 10-bit window of one ballot); an own point of a row in range that
+// is not covered is unresolved (row end or open stencil: k_feat_select decides it).  The chunk's
+// runs (and gaps of points in no row) are logged in input order as they start.  Own-tile slots
+// need each row to be at most one run in the chunk (slot = the row's base + the point's offset in
+// its run): the bit planes are built in input order and moved run by run to slot order (nothing
+// moves for runs in ascending row order without gaps), and k_feat_select finds a point at its
+// row's run start (u16, the chunk's first 64 index entries) + its offset.  A chunk with a row in
+// two runs, or more than kRunMax runs, is left to k_feat_chunk (kIrrGeneral).
+#ifndef SSF_FEAT_WAVE_RUN
+#define SSF_FEAT_WAVE_RUN 1                      // k_feat_wave_run for the non-regular chunks (A/B: 0)
+#endif
+#ifndef SSF_FEAT_RUN_WAVES
+#define SSF_FEAT_RUN_WAVES 8                     // k_feat_wave_run waves per SIMD (launch bound)
+#endif
+constexpr int kRunStep = 54;                     // new centres per 64-lane register
+constexpr int kRunMax = 64;                      // runs (and gaps) logged per chunk
+#ifndef SSF_FEAT_RUN_PF
+#define SSF_FEAT_RUN_PF 4                        // registers in flight per wave
+#endif
+constexpr int kRunPF = SSF_FEAT_RUN_PF;
+
+SSF_DEV float dpp_shr1(float v) {                // lane l <- lane l - 1 (lane 0 <- 0)
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
+}
+SSF_DEV int dpp_shr1i(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true); }
+
+// tap11 along the lanes (see k_feat_wave_run), for x, y and z: lane L gets the sum of the centre in lane L - 5
+// (valid for 10 <= L < 64).  P = x[l-1] + x[l]; three more `+ x` on the sum one lane down give
+// x[l-4] + .. + x[l]; one lane down again `- 10 x[l]` is tap11's left half and centre; then five
+// `+ x` on the sum one lane down add x[i+1] .. x[i+5] in order, the sum moving one lane each time.
+// The three coordinates' chains step by step side by side: a DPP operand must not be read in the
+// two cycles after the VALU op that wrote it, so one chain alone pays an s_nop per step.
+SSF_DEV void lane_tap11x3(float x, float y, float z, float& dx, float& dy, float& dz) {
+    float px = dpp_shr1(x) + x, py = dpp_shr1(y) + y, pz = dpp_shr1(z) + z;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+        px = dpp_shr1(px) + x;
+        py = dpp_shr1(py) + y;
+        pz = dpp_shr1(pz) + z;
+    }
+    const float tx = 10.0f * x, ty = 10.0f * y, tz = 10.0f * z;
+    px = dpp_shr1(px) - tx;
+    py = dpp_shr1(py) - ty;
+    pz = dpp_shr1(pz) - tz;
+#pragma unroll
+    for (int m = 0; m < 5; ++m) {
+        px = dpp_shr1(px) + x;
+        py = dpp_shr1(py) + y;
+        pz = dpp_shr1(pz) + z;
+    }
+    dx = px; dy = py; dz = pz;
+}
+
+// bits [a, a + n) of a bit array of nw words as the low bits (0 < n <= 64)
+SSF_DEV uint64_t bits_at(const unsigned long long* W, int a, int n, int nw) {
+    const int wi = a >> 6, sh = a & 63;
+    uint64_t v = W[wi] >> sh;
+    if (sh && wi + 1 < nw) v |= (uint64_t)W[wi + 1] << (64 - sh);
+    return n >= 64 ? v : (v & ((1ull << n) - 1ull));
+}
+
+template <bool kDebug, bool kEdge>
+__global__ __launch_bounds__(kCurvNT, kDebug ? 2 : SSF_FEAT_RUN_WAVES) void k_feat_wave_run(
+    const float* __restrict__ pts, int stride, const int64_t* __restrict__ frame_off, int n_frames,
+    int n_rows, int n_chunks, int row_start, int row_end, float plane_min, float edge_min,
+    const uint8_t* __restrict__ keep, const RingTable* __restrict__ rtab, int32_t* __restrict__ cnt,
+    uint16_t* __restrict__ gidx, uint64_t* __restrict__ gbits, float* __restrict__ curv_cm,
+    uint8_t* __restrict__ irregular, int all) {
+    constexpr int kPl = kEdge ? 3 : 2;
+    constexpr int kPW = kFeatPlanes * kFeatWords;
+    __shared__ unsigned long long wpos[kCurvNW][kPW];    // the flags in input order
+    __shared__ unsigned long long wslt[kCurvNW][kPW];    // ... in own-tile slot order
+    __shared__ int2 wrun[kCurvNW][kRunMax];              // (row or -1 for a gap, first own position)
+    __shared__ int wlen[kCurvNW][kMaxRows];              // own points per row
+    __shared__ int wnum[kCurvNW][kMaxRows];              // runs per row
+    __shared__ int wst[kCurvNW][kMaxRows];               // run start per row
+    __shared__ float wcv[kDebug ? kCurvNW : 1][kDebug ? kBinChunk : 1];   // debug: curvature, input order
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t nblk = (int64_t)n_chunks * n_frames;
+    const int64_t nwg = (nblk + kCurvNW - 1) / kCurvNW;       // XCD-aware logical work-group
+    const int64_t q8 = (nwg + 7) / 8;
+    const int64_t lw = (int64_t)(blockIdx.x % 8) * q8 + blockIdx.x / 8;
+    const int64_t lb = lw * kCurvNW + w;                      // this wave's (frame, chunk)
+    if (lw >= nwg || lb >= nblk) return;                      // uniform per wave (no barrier below)
+    if (!all && irregular[lb] != kIrrGeneral) return;          // uniform: a regular chunk, done
+    const int f = (int)(lb / n_chunks), c = (int)(lb - (int64_t)f * n_chunks);
+    const int64_t fb = frame_off[f], e = frame_off[f + 1];
+    const int64_t s = fb + (int64_t)c * kBinChunk;
+    if (s >= e) {                                             // uniform: no chunk here at all
+        if (lane == 0) irregular[lb] = kIrrRegular;
+        return;
+    }
+    const int nf = (int)(e - fb);
+    const int len = (int)(min(e, s + (int64_t)kBinChunk) - s);
+    const int nreg = (len + kRunStep - 1) / kRunStep;         // registers with own centres
+    const int q0 = (int)(s - fb) - 5;                         // frame index of register 0, lane 0
+    for (int k = lane; k < kPW; k += 64) { wpos[w][k] = 0ull; wslt[w][k] = 0ull; }
+    wlen[w][lane] = 0;
+    wnum[w][lane] = 0;
+    const float r0 = rtab->r0, rinv = rtab->inv;
+    const int rlim = n_rows - row_end;
+    // the wave's current row and its fast-ratio bounds, margins in (k_feat_wave_reg's check)
+    int g = -1;
+    float glo = INFINITY, ghi = -INFINITY;
+    bool gin_row = false;                                     // g is a row in range
+    // a register's points: frame index q = q0 + 54 k + lane through a buffer resource over the
+    // frame's points: a lane outside the frame (q < 0 wraps) reads zeros from the range check and
+    // is marked by INF (lanes [lo, hi) of the register are in the frame), so no clamp, no 64-bit
+    // address per load: one add per register
+    typedef int i3v __attribute__((ext_vector_type(3)));
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(pts + fb * stride), (short)0, nf * stride * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(keep ? keep + fb : keep), (short)0, keep ? nf : 0, 0x00020000);
+    const uint32_t sb = (uint32_t)stride * 4u;
+    const uint32_t voff0 = (uint32_t)(q0 + lane) * sb, vstep = (uint32_t)kRunStep * sb;
+    auto load_reg = [&](int k, float& x, float& y, float& z, uint32_t& kp) {
+        const i3v v = __builtin_amdgcn_raw_buffer_load_b96(prs, voff0 + (uint32_t)k * vstep, 0, 0);
+        x = __int_as_float(v.x); y = __int_as_float(v.y); z = __int_as_float(v.z);
+        kp = keep ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(krs, (uint32_t)(q0 + lane + kRunStep * k), 0, 0) : 1u;
+    };
+    auto lane_range = [](int lo, int hi) -> uint64_t {        // lanes [lo, hi) as a mask (0 <= lo, hi <= 64)
+        if (hi <= lo) return 0ull;
+        const uint64_t up = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+        return up & (~0ull << lo);
+    };
+    int nrun = 0;
+    // the flag masks of register k (bits 0 .. 53: own positions 54 k .. 54 k + 53) go to lane k
+    // of these VGPRs (v_writelane: no SALU, no LDS), and become the input-order words after the
+    // loop.  The scalar unit is the one all 32 waves of a CU share: the steady state below keeps
+    // it to a few instructions per register (SQ counters, r5e: 2.8 k SALU per chunk saturated it).
+    uint32_t vPl = 0, vPh = 0, vUl = 0, vUh = 0, vEl = 0, vEh = 0;
+    auto wl = [](uint32_t& dst, uint32_t val, int k) {        // lane k of dst <- val (uniform)
+        asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(dst) : "s"(val), "s"(k) : "m0");
+    };
+    auto put = [&](int k, uint64_t mP, uint64_t mE) {
+        wl(vPl, (uint32_t)mP, k);
+        wl(vPh, (uint32_t)(mP >> 32), k);
+        if (kEdge) {
+            wl(vEl, (uint32_t)mE, k);
+            wl(vEh, (uint32_t)(mE >> 32), k);
+        }
+    };
+    // registers 1 .. kint: every lane in the frame, 54 own centres, no keep mask ("interior")
+    const int kint = keep ? 0 : min((nf - 64 - q0) / kRunStep, len / kRunStep - 1);
+    // one register's work (k: register, c*: its points); false when the chunk has too many runs
+    auto reg = [&](int k, float cx, float cy, float cz, uint32_t ck) -> bool {
+        const float r2 = cx * cx + cy * cy;
+        const float ra = cz * __builtin_amdgcn_rsqf(r2);
+        // (no upper bound on r2 needed: r2 = +inf gives ra = 0 = the exact z / sqrtf(inf); the
+        // lower one keeps zero and denormal r2 off the fast path)
+        const uint64_t INR = __builtin_amdgcn_ballot_w64(ra >= glo) & __builtin_amdgcn_ballot_w64(ra < ghi) &
+                             __builtin_amdgcn_ballot_w64(r2 > 1e-30f);
+        if (k >= 1 && k <= kint && INR == ~0ull) {           // uniform: an interior register, all row g
+            float dx, dy, dz;
+            lane_tap11x3(cx, cy, cz, dx, dy, dz);
+            float v = dx * dx + dy * dy;                      // ((dX dX + dY dY) + dZ dZ)
+            v = v + dz * dz;
+            const uint64_t R = gin_row ? ~0x3FFull : 0ull;    // own, row in range, covered
+            const uint64_t mP = (R & __builtin_amdgcn_ballot_w64(v < plane_min)) >> 10;
+            const uint64_t mE = kEdge ? ((R & __builtin_amdgcn_ballot_w64(v > edge_min)) >> 10) : 0ull;
+            put(k, mP, mE);                                   // nothing unresolved (lanes k of vU stay 0)
+            if (kDebug && lane >= 10) wcv[kDebug ? w : 0][kRunStep * k + lane - 10] = gin_row ? v : 0.0f;
+            return true;
+        }
+        const int q = q0 + kRunStep * k;                      // frame index of lane 0 (uniform)
+        const uint64_t INF = lane_range(max(0, -q), min(64, nf - q));
+        const uint64_t OK = keep ? (INF & __builtin_amdgcn_ballot_w64(ck != 0u)) : INF;
+        const uint64_t IN = OK & INR;
+        const bool uni = IN == ~0ull;                         // the whole register is row g
+        int id = g;
+        if (!uni) {
+            const bool in = (IN >> lane) & 1ull, ok = (OK >> lane) & 1ull;
+            if (!in) id = ok ? ring_id_table(cx, cy, cz, r0, rinv, rtab->cell, rtab) : -1;
+            const int last = __builtin_amdgcn_readlane(id, 63);
+            if (last >= 0 && last != g) {                     // uniform: follow the last lane's row
+                g = last;
+                const float lo = rtab->rlo[g], hi = rtab->rhi[g];
+                const float m = 1e-6f * fmaxf(1.0f, fmaxf(fabsf(lo), fabsf(hi)));
+                glo = lo + m;
+                ghi = hi - m;
+                gin_row = g >= row_start && g < rlim;
+            }
+        }
+        float dx, dy, dz;
+        lane_tap11x3(cx, cy, cz, dx, dy, dz);
+        float v = dx * dx + dy * dy;                          // ((dX dX + dY dY) + dZ dZ)
+        v = v + dz * dz;
+        // lane L >= 10: the centre in lane L - 5, own position a0 + L - 10
+        const int a0 = kRunStep * k;
+        const int nown = min(kRunStep, len - a0);             // >= 1
+        const uint64_t OWN = lane_range(10, 10 + nown);
+        uint64_t COV, ROWIN;
+        if (uni) {                                            // from the wave's row g (SGPRs)
+            COV = ~0ull;
+            ROWIN = gin_row ? ~0ull : 0ull;
+        } else {
+            const int idp = dpp_shr1i(id);
+            const uint64_t E = __builtin_amdgcn_ballot_w64(id >= 0) & __builtin_amdgcn_ballot_w64(id == idp);
+            const uint64_t sh = E >> max(lane - 9, 0);       // inputs l - 1, l one row: bit l
+            COV = __builtin_amdgcn_ballot_w64(lane >= 10 && (sh & 0x3FFull) == 0x3FFull);
+            const int idc = __shfl(id, max(lane - 5, 0), 64);
+            ROWIN = __builtin_amdgcn_ballot_w64(idc >= row_start) & __builtin_amdgcn_ballot_w64(idc < rlim);
+        }
+        const uint64_t DEC = OWN & ROWIN & COV;
+        const uint64_t mP = (DEC & __builtin_amdgcn_ballot_w64(v < plane_min)) >> 10;   // cand_flags
+        const uint64_t mU = (OWN & ROWIN & ~COV) >> 10;
+        const uint64_t mE = kEdge ? ((DEC & __builtin_amdgcn_ballot_w64(v > edge_min)) >> 10) : 0ull;
+        put(k, mP, mE);
+        wl(vUl, (uint32_t)mU, k);
+        wl(vUh, (uint32_t)(mU >> 32), k);
+        if (kDebug && lane >= 10 && lane < 10 + nown) wcv[kDebug ? w : 0][a0 + lane - 10] = ((DEC >> lane) & 1ull) ? v : 0.0f;
+        // the runs starting here: an own centre whose input before it is another row (or none)
+        uint64_t RS;
+        if (uni) RS = k == 0 ? (1ull << 5) : 0ull;
+        else {
+            const int idm = dpp_shr1i(id);
+            RS = lane_range(5, 5 + nown) & (__builtin_amdgcn_ballot_w64(id != idm) | (k == 0 ? (1ull << 5) : 0ull));
+        }
+        while (RS) {                                          // uniform (SGPRs), in input order
+            const int i = (int)__builtin_ctzll(RS);
+            RS &= RS - 1ull;
+            const int r = __builtin_amdgcn_readlane(id, i);
+            if (nrun < kRunMax && lane == 0) wrun[w][nrun] = make_int2(r, a0 + i - 5);
+            ++nrun;
+        }
+        return nrun <= kRunMax;
+    };
+    // SSF_FEAT_RUN_PF registers in flight per wave: a register is reloaded with the one
+    // SSF_FEAT_RUN_PF ahead as soon as its points are taken
+    float X[kRunPF], Y[kRunPF], Z[kRunPF];
+    uint32_t KP[kRunPF];
+#pragma unroll
+    for (int j = 0; j < kRunPF; ++j) load_reg(j, X[j], Y[j], Z[j], KP[j]);
+    bool go = true;
+    for (int k0 = 0; k0 < nreg && go; k0 += kRunPF) {        // uniform
+#pragma unroll
+        for (int j = 0; j < kRunPF; ++j) {
+            if (go && k0 + j < nreg) {                        // uniform
+                const float cx = X[j], cy = Y[j], cz = Z[j];
+                const uint32_t ck = KP[j];
+                load_reg(k0 + j + kRunPF, X[j], Y[j], Z[j], KP[j]);
+                go = reg(k0 + j, cx, cy, cz, ck);
+            }
+        }
+    }
+    // the input-order words: lane t < 32 word t of the candidate plane, lane 32 + t of the
+    // unresolved one (the edge plane next), each from the 1 .. 3 registers overlapping its bits
+    {
+        auto word = [&](uint32_t lo, uint32_t hi, int t) -> uint64_t {
+            uint64_t wv = 0;
+            const int k0 = (64 * t) / kRunStep;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const int k = min(k0 + d, 63);
+                const uint64_t m = ((uint64_t)(uint32_t)__shfl((int)hi, k, 64) << 32) |
+                                   (uint32_t)__shfl((int)lo, k, 64);             // own bits 0 .. 53
+                const int o = kRunStep * k - 64 * t;           // bit offset of the register in the word
+                if (k0 + d < nreg && o < 64 && o > -kRunStep) wv |= o >= 0 ? (m << o) : (m >> -o);
+            }
+            return wv;
+        };
+        const int t = lane & 31;
+        // (every lane shuffles the same plane's VGPRs: a shuffle reads the SOURCE lane's value)
+        const uint64_t a0 = word(vPl, vPh, t), a1 = word(vUl, vUh, t);
+        if (64 * t < len) wpos[w][lane < 32 ? t : kFeatWords + t] = lane < 32 ? a0 : a1;
+        if (kEdge) {
+            const uint64_t e2 = word(vEl, vEh, t);
+            if (lane < 32 && 64 * t < len) wpos[w][2 * kFeatWords + t] = e2;
+        }
+    }
+    bool fail = nrun > kRunMax;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");    // the loop's LDS writes before the reads
+    __builtin_amdgcn_wave_barrier();
+    int2 rj = make_int2(-1, len);
+    int nj = 0;
+    if (!fail && lane < nrun) {
+        rj = wrun[w][lane];
+        nj = (lane + 1 < nrun ? wrun[w][lane + 1].y : len) - rj.y;
+        if (rj.x >= 0) {
+            atomicAdd(&wnum[w][rj.x], 1);
+            atomicAdd(&wlen[w][rj.x], nj);
+            wst[w][rj.x] = rj.y;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    const int cr = wlen[w][lane];                             // lane r: row r's own points
+    fail = fail || __any(wnum[w][lane] > 1);
+    if (fail) {                                               // uniform: a row in two runs, or too many runs
+        if (lane == 0) irregular[lb] = kIrrGeneral;
+        return;
+    }
+    int incl = cr;                                            // own-tile slot base of every row
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const int base = incl - cr;
+    const int bj = __shfl(base, rj.x & 63, 64);               // run lane j: its slot start
+    const bool ident = __all(lane >= nrun || rj.x < 0 || bj == rj.y);   // slots = positions
+    if (!ident) {                                             // uniform: move the runs' bits
+        for (int j = 0; j < nrun; ++j) {
+            const int r = __shfl(rj.x, j, 64), a = __shfl(rj.y, j, 64), n = __shfl(nj, j, 64);
+            const int b = __shfl(bj, j, 64);
+            if (r < 0 || n <= 0) continue;
+            const int d0 = b >> 6, nd = ((b + n - 1) >> 6) - d0 + 1;
+            for (int t = lane; t < kPl * nd; t += 64) {
+                const int pl = t / nd, d = d0 + (t - pl * nd);
+                const int lo = max(b, 64 * d), hi = min(b + n, 64 * d + 64);
+                const uint64_t bits = bits_at(&wpos[w][pl * kFeatWords], lo - b + a, hi - lo, kFeatWords);
+                if (bits)
+                    __hip_atomic_fetch_or(&wslt[w][pl * kFeatWords + d], bits << (lo - 64 * d), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
+    const unsigned long long* PL = ident ? &wpos[w][0] : &wslt[w][0];
+    uint64_t* gb = gbits + ((int64_t)f * n_chunks + c) * kPW;
+    for (int t = lane; t < kPl * kFeatWords; t += 64) gb[t] = PL[t];
+    cnt[((int64_t)f * (n_chunks + 1) + c) * kMaxRows + lane] = cr;
+    uint16_t* gi = gidx + idx_base(frame_off, f) + (int64_t)c * kBinChunk;
+    if (!kDebug) {
+        gi[lane] = (uint16_t)(cr > 0 ? wst[w][lane] : 0);     // the row's run start
+    } else {                                                  // every slot's position (kIrrRunIdx)
+        for (int j = 0; j < nrun; ++j) {
+            const int r = __shfl(rj.x, j, 64), a = __shfl(rj.y, j, 64), n = __shfl(nj, j, 64);
+            const int b = __shfl(bj, j, 64);
+            if (r < 0) continue;
+            for (int o = lane; o < n; o += 64) {
+                gi[b + o] = (uint16_t)(a + o);
+                if (curv_cm) curv_cm[s + b + o] = wcv[kDebug ? w : 0][a + o];
+            }
+        }
+    }
+    if (lane == 0) irregular[lb] = kDebug ? kIrrRunIdx : kIrrRun;
 }
 
 // k_feat_select: one 1024-thread work-group per frame.  The chunks' row counts become, in LDS,
@@ -1611,7 +1985,9 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
     // the frame-local input index of row r's point j (indexInRow) in chunk cc (rb: row bases)
     auto point_of = [&](int cc, int r, int j) -> int {
         const int o = j - rb[r][cc];                          // its place in the (chunk, row) segment
-        return cc * kBinChunk + (irc[cc] ? (int)GI[(int64_t)cc * kBinChunk + ss[cc][r] + o] : 64 * o + lmc[cc][r]);
+        const uint8_t m = irc[cc];
+        return cc * kBinChunk + (m == kIrrRun ? (int)GI[(int64_t)cc * kBinChunk + r] + o
+                                 : m ? (int)GI[(int64_t)cc * kBinChunk + ss[cc][r] + o] : 64 * o + lmc[cc][r]);
     };
     // counts -> segment starts (prefix over rows, per chunk); counts into rb
 #pragma unroll
@@ -2074,7 +2450,10 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
         // blocks it flagged (every other block returns at once)
         const bool regular = SSF_FEAT_REGULAR && !keep && R == kMaxRows && fs->irr && fs->lmap &&
                              stride <= 4096;              // k_feat_wave_reg: 32-bit window offsets
-        uint8_t* irr = regular ? fs->irr : nullptr;
+        // the run kernel next, for the chunks k_feat_wave_reg left (every chunk when it did not
+        // run: masked frames, 16 beams); then k_feat_chunk for the rest
+        const bool run = SSF_FEAT_WAVE_RUN && fs->irr && stride <= 4096;
+        uint8_t* irr = (regular || run) ? fs->irr : nullptr;
         const RingTable* rt = reinterpret_cast<const RingTable*>(fs->rtab);
         if (regular && SSF_FEAT_WAVE_REG) {                   // one wave per chunk
             kmark(s, "k_feat_wave_reg");
@@ -2099,9 +2478,22 @@ hipError_t launch_extract_planes(hipStream_t s, const ssf_config& cfg, int n_fra
             else { if (dbg) SSF_FR_LAUNCH(true, false); else SSF_FR_LAUNCH(false, false); }
 #undef SSF_FR_LAUNCH
         }
+        if (run) {
+            kmark(s, "k_feat_wave_run");
+            const int64_t nwg = (nblk + kCurvNW - 1) / kCurvNW;
+            const dim3 wgrid((unsigned)((nwg + 7) / 8 * 8));
+#define SSF_RUN_LAUNCH(D, E)                                                                        \
+            hipLaunchKernelGGL((k_feat_wave_run<D, E>), wgrid, dim3(kCurvNT), 0, s, pts, stride,     \
+                               frame_off, n_frames, R, n_chunks, cfg.row_start, cfg.row_end,         \
+                               cfg.plane_min, emin, keep, rt, fs->cnt, fs->gidx, fs->gbits, ccm, irr, \
+                               regular ? 0 : 1)
+            if (edge) { if (dbg) SSF_RUN_LAUNCH(true, true); else SSF_RUN_LAUNCH(false, true); }
+            else { if (dbg) SSF_RUN_LAUNCH(true, false); else SSF_RUN_LAUNCH(false, false); }
+#undef SSF_RUN_LAUNCH
+        }
 #define SSF_FC_COMMON pts, stride, frame_off, n_frames, R, n_chunks, cfg.row_start, cfg.row_end,         \
                       cfg.plane_min, emin, keep, rt, fs->cnt, fs->gidx, fs->gbits, ccm
-        if (regular) {
+        if (irr) {
             kmark(s, "k_feat_chunk_flagged");
             const dim3 fgrid((unsigned)((nblk + kFlagGroup - 1) / kFlagGroup));
 #define SSF_FC_LAUNCH(D, E) hipLaunchKernelGGL((k_feat_chunk_flagged<D, E>), fgrid, dim3(kCurvNT), 0, s, SSF_FC_COMMON, irr)

@@ -33,8 +33,9 @@ __device__ __forceinline__ double u01(uint64_t key) {
 __global__ __launch_bounds__(256) void k_synth_scan(int n_rows, int n_az, const double* __restrict__ elev,
                                                     const double* __restrict__ prm, int rec,
                                                     int n_box, int n_pole, int n_car,
-                                                    const uint64_t* __restrict__ seeds,
-                                                    float* __restrict__ pos, float* __restrict__ flow) {
+                                                    const uint64_t* __restrict__ seeds, int layout,
+                                                    float* __restrict__ pos, float* __restrict__ flow,
+                                                    double* __restrict__ key) {
     __shared__ double P[kHdr + kMaxObj];
     const int s = blockIdx.y;
     const double* src = prm + (size_t)s * rec;
@@ -43,7 +44,10 @@ __global__ __launch_bounds__(256) void k_synth_scan(int n_rows, int n_az, const 
     const int64_t n = (int64_t)n_rows * n_az;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const int a = (int)(i / n_rows), r = (int)(i - (int64_t)a * n_rows);
+    // layout 0: azimuth-major (index a * n_rows + r, a spinning sensor's firing order);
+    // layout 1: channel-major (index r * n_az + a, as CARLA's ray-cast LiDAR stores a sweep)
+    const int a = layout ? (int)(i % n_az) : (int)(i / n_rows);
+    const int r = layout ? (int)(i / n_az) : (int)(i - (int64_t)a * n_rows);
     const double* R = P;
     const double* p = P + 9;
     const double* R2 = P + 12;
@@ -94,14 +98,22 @@ __global__ __launch_bounds__(256) void k_synth_scan(int n_rows, int n_az, const 
     }
     const double ts = fmin(t, fmin(tb, tp));
     const bool car_hit = tc < ts;
+    // the ray's return: an object (box, pole, car), the ground plane (the road, z = -2.5), or
+    // none within the 100 m range (the dome)
+    const bool object_hit = car_hit || fmin(tb, tp) < t;
+    const bool ground_hit = !object_hit && t < 100.0;
     t = car_hit ? tc : ts;
     const int mover = car_hit ? ic : -1;
-    const uint64_t key = seeds[s] ^ ((uint64_t)i << 2);
-    const double u1 = u01(key), u2 = u01(key + 1);
+    const uint64_t hk = seeds[s] ^ ((uint64_t)i << 2);
+    // CARLA-like frames (ssf/synth.py layout "carla"): no point for a ray without a return and
+    // for road points (rm_road); the survivors get a uniform selection key (random drop-off)
+    if (key) key[(size_t)s * n + i] = (object_hit && !ground_hit) ? u01(hk ^ 0x5bd1e995ull) : 2.0;
+    const uint64_t key_ = hk;
+    const double u1 = u01(key_), u2 = u01(key_ + 1);
     const double noise = 0.01 * (sqrt(-2.0 * log(u1)) * cos(2.0 * 3.14159265358979323846 * u2));
     t = fmin(t, 100.0) + noise;
     double p1[3];
-    for (int k = 0; k < 3; ++k) p1[k] = ds[k] * t + 1e-4 * (u01(key + 2 + (uint64_t)k * 0x10000000000ull) - 0.5);
+    for (int k = 0; k < 3; ++k) p1[k] = ds[k] * t + 1e-4 * (u01(key_ + 2 + (uint64_t)k * 0x10000000000ull) - 0.5);
     double W[3];
     for (int j = 0; j < 3; ++j) W[j] = ((R[3 * j] * p1[0] + R[3 * j + 1] * p1[1]) + R[3 * j + 2] * p1[2]) + p[j];
     if (mover >= 0)
@@ -123,18 +135,21 @@ __global__ __launch_bounds__(256) void k_synth_scan(int n_rows, int n_az, const 
 
 extern "C" {
 
-// One frame for each of S sequences: rays n_rows x n_az (azimuth-major, index a * n_rows + r),
+// One frame for each of S sequences: rays n_rows x n_az,
 // parameter records prm[S][rec] on the device (layout above), seeds[S] (device), outputs
 // pos / flow [S * n_rows * n_az][3] f32 on the device.  Returns a hipError_t.
+// layout 0 / 1: azimuth- / channel-major rays; d_key (nullable) [S * n_rows * n_az] f64: per ray a
+// uniform key in (0, 1) when it returns from an object (not the road, not the 100 m dome), else 2.
 int ssf_synth_scan_batch(void* stream, int32_t n_seq, int32_t n_rows, int32_t n_az, const double* d_elev,
                          const double* d_prm, int32_t rec, int32_t n_box, int32_t n_pole, int32_t n_car,
-                         const uint64_t* d_seeds, float* d_pos, float* d_flow) {
+                         const uint64_t* d_seeds, int32_t layout, float* d_pos, float* d_flow,
+                         double* d_key) {
     if (n_seq <= 0) return 0;
     if (rec - kHdr > kMaxObj || rec < kHdr + 6 * n_box + 4 * n_pole + 9 * n_car) return (int)hipErrorInvalidValue;
     const int64_t n = (int64_t)n_rows * n_az;
     dim3 grid((unsigned)((n + 255) / 256), (unsigned)n_seq);
     hipLaunchKernelGGL(k_synth_scan, grid, dim3(256), 0, (hipStream_t)stream, n_rows, n_az, d_elev, d_prm,
-                       rec, n_box, n_pole, n_car, d_seeds, d_pos, d_flow);
+                       rec, n_box, n_pole, n_car, d_seeds, layout, d_pos, d_flow, d_key);
     return (int)hipGetLastError();
 }
 

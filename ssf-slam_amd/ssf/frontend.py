@@ -156,20 +156,33 @@ class Frontend:
         return t
 
     # ------------------------------------------------------------------ frameFeature
+    def _out(self, t, shape, dtype, what):
+        """a caller-supplied output buffer (preallocated: no allocation per call), checked"""
+        t = self._dev(t, dtype)
+        if t.dim() != len(shape) or any(a < b for a, b in zip(t.shape, shape)) or t.shape[1:] != shape[1:]:
+            raise ValueError(f"{what}: need at least {tuple(shape)} {dtype}, got {tuple(t.shape)}")
+        return t
+
     def extract_planes_batch(self, pts, off, h_off, max_points=None, point_stride=None,
-                             debug=False, keep=None):
+                             debug=False, keep=None, out=None):
         """cloudHandler for F frames packed in `pts` ([total, stride] f32) at offsets `off`.
         Returns PlaneBatch (and, with debug=True, ring-ordered points, row offsets, curvature).
         keep (uint8/bool per point, optional, beyond the reference): extract from the kept
-        points only -- e.g. the background mask of mask_pose ("mask applied before features")."""
+        points only -- e.g. the background mask of mask_pose ("mask applied before features").
+        out: optional preallocated (plane [>= total, 4] f32, count [>= F] int32) -- a pipeline
+        reuses a ring of them instead of allocating per call."""
         pts = self._dev(pts, torch.float32)
         F = h_off.numel() - 1
         total = int(h_off[-1])
         sizes = (h_off[1:] - h_off[:-1])
         mx = int(sizes.max()) if max_points is None and F > 0 else int(max_points or 0)
         stride = pts.shape[1] if point_stride is None else point_stride
-        plane = torch.empty((max(total, 1), 4), dtype=torch.float32, device=self.device)
-        count = torch.empty(max(F, 1), dtype=torch.int32, device=self.device)
+        if out is not None:
+            plane = self._out(out[0], (max(total, 1), 4), torch.float32, "plane out")
+            count = self._out(out[1], (max(F, 1),), torch.int32, "count out")
+        else:
+            plane = torch.empty((max(total, 1), 4), dtype=torch.float32, device=self.device)
+            count = torch.empty(max(F, 1), dtype=torch.int32, device=self.device)
         ring = roff = curv = None
         if debug:
             ring = torch.zeros((max(total, 1), 4), dtype=torch.float32, device=self.device)
@@ -246,24 +259,38 @@ class Frontend:
         return out[:m.value]
 
     # ------------------------------------------------------------------ lidarOdometry_onlyPC
-    def plane_table(self, pb: PlaneBatch, brute_force: bool = False, strips: bool = True):
+    def plane_table(self, pb: PlaneBatch, brute_force: bool = False, strips: bool = True, out=None):
         """-> PlaneTable (normal [total,3] f32, valid [total] u8, sorted_xyzi, sorted_idx) -- the
         plane table of frames that will be LAST frames, plus their x-sorted search index (None,
         None when brute_force=True); .strips = the y-strip image (strip_xyzi [total,4] f32,
-        strip_head [total] i32) that register() hands to the association, or None."""
+        strip_head [total] i32) that register() hands to the association, or None.
+        out: optional preallocated buffers (normal, valid, sx, si, strip_xyzi, strip_head), each
+        at least `total` rows -- reused instead of allocated per call."""
         total = pb.xyzi.shape[0]
-        normal = torch.empty((total, 3), dtype=torch.float32, device=self.device)
-        valid = torch.empty(total, dtype=torch.uint8, device=self.device)
+        if out is not None:
+            normal = self._out(out[0], (total, 3), torch.float32, "normal out")
+            valid = self._out(out[1], (total,), torch.uint8, "valid out")
+        else:
+            normal = torch.empty((total, 3), dtype=torch.float32, device=self.device)
+            valid = torch.empty(total, dtype=torch.uint8, device=self.device)
         sx = si = st = None
         if not brute_force:
-            sx = torch.empty((total, 4), dtype=torch.float32, device=self.device)
-            si = torch.empty(total, dtype=torch.int32, device=self.device)
+            if out is not None:
+                sx = self._out(out[2], (total, 4), torch.float32, "sorted_xyzi out")
+                si = self._out(out[3], (total,), torch.int32, "sorted_idx out")
+            else:
+                sx = torch.empty((total, 4), dtype=torch.float32, device=self.device)
+                si = torch.empty(total, dtype=torch.int32, device=self.device)
             # the association stages an image only for frames of STRIP_IMAGE_MIN..MAX points
             # (registration.hip strip_image_frame) and only in launches whose plane bound is
             # within MAX (float4 strips): otherwise the 20 B per plane point would be dead weight
             if strips and _abi.STRIP_IMAGE_MIN <= pb.max_points and pb.max_points <= _abi.STRIP_IMAGE_MAX:
-                st = (torch.empty((total, 4), dtype=torch.float32, device=self.device),
-                      torch.empty(total, dtype=torch.int32, device=self.device))
+                if out is not None:
+                    st = (self._out(out[4], (total, 4), torch.float32, "strip_xyzi out"),
+                          self._out(out[5], (total,), torch.int32, "strip_head out"))
+                else:
+                    st = (torch.empty((total, 4), dtype=torch.float32, device=self.device),
+                          torch.empty(total, dtype=torch.int32, device=self.device))
         rc = _abi.lib().ssf_plane_table_batch(self._h, _stream(self.device), pb.count.numel(),
                                               _ptr(pb.xyzi), _ptr(pb.off), _ptr(pb.count),
                                               pb.max_points, _ptr(normal), _ptr(valid), _ptr(sx),
@@ -346,17 +373,25 @@ class Frontend:
 
     # ------------------------------------------------------------------ PointCloudOdometry*.py
     def mask_pose(self, pts, flow, off, h_off, mode="gmm", mask_in=None, draws=None,
-                  reflection=0, want_mask=True):
+                  reflection=0, want_mask=True, out=None):
         """Mask + Kabsch for F frames -> (out [F,32] f64, bg_mask [total] u8 or None).
         pts / flow both float32 (ssf_mask_pose_batch) or both float64 (ssf_mask_pose_batch_f64:
-        no rounding of f64 inputs)."""
+        no rounding of f64 inputs).  out: optional preallocated (pose out [>= F, 32] f64,
+        bg_mask [>= total] u8 or None)."""
         dt = torch.float64 if pts.dtype == torch.float64 else torch.float32
         pts = self._dev(pts, dt)
         flow = self._dev(flow, dt)
         F = h_off.numel() - 1
         total = int(h_off[-1])
-        out = torch.empty((max(F, 1), _abi.POSE_OUT_STRIDE), dtype=torch.float64, device=self.device)
-        bg = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device) if want_mask else None
+        if out is not None:
+            bg = (self._out(out[1], (max(total, 1),), torch.uint8, "bg_mask out")
+                  if want_mask and out[1] is not None else None)
+            out = self._out(out[0], (max(F, 1), _abi.POSE_OUT_STRIDE), torch.float64, "pose out")
+            if want_mask and bg is None:
+                raise ValueError("want_mask needs a bg_mask out buffer")
+        else:
+            out = torch.empty((max(F, 1), _abi.POSE_OUT_STRIDE), dtype=torch.float64, device=self.device)
+            bg = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device) if want_mask else None
         h_off64 = h_off.to(torch.int64).contiguous()
         hd = None
         if draws is not None:

@@ -6,7 +6,14 @@ repository and there is no network, so scans are ray-cast here:
 * elevations at the bin centres of the reference's ring mapping (src/frameFeature.cpp:57-71):
   64 rows -> 2 - k/3 (k = 0..32) and -8.83 - m/2 (m = 1..31); 16 rows -> -15 + 2k.  A
   float32/float64 atan difference can therefore never move a point across a row edge;
-* azimuth-major emission order (all beams per azimuth step, like a spinning sensor);
+* azimuth-major emission order (all beams per azimuth step, like a spinning sensor) -- or, with
+  layout="carla", the layout of the reference's own data (launch/run_noSeg.launch:4 reads a
+  road-removed CARLA set, .../rm_road/SF/04): channel-major order as CARLA's ray-cast LiDAR stores
+  a sweep (every point of channel 0 in azimuth order, then channel 1, ...), no point for a ray
+  without a return within the 100 m range (CARLA drops those; Scenario_Traj.py:307-315 leaves its
+  drop-off on), no road points (the ground plane, rm_road), and a uniform random drop-off down to
+  exactly n_rows * n_az points per frame (oversample x as many rays are cast), so every frame
+  has the bench's size but ragged rows;
 * world: ground plane z = -2.5, a street of box buildings, poles (vertical cylinders), a
   100 m "sky dome" for rays that hit nothing, and moving cars (dynamic points, ~8 %);
 * ego motion ~1 m/frame with a bounded heading (ego_yaw); range noise sigma 0.01 m plus 1e-4 m jitter so
@@ -140,13 +147,26 @@ def _ray_poles(o, d, poles):
     return t.min(1).values
 
 
+LAYOUTS = ("azimuth", "carla")
+CARLA_OVERSAMPLE = 3      # rays cast per kept point in the "carla" layout (ample: ~40 % return)
+
+
 def scan(seq: int, frame: int, n_rows: int = 64, n_az: int = 1875, device="cpu",
-         scene: Scene | None = None):
+         scene: Scene | None = None, layout: str = "azimuth"):
     """One synthetic frame -> dict(pos1 [N,3] f32, flow [N,3] f32, s_fg_mask [N] u8).
 
-    N = n_rows * n_az exactly (every ray returns: rays that hit nothing land on a 100 m dome)."""
+    N = n_rows * n_az exactly.  layout "azimuth": every ray returns (rays that hit nothing land on
+    a 100 m dome), azimuth-major.  layout "carla": CARLA_OVERSAMPLE x n_az rays per channel,
+    channel-major; rays without an object return (dome or road) are dropped, then a uniform
+    random drop-off keeps exactly N points in their order (module docstring)."""
+    if layout not in LAYOUTS:
+        raise ValueError(f"layout must be one of {LAYOUTS}")
     scene = scene or Scene(seq)
     g = _gen(SEED_BASE + seq * 10000 + frame)
+    carla = layout == "carla"
+    n_keep = n_rows * n_az
+    if carla:
+        n_az = CARLA_OVERSAMPLE * n_az
     el = elevations_deg(n_rows) * (math.pi / 180.0)
     az0 = 2 * math.pi * torch.rand(1, generator=g, dtype=torch.float64).item() / n_az
     az = az0 + 2 * math.pi * torch.arange(n_az, dtype=torch.float64) / n_az
@@ -154,6 +174,8 @@ def scan(seq: int, frame: int, n_rows: int = 64, n_az: int = 1875, device="cpu",
     # azimuth-major: index = a * n_rows + r
     ds = torch.stack([ce[None, :] * torch.cos(az)[:, None], ce[None, :] * torch.sin(az)[:, None],
                       se[None, :].expand(n_az, n_rows)], 2).reshape(-1, 3)
+    if carla:                                   # channel-major: index = r * n_az + a
+        ds = ds.view(n_az, n_rows, 3).transpose(0, 1).reshape(-1, 3).contiguous()
     noise_r = 0.01 * torch.randn(ds.shape[0], generator=g, dtype=torch.float64)
     jitter = 1e-4 * (torch.rand(ds.shape[0], 3, generator=g, dtype=torch.float64) - 0.5)
     ds = ds.to(device)
@@ -163,6 +185,7 @@ def scan(seq: int, frame: int, n_rows: int = 64, n_az: int = 1875, device="cpu",
     n = dw.shape[0]
     t = torch.full((n,), 100.0, dtype=torch.float64, device=device)
     mover = torch.full((n,), -1, dtype=torch.long, device=device)
+    obj = torch.zeros(n, dtype=torch.bool, device=device)      # returned from an object
     tg = torch.where(dw[:, 2] < -1e-9, (-2.5 - p[2]) / dw[:, 2], torch.full_like(t, math.inf))
     t = torch.minimum(t, tg)
     chunk = 1 << 16
@@ -174,8 +197,10 @@ def scan(seq: int, frame: int, n_rows: int = 64, n_az: int = 1875, device="cpu",
         tb, _ = _ray_boxes(p, dw[s:e], boxes)
         tp = _ray_poles(p, dw[s:e], poles)
         tc, ic = _ray_boxes(p, dw[s:e], cars)
-        ts = torch.minimum(t[s:e], torch.minimum(tb, tp))
+        to = torch.minimum(tb, tp)
+        ts = torch.minimum(t[s:e], to)
         car_hit = tc < ts
+        obj[s:e] = car_hit | (to < t[s:e])
         t[s:e] = torch.where(car_hit, tc, ts)
         mover[s:e] = torch.where(car_hit, ic, torch.full_like(ic, -1))
     t = torch.clamp(t, max=100.0) + noise_r.to(device)
@@ -191,7 +216,24 @@ def scan(seq: int, frame: int, n_rows: int = 64, n_az: int = 1875, device="cpu",
     pos2 = (W + vel - p2) @ R2
     pos1f = pos1.to(torch.float32)
     flow = (pos2 - pos1f.to(torch.float64)).to(torch.float32)
-    return dict(pos1=pos1f, flow=flow, s_fg_mask=m.to(torch.uint8))
+    out = dict(pos1=pos1f, flow=flow, s_fg_mask=m.to(torch.uint8))
+    if carla:
+        keep = carla_keep(obj.cpu(), n_keep, torch.rand(n, generator=g, dtype=torch.float64))
+        out = {k: v[keep.to(v.device)] for k, v in out.items()}
+    return out
+
+
+def carla_keep(returned: torch.Tensor, n_keep: int, u: torch.Tensor) -> torch.Tensor:
+    """The random drop-off of the "carla" layout: of the rays that returned (bool [n]), the
+    n_keep with the smallest keys u (uniform, [n]) -> a bool mask that keeps their order."""
+    key = torch.where(returned, u, torch.full_like(u, 2.0))
+    if int(returned.sum()) < n_keep:
+        raise ValueError(f"carla layout: {int(returned.sum())} returns for {n_keep} points "
+                         f"(raise CARLA_OVERSAMPLE)")
+    thr = torch.kthvalue(key, n_keep).values
+    keep = key <= thr
+    assert int(keep.sum()) == n_keep
+    return keep
 
 
 _SYNTH_LIB = None
@@ -208,7 +250,7 @@ def _synth_lib():
         lib.ssf_synth_scan_batch.restype = C.c_int
         lib.ssf_synth_scan_batch.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                              C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
-                                             C.c_void_p, C.c_void_p, C.c_void_p]
+                                             C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
         _SYNTH_LIB = lib
     return _SYNTH_LIB
 
@@ -230,8 +272,12 @@ class BatchScanner:
     ego motion as scan(), one ray per thread; the range noise and the jitter come from a
     counter-based hash instead of torch's CPU generator.  Bench / test data only."""
 
-    def __init__(self, seqs, n_frames: int, n_rows: int = 64, n_az: int = 1875, device="cuda"):
+    def __init__(self, seqs, n_frames: int, n_rows: int = 64, n_az: int = 1875, device="cuda",
+                 layout: str = "azimuth"):
         import numpy as np
+        if layout not in LAYOUTS:
+            raise ValueError(f"layout must be one of {LAYOUTS}")
+        self.layout = layout
         self.seqs, self.n_rows, self.n_az, self.device = list(seqs), n_rows, n_az, torch.device(device)
         self.scenes = [Scene(s) for s in self.seqs]
         self.poses = [ego_poses(s, n_frames + 1) for s in self.seqs]
@@ -247,12 +293,21 @@ class BatchScanner:
         np = self._np
         S, N = len(self.seqs), self.n_rows * self.n_az
         assert pos.shape == (S * N, 3) and flow.shape == (S * N, 3) and pos.is_contiguous() and flow.is_contiguous()
+        carla = self.layout == "carla"
+        n_az = CARLA_OVERSAMPLE * self.n_az if carla else self.n_az
+        if carla:                                   # every ray first, then the drop-off to N
+            M = self.n_rows * n_az
+            rpos = torch.empty((S * M, 3), dtype=torch.float32, device=self.device)
+            rflow = torch.empty_like(rpos)
+            rkey = torch.empty(S * M, dtype=torch.float64, device=self.device)
+        else:
+            rpos, rflow, rkey = pos, flow, None
         prm = np.zeros((S, self.rec))
         seeds = np.zeros(S, dtype=np.uint64)
         for j, (seq, sc) in enumerate(zip(self.seqs, self.scenes)):
             R, p = self.poses[j]
             az0 = 2 * math.pi * torch.rand(1, generator=_gen(SEED_BASE + seq * 10000 + k),
-                                           dtype=torch.float64).item() / self.n_az
+                                           dtype=torch.float64).item() / n_az
             car = sc.car_boxes(k).numpy()
             carv = np.concatenate([sc.cars[:, 2:4].numpy(), np.zeros((self.n_car, 1))], 1)
             prm[j] = np.concatenate([R[k].ravel(), p[k], R[k + 1].ravel(), p[k + 1], [az0],
@@ -263,13 +318,25 @@ class BatchScanner:
         d_seeds = torch.from_numpy(seeds.view(np.int64)).to(self.device)
         st = torch.cuda.current_stream(self.device).cuda_stream
         rc = _synth_lib().ssf_synth_scan_batch(
-            C.c_void_p(st), S, self.n_rows, self.n_az, C.c_void_p(self.elev.data_ptr()),
+            C.c_void_p(st), S, self.n_rows, n_az, C.c_void_p(self.elev.data_ptr()),
             C.c_void_p(d_prm.data_ptr()), self.rec, self.n_box, self.n_pole, self.n_car,
-            C.c_void_p(d_seeds.data_ptr()), C.c_void_p(pos.data_ptr()), C.c_void_p(flow.data_ptr()))
+            C.c_void_p(d_seeds.data_ptr()), 1 if carla else 0, C.c_void_p(rpos.data_ptr()),
+            C.c_void_p(rflow.data_ptr()), None if rkey is None else C.c_void_p(rkey.data_ptr()))
         if rc != 0:
             raise RuntimeError(f"ssf_synth_scan_batch failed: hipError {rc}")
         d_prm.record_stream(torch.cuda.current_stream(self.device))
         d_seeds.record_stream(torch.cuda.current_stream(self.device))
+        if carla:                                   # per sequence the N smallest keys, in order
+            kv = rkey.view(S, -1)
+            if int((kv < 2.0).sum(1).min()) < N:
+                raise ValueError("carla layout: too few returns for the frame size (raise CARLA_OVERSAMPLE)")
+            thr = torch.kthvalue(kv, N, dim=1).values
+            keep = (kv <= thr[:, None]).view(-1)
+            sel = torch.nonzero(keep).view(-1)
+            if sel.numel() != S * N:
+                raise RuntimeError("carla layout: tied selection keys")
+            torch.index_select(rpos, 0, sel, out=pos)
+            torch.index_select(rflow, 0, sel, out=flow)
 
 
 def relative_pose(seq: int, frame_last: int, frame_curr: int):

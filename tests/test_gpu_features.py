@@ -387,3 +387,79 @@ def test_outermost_window_columns_not_loaded(oracle, dev):
     got = _planes_product(fe, clouds, dev)
     for f, cl in enumerate(clouds):
         assert np.array_equal(got[f].view(np.uint32), oracle.extract_planes(cl, 64).view(np.uint32)), f
+
+
+def test_carla_layout_frames(oracle, dev):
+    """The reference's own data layout (ssf/synth.py layout "carla": channel-major as CARLA stores
+    a sweep, no-return rays and road points dropped, random drop-off; rows ragged, several empty):
+    two full 120k-point frames and a cut one in one launch -- ring cloud, curvature bits and plane
+    lists bit-exact vs the oracle, debug and product instantiations, both ring-id chains."""
+    import ssf
+    from ssf import synth
+    sc = synth.Scene(12)
+    c0 = synth.scan(12, 0, n_az=1875, scene=sc, layout="carla")["pos1"].numpy()
+    c1 = synth.scan(12, 1, n_az=1875, scene=sc, layout="carla")["pos1"].numpy()
+    clouds = [c0, c1, c1[: 64 * 700 + 33]]
+    for chain in ("float", "double"):
+        fe = ssf.Frontend(64, device=dev.index or 0, ring_chain=chain)
+        out, h_off = _run(fe, clouds, dev)
+        with oracle.ring_chain(chain):
+            for f, cl in enumerate(clouds):
+                _check_frame(oracle, fe, out, h_off, f, cl, 64)
+            got = _planes_product(fe, clouds, dev)
+            for f, cl in enumerate(clouds):
+                assert np.array_equal(got[f].view(np.uint32), oracle.extract_planes(cl, 64).view(np.uint32)), f
+
+
+def test_run_kernel_orders_gaps_and_fallbacks(oracle, dev):
+    """k_feat_wave_run's cases (features.hip): rows in DESCENDING order (own-tile slots are not the
+    input order: the bit planes move run by run), points in no row between runs (gaps) and inside
+    a run (the row then forms two runs in a chunk: left to k_feat_chunk), rows alternating in
+    100-point blocks (a row in several runs per chunk: fallback), many short runs (> 64 runs in a
+    chunk: fallback), a 16-beam channel-major frame, and masked frames (keep: every masked point
+    is a gap).  Ring cloud, curvature bits and plane lists bit-exact vs the oracle, debug and
+    product instantiations."""
+    import ssf
+    from ssf import synth
+    sc = synth.Scene(13)
+    base = synth.scan(13, 2, n_az=1875, scene=sc, layout="carla")["pos1"].numpy()
+    rid = oracle.ring_ids(base, 64)
+    desc = base[np.argsort(-rid, kind="stable")]                        # rows descending
+    gaps = base.copy()
+    gaps[5000:5003] = np.nan                                            # inside a run: two runs
+    gaps[np.nonzero(np.diff(rid) != 0)[0][:6] + 1] = np.nan             # at run starts: gaps
+    rowmajor = base[np.argsort(rid, kind="stable")]
+    blocks = []                                                         # rows 10 / 11 alternating
+    r10, r11 = rowmajor[rid[np.argsort(rid, kind="stable")] == 10], rowmajor[rid[np.argsort(rid, kind="stable")] == 11]
+    for i in range(0, min(len(r10), len(r11)), 100):
+        blocks += [r10[i:i + 100], r11[i:i + 100]]
+    alt = np.concatenate(blocks + [rowmajor[:20000]])
+    short = np.concatenate([rowmajor[rid[np.argsort(rid, kind="stable")] == r][:12] for r in range(56)] * 20)
+    clouds = [desc, gaps, alt, short]
+    fe = ssf.Frontend(64, device=dev.index or 0)
+    out, h_off = _run(fe, clouds, dev)
+    for f, cl in enumerate(clouds):
+        _check_frame(oracle, fe, out, h_off, f, cl, 64)
+    got = _planes_product(fe, clouds, dev)
+    for f, cl in enumerate(clouds):
+        assert np.array_equal(got[f].view(np.uint32), oracle.extract_planes(cl, 64).view(np.uint32)), f
+    # 16 beams, channel-major
+    c16 = synth.scan(14, 1, n_rows=16, n_az=4000, layout="carla")["pos1"].numpy()
+    fe16 = ssf.Frontend(16, device=dev.index or 0)
+    out, h_off = _run(fe16, [c16], dev)
+    _check_frame(oracle, fe16, out, h_off, 0, c16, 16)
+    assert np.array_equal(_planes_product(fe16, [c16], dev)[0].view(np.uint32),
+                          oracle.extract_planes(c16, 16).view(np.uint32))
+    # masked: a random mask and a mask of contiguous blocks
+    rng = np.random.default_rng(9)
+    k1 = (rng.random(len(base)) < 0.9).astype(np.uint8)
+    k2 = np.ones(len(base), np.uint8)
+    for s0 in range(3000, len(base), 20000):
+        k2[s0:s0 + 700] = 0
+    t = torch.from_numpy(np.concatenate([base, base])).to(dev)
+    keep = torch.from_numpy(np.concatenate([k1, k2])).to(dev)
+    off, h2 = ssf.frame_offsets([len(base), len(base)], dev)
+    pb = fe.extract_planes_batch(t, off, h2, keep=keep)
+    for f, kk in enumerate((k1, k2)):
+        ref = oracle.extract_planes(base[kk != 0], 64)
+        assert np.array_equal(pb.frame(f).cpu().numpy().view(np.uint32), ref.view(np.uint32)), f

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--distinct", type=int, default=16)
     ap.add_argument("--chain", action="store_true", help="also plane table + registration")
+    ap.add_argument("--layout", default="azimuth", choices=["azimuth", "carla"])
     ap.add_argument("--tag", default=os.environ.get("SSF_LIB", "default"))
     ap.add_argument("--dump", default=None, help="with --chain: write the last plane table (normals, validity) "
                     "and registration poses to this .npz")
@@ -36,7 +37,7 @@ def main():
     for s in range(a.distinct):
         sc = synth.Scene(s)
         for k in range(2):
-            f = synth.scan(s, k, n_az=a.n_az, device=dev, scene=sc)
+            f = synth.scan(s, k, n_az=a.n_az, device=dev, scene=sc, layout=a.layout)
             for b in range(s, B, a.distinct):
                 pos[k][b * N:(b + 1) * N].copy_(f["pos1"])
     off, h_off = ssf.frame_offsets([N] * B, dev)
@@ -63,7 +64,7 @@ def main():
     if a.dump and a.chain:
         import numpy as np
         np.savez(a.dump, normal=t0[0].cpu().numpy(), valid=t0[1].cpu().numpy(), pose=res["pose_rel"].cpu().numpy())
-    print(json.dumps({"tag": a.tag, "batch": B, "points": N,
+    print(json.dumps({"tag": a.tag, "batch": B, "points": N, "layout": a.layout,
                       "kernel_ms": {k: round(ms / n, 4) for k, (n, ms) in sorted(t.items())}}))
 
 

@@ -1,0 +1,12 @@
+# round 5c: k_feat_wave_run with buffer loads + SGPR flag words: feature GPU tests (incl. the run
+# kernel's orders / gaps / fallbacks), carla + default bench lines, rocprof serial carla
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+T=r5c
+RX="--kernel-include-regex k_"
+timeout -k 10 400 python -u -m pytest tests/test_gpu_features.py tests/test_gpu_edges.py tests/test_gpu_configs.py -x -v --timeout 120 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1 && echo PYTEST_OK && \
+timeout -k 10 400 python -u bench.py --layout carla --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/${T}_carla.json 2> gpurun_out/${T}_carla.err && echo CARLA_OK && \
+timeout -k 10 300 python -u bench.py --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/${T}_default.json 2> gpurun_out/${T}_default.err && echo DEFAULT_OK && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats $RX --output-format csv -d /tmp/ps -o s -- python -u bench.py --layout carla --serial --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${T}_carla_serial.log 2>&1 && echo SERIAL_OK && \
+cp $(find /tmp/ps -name "*kernel_stats.csv" | head -1) gpurun_out/${T}_carla_serial_kernel_stats.csv

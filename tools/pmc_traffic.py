@@ -69,6 +69,7 @@ def main():
                 d = json.loads(line)
                 out["config"] = {k: d["config"][k] for k in ("sequences_per_gpu", "points_per_frame",
                                                               "mask_before_features")}
+                out["config"]["layout"] = d["config"].get("layout", "azimuth")
                 out["lib_sha16"] = d.get("lib_sha16")        # the build these counters measured
                 for k, v in d.get("kernels", {}).items():
                     if k in out["kernels"] and "bytes" in v:

@@ -1779,7 +1779,8 @@ __global__ __launch_bounds__(kCurvNT, kDebug ? 2 : SSF_FEAT_RUN_WAVES) void k_fe
         return nrun <= kRunMax;
     };
     // SSF_FEAT_RUN_PF registers in flight per wave: a register is reloaded with the one
-    // SSF_FEAT_RUN_PF ahead as soon as its points are taken
+    // SSF_FEAT_RUN_PF ahead as soon as its points are taken (reloading after its use, in place,
+    // measured slower: 0.101 against 0.099 ms, r5j)
     float X[kRunPF], Y[kRunPF], Z[kRunPF];
     uint32_t KP[kRunPF];
 #pragma unroll

@@ -101,13 +101,16 @@ __global__ __launch_bounds__(256) void k_synth_scan(int n_rows, int n_az, const 
     // the ray's return: an object (box, pole, car), the ground plane (the road, z = -2.5), or
     // none within the 100 m range (the dome)
     const bool object_hit = car_hit || fmin(tb, tp) < t;
+    // a ground return on the road (the street between the sidewalks, |y| < kRoadHalf in the world)
+    // is removed (rm_road); sidewalks and the ground between and behind the buildings stay
     const bool ground_hit = !object_hit && t < 100.0;
+    const bool road_hit = ground_hit && fabs(p[1] + t * dw[1]) < 6.0;
     t = car_hit ? tc : ts;
     const int mover = car_hit ? ic : -1;
     const uint64_t hk = seeds[s] ^ ((uint64_t)i << 2);
     // CARLA-like frames (ssf/synth.py layout "carla"): no point for a ray without a return and
     // for road points (rm_road); the survivors get a uniform selection key (random drop-off)
-    if (key) key[(size_t)s * n + i] = (object_hit && !ground_hit) ? u01(hk ^ 0x5bd1e995ull) : 2.0;
+    if (key) key[(size_t)s * n + i] = (object_hit || (ground_hit && !road_hit)) ? u01(hk ^ 0x5bd1e995ull) : 2.0;
     const uint64_t key_ = hk;
     const double u1 = u01(key_), u2 = u01(key_ + 1);
     const double noise = 0.01 * (sqrt(-2.0 * log(u1)) * cos(2.0 * 3.14159265358979323846 * u2));
@@ -139,7 +142,8 @@ extern "C" {
 // parameter records prm[S][rec] on the device (layout above), seeds[S] (device), outputs
 // pos / flow [S * n_rows * n_az][3] f32 on the device.  Returns a hipError_t.
 // layout 0 / 1: azimuth- / channel-major rays; d_key (nullable) [S * n_rows * n_az] f64: per ray a
-// uniform key in (0, 1) when it returns from an object (not the road, not the 100 m dome), else 2.
+// uniform key in (0, 1) when it returns from an object or off-road ground (not the road |y| < 6 m,
+// not the 100 m dome), else 2.
 int ssf_synth_scan_batch(void* stream, int32_t n_seq, int32_t n_rows, int32_t n_az, const double* d_elev,
                          const double* d_prm, int32_t rec, int32_t n_box, int32_t n_pole, int32_t n_car,
                          const uint64_t* d_seeds, int32_t layout, float* d_pos, float* d_flow,

@@ -11,7 +11,8 @@ repository and there is no network, so scans are ray-cast here:
   road-removed CARLA set, .../rm_road/SF/04): channel-major order as CARLA's ray-cast LiDAR stores
   a sweep (every point of channel 0 in azimuth order, then channel 1, ...), no point for a ray
   without a return within the 100 m range (CARLA drops those; Scenario_Traj.py:307-315 leaves its
-  drop-off on), no road points (the ground plane, rm_road), and a uniform random drop-off down to
+  drop-off on), no road points (ground returns with |y| < ROAD_HALF in the world, rm_road; the
+  sidewalks and the ground off the street stay), and a uniform random drop-off down to
   exactly n_rows * n_az points per frame (oversample x as many rays are cast), so every frame
   has the bench's size but ragged rows;
 * world: ground plane z = -2.5, a street of box buildings, poles (vertical cylinders), a
@@ -148,6 +149,7 @@ def _ray_poles(o, d, poles):
 
 
 LAYOUTS = ("azimuth", "carla")
+ROAD_HALF = 6.0           # the road: |y| < 6 m in the world (poles stand at 6.5, buildings from 9)
 CARLA_OVERSAMPLE = 3      # rays cast per kept point in the "carla" layout (ample: ~40 % return)
 
 
@@ -200,7 +202,11 @@ def scan(seq: int, frame: int, n_rows: int = 64, n_az: int = 1875, device="cpu",
         to = torch.minimum(tb, tp)
         ts = torch.minimum(t[s:e], to)
         car_hit = tc < ts
-        obj[s:e] = car_hit | (to < t[s:e])
+        # a return that is kept: an object, or ground off the road (|y| >= ROAD_HALF: sidewalks,
+        # the ground between and behind the buildings); road points are removed (rm_road)
+        ground = ~car_hit & ~(to < t[s:e]) & (t[s:e] < 100.0)
+        yw = p[1] + t[s:e] * dw[s:e, 1]
+        obj[s:e] = car_hit | (to < t[s:e]) | (ground & (yw.abs() >= ROAD_HALF))
         t[s:e] = torch.where(car_hit, tc, ts)
         mover[s:e] = torch.where(car_hit, ic, torch.full_like(ic, -1))
     t = torch.clamp(t, max=100.0) + noise_r.to(device)

@@ -1683,7 +1683,7 @@ __global__ __launch_bounds__(kCurvNT, kDebug ? 2 : SSF_FEAT_RUN_WAVES) void k_fe
     // it to a few instructions per register (SQ counters, r5e: 2.8 k SALU per chunk saturated it).
     uint32_t vPl = 0, vPh = 0, vUl = 0, vUh = 0, vEl = 0, vEh = 0;
     auto wl = [](uint32_t& dst, uint32_t val, int k) {        // lane k of dst <- val (uniform)
-        asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(dst) : "s"(val), "s"(k) : "m0");
+        asm("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(val), "{m0}"(k));   // lane select in m0
     };
     auto put = [&](int k, uint64_t mP, uint64_t mE) {
         wl(vPl, (uint32_t)mP, k);

@@ -1788,6 +1788,12 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     const double q[4] = {pose_rel[7 * p], pose_rel[7 * p + 1], pose_rel[7 * p + 2], pose_rel[7 * p + 3]};
     const double t[3] = {pose_rel[7 * p + 4], pose_rel[7 * p + 5], pose_rel[7 * p + 6]};
     const float4* L = last + lo;
+#ifdef SSF_STRIPS_STAMPS
+    // diagnostic build only: per work-group s_memrealtime (100 MHz) and s_memtime (core clock)
+    // at entry, after the staging and after the queries, into nn_out[co + 8 y ..] at the end
+    const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), mt0 = __builtin_amdgcn_s_memtime();
+    unsigned long long rt1 = rt0, mt1 = mt0;
+#endif
     if (ml > lds_cap) {                                                 // uniform
         const PtsF4 g{SP, SI};
         for (int i = q0; i < mc; i += qstep) {
@@ -1812,7 +1818,11 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     const int ns = geo.ns;
     auto strip_of = [&](float y) { return geo.strip_of(y); };
     const StripView<kSoa> v{SL, SX, SI16, ml};
+#ifdef SSF_STRIPS_STAMPS
+    rt1 = __builtin_amdgcn_s_memrealtime(); mt1 = __builtin_amdgcn_s_memtime();
+#else
     if (q0 >= mc) return;                                               // (after the barriers of the build)
+#endif
     for (int i = q0; i < mc; i += qstep) {
         const float4 pc = curr[co + i];
         const float4 qs = assoc_query_point(pc, q, t);
@@ -1899,6 +1909,18 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
         if (nn_out) nn_out[co + i] = vis;
 #endif
     }
+#ifdef SSF_STRIPS_STAMPS
+    __syncthreads();
+    if (tid == 0 && nn_out) {
+        const unsigned long long rt2 = __builtin_amdgcn_s_memrealtime(), mt2 = __builtin_amdgcn_s_memtime();
+        int32_t* o = nn_out + co + 8 * blockIdx.y;
+        o[0] = (int32_t)(rt1 - rt0); o[1] = (int32_t)(rt2 - rt0);
+        o[2] = (int32_t)(mt1 - mt0); o[3] = (int32_t)(mt2 - mt0);
+        o[4] = (int32_t)(rt0 & 0x7fffffff); o[5] = __smid();
+        o[6] = (int32_t)(strip_xyzi && strip_image_frame(ml) && strip_image_valid(strip_head + lo));
+        o[7] = ml;
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2084,6 +2106,10 @@ SSF_DEV int pk(int u, int v) {
 // Valid correspondences of a pair compacted (original order) into LDS once per solve, SoA floats:
 // every evaluation of the LM/GN loop then reads LDS instead of re-streaming the 48-byte records.
 constexpr int kSolveLdsCap = 4096;
+#ifndef SSF_SOLVE_COMPACT1
+#define SSF_SOLVE_COMPACT1 1                     // one-pass compaction of the correspondences (A/B: 0)
+#endif
+constexpr int kCmpPer = 8;                       // records per thread and pass of it
 struct CorrLds {
     float po[3][kSolveLdsCap], pa[3][kSolveLdsCap], n[3][kSolveLdsCap];
 };
@@ -2098,6 +2124,34 @@ SSF_DEV void quat_to_R(const double q[4], double R[9]) {
     R[3] = txy + twz;         R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
     R[6] = txz - twy;         R[7] = tyz + twx;         R[8] = 1.0 - (txx + tyy);
 }
+
+#ifndef SSF_SOLVE_RSQ
+#define SSF_SOLVE_RSQ 1                          // Cholesky pivots by refined v_rsq_f64 (A/B: 0 = sqrt + divide)
+#endif
+// 1 / sqrt(s) (s > 0, normal): v_rsq_f64 and two Newton steps, r <- r + r (1 - s r^2) / 2; the
+// pivot is d = s r (sqrt(s)) and its reciprocal r -- one short chain instead of the f64 sqrt and
+// divide expansions on the solve's critical path (every thread runs it)
+SSF_DEV double rsq_refined(double s) {
+    double r = __builtin_amdgcn_rsq(s);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const double e = __builtin_fma(-s * r, r, 1.0);
+        r = __builtin_fma(0.5 * r, e, r);
+    }
+    return r;
+}
+
+// 1 / x (x > 0, normal): v_rcp_f64 and two Newton steps, r <- r + r (1 - x r) -- the Huber
+// weight a / |r| of an outlier residual without the f64 divide expansion (within an ulp of it)
+SSF_DEV double rcp_refined(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) r = __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
+    return r;
+}
+#ifndef SSF_SOLVE_HUBER_RCP
+#define SSF_SOLVE_HUBER_RCP 0                    // 1: Huber weights by refined rcp / rsq (r5l: 0.0857 vs 0.0808 ms, slower)
+#endif
 
 // Per-correspondence residual r = (R po + t - pa) . n (PlaneFeatureCost, :25-43) and its local
 // Jacobian [2 (R po x n), n]: the EigenQuaternionParameterization's 4x3 Jacobian composed with
@@ -2126,7 +2180,11 @@ SSF_DEV void accum_corr(const double R[9], const double t[3], const double po[3]
     if (s > b) {
         const double rr = fabs(r);
         rho0 = 2.0 * a * rr - b;
+#if SSF_SOLVE_HUBER_RCP
+        rho1 = rr < 1e290 ? a * rcp_refined(rr) : a / rr;
+#else
         rho1 = a / rr;
+#endif
         if (rho1 < DBL_MIN) rho1 = DBL_MIN;
     } else {
         rho0 = s; rho1 = 1.0;
@@ -2168,9 +2226,16 @@ SSF_DEV void accum_edge(const double R[9], const double t[3], const double po[3]
     }
     double rho0, rho1;
     if (s > b) {
+#if SSF_SOLVE_HUBER_RCP
+        const double ri = s < 1e290 ? rsq_refined(s) : 1.0 / sqrt(s);
+        const double rr = s < 1e290 ? s * ri : sqrt(s);
+        rho0 = 2.0 * a * rr - b;
+        rho1 = a * ri;
+#else
         const double rr = sqrt(s);
         rho0 = 2.0 * a * rr - b;
         rho1 = a / rr;
+#endif
         if (rho1 < DBL_MIN) rho1 = DBL_MIN;
     } else {
         rho0 = s; rho1 = 1.0;
@@ -2222,8 +2287,12 @@ SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4],
 #define SSF_SOLVE_STEP 2
 #endif
 constexpr int kSolveStep = SSF_SOLVE_STEP;
+#ifndef SSF_SOLVE_RED
+#define SSF_SOLVE_RED 2                          // 0 block_sum_rs; block_sum_db: 1 DPP one barrier, 2 DPP two, 3 shuffles two
+#endif
+template <int NW>
 SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double t[3],
-                      double (&ne)[kNE], double* lds, int nve = 0) {
+                      double (&ne)[kNE], double* lds, int nve = 0, int parity = 0) {
 #pragma unroll
     for (int k = 0; k < kNE; ++k) ne[k] = 0.0;
     double R[9];
@@ -2249,7 +2318,12 @@ SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double 
                      uu[3] = {C.n[0][i], C.n[1][i], C.n[2][i]};
         accum_edge(R, t, po, pa, uu, 1.0, ne);
     }
+#if SSF_SOLVE_RED == 0
+    (void)parity;
     block_sum_rs<kNE>(ne, lds);
+#else
+    block_sum_db<kNE, NW, SSF_SOLVE_RED != 3, SSF_SOLVE_RED == 1>(ne, lds, parity);
+#endif
 #pragma unroll
     for (int k = 0; k < kNE; ++k) ne[k] *= 2.0;
 }
@@ -2324,8 +2398,14 @@ SSF_DEV int chol_solve_packed(const double (&ne)[kNE], double y[6]) {
 #pragma unroll
         for (int k = 0; k < j; ++k) s -= L[pk(k, j)] * L[pk(k, j)];
         if (!(s > 0.0)) return -1;
+#if SSF_SOLVE_RSQ
+        const double r = (s > 1e-290 && s < 1e290) ? rsq_refined(s) : 1.0 / sqrt(s);
+        const double d = (s > 1e-290 && s < 1e290) ? s * r : sqrt(s);
+        inv[j] = r;
+#else
         const double d = sqrt(s);
         inv[j] = 1.0 / d;
+#endif
         L[pk(j, j)] = d;
 #pragma unroll
         for (int i = j + 1; i < 6; ++i) {
@@ -2370,6 +2450,9 @@ SSF_DEV void write_log(double* log, int max_iter, int p, int idx, const double q
     r[7] = cost; r[8] = status; r[9] = radius;
 }
 
+#ifndef SSF_SOLVE_LM_REG
+#define SSF_SOLVE_LM_REG 1                       // LM state in every thread's registers (A/B: 0 = lane-0 step)
+#endif
 // kEdges: point-to-line blocks (ecorr at ecurr_off / ecurr_count) join every evaluation; they
 // are compacted into the same LDS arrays after the planes.
 template <bool kEdges, int NT>
@@ -2388,9 +2471,13 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
                                                          const int32_t* __restrict__ ecurr_count,
                                                          int32_t* __restrict__ ncorr_edge_out) {
     __shared__ SolveShared S;
-    __shared__ double red[(NT / 64) * kNE];
+    __shared__ double red[2 * (NT / 64 + 1) * kNE];                   // block_sum_db: two halves
     __shared__ CorrLds C;
+#if SSF_SOLVE_COMPACT1
+    __shared__ int wtot2[2][NT / 64];
+#else
     __shared__ int wtot[NT / 64];
+#endif
     const int p = blockIdx.x, tid = threadIdx.x;
     const int n = curr_count[p];
     const CorrRec* rec = corr + curr_off[p];
@@ -2413,9 +2500,53 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
         // to thread i % T in trip i / T; per trip a ballot + the wave counts give every valid
         // record its rank.  kPre trips' records are loaded before the first is used (one load
         // latency per kPre trips).
-        constexpr int kPre = 2;
         const int lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
         const int T = blockDim.x;
+#if SSF_SOLVE_COMPACT1
+        // one pass per kCmpPer x T records: wave w takes a contiguous range of kCmpPer x 64, every
+        // load of the pass in flight at once; per 64-record step a ballot, the ranks from the
+        // wave's own popcounts and ONE exchange of the wave totals (one barrier per pass; the
+        // totals alternate between two LDS rows, so the next pass needs no second barrier)
+        auto compact = [&](const CorrRec* __restrict__ src, int cnt, int start) {
+            int nv = 0;                                                 // uniform
+            for (int i0 = 0, ps = 0; i0 < cnt; i0 += kCmpPer * T, ps ^= 1) {
+                const int wb = i0 + w * kCmpPer * 64;
+                float4 c0[kCmpPer], c1[kCmpPer], c2[kCmpPer];
+#pragma unroll
+                for (int j = 0; j < kCmpPer; ++j) {
+                    const CorrRec* r = src + min(wb + j * 64 + lane, cnt - 1);   // clamped
+                    c0[j] = reinterpret_cast<const float4*>(r)[0];
+                    c1[j] = reinterpret_cast<const float4*>(r)[1];
+                    c2[j] = reinterpret_cast<const float4*>(r)[2];
+                }
+                uint64_t m[kCmpPer];
+                int wt = 0;
+#pragma unroll
+                for (int j = 0; j < kCmpPer; ++j) {
+                    m[j] = __ballot(wb + j * 64 + lane < cnt && c0[j].w != 0.0f);
+                    wt += __popcll(m[j]);
+                }
+                if (lane == 0) wtot2[ps][w] = wt;
+                __syncthreads();
+                int before = start + nv, tot = 0;
+                for (int j = 0; j < nw; ++j) { const int x = wtot2[ps][j]; if (j < w) before += x; tot += x; }
+#pragma unroll
+                for (int j = 0; j < kCmpPer; ++j) {
+                    const int pos = before + __popcll(m[j] & lanemask_lt());
+                    if (((m[j] >> lane) & 1ull) && pos < kSolveLdsCap) {
+                        C.po[0][pos] = c0[j].x; C.po[1][pos] = c0[j].y; C.po[2][pos] = c0[j].z;
+                        C.pa[0][pos] = c1[j].x; C.pa[1][pos] = c1[j].y; C.pa[2][pos] = c1[j].z;
+                        C.n[0][pos] = c2[j].x; C.n[1][pos] = c2[j].y; C.n[2][pos] = c2[j].z;
+                    }
+                    before += __popcll(m[j]);
+                }
+                nv += tot;
+            }
+            __syncthreads();                                            // the LDS records, for every wave
+            return nv;
+        };
+#else
+        constexpr int kPre = 2;
         // records [0, cnt) of src appended at LDS position `start`; returns the valid count
         auto compact = [&](const CorrRec* __restrict__ src, int cnt, int start) {
             int nv = 0;                                                 // uniform
@@ -2442,6 +2573,7 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
             }
             return nv;
         };
+#endif
         const int nv = compact(rec, n, 0);
         const int nve = kEdges ? compact(erec, en, nv) : 0;
         const bool in_lds = nv + nve <= kSolveLdsCap;                  // uniform
@@ -2450,9 +2582,11 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
 #endif
         if (tid == 0 && ncorr_out) ncorr_out[p] = nv;
         if (kEdges && tid == 0 && ncorr_edge_out) ncorr_edge_out[p] = nve;
+        int par = 0;                                                    // block_sum_dpp's LDS half
         auto eval_at = [&](const double* qq, const double* tt, double (&ne_)[kNE]) {
-            if (in_lds) evaluate(C, nv, qq, tt, ne_, red, nve);
+            if (in_lds) evaluate<NT / 64>(C, nv, qq, tt, ne_, red, nve, par);
             else evaluate(rec, n, qq, tt, ne_, red, erec, en);
+            par ^= 1;
         };
         double ne[kNE];
         double q[4], t[3];
@@ -2462,12 +2596,14 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
 #ifdef SSF_SOLVE_STAMPS
         st2 = __builtin_amdgcn_s_memtime();
 #endif
+#if !SSF_SOLVE_LM_REG
         if (tid == 0) {
             for (int k = 0; k < kNE; ++k) S.ne[k] = ne[k];
             for (int u = 0; u < 6; ++u) S.s[u] = 1.0 / (1.0 + sqrt(ne[pk(u, u)]));
             S.radius = 1e4; S.dec = 2.0; S.invalid = 0;
         }
         __syncthreads();
+#endif
         if (mode == SSF_SOLVER_GN) {
             // every thread holds the same sums after the block reduction, so every thread runs
             // the same 6x6 solve on the same bits and carries the same pose: no lane-0 step, no
@@ -2495,6 +2631,116 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
             }
             __syncthreads();
         } else {
+#if SSF_SOLVE_LM_REG
+            // every thread carries the LM state (accepted pose and normal equations, scaling,
+            // radius) in registers and runs the same step on the same bits, as the GN path does:
+            // no lane-0 section that the other 255 threads wait on at two barriers per iteration,
+            // no LDS round trips on the serial chain, the 6x6 solve by rsq pivots
+            double qa[4], ta[3], na[kNE], sc[6];
+            for (int k = 0; k < 4; ++k) qa[k] = q[k];
+            for (int k = 0; k < 3; ++k) ta[k] = t[k];
+#pragma unroll
+            for (int k = 0; k < kNE; ++k) na[k] = ne[k];
+#pragma unroll
+            for (int u = 0; u < 6; ++u) sc[u] = 1.0 / (1.0 + sqrt(ne[pk(u, u)]));
+            double radius = 1e4, dec = 2.0;
+            int invalid = 0, nl = 0;
+            for (int it = 1; it <= max_iter; ++it) {
+                // LevenbergMarquardtStrategy::ComputeStep on the Jacobi-scaled system: m holds
+                // M = As + diag(clamp(As_uu)) / radius packed, and gs, so chol_solve_packed
+                // solves M y = -gs
+                double As[21], m[kNE], y[6];
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    m[21 + u] = sc[u] * na[21 + u];
+#pragma unroll
+                    for (int v = u; v < 6; ++v) As[pk(u, v)] = sc[u] * na[pk(u, v)] * sc[v];
+                }
+#pragma unroll
+                for (int k = 0; k < 21; ++k) m[k] = As[k];
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    double d = As[pk(u, u)];
+                    if (d < 1e-6) d = 1e-6;
+                    if (d > 1e32) d = 1e32;
+                    m[pk(u, u)] += d / radius;
+                }
+                const bool ok = chol_solve_packed(m, y) == 0;             // uniform
+                double mcc = 0.0;
+                if (ok) {
+                    double yg = 0.0, yAy = 0.0;
+#pragma unroll
+                    for (int u = 0; u < 6; ++u) {
+                        yg += y[u] * m[21 + u];
+                        double Ay = 0.0;
+#pragma unroll
+                        for (int v = 0; v < 6; ++v) Ay += As[pk(u, v)] * y[v];
+                        yAy += y[u] * Ay;
+                    }
+                    mcc = -(yg + 0.5 * yAy);
+                }
+                if (!ok || !(mcc > 0.0)) {
+                    radius /= dec; dec *= 2.0;
+                    if (tid == 0) write_log(log, max_iter, p, nl, qa, ta, na[27], 2, radius);
+                    ++nl;
+                    if (++invalid > 5) break;
+                    continue;
+                }
+                invalid = 0;
+                double delta[6], qc[4], tc[3];
+#pragma unroll
+                for (int u = 0; u < 6; ++u) delta[u] = y[u] * sc[u];
+                quat_plus_step(qa, delta, qc);
+                tc[0] = ta[0] + delta[3]; tc[1] = ta[1] + delta[4]; tc[2] = ta[2] + delta[5];
+                eval_at(qc, tc, ne);
+                double xn = 0.0, sn = 0.0;
+                for (int u = 0; u < 4; ++u) { xn += qa[u] * qa[u]; sn += (qa[u] - qc[u]) * (qa[u] - qc[u]); }
+                for (int u = 0; u < 3; ++u) { xn += ta[u] * ta[u]; sn += (ta[u] - tc[u]) * (ta[u] - tc[u]); }
+                xn = sqrt(xn); sn = sqrt(sn);
+                const double dcost = na[27] - ne[27];
+                if (!(sn > (xn + 1e-8) * 1e-8)) {                       // ParameterToleranceReached
+                    if (tid == 0) write_log(log, max_iter, p, nl, qa, ta, na[27], 3, radius);
+                    ++nl;
+                    break;
+                }
+                if (!(fabs(dcost) > 1e-6 * na[27])) {                   // FunctionToleranceReached
+                    if (tid == 0) write_log(log, max_iter, p, nl, qa, ta, na[27], 4, radius);
+                    ++nl;
+                    break;
+                }
+                const double rho = dcost / mcc;
+                if (rho > 1e-3) {                                       // accept
+                    for (int k = 0; k < 4; ++k) qa[k] = qc[k];
+                    for (int k = 0; k < 3; ++k) ta[k] = tc[k];
+#pragma unroll
+                    for (int k = 0; k < kNE; ++k) na[k] = ne[k];
+                    const double f = 2.0 * rho - 1.0;
+                    double den = 1.0 - f * f * f;
+                    if (den < 1.0 / 3.0) den = 1.0 / 3.0;
+                    radius = radius / den;
+                    if (radius > 1e16) radius = 1e16;
+                    dec = 2.0;
+                    const double mg[3] = {-ne[21], -ne[22], -ne[23]};
+                    double qg[4], gm = 0.0;
+                    quat_plus(qa, mg, qg);
+                    for (int u = 0; u < 4; ++u) gm = fmax(gm, fabs(qa[u] - qg[u]));
+                    for (int u = 3; u < 6; ++u) gm = fmax(gm, fabs(ne[21 + u]));
+                    const bool conv = gm <= 1e-10;                      // GradientToleranceReached
+                    if (tid == 0) write_log(log, max_iter, p, nl, qa, ta, na[27], conv ? 5 : 1, radius);
+                    ++nl;
+                    if (conv) break;
+                } else {                                                // reject
+                    radius /= dec; dec *= 2.0;
+                    if (tid == 0) write_log(log, max_iter, p, nl, qa, ta, na[27], 0, radius);
+                    ++nl;
+                }
+            }
+            if (tid == 0) {
+                for (int k = 0; k < 4; ++k) S.q[k] = qa[k];
+                for (int k = 0; k < 3; ++k) S.t[k] = ta[k];
+                S.nlog = nl;
+            }
+#else
             for (int it = 1; it <= max_iter; ++it) {
                 if (tid == 0) {
                     // LevenbergMarquardtStrategy::ComputeStep on the Jacobi-scaled system
@@ -2589,6 +2835,7 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
                 __syncthreads();
                 if (S.done) break;
             }
+#endif
         }
     } else if (tid == 0) {
         if (ncorr_out) ncorr_out[p] = -1;

@@ -87,6 +87,83 @@ SSF_DEV void block_sum_rs(double (&v)[N], double* lds) {
     __syncthreads();
 }
 
+// block_sum_rs with the first four butterfly steps as DPP lane permutes (VALU; a shuffle is an
+// LDS-unit round trip, and with one wave per SIMD k_solve's evaluations wait on each one) and
+// the LDS staging double-buffered: the partials go to one of two LDS halves, alternating per call
+// (`parity`), so no trailing barrier protects them from the next call.  The steps pair lanes as
+// row_mirror (i <-> 15 - i: bit 3), row_half_mirror (i <-> 7 - i: bit 2), quad_perm xor 2 and
+// xor 1 -- each pairs lanes that hold the same value subset -- then xor 16 and xor 32 by
+// shuffles; lane L ends with value idx = L3 L2 L1 L0 L4 (bits).  ONE_BARRIER: every thread adds
+// the NW waves' partials of all N values itself (NW x N broadcast LDS reads, one barrier); else
+// thread k < N adds value k's and all threads read the N totals (two barriers).  lds must hold
+// 2 x (NW + 1) x N doubles.  Fixed order: the same bits on every run.
+SSF_DEV double dpp_perm_f64(double v, int ctrl_id) {
+    const uint64_t b = __double_as_longlong(v);
+    int lo = (int)(uint32_t)b, hi = (int)(uint32_t)(b >> 32);
+    switch (ctrl_id) {                                         // compile-time after unrolling
+        case 0: lo = __builtin_amdgcn_mov_dpp(lo, 0x140, 0xf, 0xf, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x140, 0xf, 0xf, false); break;
+        case 1: lo = __builtin_amdgcn_mov_dpp(lo, 0x141, 0xf, 0xf, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x141, 0xf, 0xf, false); break;
+        case 2: lo = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xf, 0xf, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xf, 0xf, false); break;
+        default: lo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xf, 0xf, false); hi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xf, 0xf, false); break;
+    }
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
+template <int N, int NW, bool DPP, bool ONE_BARRIER>
+SSF_DEV void block_sum_db(double (&v)[N], double* lds, int parity) {
+    static_assert(N <= 32, "block_sum_db: N <= 32");
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    double a[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) a[i] = i < N ? v[i] : 0.0;
+    constexpr int kBitDpp[5] = {8, 4, 2, 1, 16}, kBitShfl[5] = {32, 16, 8, 4, 2};
+#pragma unroll
+    for (int st = 0, h = 16; st < 5; ++st, h >>= 1) {
+        const int bit = DPP ? kBitDpp[st] : kBitShfl[st];
+        const bool up = (lane & bit) != 0;
+#pragma unroll
+        for (int i = 0; i < h; ++i) {
+            const double keep = up ? a[h + i] : a[i];
+            const double send = up ? a[i] : a[h + i];
+            a[i] = keep + ((DPP && st < 4) ? dpp_perm_f64(send, st) : __shfl_xor(send, bit, kWave));
+        }
+    }
+    int idx;
+    bool wr;
+    if (DPP) {
+        a[0] += __shfl_xor(a[0], 32, kWave);
+        idx = (((lane >> 3) & 1) << 4) | (((lane >> 2) & 1) << 3) | (((lane >> 1) & 1) << 2) |
+              ((lane & 1) << 1) | ((lane >> 4) & 1);
+        wr = lane < 32;
+    } else {
+        a[0] += __shfl_xor(a[0], 1, kWave);
+        idx = lane >> 1;
+        wr = (lane & 1) == 0;
+    }
+    double* L = lds + parity * (NW + 1) * N;
+    if (wr && idx < N) L[w * N + idx] = a[0];
+    __syncthreads();
+    if (ONE_BARRIER) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            double s = L[k];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) s += L[i * N + k];
+            v[k] = s;
+        }
+    } else {
+        if (threadIdx.x < N) {
+            double s = L[threadIdx.x];
+#pragma unroll
+            for (int i = 1; i < NW; ++i) s += L[i * N + threadIdx.x];
+            L[NW * N + threadIdx.x] = s;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] = L[NW * N + k];
+    }
+}
+
 template <typename T>
 SSF_DEV T block_sum_scalar(T x, T* lds) {
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--distinct", type=int, default=16)
     ap.add_argument("--chain", action="store_true", help="also plane table + registration")
     ap.add_argument("--layout", default="azimuth", choices=["azimuth", "carla"])
+    ap.add_argument("--solver", default="gn", choices=["gn", "ceres_lm"])
     ap.add_argument("--tag", default=os.environ.get("SSF_LIB", "default"))
     ap.add_argument("--dump", default=None, help="with --chain: write the last plane table (normals, validity) "
                     "and registration poses to this .npz")
@@ -41,7 +42,7 @@ def main():
             for b in range(s, B, a.distinct):
                 pos[k][b * N:(b + 1) * N].copy_(f["pos1"])
     off, h_off = ssf.frame_offsets([N] * B, dev)
-    fe = ssf.Frontend(64, device=0, solver="gn", max_iter=10)
+    fe = ssf.Frontend(64, device=0, solver=a.solver, max_iter=10 if a.solver == "gn" else 8)
     fe.reserve(B, N)
     rel = ssf.identity_poses(B, dev)
     for r in range(a.reps + 1):

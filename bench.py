@@ -131,6 +131,9 @@ def parse(argv=None):
                          "prints the world it sees and exits (no GPU is touched)")
     ap.add_argument("--mask-split", type=int, default=0,
                     help="work-groups per frame of the GMM fit (0: automatic, ssf_set_mask_split)")
+    ap.add_argument("--no-chain-api", action="store_true",
+                    help="with --consecutive and one sequence: one ssf_register_batch call per chained pair "
+                         "(the round-4 path) instead of ssf_register_chain")
     ap.add_argument("--consecutive", type=int, default=0,
                     help="BASELINE configs[2] as written: K consecutive frame pairs of each sequence "
                          "per step (mask of K frames in one launch, masked features, K chained "
@@ -911,6 +914,20 @@ def sequences(args, world=1, rank=0, local=0):
                 if K > 1:
                     fe_reg.register(*view(pb, table, 0, K - 1), view(pb, table, 1, K)[0], ws[B:])
                 rel_k = ws.view(K, B, 7)
+            elif B == 1 and not args.no_chain_api:
+                # one sequence: the boundary pair (the previous step's last frame -> frame 0) by
+                # ssf_register_batch, then the K - 1 pairs inside this step's batch by ONE
+                # ssf_register_chain call (each link reads the previous solution in place: no
+                # per-pair copy launches, no per-pair host calls)
+                seq = torch.empty((K, 7), dtype=torch.float64, device=dev)
+                seq[0:1].copy_(rel)
+                fe_reg.register(lpb, ltab, view(pb, table, 0)[0], seq[0:1], ab)
+                if K > 1:
+                    ch = fe_reg.register_chain(view(pb, table, 0, K)[0], table, seq[0], pose_abs_init=ab,
+                                               out=seq[1:])
+                    ab.copy_(ch["pose_abs_seq"][-1:])
+                rel.copy_(seq[K - 1:K])
+                rel_k = seq.view(K, 1, 7)
             else:
                 snaps = []
                 for kk in range(K):
@@ -984,7 +1001,9 @@ def sequences(args, world=1, rank=0, local=0):
     frames = total_seq * K * S
     ws_note = ("every pair warm-started from its own SSF Kabsch pose (beyond the reference: "
                "independent pairs, 2 launches per step)" if kws else
-               f"{K} chained registrations per step (warm start = previous solution)")
+               f"{K} chained registrations per step (warm start = previous solution"
+               + ("; the boundary pair + one ssf_register_chain call of K - 1 pairs)"
+                  if B == 1 and not args.no_chain_api else "; one call per pair)"))
     if strong:
         workload = (f"configs[3] as written: {total_seq} sequences sharded over {world} GPU(s) "
                     f"(sequence_shard), {K} consecutive frames of each per step, {S} steps "

@@ -188,6 +188,27 @@ int32_t ssf_register_batch(ssf_ctx* ctx, void* stream, int32_t n_pairs,
                            double* d_log, int32_t* d_nlog, int32_t* d_ncorr, int32_t* d_nn,
                            const float* d_last_strip_xyzi, const int32_t* d_last_strip_head);
 
+/* A sequence's consecutive pairs in one call (lidarOdometry_onlyPC's frame loop over a sequence:
+ * every pair is warm-started from the previous pair's solution, src/lidarOdometry_onlyPC.cpp:164,
+ * 251-252).  Frames 0..n_pairs of ONE plane batch (d_off / d_count: n_pairs + 2 / n_pairs + 1
+ * entries, the table / search index / strip image of ssf_plane_table_batch on the same batch);
+ * pair k registers frame k + 1 (curr) against frame k (last).
+ *   d_pose_init [7]          warm start of pair 0 (q xyzw, t)
+ *   d_pose_seq [n_pairs*7]   out: pair k's solution (the warm start of pair k + 1)
+ *   d_pose_abs_init [7] / d_pose_abs_seq [n_pairs*7]  nullable (both or neither): the pose of
+ *                            frame 0, and out the pose of frame k + 1 (:87-90)
+ *   d_ncorr [n_pairs]        nullable: correspondences per pair (-1 when skipped, :158)
+ * Results are identical to n_pairs ssf_register_batch calls of one pair each with the warm start
+ * copied between them; the links read the previous output in place (no copy launches). */
+int32_t ssf_register_chain(ssf_ctx* ctx, void* stream, int32_t n_pairs, const float* d_xyzi,
+                           const int64_t* d_off, const int32_t* d_count, const float* d_normal,
+                           const uint8_t* d_valid, const float* d_sorted_xyzi,
+                           const int32_t* d_sorted_idx, int64_t total_points,
+                           int64_t max_plane_points, const double* d_pose_init,
+                           double* d_pose_seq, const double* d_pose_abs_init,
+                           double* d_pose_abs_seq, int32_t* d_ncorr,
+                           const float* d_strip_xyzi, const int32_t* d_strip_head);
+
 /* Single-pair form with the SURVEY §8(b) signature: frameRegistration() on the globals
  * lastFramePlanePtr / currFramePlanePtr / para_q / para_t (src/lidarOdometry_onlyPC.cpp:51-71,
  * 147-252).  The plane clouds are device float4 (x, y, z, intensity) as frameFeature publishes

@@ -538,6 +538,45 @@ int32_t ssf_register_batch(ssf_ctx* c, void* stream, int32_t n_pairs, const floa
     return SSF_OK;
 }
 
+int32_t ssf_register_chain(ssf_ctx* c, void* stream, int32_t n_pairs, const float* d_xyzi,
+                           const int64_t* d_off, const int32_t* d_count, const float* d_normal,
+                           const uint8_t* d_valid, const float* d_sorted_xyzi,
+                           const int32_t* d_sorted_idx, int64_t total_points,
+                           int64_t max_plane_points, const double* d_pose_init,
+                           double* d_pose_seq, const double* d_pose_abs_init,
+                           double* d_pose_abs_seq, int32_t* d_ncorr,
+                           const float* d_strip_xyzi, const int32_t* d_strip_head) {
+    if (!c) return SSF_E_ARG;
+    if (n_pairs < 0 || total_points < 0 || max_plane_points < 0 ||
+        (n_pairs > 0 && (!d_xyzi || !d_off || !d_count || !d_normal || !d_valid || !d_pose_init ||
+                         !d_pose_seq)) ||
+        (!d_pose_abs_init != !d_pose_abs_seq))
+        return fail(c, SSF_E_ARG, "register_chain: bad arguments");
+    if (!d_strip_xyzi != !d_strip_head || (d_strip_xyzi && (!d_sorted_xyzi || !d_sorted_idx)))
+        return fail(c, SSF_E_ARG, "register_chain: the strip image needs both strip buffers and the sorted buffers");
+    if (n_pairs == 0) return SSF_OK;
+    SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
+    SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(total_points, 1)), "alloc corr");
+    ProfScope prof(c, stream);
+    // pair k = (frame k, frame k + 1) of the same arrays: its warm start is pair k - 1's output
+    // slot (lidarOdometry_onlyPC.cpp:164,251-252), read in place by the association and the
+    // solve -- no copy between the links, two launches per pair, all enqueued here
+    const float4* X = reinterpret_cast<const float4*>(d_xyzi);
+    for (int k = 0; k < n_pairs; ++k) {
+        hipError_t e = ssf::launch_register(
+            (hipStream_t)stream, c->cfg, 1, X, d_off + k, d_count + k, d_normal, d_valid,
+            reinterpret_cast<const float4*>(d_sorted_xyzi), d_sorted_idx, X, d_off + k + 1,
+            d_count + k + 1, max_plane_points, c->corr.as<ssf::CorrRec>(), d_pose_seq + 7 * k,
+            d_pose_abs_seq ? d_pose_abs_seq + 7 * k : nullptr, nullptr, nullptr,
+            d_ncorr ? d_ncorr + k : nullptr, nullptr, nullptr,
+            reinterpret_cast<const float4*>(d_strip_xyzi), d_strip_head,
+            k == 0 ? d_pose_init : d_pose_seq + 7 * (k - 1),
+            d_pose_abs_seq ? (k == 0 ? d_pose_abs_init : d_pose_abs_seq + 7 * (k - 1)) : nullptr);
+        if (e != hipSuccess) return hip_fail(c, e, "register_chain launch");
+    }
+    return SSF_OK;
+}
+
 int32_t ssf_register_batch_edges(ssf_ctx* c, void* stream, int32_t n_pairs,
                                  const float* d_last_xyzi, const int64_t* d_last_off,
                                  const int32_t* d_last_count, const float* d_last_normal,

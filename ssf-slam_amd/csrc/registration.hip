@@ -1765,7 +1765,27 @@ __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
 // kSoa: the strip-major points as x | y | z float arrays and a u16 original index (configs[4]
 // frames); otherwise float4 with the index in .w.  A last frame above the launch's staging
 // capacity walks the x-sorted copy in global memory, unbounded (exact, slow, not expected).
-template <bool kSoa>
+#ifndef SSF_ASSOC_DEFER
+#define SSF_ASSOC_DEFER 0                        // 1: far queries of the lane mode to a wave each (r5u: 256-pair launch 0.135 -> 0.200 ms)
+#endif
+#ifndef SSF_ASSOC_DEFER_R
+#define SSF_ASSOC_DEFER_R 4.0f
+#endif
+constexpr int kAssocDeferMax = 512;              // deferred queries per work-group (more: the lane goes on)
+constexpr float kAssocDeferR = SSF_ASSOC_DEFER_R; // a query still open after this level is deferred
+// kCoopG > 0 (launches of few pairs: a node's one pair, configs[2]'s chained pairs): one query
+// per group of kCoopG lanes instead of one per lane -- the query's strips of each search level
+// spread over the group's lanes (one strip per lane), so no lane walks ring after ring alone,
+// and (kStripThreads / kCoopG) queries per work-group over ceil(m / that) work-groups per pair
+// (each stages the last frame).  The lane mode's nested divergent loops (levels, rings, walks)
+// leave a wave at the pace of its slowest lane: SQ counters in the chain, r5w: ~138 LDS
+// instructions per wave over ~51 k wave-cycles, 56 % of them waiting.
+#ifndef SSF_ASSOC_COOP_G
+#define SSF_ASSOC_COOP_G 16
+#endif
+constexpr int kAssocCoopG = SSF_ASSOC_COOP_G;
+constexpr int kAssocCoopPairs = 16;             // launches of at most this many pairs take the group mode
+template <bool kSoa, int kCoopG = 0>
 __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     const float4* __restrict__ last, const int64_t* __restrict__ last_off,
     const int32_t* __restrict__ last_count, const float* __restrict__ last_normal,
@@ -1776,12 +1796,21 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     int lds_cap, const float4* __restrict__ strip_xyzi, const int32_t* __restrict__ strip_head) {
     extern __shared__ float4 SL[];                  // [ml] strip-major, x-sorted in each strip
     __shared__ StripLds T;
+#if SSF_ASSOC_DEFER
+    // far queries, answered a wave each at the end (the SoA launch has ~0.3 KiB of LDS left)
+    constexpr int kDq = kSoa ? kAssocDeferMax / 4 : kAssocDeferMax;
+    __shared__ int dq[kDq];
+    __shared__ int dqn;
+    if (threadIdx.x == 0) dqn = 0;                  // (the staging's barriers order it)
+#endif
     // gridDim.y work-groups per pair (few pairs in a launch): each stages the whole last frame
     // and answers every gridDim.y-th block of kStripThreads queries
     const int p = blockIdx.x, tid = threadIdx.x;
     const int q0 = tid + (int)blockIdx.y * kStripThreads, qstep = kStripThreads * (int)gridDim.y;
     const int mc = curr_count[p], ml = last_count[p];
     if (mc <= 0 || ml <= 10) return;                                    // uniform (:158)
+    constexpr int kQpw = kCoopG > 0 ? kStripThreads / kCoopG : kStripThreads;   // queries per work-group
+    if (kCoopG > 0 && (int)blockIdx.y * kQpw >= mc) return;             // uniform: no query here
     const int64_t lo = last_off[p], co = curr_off[p];
     const float4* SP = last_sorted + lo;
     const int32_t* SI = last_sidx + lo;
@@ -1820,60 +1849,102 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     const StripView<kSoa> v{SL, SX, SI16, ml};
 #ifdef SSF_STRIPS_STAMPS
     rt1 = __builtin_amdgcn_s_memrealtime(); mt1 = __builtin_amdgcn_s_memtime();
-#else
-    if (q0 >= mc) return;                                               // (after the barriers of the build)
+#elif !SSF_ASSOC_DEFER
+    if (kCoopG == 0 && q0 >= mc) return;                                // (after the barriers of the build)
 #endif
-    for (int i = q0; i < mc; i += qstep) {
+#ifdef SSF_ASSOC_COUNT
+    int vis = 0;
+#endif
+    // one strip: points with dx^2 + dymin^2 <= min(best, lim) (lim = R^2 of the search radius)
+    auto search = [&](int sidx, float lim, const float4& qs, float& best, int& bc) __attribute__((always_inline)) {
+        const int a = T.start[sidx], b = T.start[sidx + 1];
+        if (a >= b) return;
+        const float yl = T.ylo[sidx], yh = T.yhi[sidx];
+        const float dyl = qs.y < yl ? yl - qs.y : (qs.y > yh ? qs.y - yh : 0.0f);
+        const float dy2 = dyl * dyl;
+        if (dy2 > fminf(best, lim)) return;
+#ifdef SSF_ASSOC_COUNT
+        vis += 1 << 16;                                                  // strip searches (high half)
+#endif
+        int l = a, h = b;                                                // first x >= qs.x
+        while (l < h) {
+            const int mid = (l + h) >> 1;
+            if (v.x(mid) < qs.x) l = mid + 1; else h = mid;
+        }
+        // the next record is read while the current one is processed (clamped into the strip)
+        if (l < b) {
+            float4 pn = v.pt(l);
+            for (int c = l; c < b; ++c) {
+                const float4 pl = pn;
+                pn = v.pt(min(c + 1, b - 1));
+                const float dx = qs.x - pl.x;
+                if (dx * dx + dy2 > fminf(best, lim)) break;
+                const float d = l2_simple(qs, pl);
+                if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
+#ifdef SSF_ASSOC_COUNT
+                ++vis;
+#endif
+            }
+        }
+        if (l > a) {
+            float4 pn = v.pt(l - 1);
+            for (int c = l - 1; c >= a; --c) {
+                const float4 pl = pn;
+                pn = v.pt(max(c - 1, a));
+                const float dx = qs.x - pl.x;
+                if (dx * dx + dy2 > fminf(best, lim)) break;
+                const float d = l2_simple(qs, pl);
+                if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
+#ifdef SSF_ASSOC_COUNT
+                ++vis;
+#endif
+            }
+        }
+    };
+    if (kCoopG > 0) {
+        // one query per kCoopG-lane group (groups are aligned lane ranges: the reductions stay
+        // inside one), the same levels and bounds as the deferred pass below
+        const int gl = tid % kCoopG, i = (int)blockIdx.y * kQpw + tid / kCoopG;
+        if (i < mc) {                                                   // uniform per group
+            const float4 pc = curr[co + i];
+            const float4 qs = assoc_query_point(pc, q, t);
+            float best = __builtin_inff();
+            int bc = -1;
+            unsigned long long key = ~0ull;
+            for (float R = 2.0f;; R *= 2.0f) {
+                const bool unbounded = R > 4096.0f;
+                const float lim = unbounded ? __builtin_inff() : R * R;
+                const int sa = unbounded ? 0 : strip_of(qs.y - R - W - 1e-3f);
+                const int sb = unbounded ? ns - 1 : strip_of(qs.y + R + W + 1e-3f);
+                for (int sidx = sa + gl; sidx <= sb; sidx += kCoopG) search(sidx, lim, qs, best, bc);
+                unsigned long long k = bc >= 0
+                    ? ((unsigned long long)__float_as_uint(best) << 32) | (unsigned)v.id(bc) : ~0ull;
+#pragma unroll
+                for (int o = kCoopG / 2; o >= 1; o >>= 1) {
+                    const unsigned long long x = __shfl_xor(k, o, kWave);
+                    k = x < k ? x : k;
+                }
+                key = k < key ? k : key;
+                const float wb = key == ~0ull ? __builtin_inff() : __uint_as_float((unsigned)(key >> 32));
+                if (wb <= lim || unbounded) break;
+                best = wb; bc = -1;
+            }
+            if (gl == 0) {
+                assoc_finish(L, lo, last_normal, last_valid, pc, (int)(key & 0xffffffffu), corr, nn_out, co + i);
+#ifdef SSF_ASSOC_COUNT
+                if (nn_out) nn_out[co + i] = vis;
+#endif
+            }
+        }
+    }
+    for (int i = q0; i < (kCoopG > 0 ? 0 : mc); i += qstep) {
         const float4 pc = curr[co + i];
         const float4 qs = assoc_query_point(pc, q, t);
         float best = __builtin_inff();
         int bc = -1;
 #ifdef SSF_ASSOC_COUNT
-        int vis = 0;
+        vis = 0;
 #endif
-        // walks stop at min(best, lim): lim = R^2 of the current search radius
-        auto search = [&](int sidx, float lim) __attribute__((always_inline)) {
-            const int a = T.start[sidx], b = T.start[sidx + 1];
-            if (a >= b) return;
-            const float yl = T.ylo[sidx], yh = T.yhi[sidx];
-            const float dyl = qs.y < yl ? yl - qs.y : (qs.y > yh ? qs.y - yh : 0.0f);
-            const float dy2 = dyl * dyl;
-            if (dy2 > fminf(best, lim)) return;
-            int l = a, h = b;                                            // first x >= qs.x
-            while (l < h) {
-                const int mid = (l + h) >> 1;
-                if (v.x(mid) < qs.x) l = mid + 1; else h = mid;
-            }
-            // the next record is read while the current one is processed (clamped into the strip)
-            if (l < b) {
-                float4 pn = v.pt(l);
-                for (int c = l; c < b; ++c) {
-                    const float4 pl = pn;
-                    pn = v.pt(min(c + 1, b - 1));
-                    const float dx = qs.x - pl.x;
-                    if (dx * dx + dy2 > fminf(best, lim)) break;
-                    const float d = l2_simple(qs, pl);
-                    if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
-#ifdef SSF_ASSOC_COUNT
-                    ++vis;
-#endif
-                }
-            }
-            if (l > a) {
-                float4 pn = v.pt(l - 1);
-                for (int c = l - 1; c >= a; --c) {
-                    const float4 pl = pn;
-                    pn = v.pt(max(c - 1, a));
-                    const float dx = qs.x - pl.x;
-                    if (dx * dx + dy2 > fminf(best, lim)) break;
-                    const float d = l2_simple(qs, pl);
-                    if (assoc_better(v, c, d, best, bc)) { best = d; bc = c; }
-#ifdef SSF_ASSOC_COUNT
-                    ++vis;
-#endif
-                }
-            }
-        };
         // Radius doubling (R = 2, 4, 8, ... m, then unbounded): a level visits, strip ring by
         // strip ring from the query's, every point with dx^2 + dymin^2 <= min(best, R^2).  Once
         // best <= R^2 every point as close as best has been seen (its lower bound is <= its
@@ -1881,10 +1952,11 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
         // hole, BASELINE configs[2]) therefore walks the points within ~2x its 1-NN distance,
         // not every point within the distance of the first point its own strip happens to hold.
         const int s0 = strip_of(qs.y);
+        bool deferred = false;
         for (float R = 2.0f;; R *= 2.0f) {
             const bool unbounded = R > 4096.0f;                          // uniform per lane
             const float lim = unbounded ? __builtin_inff() : R * R;
-            search(s0, lim);
+            search(s0, lim, qs, best, bc);
             bool up = true, dn = true;
             for (int rr = 1; up || dn; ++rr) {
                 const float bnd = fminf(best, lim);
@@ -1893,29 +1965,90 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
                     // every point of strips >= su has y >= y0 + su W (less float slack)
                     const float gap = (y0 + (float)su * W) - qs.y - 1e-3f;
                     if (su >= ns || (gap > 0.0f && gap * gap > bnd)) up = false;
-                    else search(su, lim);
+                    else search(su, lim, qs, best, bc);
                 }
                 if (dn) {
                     const int sd = s0 - rr;
                     const float gap = qs.y - (y0 + (float)(sd + 1) * W) - 1e-3f;
                     if (sd < 0 || (gap > 0.0f && gap * gap > bnd)) dn = false;
-                    else search(sd, lim);
+                    else search(sd, lim, qs, best, bc);
                 }
             }
             if (best <= lim || unbounded) break;
+#if SSF_ASSOC_DEFER
+            // a far 1-NN: the next levels' ~4 R / W strip searches in a row on one lane set the
+            // wave's (and often the launch's) time -- hand the query to the work-group's queue,
+            // answered below by a whole wave, one strip per lane
+            if (R >= kAssocDeferR) {
+                const int slot = atomicAdd(&dqn, 1);
+                if (slot < kDq) { dq[slot] = i; deferred = true; break; }
+            }
+#endif
         }
-        assoc_finish(L, lo, last_normal, last_valid, pc, v.id(max(bc, 0)), corr, nn_out, co + i);
+        if (!deferred) assoc_finish(L, lo, last_normal, last_valid, pc, v.id(max(bc, 0)), corr, nn_out, co + i);
 #ifdef SSF_ASSOC_COUNT
-        if (nn_out) nn_out[co + i] = vis;
+        if (nn_out && !deferred) nn_out[co + i] = vis;
 #endif
     }
+#if SSF_ASSOC_DEFER
+    // Deferred queries, one per wave: each level R searches every strip that can hold a point
+    // within R (nominal band [qy - R - W, qy + R + W]), one strip per lane, each lane bounded by
+    // min(its best, R^2) and, from the second level on, by the wave's best; then the wave's
+    // minimum of (distance, original index).  The same exact 1-NN as the lane walk: at the level
+    // where the wave's best is <= R^2, every point at least as close was in a searched strip and
+    // within every lane's bound.
+    __syncthreads();
+#ifdef SSF_STRIPS_STAMPS
+    const unsigned long long rtl = __builtin_amdgcn_s_memrealtime();   // the slowest wave's lane pass
+#endif
+    if (kCoopG == 0) {
+        const int nq = min(dqn, kDq), lane = tid & 63;
+        for (int e = tid >> 6; e < nq; e += kStripThreads / 64) {
+            const int i = dq[e];                                          // uniform per wave
+            const float4 pc = curr[co + i];
+            const float4 qs = assoc_query_point(pc, q, t);
+            float best = __builtin_inff();
+            int bc = -1;
+            unsigned long long key = ~0ull;
+            for (float R = 2.0f;; R *= 2.0f) {
+                const bool unbounded = R > 4096.0f;
+                const float lim = unbounded ? __builtin_inff() : R * R;
+                const int sa = unbounded ? 0 : strip_of(qs.y - R - W - 1e-3f);
+                const int sb = unbounded ? ns - 1 : strip_of(qs.y + R + W + 1e-3f);
+                for (int sidx = sa + lane; sidx <= sb; sidx += 64) search(sidx, lim, qs, best, bc);
+                unsigned long long k = bc >= 0
+                    ? ((unsigned long long)__float_as_uint(best) << 32) | (unsigned)v.id(bc) : ~0ull;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) {
+                    const unsigned long long x = __shfl_xor(k, o, kWave);
+                    k = x < k ? x : k;
+                }
+                key = k < key ? k : key;
+                const float wb = key == ~0ull ? __builtin_inff() : __uint_as_float((unsigned)(key >> 32));
+                if (wb <= lim || unbounded) break;
+                best = wb; bc = -1;          // the wave's bound (a tie taken later only raises a key)
+            }
+            if (lane == 0) {
+                assoc_finish(L, lo, last_normal, last_valid, pc, (int)(key & 0xffffffffu), corr, nn_out, co + i);
+#ifdef SSF_ASSOC_COUNT
+                if (nn_out) nn_out[co + i] = -1;                        // deferred (diagnostic build)
+#endif
+            }
+        }
+    }
+#endif
 #ifdef SSF_STRIPS_STAMPS
     __syncthreads();
     if (tid == 0 && nn_out) {
         const unsigned long long rt2 = __builtin_amdgcn_s_memrealtime(), mt2 = __builtin_amdgcn_s_memtime();
-        int32_t* o = nn_out + co + 8 * blockIdx.y;
+        int32_t* o = nn_out + co + kQpw * blockIdx.y;                // this work-group's own query slots
         o[0] = (int32_t)(rt1 - rt0); o[1] = (int32_t)(rt2 - rt0);
-        o[2] = (int32_t)(mt1 - mt0); o[3] = (int32_t)(mt2 - mt0);
+#if SSF_ASSOC_DEFER
+        o[2] = (int32_t)(rtl - rt0); o[3] = dqn;
+#else
+        o[2] = (int32_t)(rt2 - rt0); o[3] = 0;
+#endif
+        (void)mt1; (void)mt2;
         o[4] = (int32_t)(rt0 & 0x7fffffff); o[5] = __smid();
         o[6] = (int32_t)(strip_xyzi && strip_image_frame(ml) && strip_image_valid(strip_head + lo));
         o[7] = ml;
@@ -2461,8 +2594,10 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
                                                          const int32_t* __restrict__ curr_count,
                                                          const int32_t* __restrict__ last_count,
                                                          int mode, int max_iter,
-                                                         double* __restrict__ pose_rel,
-                                                         double* __restrict__ pose_abs,
+                                                         const double* pose_in,
+                                                         const double* pose_abs_in,
+                                                         double* pose_rel,
+                                                         double* pose_abs,
                                                          double* __restrict__ log,
                                                          int32_t* __restrict__ nlog_out,
                                                          int32_t* __restrict__ ncorr_out,
@@ -2489,8 +2624,8 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
     unsigned long long st1 = st0, st2 = st0;
 #endif
     if (tid == 0) {
-        for (int k = 0; k < 4; ++k) S.q[k] = pose_rel[7 * p + k];
-        for (int k = 0; k < 3; ++k) S.t[k] = pose_rel[7 * p + 4 + k];
+        for (int k = 0; k < 4; ++k) S.q[k] = pose_in[7 * p + k];
+        for (int k = 0; k < 3; ++k) S.t[k] = pose_in[7 * p + 4 + k];
         S.nlog = 0; S.done = 0;
     }
     __syncthreads();
@@ -2854,8 +2989,8 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
         if (nlog_out) nlog_out[p] = S.nlog;
         if (pose_abs) {                                                 // :87-90
             double q0l[4], t0l[3], q0c[4], r[3];
-            for (int k = 0; k < 4; ++k) q0l[k] = pose_abs[7 * p + k];
-            for (int k = 0; k < 3; ++k) t0l[k] = pose_abs[7 * p + 4 + k];
+            for (int k = 0; k < 4; ++k) q0l[k] = pose_abs_in[7 * p + k];
+            for (int k = 0; k < 3; ++k) t0l[k] = pose_abs_in[7 * p + 4 + k];
             quat_mul(q0l, S.q, q0c);
             quat_rotate(q0l, S.t, r);
             for (int k = 0; k < 4; ++k) pose_abs[7 * p + k] = q0c[k];
@@ -2925,8 +3060,13 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
                            const int64_t* curr_off, const int32_t* curr_count, int64_t max_m,
                            CorrRec* corr, double* pose_rel, double* pose_abs, double* log,
                            int32_t* nlog, int32_t* ncorr, int32_t* nn, const EdgeReg* edge,
-                           const float4* last_strip_xyzi, const int32_t* last_strip_head) {
+                           const float4* last_strip_xyzi, const int32_t* last_strip_head,
+                           const double* pose_in, const double* pose_abs_in) {
     if (n_pairs <= 0) return hipSuccess;
+    // warm starts / start poses read from pose_in / pose_abs_in (default: in place), results
+    // written to pose_rel / pose_abs: a chain reads pair k - 1's output slot directly
+    const double* pin = pose_in ? pose_in : pose_rel;
+    const double* ain = pose_abs_in ? pose_abs_in : pose_abs;
     if (max_m > 0) {
         const int bx = (int)((max_m + 255) / 256);
 #ifndef SSF_ASSOC_XBAND
@@ -2937,13 +3077,17 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
             // few pairs (a node's one pair, configs[2]'s chained pairs): up to 8 work-groups per
             // pair, each staging the last frame and taking a share of the queries, so the launch
             // spreads over ~256 CUs instead of n_pairs
-            const int qsplit = (int)std::max<int64_t>(1, std::min<int64_t>({8, 256 / n_pairs,
-                                                                 (max_m + kStripThreads - 1) / kStripThreads}));
-            kmark(s, soa ? "k_associate_strips_soa" : "k_associate_strips");
-            hipLaunchKernelGGL(soa ? k_associate_strips<true> : k_associate_strips<false>,
+            const bool coop = kAssocCoopG > 0 && n_pairs <= kAssocCoopPairs;
+            constexpr int kQpwCoop = kAssocCoopG > 0 ? kStripThreads / kAssocCoopG : kStripThreads;
+            const int qsplit = coop ? (int)((max_m + kQpwCoop - 1) / kQpwCoop)
+                                    : (int)std::max<int64_t>(1, std::min<int64_t>({8, 256 / n_pairs,
+                                                             (max_m + kStripThreads - 1) / kStripThreads}));
+            kmark(s, coop ? "k_associate_strips_coop" : soa ? "k_associate_strips_soa" : "k_associate_strips");
+            hipLaunchKernelGGL(coop ? (soa ? k_associate_strips<true, kAssocCoopG> : k_associate_strips<false, kAssocCoopG>)
+                                    : (soa ? k_associate_strips<true> : k_associate_strips<false>),
                                dim3(n_pairs, qsplit), dim3(kStripThreads), lds, s, last, last_off, last_count,
                                last_normal, last_valid, last_sorted, last_sidx, curr, curr_off,
-                               curr_count, pose_rel, corr, nn, cap,
+                               curr_count, pin, corr, nn, cap,
                                last_strip_head ? last_strip_xyzi : nullptr, last_strip_head);
         } else
 #endif
@@ -2955,17 +3099,17 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
             hipLaunchKernelGGL(soa ? k_associate_lds<true> : k_associate_lds<false>,
                                dim3(qx, n_pairs), dim3(kAssocThreads), lds, s, last, last_off,
                                last_count, last_normal, last_valid, last_sorted, last_sidx, curr,
-                               curr_off, curr_count, pose_rel, corr, nn, (int)max_m);
+                               curr_off, curr_count, pin, corr, nn, (int)max_m);
         } else if (max_m <= kSortMax && last_sorted && last_sidx) {
             kmark(s, "k_associate_sorted");
             hipLaunchKernelGGL(k_associate_sorted, dim3(bx, n_pairs), dim3(256), 0, s, last, last_off,
                                last_count, last_normal, last_valid, last_sorted, last_sidx, curr,
-                               curr_off, curr_count, pose_rel, corr, nn);
+                               curr_off, curr_count, pin, corr, nn);
         } else {
             kmark(s, "k_associate");
             hipLaunchKernelGGL(k_associate, dim3(bx, n_pairs), dim3(256), 0, s, last, last_off,
                                last_count, last_normal, last_valid, curr, curr_off, curr_count,
-                               pose_rel, corr, nn);
+                               pin, corr, nn);
         }
     }
     if (edge && edge->max_m > 0) {
@@ -2973,13 +3117,13 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
         kmark(s, "k_edge_associate");
         hipLaunchKernelGGL(k_edge_associate, dim3(n_pairs), dim3(kEdgeAssocThreads), (size_t)cap * sizeof(float4),
                            s, edge->last, edge->last_off, edge->last_count, edge->line,
-                           edge->line_valid, edge->curr, edge->curr_off, edge->curr_count, pose_rel,
+                           edge->line_valid, edge->curr, edge->curr_off, edge->curr_count, pin,
                            edge->corr, cap);
     }
     kmark(s, "k_solve");
 #define SSF_SOLVE_LAUNCH(E, NT, ...)                                                               \
     hipLaunchKernelGGL((k_solve<E, NT>), dim3(n_pairs), dim3(NT), 0, s, corr, curr_off, curr_count, \
-                       last_count, cfg.solver, cfg.max_iter, pose_rel, pose_abs, log, nlog, ncorr,  \
+                       last_count, cfg.solver, cfg.max_iter, pin, ain, pose_rel, pose_abs, log, nlog, ncorr, \
                        __VA_ARGS__)
     if (edge)
         SSF_SOLVE_LAUNCH(true, kSolveThreads, edge->corr, edge->curr_off, edge->curr_count, edge->ncorr);

@@ -33,7 +33,7 @@ POSE_EMPTY, POSE_REFLECTION, POSE_NOT_ORTHOGONAL, POSE_GMM_FAILED, POSE_SYNC_FAI
 EXPORTS = [
     "ssf_abi_version", "ssf_config_default", "ssf_create", "ssf_destroy", "ssf_last_error",
     "ssf_reserve", "ssf_extract_planes_batch", "ssf_extract_planes", "ssf_plane_table_batch",
-    "ssf_register_batch", "ssf_mask_pose_batch", "ssf_rng_seed", "ssf_accumulate_sequence",
+    "ssf_register_batch", "ssf_register_chain", "ssf_mask_pose_batch", "ssf_rng_seed", "ssf_accumulate_sequence",
     "ssf_voxel_grid_batch", "ssf_icp_params_default", "ssf_icp_batch",
     "ssf_extract_planes_batch_masked", "ssf_register_pair", "ssf_profile_enable",
     "ssf_profile_read", "ssf_set_mask_split", "ssf_mask_pose_batch_f64",
@@ -129,6 +129,9 @@ def lib():
     L.ssf_register_batch.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64,
                                      vp, vp, vp, vp, vp, vp, vp, vp]
     L.ssf_register_batch.restype = i32
+    L.ssf_register_chain.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, i64, i64,
+                                     vp, vp, vp, vp, vp, vp, vp]
+    L.ssf_register_chain.restype = i32
     L.ssf_register_pair.argtypes = [vp, vp, vp, i64, vp, i64, vp, vp, vp, vp, C.POINTER(StepLog)]
     L.ssf_register_pair.restype = i32
     L.ssf_set_mask_split.argtypes = [vp, i32]

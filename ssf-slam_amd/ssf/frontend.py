@@ -324,6 +324,38 @@ class Frontend:
                     radius=steps[i].radius) for i in range(log.n_steps)]
         return list(qo), list(to), out, int(log.n_corr)
 
+    def register_chain(self, pb: PlaneBatch, table, pose_init, pose_abs_init=None, out=None,
+                       want_ncorr=False):
+        """frameRegistration over a sequence (ssf_register_chain): pair k registers frame k + 1 of
+        pb against frame k, warm-started from pair k - 1's solution (pose_init [7] or [1, 7] for
+        pair 0; lidarOdometry_onlyPC.cpp:164,251-252).  table = plane_table(pb).  Returns
+        dict(pose_seq [K, 7], pose_abs_seq [K, 7] (frame k + 1's pose from pose_abs_init) or None,
+        ncorr [K] or None); out: optional preallocated pose_seq."""
+        F = pb.count.numel()
+        K = max(F - 1, 0)
+        pose_init = self._dev(pose_init, torch.float64).reshape(-1)
+        if pose_init.numel() != 7:
+            raise ValueError("pose_init must hold 7 values (q xyzw, t)")
+        seq = self._out(out, (max(K, 1), 7), torch.float64, "pose_seq out") if out is not None else \
+            torch.empty((max(K, 1), 7), dtype=torch.float64, device=self.device)
+        abs_seq = None
+        if pose_abs_init is not None:
+            pose_abs_init = self._dev(pose_abs_init, torch.float64).reshape(-1)
+            if pose_abs_init.numel() != 7:
+                raise ValueError("pose_abs_init must hold 7 values (q xyzw, t)")
+            abs_seq = torch.empty((max(K, 1), 7), dtype=torch.float64, device=self.device)
+        ncorr = torch.empty(max(K, 1), dtype=torch.int32, device=self.device) if want_ncorr else None
+        normal, valid, sx, si = table
+        st = getattr(table, "strips", None) or (None, None)
+        rc = _abi.lib().ssf_register_chain(
+            self._h, _stream(self.device), K, _ptr(pb.xyzi), _ptr(pb.off), _ptr(pb.count),
+            _ptr(normal), _ptr(valid), _ptr(sx), _ptr(si), int(pb.xyzi.shape[0]), pb.max_points,
+            _ptr(pose_init), _ptr(seq), _ptr(pose_abs_init), _ptr(abs_seq), _ptr(ncorr),
+            _ptr(st[0]), _ptr(st[1]))
+        self._check(rc, "ssf_register_chain")
+        return dict(pose_seq=seq[:K], pose_abs_seq=None if abs_seq is None else abs_seq[:K],
+                    ncorr=None if ncorr is None else ncorr[:K])
+
     def register(self, last: PlaneBatch, last_table, curr: PlaneBatch, pose_rel, pose_abs=None,
                  want_log=False, want_nn=False, want_nlog=False, edges=None):
         """frameRegistration for P pairs (last[p], curr[p]).  pose_rel [P,7] f64 (q xyzw, t) is the

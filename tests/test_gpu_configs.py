@@ -97,6 +97,60 @@ def test_config2_noseg_mask_before_features_32_pairs(oracle, dev):
     assert 25.0 < np.linalg.norm(ab[0, 4:].cpu().numpy()) < 40.0
 
 
+def test_register_chain_matches_pairwise_calls(oracle, dev):
+    """ssf_register_chain (a sequence's pairs in one call, each warm start read from the previous
+    pair's output slot) == one ssf_register_batch call per pair with the warm start copied in,
+    bit for bit (poses, accumulated poses, correspondence counts); a frame of <= 10 plane points
+    skips its pair as the reference does (:158) and the chain carries the warm start across it;
+    and the chain's poses vs the oracle's chained register_pair."""
+    import ssf
+    F = 9
+    clouds = [frame(3, k, n_az=1875)[0] for k in range(F)]
+    pts = torch.from_numpy(np.concatenate(clouds)).to(dev)
+    off, h_off = ssf.frame_offsets([c.shape[0] for c in clouds], dev)
+    fe = ssf.Frontend(64, device=dev.index or 0, solver="gn", max_iter=10)
+    pb = fe.extract_planes_batch(pts, off, h_off)
+    table = fe.plane_table(pb)
+    cnt = pb.count.clone()
+    cnt[5] = 7                                   # frame 5: too few plane points to be a last frame
+    pbk = ssf.PlaneBatch(pb.xyzi, cnt, pb.off, pb.h_off, pb.max_points)
+    q0 = np.array([0.0, 0.0, 0.002, 1.0]); q0 /= np.linalg.norm(q0)
+    init = torch.tensor([[*q0, 0.8, 0.02, 0.0]], dtype=torch.float64, device=dev)
+    abs0 = ssf.identity_poses(1, dev)
+    ch = fe.register_chain(pbk, table, init, pose_abs_init=abs0, want_ncorr=True)
+    torch.cuda.synchronize()
+    assert ch["pose_seq"].shape == (F - 1, 7) and ch["pose_abs_seq"].shape == (F - 1, 7)
+    rel, ab = init.clone(), abs0.clone()
+    seq, aseq, nc = [], [], []
+    for k in range(F - 1):
+        last, curr = _pair(pbk, k, k + 1)
+        res = fe.register(last, table, curr, rel, ab)
+        seq.append(rel.clone()); aseq.append(ab.clone()); nc.append(res["ncorr"].clone())
+    torch.cuda.synchronize()
+    seq = torch.cat(seq).cpu().numpy(); aseq = torch.cat(aseq).cpu().numpy()
+    nc = torch.cat(nc).cpu().numpy()
+    assert np.array_equal(ch["pose_seq"].cpu().numpy().view(np.uint64), seq.view(np.uint64))
+    assert np.array_equal(ch["pose_abs_seq"].cpu().numpy().view(np.uint64), aseq.view(np.uint64))
+    assert np.array_equal(ch["ncorr"].cpu().numpy(), nc)
+    assert nc[5] == -1 and np.array_equal(seq[5], seq[4])         # the skipped pair keeps its warm start
+    # vs the oracle, chained the same way
+    h = pbk.count.cpu().numpy()
+    planes = [pb.frame(k).cpu().numpy()[:h[k]] for k in range(F)]
+    qw, tw = q0, np.array([0.8, 0.02, 0.0])
+    got = ch["pose_seq"].cpu().numpy()
+    for k in range(F - 1):
+        q, t, _, c = oracle.register_pair(planes[k], planes[k + 1], 0.05, mode=oracle.MODE_GN,
+                                          max_iter=10, q_init=qw, t_init=tw)
+        assert (c if len(planes[k]) > 10 else -1) == nc[k], k
+        if k != 4:          # pair 4's curr frame is the truncated one: 7 residuals for 6 DoF, an
+            # ill-conditioned GN path (the chain-vs-pairwise bit equality above covers it)
+            assert np.abs(got[k, 4:] - t).max() < TOL_T and _angle(got[k, :4], q) < TOL_R, k
+        qw, tw = got[k, :4], got[k, 4:]
+    # no pairs: nothing to do, nothing written
+    one = ssf.PlaneBatch(pb.xyzi, pb.count[:1], pb.off[:2], pb.h_off[:2], pb.max_points)
+    assert fe.register_chain(one, table, init)["pose_seq"].shape == (0, 7)
+
+
 @pytest.fixture(scope="module")
 def c4_frames():
     return [frame(9, k, n_az=4000) for k in range(2)]

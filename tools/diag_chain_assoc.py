@@ -16,8 +16,8 @@ def main():
     import ssf
     from ssf import synth
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 32
-    count = os.environ.get("SSF_LIB", "").endswith("acount.so")
-    stamps = os.environ.get("SSF_LIB", "").endswith("sstamp.so")
+    count = "acount" in os.path.basename(os.environ.get("SSF_LIB", ""))
+    stamps = "sstamp" in os.path.basename(os.environ.get("SSF_LIB", ""))
     dev = torch.device("cuda", 0)
     N = 64 * 1875
     sc = synth.BatchScanner([0], K + 1, n_rows=64, n_az=1875, device=dev)
@@ -56,18 +56,25 @@ def main():
             if count:
                 o = int(pb.h_off[k + 1])
                 v = res["nn"][o:o + cnt[k + 1]].cpu().numpy().astype(np.int64)
+                nd = int((v < 0).sum())
+                v = v[v >= 0]
+                ns = v >> 16
+                v = v & 0xffff
                 wm = [v[i:i + 64].max() for i in range(0, len(v), 64)]
                 line += "  visits mean %.1f p99 %.0f max %d  wave-max mean %.1f  >500: %d" % (
                     v.mean(), np.percentile(v, 99), v.max(), np.mean(wm), int((v > 500).sum()))
+                line += "  deferred %d" % nd
+                line += "  strip searches mean %.1f p99 %.0f max %d wave-max mean %.1f" % (
+                    ns.mean(), np.percentile(ns, 99), ns.max(), np.mean([ns[i:i + 64].max() for i in range(0, len(ns), 64)]))
             if stamps:
                 o = int(pb.h_off[k + 1])
-                st = res["nn"][o:o + 64].cpu().numpy().reshape(8, 8)
+                ny = (cnt[k + 1] + 1023) // 1024
+                st = np.stack([res["nn"][o + 1024 * y:o + 1024 * y + 8].cpu().numpy() for y in range(ny)])
                 r0 = st[:, 4].min()
                 line += "\n   " + "  ".join(
-                    "wg%d cu%d img%d stage %.1f/%.1f us total %.1f us (%.2f GHz) start +%.1f" % (
-                        y, st[y, 5], st[y, 6], st[y, 0] / 100, st[y, 2] / 1e3 / (st[y, 0] / 100 + 1e-9),
-                        st[y, 1] / 100, st[y, 3] / (st[y, 1] * 10 + 1e-9), (st[y, 4] - r0) / 100)
-                    for y in range(8) if st[y, 7] > 0)
+                    "wg%d: stage %.1f lanes %.1f total %.1f us, %d deferred, start +%.1f" % (
+                        y, st[y, 0] / 100, st[y, 2] / 100, st[y, 1] / 100, st[y, 3], (st[y, 4] - r0) / 100)
+                    for y in range(ny))
             print(line, flush=True)
 
 

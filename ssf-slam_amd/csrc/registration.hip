@@ -1052,6 +1052,10 @@ SSF_DEV bool pick_beyond_invalid(const StripView<false>& v, const StripLds& T, c
     return C < need;
 }
 
+#ifndef SSF_TABLE_COOP_G
+#define SSF_TABLE_COOP_G 4                       // lanes per deferred pick query (0: one lane each)
+#endif
+constexpr int kTableCoopG = SSF_TABLE_COOP_G;
 // Whole work-group: every query of the frame (m > 30, every ring code < 255).  Queries that need
 // points beyond 1 m (K1 < 30, fewer than two other-ring points inside) are queued and finished
 // afterwards, spread over the waves.
@@ -1096,6 +1100,80 @@ SSF_DEV void table_pick_walks(const float4* __restrict__ P, const StripView<fals
     if (threadIdx.x == 0 && stamp_out) { stamp_out[0] = (int32_t)((__builtin_amdgcn_s_memtime() - stamp0) >> 4); stamp_out[1] = *qlen; }
 #endif
     const int nq = min(*qlen, qcap);
+#if SSF_TABLE_COOP_G
+    // one deferred query per group of kTableCoopG lanes: the group's lanes run the 1-m pick
+    // redundantly (same bits), then both beyond-1-m searches of pick_beyond_invalid with the
+    // strips of each ring round one per lane (strip i of the round order s0, s0+1, s0-1, s0+2,
+    // ...), the group's minimum E / sum C after each round -- a lane alone walked every ring
+    // (the slowest deferred query set the frame's time: ~0.127 M of ~0.60 M cycles, r03 stamps)
+    {
+        constexpr int G = kTableCoopG;
+        const int gl = threadIdx.x % G, ng = blockDim.x / G;
+        for (int k = threadIdx.x / G; k < nq; k += ng) {
+            const int j = queue[k];                                       // uniform per group
+            const float4 q = v.pt(j);
+            const int64_t o = base + v.id(j);
+            PickState s;
+            pick_1m(P, v, T, g, j, q, s);
+            const bool f1 = key_dist(s.d1) < 1.0f;
+            const int prow = s.prow, s0 = g.strip_of(q.y), nstrip = 2 * g.ns;   // round order
+            auto strip_at = [&](int i) { return i == 0 ? s0 : ((i & 1) ? s0 + (i + 1) / 2 : s0 - i / 2); };
+            auto ring_at = [&](int i) { return (i + 1) / 2; };
+            // E: the smallest key of an other-ring point beyond 1 m
+            double E = knn_key(__builtin_inff(), 0x7fffffff);
+            for (int i0 = 0; i0 < nstrip; i0 += G) {
+                // a round's strips all have rings >= ring_at(i0): their |dy| >= (r - 1) W
+                const float lb = (float)(ring_at(i0) - 1) * g.W - 0.001f;
+                if (i0 > 0 && lb > 0.0f && lb * lb > key_dist(E)) break;   // uniform per group
+                const int i = i0 + gl, sidx = strip_at(i);
+                if (i < nstrip && sidx >= 0 && sidx < g.ns) {
+                    int st = sidx == s0 ? j : -1;
+                    strip_visit(v, T, sidx, st, q, __builtin_inff(), [&] { return key_dist(E); },
+                                [&](const float4& p) {
+                                    const float d = l2_simple(q, p);
+                                    const int row = pt_row(p);
+                                    const double key = knn_key(d, pt_id(p));
+                                    if (d >= 1.0f && row != prow && row <= 63 && key < E) E = key;
+                                });
+                }
+#pragma unroll
+                for (int x = G / 2; x >= 1; x >>= 1) {
+                    const double y = __shfl_xor(E, x, kWave);
+                    E = y < E ? y : E;
+                }
+            }
+            bool inval = false;
+            if (key_dist(E) < __builtin_inff()) {
+                // C: keys beyond 1 m below E; invalid iff C < 30 - K1
+                const int need = 30 - s.K1;
+                const float lim = key_dist(E);
+                int C = 0;
+                for (int i0 = 0; i0 < nstrip; i0 += G) {
+                    const float lb = (float)(ring_at(i0) - 1) * g.W - 0.001f;
+                    if (C >= need || (i0 > 0 && lb > 0.0f && lb * lb > lim)) break;   // uniform per group
+                    const int i = i0 + gl, sidx = strip_at(i);
+                    int c = 0;
+                    if (i < nstrip && sidx >= 0 && sidx < g.ns) {
+                        int st = sidx == s0 ? j : -1;
+                        strip_visit(v, T, sidx, st, q, __builtin_inff(), [&] { return lim; },
+                                    [&](const float4& p) {
+                                        const float d = l2_simple(q, p);
+                                        c += (d >= 1.0f && knn_key(d, pt_id(p)) < E);
+                                    });
+                    }
+#pragma unroll
+                    for (int x = G / 2; x >= 1; x >>= 1) c += __shfl_xor(c, x, kWave);
+                    C += c;
+                }
+                inval = C < need;
+            }
+            if (gl == 0) {
+                if (inval) pick_invalid(o, normal, valid);
+                else pick_finish(P, s, f1 ? 1 : 0, plane_max, o, normal, valid);
+            }
+        }
+    }
+#else
     const int nw = blockDim.x >> 6, t2 = (threadIdx.x & 63) * nw + (threadIdx.x >> 6);
     for (int k = t2; k < nq; k += blockDim.x) {
         const int j = queue[k];
@@ -1108,6 +1186,7 @@ SSF_DEV void table_pick_walks(const float4* __restrict__ P, const StripView<fals
         if (inval) pick_invalid(o, normal, valid);
         else pick_finish(P, s, f1 ? 1 : 0, plane_max, o, normal, valid);
     }
+#endif
 #ifdef SSF_TABLE_STAMPS
     __syncthreads();
     if (threadIdx.x == 0 && stamp_out) stamp_out[4] = (int32_t)((__builtin_amdgcn_s_memtime() - stamp0) >> 4);

@@ -46,8 +46,10 @@ F64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector, spec (AMD datasheet); f64 MFMA
 # HBM bytes per launch of every kernel / f64 FLOPs per k_mask_pose launch, measured with rocprofv3
 # PMC passes on a serial run of this bench (tools/pmc_traffic.py, tools/pmc_f64.py); used when
 # their workload config matches the run's.
-TRAFFIC_JSON = os.path.join(REPO, "profiles", "r04by_traffic.json")
-F64_JSON = os.path.join(REPO, "profiles", "r04by_f64.json")
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "r05fin_traffic.json")
+# PMC traffic of the same build on the reference's own layout (--layout carla)
+TRAFFIC_JSONS = {"azimuth": TRAFFIC_JSON, "carla": os.path.join(REPO, "profiles", "r05fin_carla_traffic.json")}
+F64_JSON = os.path.join(REPO, "profiles", "r05fin_f64.json")
 METRIC = "LiDAR front-end frames/sec (mask+feature+GN), 64-beam 120k pts, 1/2/4/8 GPUs"
 
 
@@ -1204,13 +1206,14 @@ def main():
     if args.f64_inputs:
         line["config"]["mask_inputs"] = "float64 pos / flow (ssf_mask_pose_batch_f64), float32 features"
         line["dtype"] = "f32 features / f64 mask inputs + f64 mask+solve"
-    traffic = None if args.edges else _load_profile(TRAFFIC_JSON, B, N, args.mask_before_features, args.layout)
+    tjson = TRAFFIC_JSONS.get(args.layout, TRAFFIC_JSON)
+    traffic = None if args.edges else _load_profile(tjson, B, N, args.mask_before_features, args.layout)
     lib_sha = _lib_sha16()
     tsrc = None
     if traffic:
         # the traffic is a committed PMC measurement, not this run's: say which, and whether it
         # was measured on this very library build
-        tsrc = {"traffic_source": os.path.relpath(TRAFFIC_JSON, REPO),
+        tsrc = {"traffic_source": os.path.relpath(tjson, REPO),
                 "traffic_lib_sha16": traffic.get("lib_sha16"),
                 "traffic_stale": traffic.get("lib_sha16") != lib_sha}
         for k, v in kernels.items():

@@ -133,7 +133,7 @@ class MaskPose(tuple):
 
 def mask_and_pose(points, flow, mode: str = "gmm", gt_mask=None, seed: int | None = None,
                   draws=None, reflection: str = "raise", device=None, frame_sizes=None,
-                  kabsch_dtype: str = "float64"):
+                  kabsch_dtype: str = "float64", errors: str = "raise"):
     """The PointCloudOdometry_noSeg.py:97-125 block for one frame (or F frames packed back to
     back with `frame_sizes`).  mode 'gmm' (GaussianMixture on [flow, xyz]), 'gt'
     (background = s_fg_mask == 0, PointCloudOdometry.py:91) or 'given' (background = mask != 0).
@@ -141,8 +141,14 @@ def mask_and_pose(points, flow, mode: str = "gmm", gt_mask=None, seed: int | Non
     arithmetic on float64 arrays; "float32": the reference's float32 arithmetic, as the ASF block
     runs it on float32 network flow (main_sju_occ_ros.py:273-284; inputs stored as float32,
     ssf_kabsch_f32_batch after the mask kernel, same stream).
+    errors "raise" (default): a frame whose pose fails raises as the reference does (one frame,
+    one call); "status": nothing raises, info["status"] holds every frame's status (0 or a
+    POSE_* code) -- a batch keeps its good frames when one frame fails, e.g. a float32 R whose
+    orthogonality test (atol 1e-8) sits at the rounding level.
     -> MaskPose: (R, t, q_xyzw, bg_mask), plus keyed batched fields (see MaskPose)."""
     _check_kabsch_dtype(kabsch_dtype)
+    if errors not in ("raise", "status"):
+        raise ValueError(f"errors must be 'raise' or 'status', not {errors!r}")
     fe = _frontend(device)
     dt = torch.float32 if kabsch_dtype == "float32" else _storage(points, flow)
     pts = _as_dev(points, fe.device, dt)
@@ -163,14 +169,16 @@ def mask_and_pose(points, flow, mode: str = "gmm", gt_mask=None, seed: int | Non
         fe.kabsch_f32(pts, off, h_off, flow=fl, mask=bg, reflection=1 if reflection == "fix" else 0,
                       out=out)
     o = out.cpu().numpy()
-    for st in o[:, _abi.POSE_OUT["STATUS"]]:
-        if int(st) != 0:
-            _raise_status(st)
+    status = o[:, _abi.POSE_OUT["STATUS"]].astype(np.int32)
+    if errors == "raise":
+        for st in status:
+            if int(st) != 0:
+                _raise_status(st)
     fields = dict(R=o[:, 7:16].reshape(-1, 3, 3), t=o[:, 0:3], q_xyzw=o[:, 3:7],
                   para_t_q=o[:, 0:7], bg_mask=bg,
                   info=dict(bg_label=o[:, 18], n_bg=o[:, 17], kmeans_iter=o[:, 19], em_iter=o[:, 20],
                             converged=o[:, 21], centers=o[:, 22:24], lower_bound=o[:, 24],
-                            passes=o[:, 25]))
+                            passes=o[:, 25], status=status))
     R, t, q = fields["R"].copy(), fields["t"].reshape(-1, 3, 1).copy(), fields["q_xyzw"].copy()
     if frame_sizes is None:                      # one frame: the shapes of slove_RT_by_SVD
         R, t, q = R[0], t[0], q[0]

@@ -50,6 +50,7 @@ def test_error_paths_without_gpu():
     assert L.ssf_rng_seed(None, 1) == _abi.SSF_E_ARG
     assert L.ssf_extract_planes_batch(None, None, 1, None, 3, None, 0, 0, None, None, None, None, None) == _abi.SSF_E_ARG
     assert L.ssf_last_error(None) == b"null context"
+    assert L.ssf_register_chain(None, None, 1, *([None] * 7), 0, 0, *([None] * 7)) == _abi.SSF_E_ARG
     assert L.ssf_voxel_grid_batch(None, None, 1, None, None, None, 0.1, None, None) == _abi.SSF_E_ARG
     prm = _abi.IcpParams()
     assert L.ssf_icp_params_default(C.byref(prm)) == _abi.SSF_OK

@@ -230,6 +230,27 @@ def test_reflection_status(dev):
     assert abs(np.linalg.det(R) - 1.0) < 1e-9
 
 
+def test_mask_and_pose_per_frame_status(dev):
+    """errors='status': a batch with one failing frame (empty background: every point masked out)
+    keeps the other frames' poses and reports each frame's status; the default raises."""
+    import ssf
+    p, fl, fg = frame(7, 2)
+    bgm = (fg == 0).astype(np.uint8)
+    pts = np.concatenate([p, p]); flow = np.concatenate([fl, fl])
+    gm = np.concatenate([fg, np.ones_like(fg)])                    # frame 1: all foreground
+    r = ssf.mask_and_pose(pts, flow, mode="gt", gt_mask=gm, frame_sizes=[len(p), len(p)],
+                          device=dev.index, errors="status")
+    st = r["info"]["status"]
+    assert st[0] == 0 and st[1] == ssf._abi.POSE_EMPTY, st
+    one = ssf.mask_and_pose(p, fl, mode="gt", gt_mask=fg, device=dev.index)
+    assert np.array_equal(r[0][0], one[0]) and np.array_equal(r[1][0], one[1])
+    with pytest.raises(ValueError):
+        ssf.mask_and_pose(pts, flow, mode="gt", gt_mask=gm, frame_sizes=[len(p), len(p)], device=dev.index)
+    with pytest.raises(ValueError):
+        ssf.mask_and_pose(p, fl, mode="gt", gt_mask=fg, device=dev.index, errors="ignore")
+    assert bgm.sum() > 0
+
+
 def _rot_angle(Ra, Rb):
     """Rotation angle of Ra^T Rb, from ||Ra - Rb||_F = 2 sqrt(2) sin(theta / 2) (no arccos near 1)."""
     return float(2.0 * np.arcsin(min(1.0, np.linalg.norm(Ra - Rb) / (2.0 * np.sqrt(2.0)))))

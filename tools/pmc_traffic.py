@@ -21,7 +21,7 @@ import csv
 import json
 from collections import defaultdict
 
-KERNELS = ("k_mask_pose_f64", "k_mask_pose", "k_feat_wave_reg", "k_feat_chunk_reg", "k_feat_chunk_flagged", "k_feat_chunk", "k_feat_select", "k_bin_count", "k_bin_scan", "k_bin_curv", "k_select",
+KERNELS = ("k_mask_pose_f64", "k_mask_pose", "k_feat_wave_reg", "k_feat_wave_run", "k_feat_chunk_reg", "k_feat_chunk_flagged", "k_feat_chunk", "k_feat_select", "k_bin_count", "k_bin_scan", "k_bin_curv", "k_select",
            "k_plane_table_sorted", "k_associate_strips", "k_associate_lds", "k_associate_sorted", "k_solve")
 
 

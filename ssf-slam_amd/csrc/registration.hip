@@ -2321,7 +2321,10 @@ constexpr int kSolveLdsCap = 4096;
 #ifndef SSF_SOLVE_COMPACT1
 #define SSF_SOLVE_COMPACT1 1                     // one-pass compaction of the correspondences (A/B: 0)
 #endif
-constexpr int kCmpPer = 8;                       // records per thread and pass of it
+#ifndef SSF_SOLVE_CMP_PER
+#define SSF_SOLVE_CMP_PER 8
+#endif
+constexpr int kCmpPer = SSF_SOLVE_CMP_PER;        // records per thread and pass of it
 struct CorrLds {
     float po[3][kSolveLdsCap], pa[3][kSolveLdsCap], n[3][kSolveLdsCap];
 };
@@ -2365,6 +2368,25 @@ SSF_DEV double rcp_refined(double x) {
 #define SSF_SOLVE_HUBER_RCP 0                    // 1: Huber weights by refined rcp / rsq (r5l: 0.0857 vs 0.0808 ms, slower)
 #endif
 
+// The rotational Jacobian columns carry a factor 2 (the quaternion parameterisation below).
+// With SSF_SOLVE_JSCALE it is applied to the block sums instead of every correspondence: every
+// product and partial sum of those entries is then exactly 2 or 4 times the unscaled one (a
+// power-of-two scaling commutes with rounding), so the sums are bit-identical and each
+// correspondence saves three f64 multiplies.  kNeScale folds it into the evaluation's final x2
+// (the duplicated residual blocks): packed J^T W J entries (u, v) x4 (u, v < 3) / x2 (u < 3 <= v)
+// / x1, J^T W r entries x2 (u < 3), the cost x1 -- each times that 2.
+#ifndef SSF_SOLVE_JSCALE
+#define SSF_SOLVE_JSCALE 1
+#endif
+#if SSF_SOLVE_JSCALE
+constexpr double kJ2 = 1.0;
+__device__ constexpr double kNeScale[kNE] = {8, 8, 8, 4, 4, 4, 8, 8, 4, 4, 4, 8, 4, 4, 4, 2, 2, 2, 2, 2, 2,
+                                             4, 4, 4, 2, 2, 2, 2};
+#else
+constexpr double kJ2 = 2.0;
+__device__ constexpr double kNeScale[kNE] = {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
+                                             2, 2, 2, 2, 2, 2, 2};
+#endif
 // Per-correspondence residual r = (R po + t - pa) . n (PlaneFeatureCost, :25-43) and its local
 // Jacobian [2 (R po x n), n]: the EigenQuaternionParameterization's 4x3 Jacobian composed with
 // the autodiff gradient (what the oracle's residual_jac spells out) reduces to that for a unit
@@ -2383,9 +2405,9 @@ SSF_DEV void accum_corr(const double R[9], const double t[3], const double po[3]
     const double d0 = (u[0] + t[0]) - pa[0], d1 = (u[1] + t[1]) - pa[1], d2 = (u[2] + t[2]) - pa[2];
     const double r = __builtin_fma(d2, nn[2], __builtin_fma(d1, nn[1], d0 * nn[0]));
     double J[6];
-    J[0] = 2.0 * __builtin_fma(u[1], nn[2], -u[2] * nn[1]);
-    J[1] = 2.0 * __builtin_fma(u[2], nn[0], -u[0] * nn[2]);
-    J[2] = 2.0 * __builtin_fma(u[0], nn[1], -u[1] * nn[0]);
+    J[0] = kJ2 * __builtin_fma(u[1], nn[2], -u[2] * nn[1]);
+    J[1] = kJ2 * __builtin_fma(u[2], nn[0], -u[0] * nn[2]);
+    J[2] = kJ2 * __builtin_fma(u[0], nn[1], -u[1] * nn[0]);
     J[3] = nn[0]; J[4] = nn[1]; J[5] = nn[2];
     const double s = r * r;
     double rho0, rho1;
@@ -2430,9 +2452,9 @@ SSF_DEV void accum_edge(const double R[9], const double t[3], const double po[3]
 #pragma unroll
         for (int j = 0; j < 3; ++j) nk[j] = (j == k ? 1.0 : 0.0) - uu[k] * uu[j];
         r[k] = __builtin_fma(d[2], nk[2], __builtin_fma(d[1], nk[1], d[0] * nk[0]));
-        J[k][0] = 2.0 * __builtin_fma(g[1], nk[2], -g[2] * nk[1]);
-        J[k][1] = 2.0 * __builtin_fma(g[2], nk[0], -g[0] * nk[2]);
-        J[k][2] = 2.0 * __builtin_fma(g[0], nk[1], -g[1] * nk[0]);
+        J[k][0] = kJ2 * __builtin_fma(g[1], nk[2], -g[2] * nk[1]);
+        J[k][1] = kJ2 * __builtin_fma(g[2], nk[0], -g[0] * nk[2]);
+        J[k][2] = kJ2 * __builtin_fma(g[0], nk[1], -g[1] * nk[0]);
         J[k][3] = nk[0]; J[k][4] = nk[1]; J[k][5] = nk[2];
         s = __builtin_fma(r[k], r[k], s);
     }
@@ -2490,7 +2512,7 @@ SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4],
     }
     block_sum_rs<kNE>(ne, lds);
 #pragma unroll
-    for (int k = 0; k < kNE; ++k) ne[k] *= 2.0;
+    for (int k = 0; k < kNE; ++k) ne[k] *= kNeScale[k];
 }
 
 // LDS-resident correspondences, kSolveStep per step (i, i + T, ...; a missing one is a clamped
@@ -2537,7 +2559,7 @@ SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double 
     block_sum_db<kNE, NW, SSF_SOLVE_RED != 3, SSF_SOLVE_RED == 1>(ne, lds, parity);
 #endif
 #pragma unroll
-    for (int k = 0; k < kNE; ++k) ne[k] *= 2.0;
+    for (int k = 0; k < kNE; ++k) ne[k] *= kNeScale[k];
 }
 
 // quat_plus for a GN step: |d| = theta < 2^-7 (a step of a converging solve) takes sin(theta) /

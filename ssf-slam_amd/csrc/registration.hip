@@ -2387,6 +2387,30 @@ constexpr double kJ2 = 2.0;
 __device__ constexpr double kNeScale[kNE] = {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
                                              2, 2, 2, 2, 2, 2, 2};
 #endif
+#ifndef SSF_SOLVE_HF32
+#define SSF_SOLVE_HF32 0
+#endif
+// SSF_SOLVE_HF32: J^T W J (the 21 packed entries) accumulated per thread in packed f32 FMAs
+// (v_pk_fma_f32, two entries per instruction at the f32 rate) and added to the f64 sums before
+// the block reduction; the gradient J^T W r and the cost stay f64.  A GN / LM fixed point is set
+// by the f64 gradient; the f32 Hessian (~1e-7 relative per thread sum) moves the steps, not the
+// converged pose.  A/B switch.
+typedef float hf2 __attribute__((ext_vector_type(2)));
+constexpr int kHF = 11;                          // 21 entries in pk order, as pairs (+1 pad)
+SSF_DEV constexpr int pk_u(int e) { return e < 6 ? 0 : e < 11 ? 1 : e < 15 ? 2 : e < 18 ? 3 : e < 20 ? 4 : 5; }
+SSF_DEV constexpr int pk_v(int e) {
+    return e < 6 ? e : e < 11 ? e - 6 + 1 : e < 15 ? e - 11 + 2 : e < 18 ? e - 15 + 3 : e < 20 ? e - 18 + 4 : 5;
+}
+SSF_DEV void hess_f32(const float (&wj)[6], const float (&J)[6], hf2 (&H)[kHF]) {
+#pragma unroll
+    for (int p = 0; p < kHF; ++p) {
+        const int e0 = 2 * p, e1 = 2 * p + 1 < 21 ? 2 * p + 1 : 20;
+        const hf2 a = {wj[pk_u(e0)], 2 * p + 1 < 21 ? wj[pk_u(e1)] : 0.0f};
+        const hf2 b = {J[pk_v(e0)], J[pk_v(e1)]};
+        H[p] = __builtin_elementwise_fma(a, b, H[p]);
+    }
+}
+
 // Per-correspondence residual r = (R po + t - pa) . n (PlaneFeatureCost, :25-43) and its local
 // Jacobian [2 (R po x n), n]: the EigenQuaternionParameterization's 4x3 Jacobian composed with
 // the autodiff gradient (what the oracle's residual_jac spells out) reduces to that for a unit
@@ -2397,7 +2421,7 @@ __device__ constexpr double kNeScale[kNE] = {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
 // One correspondence's Huber-weighted contribution (x wgt: 0 for a padding slot) to the
 // normal equations ne (21 packed upper J^T W J, 6 J^T W r, cost).
 SSF_DEV void accum_corr(const double R[9], const double t[3], const double po[3], const double pa[3],
-                        const double nn[3], double wgt, double (&ne)[kNE]) {
+                        const double nn[3], double wgt, double (&ne)[kNE], hf2 (&H)[kHF]) {
     const double a = 0.1, b = 0.1 * 0.1;
     double u[3];
 #pragma unroll
@@ -2425,6 +2449,20 @@ SSF_DEV void accum_corr(const double R[9], const double t[3], const double po[3]
     }
     ne[27] = __builtin_fma(0.5 * wgt, rho0, ne[27]);
     rho1 *= wgt;
+#if SSF_SOLVE_HF32
+    {
+        float jf[6], wf[6];
+        const float rf = (float)rho1;
+#pragma unroll
+        for (int uu = 0; uu < 6; ++uu) { jf[uu] = (float)J[uu]; wf[uu] = rf * jf[uu]; }
+        hess_f32(wf, jf, H);
+#pragma unroll
+        for (int uu = 0; uu < 6; ++uu) ne[21 + uu] = __builtin_fma(rho1 * J[uu], r, ne[21 + uu]);
+        return;
+    }
+#else
+    (void)H;
+#endif
     int k = 0;
 #pragma unroll
     for (int uu = 0; uu < 6; ++uu) {             // explicit FMAs: the file is built without
@@ -2496,13 +2534,20 @@ SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4],
     for (int k = 0; k < kNE; ++k) ne[k] = 0.0;
     double R[9];
     quat_to_R(q, R);
+    hf2 H[kHF];
+#pragma unroll
+    for (int k = 0; k < kHF; ++k) H[k] = hf2{0.0f, 0.0f};
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const CorrRec c = rec[i];
         if (c.valid == 0.0f) continue;
         const double po[3] = {c.po[0], c.po[1], c.po[2]}, pa[3] = {c.pa[0], c.pa[1], c.pa[2]},
                      nn[3] = {c.n[0], c.n[1], c.n[2]};
-        accum_corr(R, t, po, pa, nn, 1.0, ne);
+        accum_corr(R, t, po, pa, nn, 1.0, ne, H);
     }
+#if SSF_SOLVE_HF32
+#pragma unroll
+    for (int e = 0; e < 21; ++e) ne[e] += (double)H[e >> 1][e & 1];
+#endif
     for (int i = threadIdx.x; i < en; i += blockDim.x) {          // edge blocks (en = 0: none)
         const CorrRec c = erec[i];
         if (c.valid == 0.0f) continue;
@@ -2532,6 +2577,9 @@ SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double 
     double R[9];
     quat_to_R(q, R);
     const int T = blockDim.x;
+    hf2 H[kHF];
+#pragma unroll
+    for (int k = 0; k < kHF; ++k) H[k] = hf2{0.0f, 0.0f};
     for (int i = threadIdx.x; i < nv; i += kSolveStep * T) {
         float f[kSolveStep][9];
 #pragma unroll
@@ -2544,9 +2592,13 @@ SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double 
         for (int h = 0; h < kSolveStep; ++h) {
             const double po[3] = {f[h][0], f[h][1], f[h][2]}, pa[3] = {f[h][3], f[h][4], f[h][5]},
                          nn[3] = {f[h][6], f[h][7], f[h][8]};
-            accum_corr(R, t, po, pa, nn, (h == 0 || i + h * T < nv) ? 1.0 : 0.0, ne);
+            accum_corr(R, t, po, pa, nn, (h == 0 || i + h * T < nv) ? 1.0 : 0.0, ne, H);
         }
     }
+#if SSF_SOLVE_HF32
+#pragma unroll
+    for (int e = 0; e < 21; ++e) ne[e] += (double)H[e >> 1][e & 1];
+#endif
     for (int i = nv + threadIdx.x; i < nv + nve; i += T) {        // edge blocks after the planes
         const double po[3] = {C.po[0][i], C.po[1][i], C.po[2][i]}, pa[3] = {C.pa[0][i], C.pa[1][i], C.pa[2][i]},
                      uu[3] = {C.n[0][i], C.n[1][i], C.n[2][i]};

@@ -1566,9 +1566,15 @@ __global__ __launch_bounds__(kCurvNT, (kDebug || kEdge) ? 3 : SSF_FEAT_WAVE_WAVE
 constexpr int kRunStep = 54;                     // new centres per 64-lane register
 constexpr int kRunMax = 64;                      // runs (and gaps) logged per chunk
 #ifndef SSF_FEAT_RUN_PF
-#define SSF_FEAT_RUN_PF 4                        // registers in flight per wave
+#define SSF_FEAT_RUN_PF 3                        // registers in flight per wave (r5ao: 3 0.0955 vs 4 0.0966 ms)
 #endif
 constexpr int kRunPF = SSF_FEAT_RUN_PF;
+#ifndef SSF_FEAT_RUN_SOFF
+#define SSF_FEAT_RUN_SOFF 0                      // A/B: the register step as the buffer load's SGPR offset
+#endif
+#ifndef SSF_FEAT_RUN_BALLOT1
+#define SSF_FEAT_RUN_BALLOT1 0                   // A/B: the interior test as one ballot of a combined predicate
+#endif
 
 SSF_DEV float dpp_shr1(float v) {                // lane l <- lane l - 1 (lane 0 <- 0)
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
@@ -1667,7 +1673,12 @@ __global__ __launch_bounds__(kCurvNT, kDebug ? 2 : SSF_FEAT_RUN_WAVES) void k_fe
     const uint32_t sb = (uint32_t)stride * 4u;
     const uint32_t voff0 = (uint32_t)(q0 + lane) * sb, vstep = (uint32_t)kRunStep * sb;
     auto load_reg = [&](int k, float& x, float& y, float& z, uint32_t& kp) {
+#if SSF_FEAT_RUN_SOFF
+        // the register's step as the scalar offset (SGPR): no vector add per load
+        const i3v v = __builtin_amdgcn_raw_buffer_load_b96(prs, voff0, (int)((uint32_t)k * vstep), 0);
+#else
         const i3v v = __builtin_amdgcn_raw_buffer_load_b96(prs, voff0 + (uint32_t)k * vstep, 0, 0);
+#endif
         x = __int_as_float(v.x); y = __int_as_float(v.y); z = __int_as_float(v.z);
         kp = keep ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(krs, (uint32_t)(q0 + lane + kRunStep * k), 0, 0) : 1u;
     };
@@ -1701,8 +1712,12 @@ __global__ __launch_bounds__(kCurvNT, kDebug ? 2 : SSF_FEAT_RUN_WAVES) void k_fe
         const float ra = cz * __builtin_amdgcn_rsqf(r2);
         // (no upper bound on r2 needed: r2 = +inf gives ra = 0 = the exact z / sqrtf(inf); the
         // lower one keeps zero and denormal r2 off the fast path)
+#if SSF_FEAT_RUN_BALLOT1
+        const uint64_t INR = __builtin_amdgcn_ballot_w64((ra >= glo) & (ra < ghi) & (r2 > 1e-30f));
+#else
         const uint64_t INR = __builtin_amdgcn_ballot_w64(ra >= glo) & __builtin_amdgcn_ballot_w64(ra < ghi) &
                              __builtin_amdgcn_ballot_w64(r2 > 1e-30f);
+#endif
         if (k >= 1 && k <= kint && INR == ~0ull) {           // uniform: an interior register, all row g
             float dx, dy, dz;
             lane_tap11x3(cx, cy, cz, dx, dy, dz);

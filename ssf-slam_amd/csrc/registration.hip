@@ -639,7 +639,8 @@ constexpr int kStripPerMax = kSortMax / kStripThreads;   // x-order points per t
 // r = k kStripThreads + tid with its original index in .w.  Writes the strip-major points (F,
 // or X | Y | Z + I16), T.start / T.ylo / T.yhi; returns the strip geometry.
 template <bool kSoa, int kPer, class Get>
-SSF_DEV StripGeo strips_build(Get get, int m, StripLds& T, float4* F, float* X, uint16_t* I16) {
+SSF_DEV StripGeo strips_build(Get get, int m, StripLds& T, float4* F, float* X, uint16_t* I16,
+                              float wmin = 1.001f) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     float y0 = __builtin_inff(), y1 = -__builtin_inff();
 #pragma unroll
@@ -657,10 +658,11 @@ SSF_DEV StripGeo strips_build(Get get, int m, StripLds& T, float4* F, float* X, 
     y0 = __builtin_inff(); y1 = -__builtin_inff();
     for (int k = 0; k < kStripWaves; ++k) { y0 = fminf(y0, T.red[2 * k]); y1 = fmaxf(y1, T.red[2 * k + 1]); }
     g.y0 = y0;
-    // W > 1 m by a margin far above the float error of the strip assignment: a point two strips
-    // away from the query's is then always more than 1 m away (the bounded 30-NN searches the
-    // query's strip and its two neighbours only)
-    g.W = fmaxf(1.001f, (y1 - y0) / (float)(kStripMax - 1));
+    // W > 1 m (wmin) by a margin far above the float error of the strip assignment: a point two
+    // strips away from the query's is then always more than 1 m away (the bounded 30-NN searches
+    // the query's strip and its two neighbours only).  The plane table's pick walks take
+    // wmin = 0.5005 (visit_1m then covers two strips on each side).
+    g.W = fmaxf(wmin, (y1 - y0) / (float)(kStripMax - 1));
     g.invW = 1.0f / g.W;
     g.ns = min(kStripMax, (int)((y1 - y0) * g.invW) + 1);
     // histogram (cursor holds the counts), exclusive scan into start
@@ -888,15 +890,25 @@ SSF_DEV void strip_visit(const StripView<false>& v, const StripLds& T, int sidx,
     }
 }
 
-// The 1-m region: the query's strip and its two neighbours (strip width > 1 m).
-// pos[3]: the start positions in the query's strip (its own) and the neighbours (-1 until found).
+// The 1-m region: the query's strip and its neighbours -- one on each side for strips wider
+// than 1 m, two for strips of 0.5 .. 1 m (SSF_TABLE_PICK_W).  pos: the start positions in the
+// query's strip (its own) and the neighbours (-1 until found).
+#ifndef SSF_TABLE_PICK_W
+#define SSF_TABLE_PICK_W 1.001f                  // pick-walk strip width floor (0.5005f: five strips, r5aq: 0.342 vs 0.276 ms, slower)
+#endif
+constexpr float kPickStripW = SSF_TABLE_PICK_W;
+constexpr int kPos1m = kPickStripW < 1.0f ? 5 : 3;
 template <class Bound, class Body>
-SSF_DEV void visit_1m(const StripView<false>& v, const StripLds& T, const StripGeo& g, int (&pos)[3],
+SSF_DEV void visit_1m(const StripView<false>& v, const StripLds& T, const StripGeo& g, int (&pos)[kPos1m],
                       const float4& q, Bound&& bound, Body&& body) {
     const int s0 = g.strip_of(q.y);
     strip_visit(v, T, s0, pos[0], q, 1.0f, bound, body);
     if (s0 + 1 < g.ns) strip_visit(v, T, s0 + 1, pos[1], q, 1.0f, bound, body);
     if (s0 - 1 >= 0) strip_visit(v, T, s0 - 1, pos[2], q, 1.0f, bound, body);
+    if (kPos1m == 5 && g.W < 1.0f) {                                   // uniform per frame
+        if (s0 + 2 < g.ns) strip_visit(v, T, s0 + 2, pos[kPos1m == 5 ? 3 : 0], q, 1.0f, bound, body);
+        if (s0 - 2 >= 0) strip_visit(v, T, s0 - 2, pos[kPos1m == 5 ? 4 : 0], q, 1.0f, bound, body);
+    }
 }
 
 // Every strip outward from q's, in rings of strips, while a strip can still hold a point with
@@ -949,7 +961,7 @@ SSF_DEV void plane_from_pick(const float4* __restrict__ P, const int (&v5)[5], f
 }
 
 struct PickState {
-    int pos[3];         // strip start positions of the 1-m region (visit_1m)
+    int pos[kPos1m];    // strip start positions of the 1-m region (visit_1m)
     double t5[5];       // ranks 0..4
     double d1, d2;      // the first two other-ring keys of rank >= 5 within 1 m (sentinel: 1 m)
     int K1, prow;
@@ -969,7 +981,9 @@ SSF_DEV void pick_1m(const float4* __restrict__ P, const StripView<false>& v, co
     for (int k = 0; k < 6; ++k) o6[k] = sent;
     const int qrow = pt_row(q);
     int K1 = 0;
-    s.pos[0] = j; s.pos[1] = -1; s.pos[2] = -1;
+    s.pos[0] = j;
+#pragma unroll
+    for (int k = 1; k < kPos1m; ++k) s.pos[k] = -1;
     visit_1m(v, T, g, s.pos, q, [] { return 1.0f; }, [&](const float4& p) {
         const float d = l2_simple(q, p);
         if (d < 1.0f) {
@@ -1493,7 +1507,10 @@ __global__ __launch_bounds__(kTableThreads) void k_plane_table_sorted(
                 p.w = __int_as_float(own[k] | (int)(row_code(p.w) << 16));
                 return p;
             };
-            const StripGeo g = strips_build<false, kStripPerMax>(getp, m, T, F, X, I16);
+            // the pick walks (rows_ok, m > kK) take the narrower strips; table_strip_walks' ring
+            // searches (strip_knn_radius) count rings in metres and need W > 1 m
+            const StripGeo g = strips_build<false, kStripPerMax>(getp, m, T, F, X, I16,
+                                                                 (rows_ok && m > kK) ? kPickStripW : 1.001f);
             SSF_TSTAMP_BUILD();
             // results staged in LDS at their original index and stored coalesced at the end when
             // 13 B per point fit behind the strip image with a queue of m / 4 entries (m <= ~5000):

@@ -1881,6 +1881,10 @@ constexpr float kAssocDeferR = SSF_ASSOC_DEFER_R; // a query still open after th
 #endif
 constexpr int kAssocCoopG = SSF_ASSOC_COOP_G;
 constexpr int kAssocCoopPairs = 16;             // launches of at most this many pairs take the group mode
+#ifndef SSF_ASSOC_BIG_G
+#define SSF_ASSOC_BIG_G 0                        // A/B: group mode with this many lanes for big launches too
+#endif
+constexpr int kAssocBigG = SSF_ASSOC_BIG_G;
 template <bool kSoa, int kCoopG = 0>
 __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     const float4* __restrict__ last, const int64_t* __restrict__ last_off,
@@ -2000,8 +2004,8 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     if (kCoopG > 0) {
         // one query per kCoopG-lane group (groups are aligned lane ranges: the reductions stay
         // inside one), the same levels and bounds as the deferred pass below
-        const int gl = tid % kCoopG, i = (int)blockIdx.y * kQpw + tid / kCoopG;
-        if (i < mc) {                                                   // uniform per group
+        const int gl = tid % kCoopG;
+        for (int i = (int)blockIdx.y * kQpw + tid / kCoopG; i < mc; i += (int)gridDim.y * kQpw) {   // uniform per group
             const float4 pc = curr[co + i];
             const float4 qs = assoc_query_point(pc, q, t);
             float best = __builtin_inff();
@@ -3249,11 +3253,14 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
             // spreads over ~256 CUs instead of n_pairs
             const bool coop = kAssocCoopG > 0 && n_pairs <= kAssocCoopPairs;
             constexpr int kQpwCoop = kAssocCoopG > 0 ? kStripThreads / kAssocCoopG : kStripThreads;
+            // big launches: one work-group per pair, the lane mode (or SSF_ASSOC_BIG_G-lane groups, A/B)
+            const bool bigc = !coop && kAssocBigG > 0;
             const int qsplit = coop ? (int)((max_m + kQpwCoop - 1) / kQpwCoop)
                                     : (int)std::max<int64_t>(1, std::min<int64_t>({8, 256 / n_pairs,
                                                              (max_m + kStripThreads - 1) / kStripThreads}));
             kmark(s, coop ? "k_associate_strips_coop" : soa ? "k_associate_strips_soa" : "k_associate_strips");
             hipLaunchKernelGGL(coop ? (soa ? k_associate_strips<true, kAssocCoopG> : k_associate_strips<false, kAssocCoopG>)
+                                    : bigc ? (soa ? k_associate_strips<true, kAssocBigG> : k_associate_strips<false, kAssocBigG>)
                                     : (soa ? k_associate_strips<true> : k_associate_strips<false>),
                                dim3(n_pairs, qsplit), dim3(kStripThreads), lds, s, last, last_off, last_count,
                                last_normal, last_valid, last_sorted, last_sidx, curr, curr_off,

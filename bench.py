@@ -374,6 +374,11 @@ class Pipeline:
                        torch.empty(T, dtype=torch.int32, device=d),
                        torch.empty((T, 4), dtype=torch.float32, device=d),
                        torch.empty(T, dtype=torch.int32, device=d))))
+            if self.args.edges:             # the edge cloud and its line table (--edges)
+                self.ring[-1].update(edge=torch.empty((T, 4), dtype=torch.float32, device=d),
+                                     ecount=torch.empty(B, dtype=torch.int32, device=d),
+                                     etable=(torch.empty((T, 6), dtype=torch.float32, device=d),
+                                             torch.empty(T, dtype=torch.uint8, device=d)))
         return self.ring[i]
 
     def contexts(self):
@@ -415,14 +420,16 @@ class Pipeline:
             es = [mk() for _ in range(3)]
             es[0].record(s_feat)
             if a.edges:                     # beyond the reference: edge features as well
-                pb, eb = self.fe_feat.extract_features_batch(pos, off, h_off, max_points=self.N, keep=keep)
+                pb, eb = self.fe_feat.extract_features_batch(
+                    pos, off, h_off, max_points=self.N, keep=keep,
+                    out=None if ring is None else (ring["plane"], ring["count"], ring["edge"], ring["ecount"]))
             else:
                 pb = self.fe_feat.extract_planes_batch(pos, off, h_off, max_points=self.N, keep=keep,
                                                        out=None if ring is None else (ring["plane"], ring["count"]))
             es[1].record(s_feat)
-            table = self.fe_feat.plane_table(pb, out=None if ring is None or a.edges else ring["table"])
+            table = self.fe_feat.plane_table(pb, out=None if ring is None else ring["table"])
             if a.edges:
-                etable = self.fe_feat.edge_table(eb)
+                etable = self.fe_feat.edge_table(eb, out=None if ring is None else ring["etable"])
             es[2].record(s_feat)
         if s_reg is not s_feat:
             # registration k needs the plane cloud of step k and the TABLE OF STEP k - 1 (on s_feat
@@ -432,7 +439,7 @@ class Pipeline:
             # the plane batch and its table are read on s_reg in this step and the next: keep
             # the caching allocator from handing their blocks to s_feat until s_reg is done
             extra = (eb.xyzi, eb.count, *etable) if a.edges else ()
-            if ring is None or a.edges:     # ring buffers are guarded by the events above instead
+            if ring is None:                # ring buffers are guarded by the events above instead
                 for t in (pb.xyzi, pb.count, *table.tensors(), *extra):
                     t.record_stream(s_reg)
         stats = None

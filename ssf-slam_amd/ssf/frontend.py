@@ -208,18 +208,26 @@ class Frontend:
             return pb, ring, roff.view(max(F, 1), self.n_rows + 1)[:F], curv
         return pb
 
-    def extract_features_batch(self, pts, off, h_off, max_points=None, keep=None):
+    def extract_features_batch(self, pts, off, h_off, max_points=None, keep=None, out=None):
         """extract_planes_batch plus the edge cloud (beyond the reference: edge features,
-        ssf_extract_features_batch) -> (planes PlaneBatch, edges PlaneBatch)."""
+        ssf_extract_features_batch) -> (planes PlaneBatch, edges PlaneBatch).
+        out: optional preallocated (plane [>= total, 4], count [>= F], edge [>= total, 4],
+        ecount [>= F])."""
         pts = self._dev(pts, torch.float32)
         F = h_off.numel() - 1
         total = int(h_off[-1])
         sizes = (h_off[1:] - h_off[:-1])
         mx = int(sizes.max()) if max_points is None and F > 0 else int(max_points or 0)
-        plane = torch.empty((max(total, 1), 4), dtype=torch.float32, device=self.device)
-        count = torch.empty(max(F, 1), dtype=torch.int32, device=self.device)
-        edge = torch.empty((max(total, 1), 4), dtype=torch.float32, device=self.device)
-        ecount = torch.empty(max(F, 1), dtype=torch.int32, device=self.device)
+        if out is not None:
+            plane = self._out(out[0], (max(total, 1), 4), torch.float32, "plane out")
+            count = self._out(out[1], (max(F, 1),), torch.int32, "count out")
+            edge = self._out(out[2], (max(total, 1), 4), torch.float32, "edge out")
+            ecount = self._out(out[3], (max(F, 1),), torch.int32, "edge count out")
+        else:
+            plane = torch.empty((max(total, 1), 4), dtype=torch.float32, device=self.device)
+            count = torch.empty(max(F, 1), dtype=torch.int32, device=self.device)
+            edge = torch.empty((max(total, 1), 4), dtype=torch.float32, device=self.device)
+            ecount = torch.empty(max(F, 1), dtype=torch.int32, device=self.device)
         if keep is not None:
             keep = self._dev(keep, torch.uint8)
             if keep.numel() != total:
@@ -234,12 +242,17 @@ class Frontend:
         eb = PlaneBatch(edge, ecount[:F], off, h_off, min(mx, mx // max(1, span) + self.n_rows + 1))
         return pb, eb
 
-    def edge_table(self, eb: PlaneBatch):
+    def edge_table(self, eb: PlaneBatch, out=None):
         """Line table of frames that will be LAST frames (beyond the reference):
-        -> (line [total, 6] f32: centroid, direction; valid [total] u8)."""
+        -> (line [total, 6] f32: centroid, direction; valid [total] u8).
+        out: optional preallocated (line, valid)."""
         total = eb.xyzi.shape[0]
-        line = torch.empty((total, 6), dtype=torch.float32, device=self.device)
-        valid = torch.empty(total, dtype=torch.uint8, device=self.device)
+        if out is not None:
+            line = self._out(out[0], (total, 6), torch.float32, "line out")
+            valid = self._out(out[1], (total,), torch.uint8, "line valid out")
+        else:
+            line = torch.empty((total, 6), dtype=torch.float32, device=self.device)
+            valid = torch.empty(total, dtype=torch.uint8, device=self.device)
         rc = _abi.lib().ssf_edge_table_batch(self._h, _stream(self.device), eb.count.numel(),
                                              _ptr(eb.xyzi), _ptr(eb.off), _ptr(eb.count),
                                              eb.max_points, _ptr(line), _ptr(valid))

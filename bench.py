@@ -67,6 +67,13 @@ def _load_profile(path, B, N, masked, layout="azimuth"):
     return t
 
 
+def _alloc_delta(mem0, mem1):
+    """the caching allocator inside the timed region: device allocations (hipMalloc) and retries
+    (a retry frees cached blocks and synchronises the device)"""
+    return {k: int(mem1.get(k, 0)) - int(mem0.get(k, 0))
+            for k in ("num_alloc_retries", "num_device_alloc", "num_device_free", "num_ooms")}
+
+
 def _lib_sha16():
     """sha256[:16] of the front-end library this run loads (ties committed PMC profiles to a build)"""
     import hashlib
@@ -970,6 +977,7 @@ def sequences(args, world=1, rank=0, local=0):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    mem0 = torch.cuda.memory_stats(dev)
     t0 = time.perf_counter()
     for j in range(W, W + S):
         step(j, True)
@@ -986,6 +994,7 @@ def sequences(args, world=1, rank=0, local=0):
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    allocator = _alloc_delta(mem0, torch.cuda.memory_stats(dev))
     if tl and rank == 0:
         z = tl[0]["mask"][0]
         h0 = tl[0]["host"][0]
@@ -1043,6 +1052,7 @@ def sequences(args, world=1, rank=0, local=0):
         "gather_check": gather_ok, "poses_finite": finite,
         "data_gen_s": round(t_data, 2),
         "final_t_norm": float(mine[-1, :, 4:7].norm(dim=1).mean()),
+        "allocator_timed_region": allocator,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -1144,11 +1154,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    mem1 = torch.cuda.memory_stats(dev)
-    # the caching allocator inside the timed region: device allocations (hipMalloc) and retries
-    # (a retry frees cached blocks and synchronises the device) -- both 0 with the buffer ring
-    allocator = {k: int(mem1.get(k, 0)) - int(mem0.get(k, 0))
-                 for k in ("num_alloc_retries", "num_device_alloc", "num_device_free", "num_ooms")}
+    # the caching allocator inside the timed region: 0 device allocations and retries with the
+    # buffer ring
+    allocator = _alloc_delta(mem0, torch.cuda.memory_stats(dev))
     if args.dump_poses and rank == 0:
         np.save(args.dump_poses, pipe.pose_abs.cpu().numpy())
     gather_ok = None

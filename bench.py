@@ -140,6 +140,8 @@ def parse(argv=None):
                          "prints the world it sees and exits (no GPU is touched)")
     ap.add_argument("--mask-split", type=int, default=0,
                     help="work-groups per frame of the GMM fit (0: automatic, ssf_set_mask_split)")
+    ap.add_argument("--seq-ring", type=int, default=8,
+                    help="with --consecutive / --sequences-total: step buffers in the ring (>= 3)")
     ap.add_argument("--no-chain-api", action="store_true",
                     help="with --consecutive and one sequence: one ssf_register_batch call per chained pair "
                          "(the round-4 path) instead of ssf_register_chain")
@@ -858,12 +860,36 @@ def sequences(args, world=1, rank=0, local=0):
         return ssf.PlaneBatch(pb.xyzi, pb.count[a * B:b * B], pb.off[a * B:b * B + 1],
                               pb.h_off[a * B:b * B + 1], pb.max_points), table
 
-    def warm_start(out):
-        """the SSF Kabsch poses [t, q] of mask_pose -> registration warm starts [q, t] (identity
-        where the mask reported a failure)"""
-        w = torch.cat([out[:, 3:7], out[:, 0:3]], 1)
-        ok = (out[:, 16] == 0).unsqueeze(1)
-        return torch.where(ok, w, ssf.identity_poses(out.shape[0], dev)).contiguous()
+    def warm_start(out, dst):
+        """the SSF Kabsch poses [t, q] of mask_pose -> registration warm starts [q, t] written into
+        dst (identity where the mask reported a failure)"""
+        dst[:, 0:4].copy_(out[:, 3:7])
+        dst[:, 4:7].copy_(out[:, 0:3])
+        bad = out[:, 16] != 0
+        dst[:, 0:3].masked_fill_(bad.unsqueeze(1), 0.0)
+        dst[:, 3].masked_fill_(bad, 1.0)
+        dst[:, 4:7].masked_fill_(bad.unsqueeze(1), 0.0)
+
+    # a ring of step buffers (mask output and background, plane cloud, plane table), allocated
+    # here instead of per step: slot j % SR holds step j's; its last reader is the registration of
+    # step j + 1, so step j waits for the registration of step j + 1 - SR before overwriting it.
+    # The per-step pose records go to preallocated [steps, K, B, 7] arrays.
+    SR = max(3, args.seq_ring)
+    T_ = K * B * N
+    ring = [dict(out=torch.empty((K * B, 32), dtype=torch.float64, device=dev),
+                 bg=torch.empty(T_, dtype=torch.uint8, device=dev),
+                 plane=torch.empty((T_, 4), dtype=torch.float32, device=dev),
+                 count=torch.empty(K * B, dtype=torch.int32, device=dev),
+                 table=(torch.empty((T_, 3), dtype=torch.float32, device=dev),
+                        torch.empty(T_, dtype=torch.uint8, device=dev),
+                        torch.empty((T_, 4), dtype=torch.float32, device=dev),
+                        torch.empty(T_, dtype=torch.int32, device=dev),
+                        torch.empty((T_, 4), dtype=torch.float32, device=dev),
+                        torch.empty(T_, dtype=torch.int32, device=dev)))
+            for _ in range(SR)]
+    rec_rel = torch.empty((n_steps, K, B, 7), dtype=torch.float64, device=dev)
+    rec_m = torch.empty((n_steps, K, B, 7), dtype=torch.float64, device=dev)
+    reg_done = {}
 
     # prologue: frame 0 -> the first last frames (and its Kabsch pose: pair (0, 1)'s warm start)
     with torch.cuda.stream(s_feat):
@@ -887,37 +913,41 @@ def sequences(args, world=1, rank=0, local=0):
         nonlocal last, prev_out
         pos, flow = steps[j]
         sm = s_masks[j % len(s_masks)]
+        slot = ring[j % SR]
+        if (j + 1 - SR) in reg_done:                        # the slot's last reader is done
+            prev = reg_done.pop(j + 1 - SR)
+            sm.wait_event(prev)
+            s_feat.wait_event(prev)
         rec = {} if (timing and (args.timeline or args.timeline_host)) else None
         hst = [time.perf_counter()] if rec is not None else None   # host enqueue times
         with torch.cuda.stream(sm):
             if rec is not None:
                 rec["mask"] = [ev(sm)]
-            out, bg = fe_mask.mask_pose(pos, flow, offK, hK, mode="gmm", want_mask=True)
+            out, bg = fe_mask.mask_pose(pos, flow, offK, hK, mode="gmm", want_mask=True,
+                                        out=(slot["out"], slot["bg"]))
             if rec is not None:
                 hst.append(time.perf_counter())
                 rec["mask"].append(ev(sm))
-            mrec = out[:, 0:7].view(K, B, 7).clone()       # the SSF poses, on their stream
+            mrec = rec_m[j]
+            mrec.copy_(out[:, 0:7].view(K, B, 7))           # the SSF poses, on their stream
             done = torch.cuda.Event()
             done.record(sm)
-        if masked:
+        if masked:                                          # configs[2]: the features wait for the mask
             s_feat.wait_event(done)
-            bg.record_stream(s_feat)
         with torch.cuda.stream(s_feat):
             if rec is not None:
                 hst.append(time.perf_counter())
                 rec["feat"] = [ev(s_feat)]
-            pb = fe_feat.extract_planes_batch(pos, offK, hK, max_points=N, keep=bg if masked else None)
-            table = fe_feat.plane_table(pb)
+            pb = fe_feat.extract_planes_batch(pos, offK, hK, max_points=N, keep=bg if masked else None,
+                                              out=(slot["plane"], slot["count"]))
+            table = fe_feat.plane_table(pb, out=slot["table"])
             tdone = torch.cuda.Event()
             tdone.record(s_feat)
             if rec is not None:
                 rec["feat"].append(ev(s_feat))
         s_reg.wait_event(tdone)
-        for t in (pb.xyzi, pb.count, *table.tensors()):
-            t.record_stream(s_reg)
         if kws:
             s_reg.wait_event(done)
-            out.record_stream(s_reg)
         with torch.cuda.stream(s_reg):
             if rec is not None:
                 hst.append(time.perf_counter())
@@ -925,17 +955,20 @@ def sequences(args, world=1, rank=0, local=0):
             (lpb, ltab) = last
             if kws:
                 # pair (slot kk - 1 -> slot kk) starts from the Kabsch pose of frame kk - 1
-                ws = torch.cat([warm_start(prev_out), warm_start(out[:(K - 1) * B])], 0)
+                ws = rec_rel[j].view(K * B, 7)
+                warm_start(prev_out, ws[:B])
+                if K > 1:
+                    warm_start(out[:(K - 1) * B], ws[B:])
                 fe_reg.register(lpb, ltab, view(pb, table, 0)[0], ws[:B])
                 if K > 1:
                     fe_reg.register(*view(pb, table, 0, K - 1), view(pb, table, 1, K)[0], ws[B:])
-                rel_k = ws.view(K, B, 7)
+                rel_k = rec_rel[j]
             elif B == 1 and not args.no_chain_api:
                 # one sequence: the boundary pair (the previous step's last frame -> frame 0) by
                 # ssf_register_batch, then the K - 1 pairs inside this step's batch by ONE
                 # ssf_register_chain call (each link reads the previous solution in place: no
                 # per-pair copy launches, no per-pair host calls)
-                seq = torch.empty((K, 7), dtype=torch.float64, device=dev)
+                seq = rec_rel[j].view(K, 7)
                 seq[0:1].copy_(rel)
                 fe_reg.register(lpb, ltab, view(pb, table, 0)[0], seq[0:1], ab)
                 if K > 1:
@@ -943,15 +976,17 @@ def sequences(args, world=1, rank=0, local=0):
                                                out=seq[1:])
                     ab.copy_(ch["pose_abs_seq"][-1:])
                 rel.copy_(seq[K - 1:K])
-                rel_k = seq.view(K, 1, 7)
+                rel_k = rec_rel[j]
             else:
-                snaps = []
                 for kk in range(K):
                     cur = view(pb, table, kk)
                     fe_reg.register(lpb, ltab, cur[0], rel, ab)
-                    snaps.append(rel.clone())
+                    rec_rel[j][kk].copy_(rel)
                     (lpb, ltab) = cur
-                rel_k = torch.stack(snaps, 0)
+                rel_k = rec_rel[j]
+            rdone = torch.cuda.Event()
+            rdone.record(s_reg)
+            reg_done[j] = rdone
             records.append((rel_k, mrec, sm))                # (warmup records are dropped)
             if rec is not None:
                 rec["reg"].append(ev(s_reg))

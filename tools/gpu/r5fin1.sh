@@ -24,3 +24,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats $RX --output-format csv -d /t
 cp $(find /tmp/pl -name "*kernel_stats.csv" | head -1) gpurun_out/${T}_latency_kernel_stats.csv && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats $RX --output-format csv -d /tmp/pc -o c -- python -u bench.py --layout carla --serial --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${T}_carla_serial.log 2>&1 && echo CARLA_SERIAL_OK && \
 cp $(find /tmp/pc -name "*kernel_stats.csv" | head -1) gpurun_out/${T}_carla_serial_kernel_stats.csv && echo PART1_DONE
+# (round 5, second pass) the carla PMC traffic of the same build, for the carla lines of part 2
+BC="python -u bench.py --layout carla --serial --steps 3 --warmup 1 --no-cpu-baseline --distinct 32"
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE $RX --output-format csv -d /tmp/pcf -o f -- $BC > gpurun_out/${T}_carla_pmc_fetch.log 2>&1 && echo CFETCH_OK && \
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE $RX --output-format csv -d /tmp/pcw -o w -- $BC > gpurun_out/${T}_carla_pmc_write.log 2>&1 && echo CWRITE_OK && \
+python tools/pmc_traffic.py $(find /tmp/pcf -name "*counter_collection.csv" | head -1) $(find /tmp/pcw -name "*counter_collection.csv" | head -1) --bench-log gpurun_out/${T}_carla_pmc_fetch.log --out gpurun_out/${T}_carla_traffic.json > /dev/null && echo CTRAFFIC_OK

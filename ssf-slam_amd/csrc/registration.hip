@@ -1869,6 +1869,10 @@ __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
 #endif
 constexpr int kAssocDeferMax = 512;              // deferred queries per work-group (more: the lane goes on)
 constexpr float kAssocDeferR = SSF_ASSOC_DEFER_R; // a query still open after this level is deferred
+#ifndef SSF_ASSOC_DEFER_G
+#define SSF_ASSOC_DEFER_G 64
+#endif
+constexpr int kAssocDeferG = SSF_ASSOC_DEFER_G;  // lanes per deferred query (a wave at 64)
 // kCoopG > 0 (launches of few pairs: a node's one pair, configs[2]'s chained pairs): one query
 // per group of kCoopG lanes instead of one per lane -- the query's strips of each search level
 // spread over the group's lanes (one strip per lane), so no lane walks ring after ring alone,
@@ -2102,9 +2106,10 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     const unsigned long long rtl = __builtin_amdgcn_s_memrealtime();   // the slowest wave's lane pass
 #endif
     if (kCoopG == 0) {
-        const int nq = min(dqn, kDq), lane = tid & 63;
-        for (int e = tid >> 6; e < nq; e += kStripThreads / 64) {
-            const int i = dq[e];                                          // uniform per wave
+        constexpr int DG = kAssocDeferG;                                  // lanes per deferred query
+        const int nq = min(dqn, kDq), lane = tid % DG;
+        for (int e = tid / DG; e < nq; e += kStripThreads / DG) {
+            const int i = dq[e];                                          // uniform per group
             const float4 pc = curr[co + i];
             const float4 qs = assoc_query_point(pc, q, t);
             float best = __builtin_inff();
@@ -2115,11 +2120,11 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
                 const float lim = unbounded ? __builtin_inff() : R * R;
                 const int sa = unbounded ? 0 : strip_of(qs.y - R - W - 1e-3f);
                 const int sb = unbounded ? ns - 1 : strip_of(qs.y + R + W + 1e-3f);
-                for (int sidx = sa + lane; sidx <= sb; sidx += 64) search(sidx, lim, qs, best, bc);
+                for (int sidx = sa + lane; sidx <= sb; sidx += DG) search(sidx, lim, qs, best, bc);
                 unsigned long long k = bc >= 0
                     ? ((unsigned long long)__float_as_uint(best) << 32) | (unsigned)v.id(bc) : ~0ull;
 #pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) {
+                for (int o = DG / 2; o >= 1; o >>= 1) {
                     const unsigned long long x = __shfl_xor(k, o, kWave);
                     k = x < k ? x : k;
                 }

@@ -363,6 +363,9 @@ class Pipeline:
         self.records = []           # per timed step: the pose record this rank contributed
         self.gathered = []          # per timed step: the all-gathered records of every rank
         self.snaps = []             # (pose snapshot on s_reg, mask out, its streams) until exchange()
+        # the per-step pose snapshots of N > 1 (exchange()), allocated here, not per step
+        self.snapbuf = (torch.empty((args.steps, B, 7), dtype=torch.float64, device=dev)
+                        if world > 1 else None)
         self.ev = {k: [] for k in ("mask", "feat", "table", "reg")}
 
     RING = 4
@@ -462,7 +465,10 @@ class Pipeline:
                 if want_stats:
                     stats = (res["ncorr"], res["nlog"])
             r1.record(s_reg)
-            snap = self.pose_abs.clone() if self.world > 1 else None   # step-k poses, on s_reg
+            snap = None
+            if self.world > 1 and timing:     # step-k poses, on s_reg, into the preallocated records
+                snap = self.snapbuf[len(self.snaps)]
+                snap.copy_(self.pose_abs)
         if ring is not None:
             self.reg_done[k] = r1
             if a.mask_before_features:

@@ -1920,6 +1920,9 @@ __global__ __launch_bounds__(kCurvNT, kDebug ? 2 : SSF_FEAT_RUN_WAVES) void k_fe
 // chunk its indexInRow falls in).  After a row prefix every thread emits framePlanePtr-ordered
 // output: the point gathered through the slot's index, intensity = indexInRow + row / 100.0 (:77).
 constexpr int kFeatRowWords = kFeatMaxChunks * kFeatWords + 1;   // ring-order words of a frame (+1)
+#ifndef SSF_SEL_OUT_U
+#define SSF_SEL_OUT_U 1                          // r5az: 1 0.0477, 2 0.0495, 4 0.0515, 8 0.0556 ms
+#endif
 
 template <bool kEdge>
 __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __restrict__ pts, int stride,
@@ -2223,7 +2226,7 @@ __global__ __launch_bounds__(kSelThreads) void k_feat_select(const float* __rest
         const int32_t* S = e ? esel + fb : (lds_in ? sel_l : sel + fb);
         const int* SB = lds_in ? lb : ro;                     // per-row slot bases
         float4* O = e ? edge : plane;
-        constexpr int U = 4;
+        constexpr int U = SSF_SEL_OUT_U;          // outputs per thread per trip (loads in flight)
         for (int k0 = 0; k0 < total; k0 += U * kSelThreads) {   // uniform
             int kk[U], rr[U], jj[U], ii[U];
 #pragma unroll

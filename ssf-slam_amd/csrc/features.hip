@@ -512,7 +512,10 @@ __global__ __launch_bounds__(kCurvNT) void k_bin_curv(const float* __restrict__ 
 // after one barrier the row counts are prefixed and every thread of the work-group emits
 // output slots in framePlanePtr order (row major): x, y, z gathered from the input through the
 // ring index, intensity = indexInRow + row / 100.0 (:77).
-constexpr int kSelThreads = 1024;
+#ifndef SSF_SEL_THREADS
+#define SSF_SEL_THREADS 1024
+#endif
+constexpr int kSelThreads = SSF_SEL_THREADS;
 constexpr int kSelWordsLds = 6144;              // candidate words staged per array (48 KiB: 393k points)
 
 // bit b of the result = bit `bit` of byte b of x (bytes' bits gathered by one multiply: the

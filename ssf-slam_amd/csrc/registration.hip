@@ -1900,7 +1900,14 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     int lds_cap, const float4* __restrict__ strip_xyzi, const int32_t* __restrict__ strip_head) {
     extern __shared__ float4 SL[];                  // [ml] strip-major, x-sorted in each strip
     __shared__ StripLds T;
-#if SSF_ASSOC_DEFER
+#if SSF_ASSOC_DEFER == 2
+    // far queries kept by their own wave (no barrier): each wave answers its list in groups of
+    // kAssocDeferG lanes after its lane walks (not in the SoA launch: no LDS left there)
+    constexpr int kDqW = 32;
+    __shared__ int dqw[kSoa ? 1 : kStripWaves][kSoa ? 1 : kDqW];
+    __shared__ int dqnw[kSoa ? 1 : kStripWaves];
+    if (!kSoa && (threadIdx.x & 63) == 0) dqnw[threadIdx.x >> 6] = 0;
+#elif SSF_ASSOC_DEFER
     // far queries, answered a wave each at the end (the SoA launch has ~0.3 KiB of LDS left)
     constexpr int kDq = kSoa ? kAssocDeferMax / 4 : kAssocDeferMax;
     __shared__ int dq[kDq];
@@ -2084,8 +2091,16 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
             // wave's (and often the launch's) time -- hand the query to the work-group's queue,
             // answered below by a whole wave, one strip per lane
             if (R >= kAssocDeferR) {
+#if SSF_ASSOC_DEFER == 2
+                if (!kSoa) {
+                    const int wq = tid >> 6;
+                    const int slot = atomicAdd(&dqnw[kSoa ? 0 : wq], 1);
+                    if (slot < kDqW) { dqw[kSoa ? 0 : wq][kSoa ? 0 : slot] = i; deferred = true; break; }
+                }
+#else
                 const int slot = atomicAdd(&dqn, 1);
                 if (slot < kDq) { dq[slot] = i; deferred = true; break; }
+#endif
             }
 #endif
         }
@@ -2101,6 +2116,19 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     // minimum of (distance, original index).  The same exact 1-NN as the lane walk: at the level
     // where the wave's best is <= R^2, every point at least as close was in a searched strip and
     // within every lane's bound.
+#if SSF_ASSOC_DEFER == 2
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");             // this wave's list is complete
+    __builtin_amdgcn_wave_barrier();
+#ifdef SSF_STRIPS_STAMPS
+    const unsigned long long rtl = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (kCoopG == 0 && !kSoa) {
+        constexpr int DG = kAssocDeferG;                                  // lanes per deferred query
+        const int wq = tid >> 6, lane = tid % DG;
+        const int nq = min(dqnw[kSoa ? 0 : wq], kDqW);
+        for (int e = (tid & 63) / DG; e < nq; e += 64 / DG) {
+            const int i = dqw[kSoa ? 0 : wq][kSoa ? 0 : e];               // uniform per group
+#else
     __syncthreads();
 #ifdef SSF_STRIPS_STAMPS
     const unsigned long long rtl = __builtin_amdgcn_s_memrealtime();   // the slowest wave's lane pass
@@ -2110,6 +2138,7 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
         const int nq = min(dqn, kDq), lane = tid % DG;
         for (int e = tid / DG; e < nq; e += kStripThreads / DG) {
             const int i = dq[e];                                          // uniform per group
+#endif
             const float4 pc = curr[co + i];
             const float4 qs = assoc_query_point(pc, q, t);
             float best = __builtin_inff();
@@ -2149,7 +2178,11 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
         int32_t* o = nn_out + co + kQpw * blockIdx.y;                // this work-group's own query slots
         o[0] = (int32_t)(rt1 - rt0); o[1] = (int32_t)(rt2 - rt0);
 #if SSF_ASSOC_DEFER
+#if SSF_ASSOC_DEFER == 1
         o[2] = (int32_t)(rtl - rt0); o[3] = dqn;
+#else
+        o[2] = (int32_t)(rtl - rt0); o[3] = 0;
+#endif
 #else
         o[2] = (int32_t)(rt2 - rt0); o[3] = 0;
 #endif

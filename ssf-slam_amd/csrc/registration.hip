@@ -1873,6 +1873,9 @@ constexpr float kAssocDeferR = SSF_ASSOC_DEFER_R; // a query still open after th
 #define SSF_ASSOC_DEFER_G 64
 #endif
 constexpr int kAssocDeferG = SSF_ASSOC_DEFER_G;  // lanes per deferred query (a wave at 64)
+#ifndef SSF_ASSOC_DEFER_EMPTY
+#define SSF_ASSOC_DEFER_EMPTY 0                  // defer only queries with no candidate yet (empty regions)
+#endif
 // kCoopG > 0 (launches of few pairs: a node's one pair, configs[2]'s chained pairs): one query
 // per group of kCoopG lanes instead of one per lane -- the query's strips of each search level
 // spread over the group's lanes (one strip per lane), so no lane walks ring after ring alone,
@@ -2090,7 +2093,7 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
             // a far 1-NN: the next levels' ~4 R / W strip searches in a row on one lane set the
             // wave's (and often the launch's) time -- hand the query to the work-group's queue,
             // answered below by a whole wave, one strip per lane
-            if (R >= kAssocDeferR) {
+            if (R >= kAssocDeferR && (!SSF_ASSOC_DEFER_EMPTY || !(best < __builtin_inff()))) {
 #if SSF_ASSOC_DEFER == 2
                 if (!kSoa) {
                     const int wq = tid >> 6;

@@ -140,6 +140,8 @@ def parse(argv=None):
                          "prints the world it sees and exits (no GPU is touched)")
     ap.add_argument("--mask-split", type=int, default=0,
                     help="work-groups per frame of the GMM fit (0: automatic, ssf_set_mask_split)")
+    ap.add_argument("--ring-depth", type=int, default=4,
+                    help="step buffers in the default pipeline's ring (>= 3)")
     ap.add_argument("--seq-ring", type=int, default=8,
                     help="with --consecutive / --sequences-total: step buffers in the ring (>= 3)")
     ap.add_argument("--no-chain-api", action="store_true",
@@ -358,6 +360,7 @@ class Pipeline:
         # registrations of steps k and k + 1, so step k waits for the registration of step
         # k + 2 - RING before it overwrites the slot
         self.ring, self.reg_done, self.feat_done = [], {}, {}
+        self.RING = max(3, args.ring_depth)
         if args.ring:
             self.slot(self.RING - 1)                          # every slot now, not in the timed region
         self.records = []           # per timed step: the pose record this rank contributed

@@ -175,6 +175,9 @@ def parse(argv=None):
     ap.add_argument("--no-ring", dest="ring", action="store_false",
                     help="allocate every step's plane cloud / plane table / mask outputs anew, with "
                          "cross-stream record_stream (the pipeline before round 5; A/B of the ring)")
+    ap.add_argument("--stagger", type=int, default=200,
+                    help="sequence b of a batch starts at frame (7 b) mod STAGGER (0: every sequence "
+                         "at frame 0), so the timed steps sample the whole sequence length")
     ap.add_argument("--mask-streams", type=int, default=3,
                     help="mask launches of consecutive steps alternate over this many streams: the "
                          "GMM of a frame depends on no other frame, so a step's slow frames overlap "
@@ -300,6 +303,23 @@ def cpu_baseline(args):
 
 
 # ---------------------------------------------------------------------------- data
+def stagger_starts(args, B):
+    """First frame of each sequence of the batch: sequence b starts at frame
+    (7 b) mod --stagger, so one step's B frames sit at B different points of their trajectories
+    and a short timed window samples the whole sequence length the reference replays
+    (PointCloudOdometry_noSeg.py:58-66 walks every frame of DATASET_PATH); --stagger 0 starts
+    every sequence at frame 0 (the lines before round 6)."""
+    P = int(getattr(args, "stagger", 0) or 0)
+    return [(7 * b) % P for b in range(B)] if P > 0 else None
+
+
+def frame_window(args, B, n_frames):
+    st = stagger_starts(args, B) or [0]
+    return {"stagger": int(getattr(args, "stagger", 0) or 0), "first_frame_min": min(st),
+            "first_frame_max": max(st), "frames_per_sequence": n_frames,
+            "timed_frames": [args.warmup, args.warmup + args.steps]}
+
+
 def make_data(args, dev, n_frames, rank, batch=None):
     """[n_frames] batches of B frames: pos/flow packed [B*N, 3] f32, resident in HBM.  Sequence
     b of rank r is synth sequence r * 100000 + (b mod distinct), ray-cast on the GPU
@@ -310,7 +330,8 @@ def make_data(args, dev, n_frames, rank, batch=None):
     S = max(1, min(args.distinct or B, B))
     N = args.rows * args.n_az
     scanner = synth.BatchScanner([rank * 100000 + (b % S) for b in range(B)], n_frames,
-                                 n_rows=args.rows, n_az=args.n_az, device=dev, layout=args.layout)
+                                 n_rows=args.rows, n_az=args.n_az, device=dev, layout=args.layout,
+                                 start=stagger_starts(args, B))
     out = []
     for k in range(n_frames):
         pos = torch.empty((B * N, 3), dtype=torch.float32, device=dev)
@@ -1255,6 +1276,7 @@ def main():
                    "world_size_initialised": (dist.get_world_size() if world > 1 else 1),
                    "backend": backend or "none",
                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) or None,
+                   "frame_window": frame_window(args, B, n_frames),
                    **({"rehearsal": "all ranks on one GPU, gloo"} if args.rehearse_one_gpu else {})},
         "roofline": None, "cpu_baseline": cpu,
         "kernels": kernels, "overlapped_event_ms": overlapped,

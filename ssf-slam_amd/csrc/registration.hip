@@ -2044,7 +2044,10 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
                 best = wb; bc = -1;
             }
             if (gl == 0) {
-                assoc_finish(L, lo, last_normal, last_valid, pc, (int)(key & 0xffffffffu), corr, nn_out, co + i);
+                // no candidate at all (a NaN query, e.g. after a NaN warm start): the lane mode's
+                // fallback, sorted rank 0, instead of index -1
+                assoc_finish(L, lo, last_normal, last_valid, pc, key == ~0ull ? v.id(0) : (int)(key & 0xffffffffu),
+                             corr, nn_out, co + i);
 #ifdef SSF_ASSOC_COUNT
                 if (nn_out) nn_out[co + i] = vis;
 #endif
@@ -2166,7 +2169,8 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
                 best = wb; bc = -1;          // the wave's bound (a tie taken later only raises a key)
             }
             if (lane == 0) {
-                assoc_finish(L, lo, last_normal, last_valid, pc, (int)(key & 0xffffffffu), corr, nn_out, co + i);
+                assoc_finish(L, lo, last_normal, last_valid, pc, key == ~0ull ? v.id(0) : (int)(key & 0xffffffffu),
+                             corr, nn_out, co + i);
 #ifdef SSF_ASSOC_COUNT
                 if (nn_out) nn_out[co + i] = -1;                        // deferred (diagnostic build)
 #endif
@@ -3296,7 +3300,10 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
             constexpr int kQpwCoop = kAssocCoopG > 0 ? kStripThreads / kAssocCoopG : kStripThreads;
             // big launches: one work-group per pair, the lane mode (or SSF_ASSOC_BIG_G-lane groups, A/B)
             const bool bigc = !coop && kAssocBigG > 0;
-            const int qsplit = coop ? (int)((max_m + kQpwCoop - 1) / kQpwCoop)
+            // (group mode: every work-group stages the whole last frame, so the split is capped at
+            // ~4 launch-filling waves of work-groups; the query loop strides over gridDim.y)
+            const int qsplit = coop ? (int)std::min<int64_t>((max_m + kQpwCoop - 1) / kQpwCoop,
+                                                             std::max(8, 1024 / n_pairs))
                                     : (int)std::max<int64_t>(1, std::min<int64_t>({8, 256 / n_pairs,
                                                              (max_m + kStripThreads - 1) / kStripThreads}));
             kmark(s, coop ? "k_associate_strips_coop" : soa ? "k_associate_strips_soa" : "k_associate_strips");

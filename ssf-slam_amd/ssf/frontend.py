@@ -202,7 +202,9 @@ class Frontend:
                 _ptr(plane), _ptr(count), _ptr(ring), _ptr(roff), _ptr(curv))
             self._check(rc, "ssf_extract_planes_batch_masked")
         # plane points per frame <= sum over rows of ceil(n_r / planeSpan) <= n/span + rows
-        pb = PlaneBatch(plane, count[:F], off, h_off,
+        # out= buffers may be larger than this call needs: hand on the first max(total, 1) rows
+        # (a view), so downstream sizes (plane_table, register_chain) follow the real point count
+        pb = PlaneBatch(plane[:max(total, 1)], count[:F], off, h_off,
                         min(mx, mx // max(1, self.cfg.plane_span) + self.n_rows + 1))
         if debug:
             return pb, ring, roff.view(max(F, 1), self.n_rows + 1)[:F], curv
@@ -237,9 +239,9 @@ class Frontend:
             _ptr(keep), _ptr(plane), _ptr(count), _ptr(edge), _ptr(ecount))
         self._check(rc, "ssf_extract_features_batch")
         span = getattr(self, "_edge_span", None) or (10 if self.n_rows == 64 else 3)
-        pb = PlaneBatch(plane, count[:F], off, h_off,
+        pb = PlaneBatch(plane[:max(total, 1)], count[:F], off, h_off,
                         min(mx, mx // max(1, self.cfg.plane_span) + self.n_rows + 1))
-        eb = PlaneBatch(edge, ecount[:F], off, h_off, min(mx, mx // max(1, span) + self.n_rows + 1))
+        eb = PlaneBatch(edge[:max(total, 1)], ecount[:F], off, h_off, min(mx, mx // max(1, span) + self.n_rows + 1))
         return pb, eb
 
     def edge_table(self, eb: PlaneBatch, out=None):

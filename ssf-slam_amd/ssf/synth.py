@@ -83,14 +83,26 @@ class Scene:
         self.cars = torch.tensor(cars, dtype=torch.float64)  # x0, y, vx, vy
         self.car_half = torch.tensor([2.3, 0.95, 0.75], dtype=torch.float64)
 
+    # Cars stay in a window around the ego (x relative to frame * EGO_SPEED in [CAR_LO, CAR_LO +
+    # CAR_SPAN), wrapping round): a car that leaves it ahead or behind re-enters at the other end,
+    # so the dynamic-point share stays steady along a sequence of any length, as in the CARLA
+    # sequences the reference replays (before round 6 the cars drifted out of range: ~2 % dynamic
+    # points at the first frames, none after frame ~60).  The motion within a frame (the flow's
+    # velocity) is unchanged.
+    CAR_LO, CAR_SPAN = -30.0, 70.0
+
     def car_boxes(self, frame: int) -> torch.Tensor:
         c = self.cars
-        cx = c[:, 0] + frame * c[:, 2]
+        ego = frame * EGO_SPEED
+        cx = ego + self.CAR_LO + torch.remainder(c[:, 0] + frame * c[:, 2] - ego - self.CAR_LO, self.CAR_SPAN)
         cy = c[:, 1] + frame * c[:, 3]
         cz = torch.full_like(cx, -2.5 + self.car_half[2].item())
         lo = torch.stack([cx, cy, cz], 1) - self.car_half
         hi = torch.stack([cx, cy, cz], 1) + self.car_half
         return torch.cat([lo, hi], 1)
+
+
+EGO_SPEED = 1.0           # m per frame (ego_pose / ego_poses default speed)
 
 
 def ego_yaw(seq: int, frame: int, yaw_rate: float = 0.004) -> float:
@@ -279,22 +291,28 @@ class BatchScanner:
     counter-based hash instead of torch's CPU generator.  Bench / test data only."""
 
     def __init__(self, seqs, n_frames: int, n_rows: int = 64, n_az: int = 1875, device="cuda",
-                 layout: str = "azimuth"):
+                 layout: str = "azimuth", start=None):
+        """start: optional first frame per sequence (frame(k) gives frame start[j] + k of sequence
+        j), so a batch's sequences sit at different points of their trajectories."""
         import numpy as np
         if layout not in LAYOUTS:
             raise ValueError(f"layout must be one of {LAYOUTS}")
         self.layout = layout
         self.seqs, self.n_rows, self.n_az, self.device = list(seqs), n_rows, n_az, torch.device(device)
+        self.start = [0] * len(self.seqs) if start is None else [int(v) for v in start]
+        if len(self.start) != len(self.seqs) or min(self.start, default=0) < 0:
+            raise ValueError("start must hold one frame index >= 0 per sequence")
         self.scenes = [Scene(s) for s in self.seqs]
-        self.poses = [ego_poses(s, n_frames + 1) for s in self.seqs]
+        self.poses = [ego_poses(s, n_frames + st + 1) for s, st in zip(self.seqs, self.start)]
         sc = self.scenes[0]
         self.n_box, self.n_pole, self.n_car = sc.boxes.shape[0], sc.poles.shape[0], sc.cars.shape[0]
         self.rec = 25 + 6 * self.n_box + 4 * self.n_pole + 9 * self.n_car
         self.elev = (elevations_deg(n_rows) * (math.pi / 180.0)).to(self.device)
         self._np = np
 
-    def frame(self, k: int, pos: torch.Tensor, flow: torch.Tensor):
-        """frame k of every sequence into pos / flow [S * N, 3] f32 (device, contiguous)."""
+    def frame(self, k0: int, pos: torch.Tensor, flow: torch.Tensor):
+        """frame start[j] + k0 of every sequence j into pos / flow [S * N, 3] f32 (device,
+        contiguous)."""
         import ctypes as C
         np = self._np
         S, N = len(self.seqs), self.n_rows * self.n_az
@@ -311,6 +329,7 @@ class BatchScanner:
         prm = np.zeros((S, self.rec))
         seeds = np.zeros(S, dtype=np.uint64)
         for j, (seq, sc) in enumerate(zip(self.seqs, self.scenes)):
+            k = k0 + self.start[j]
             R, p = self.poses[j]
             az0 = 2 * math.pi * torch.rand(1, generator=_gen(SEED_BASE + seq * 10000 + k),
                                            dtype=torch.float64).item() / n_az

@@ -92,6 +92,30 @@ def test_plane_table_duplicates_and_sizes(oracle, dev):
         assert np.array_equal(g.view(np.uint32), nr.view(np.uint32)), f
 
 
+def test_nan_warm_start_association_stays_in_frame(dev):
+    """A NaN warm start (an ill-conditioned link of a chain) makes every query point NaN: no
+    candidate wins.  Both association modes -- the group mode of launches of <= 16 pairs and the
+    lane mode of big launches -- fall back to the last frame's first staged point (the
+    group mode used index -1, reading the neighbouring frame's records), and the call returns."""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index)
+    clouds = [frame(0, 2, n_az=600)[0], frame(0, 3, n_az=600)[0]]
+    pb = _planes(fe, dev, clouds)
+    table = fe.plane_table(pb)
+    m_last = int(pb.count[0])
+    o1, m1 = int(pb.h_off[1]), int(pb.count[1])
+    got = []
+    for n_pairs in (1, 20):
+        last, curr = _sub(pb, [0] * n_pairs), _sub(pb, [1] * n_pairs)
+        pose = torch.full((n_pairs, 7), float("nan"), dtype=torch.float64, device=dev)
+        res = fe.register(last, table, curr, pose, want_nn=True)
+        torch.cuda.synchronize()
+        got.append(res["nn"][o1:o1 + m1].cpu().numpy())
+    for nn in got:
+        assert m1 > 0 and np.all(nn == nn[0]) and 0 <= nn[0] < m_last, (np.unique(nn), m_last)
+    assert np.array_equal(got[0], got[1])
+
+
 @pytest.mark.parametrize("solver,iters,mode,brute", [("ceres_lm", 8, 0, False), ("gn", 10, 1, False),
                                                      ("ceres_lm", 8, 0, True)])
 def test_register_pair_per_step(oracle, dev, solver, iters, mode, brute):

@@ -178,6 +178,13 @@ def parse(argv=None):
     ap.add_argument("--stagger", type=int, default=200,
                     help="sequence b of a batch starts at frame (7 b) mod STAGGER (0: every sequence "
                          "at frame 0), so the timed steps sample the whole sequence length")
+    ap.add_argument("--mask-order", default="none", choices=["none", "prev"],
+                    help="dispatch order of a mask launch's frames (ssf_set_mask_schedule): 'prev' = "
+                         "longest-first by the passes of the previous launch on the same mask stream "
+                         "(the same sequences' frames one stream cycle earlier); outputs are unchanged")
+    ap.add_argument("--mask-queue", type=int, default=0,
+                    help="mask launches as frame queues of at most this many work-groups (0: one "
+                         "work-group per frame)")
     ap.add_argument("--mask-streams", type=int, default=3,
                     help="mask launches of consecutive steps alternate over this many streams: the "
                          "GMM of a frame depends on no other frame, so a step's slow frames overlap "
@@ -391,6 +398,11 @@ class Pipeline:
         self.snapbuf = (torch.empty((args.steps, B, 7), dtype=torch.float64, device=dev)
                         if world > 1 else None)
         self.ev = {k: [] for k in ("mask", "feat", "table", "reg")}
+        # --mask-order prev: per mask stream, the previous launch's pose out and the order buffers
+        # (int32 permutation the kernel reads; sort scratch), all on that stream
+        self.mask_prev = [None] * len(self.s_masks)
+        self.mask_ord = [(torch.empty(B, dtype=torch.float64, device=dev), torch.empty(B, dtype=torch.int64, device=dev),
+                          torch.empty(B, dtype=torch.int32, device=dev)) for _ in self.s_masks]
 
     RING = 4
 
@@ -439,11 +451,24 @@ class Pipeline:
         with torch.cuda.stream(s_mask):
             m0, m1 = mk(), mk()
             m0.record(s_mask)
+            si = k % len(self.s_masks)
+            if streams is None and (a.mask_order == "prev" or a.mask_queue > 0):
+                order = None
+                prev = self.mask_prev[si]
+                if a.mask_order == "prev" and prev is not None:
+                    vals, idx, order = self.mask_ord[si]
+                    torch.sort(prev[:, 25], descending=True, stable=True, out=(vals, idx))
+                    order.copy_(idx)
+                self.fe_mask.mask_schedule(order, a.mask_queue)
             out, bg = self.fe_mask.mask_pose(mpos, mflow, off, h_off, mode="gmm", want_mask=True,
                                              out=None if ring is None else (
                                                  torch.empty((self.B, 32), dtype=torch.float64, device=self.dev),
                                                  ring["bg"]))
             m1.record(s_mask)
+            if streams is None:
+                self.mask_prev[si] = out
+                if a.mask_order == "prev" or a.mask_queue > 0:
+                    self.fe_mask.mask_schedule()
         keep = None
         if a.mask_before_features:          # configs[2]: the features wait for the mask
             if s_feat is not s_mask:
@@ -1277,6 +1302,7 @@ def main():
                    "backend": backend or "none",
                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")) or None,
                    "frame_window": frame_window(args, B, n_frames),
+                   "mask_schedule": {"order": args.mask_order, "queue": args.mask_queue},
                    **({"rehearsal": "all ranks on one GPU, gloo"} if args.rehearse_one_gpu else {})},
         "roofline": None, "cpu_baseline": cpu,
         "kernels": kernels, "overlapped_event_ms": overlapped,

@@ -380,6 +380,17 @@ int32_t ssf_kabsch_f32_batch(ssf_ctx* ctx, void* stream, int32_t n_frames, const
  * than one, a frame's points are cut into contiguous parts whose per-pass sums are exchanged
  * in global memory; a partner that never arrives gives status SSF_POSE_SYNC_FAILED. */
 int32_t ssf_set_mask_split(ssf_ctx* ctx, int32_t parts_per_frame);
+/* Frame scheduling of the next ssf_mask_pose_batch / _f64 launches (no reference counterpart: a
+ * frame's result does not depend on when it runs, so every schedule gives the same outputs).
+ *   d_order  nullable device int32 [n_order], a permutation of 0 .. n_order - 1 (caller-owned; it
+ *            must stay valid until the launches that read it have run): the k-th frame dispatched
+ *            is d_order[k].  Longest-first by the previous step's SSF_POSE_OUT_PASSES of the same
+ *            sequences starts the slow frames first and shortens a launch's straggler tail.  A
+ *            launch of n_frames != n_order fails with SSF_E_ARG; an entry out of range is skipped.
+ *   queue    > 0 (frames on one work-group each): at most `queue` work-groups, each taking the
+ *            next frame when its own is done (a frame queue: a slow frame holds one CU while the
+ *            others drain the batch); 0 = one work-group per frame. */
+int32_t ssf_set_mask_schedule(ssf_ctx* ctx, const int32_t* d_order, int32_t n_order, int32_t queue);
 /* Seed the context's numpy-legacy RandomState (MT19937) -- the `np.random.seed(s)` the reference
  * never calls; every GMM frame then consumes 3 doubles in frame order, as the reference's global
  * RandomState does across frames. */

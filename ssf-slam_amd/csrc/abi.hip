@@ -73,6 +73,8 @@ struct ssf_ctx {
     ssf_edge_config ecfg{};
     DevBuf esel, ecorr;
     int mask_split = 0;                // ssf_set_mask_split: 0 = automatic
+    const int32_t* mask_order = nullptr;   // ssf_set_mask_schedule
+    int mask_order_n = 0, mask_queue = 0;
     int mask_slots = -1;               // resident k_mask_pose work-groups (queried once)
     DrawSlot dslot[kDrawSlots];
     int dnext = 0;
@@ -282,6 +284,15 @@ int32_t ssf_profile_read(ssf_ctx* c, ssf_kernel_time* out, int32_t cap, int32_t*
 }
 
 const char* ssf_last_error(const ssf_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int32_t ssf_set_mask_schedule(ssf_ctx* c, const int32_t* d_order, int32_t n_order, int32_t queue) {
+    if (!c) return SSF_E_ARG;
+    if (queue < 0 || (d_order && n_order <= 0)) return fail(c, SSF_E_ARG, "set_mask_schedule: bad arguments");
+    c->mask_order = d_order;
+    c->mask_order_n = d_order ? n_order : 0;
+    c->mask_queue = queue;
+    return SSF_OK;
+}
 
 int32_t ssf_set_mask_split(ssf_ctx* c, int32_t parts_per_frame) {
     if (!c || parts_per_frame < 0 || parts_per_frame > ssf::kMaskMaxSplit) return SSF_E_ARG;
@@ -729,6 +740,8 @@ static int32_t mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const
         (mode != SSF_MASK_GMM && !d_mask_in))
         return fail(c, SSF_E_ARG, "mask_pose_batch: bad arguments");
     if (n_frames == 0) return SSF_OK;
+    if (c->mask_order && c->mask_order_n != n_frames)
+        return fail(c, SSF_E_ARG, "mask_pose_batch: the frame order (ssf_set_mask_schedule) has another length");
     const int64_t total = h_frame_off[n_frames];
     for (int f = 0; f < n_frames; ++f)
         if (h_frame_off[f + 1] < h_frame_off[f]) return fail(c, SSF_E_ARG, "mask_pose_batch: offsets not monotone");
@@ -753,7 +766,8 @@ static int32_t mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const
     if (G <= 0) G = c->mask_slots > 0 ? c->mask_slots / n_frames : 1;
     G = std::max(1, std::min(G, ssf::kMaskMaxSplit));
     if (mode != SSF_MASK_GMM) G = 1;
-    const size_t sync_need = G > 1 ? ssf::mask_sync_bytes(n_frames) + 16 : 0;
+    const bool queued = G == 1 && c->mask_queue > 0 && c->mask_queue < n_frames;
+    const size_t sync_need = (G > 1 || queued) ? ssf::mask_sync_bytes(n_frames) + 16 : 0;
     const size_t parts_need = G > 1 ? ssf::mask_parts_bytes(n_frames, G) : 0;
     if (ds.d.bytes < sizeof(double) * need || ds.rec.bytes < rec_need || ds.sync.bytes < sync_need ||
         ds.parts.bytes < parts_need) {                                    // growing frees the old buffer
@@ -788,7 +802,8 @@ static int32_t mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const
     ProfScope prof(c, stream);
     hipError_t e = ssf::launch_mask_pose(s, n_frames, d_pts, d_flow, d_frame_off, mode, d_mask_in,
                                          ds.d.as<double>(), ds.rec.as<uint2>(), reflection, d_bg_mask, d_out,
-                                         G, c->mask_slots, ds.sync.as<uint32_t>(), ds.parts.as<double>());
+                                         G, c->mask_slots, ds.sync.as<uint32_t>(), ds.parts.as<double>(),
+                                         c->mask_order, queued ? c->mask_queue : 0);
     if (e == hipSuccess) e = hipEventRecord(ds.used, s);
     if (e != hipSuccess) return hip_fail(c, e, "mask_pose launch");
     return SSF_OK;

@@ -674,7 +674,8 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     const int64_t* __restrict__ frame_off, int mode, const uint8_t* __restrict__ mask_in,
     const double* __restrict__ draws, uint2* __restrict__ lloyd_rec, int reflection,
     uint8_t* __restrict__ bg_mask, double* __restrict__ out_all, int n_frames, int G,
-    uint32_t* __restrict__ sync, double* __restrict__ parts) {
+    uint32_t* __restrict__ sync, double* __restrict__ parts, const int32_t* __restrict__ order,
+    int tickets) {
     __shared__ MaskShared S;
     __shared__ double red[kNW * 32];
     __shared__ int ired[kNW];
@@ -684,10 +685,13 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     __shared__ double xtmp[kSlot + kMaxSplit * kSlot];   // exchange totals + the gathered parts
     __shared__ int tk, okflag;
     const int tid = threadIdx.x;
-    // G == 1: work-group = frame.  G > 1: (frame, part) tickets in order (see Split).
+    // G == 1 without tickets: work-group = frame.  Otherwise (frame, part) tickets in order (see
+    // Split; with G == 1 a frame queue: a work-group takes the next frame when its frame is
+    // done, so a slow frame holds one CU while the others drain the batch).  order (optional): the
+    // k-th frame dispatched is order[k] (a permutation; results do not depend on it).
     for (int iter = 0;; ++iter) {
     int f, g = 0;
-    if (G == 1) {
+    if (G == 1 && !tickets) {
         if (iter > 0) break;
         f = blockIdx.x;
     } else {
@@ -697,6 +701,10 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         f = tk / G;
         g = tk - f * G;
         if (f >= n_frames) break;              // uniform: every wave leaves
+    }
+    if (order) {
+        f = order[f];
+        if ((unsigned)f >= (unsigned)n_frames) continue;   // uniform: not a frame (skipped)
     }
     [&]() {                                    // one frame part; `return` ends it
     const int64_t fb = frame_off[f], n = frame_off[f + 1] - fb;
@@ -1524,23 +1532,26 @@ static hipError_t launch_mask_pose_t(hipStream_t s, int n_frames, const T* pts, 
                                      const int64_t* frame_off, int mode, const uint8_t* mask_in,
                                      const double* draws, uint2* lloyd_rec, int reflection,
                                      uint8_t* bg_mask, double* out, int G, int slots,
-                                     uint32_t* sync, double* parts) {
+                                     uint32_t* sync, double* parts, const int32_t* order, int queue) {
     if (n_frames <= 0) return hipSuccess;
     if (mode != SSF_MASK_GMM || G < 1 || !sync || !parts) G = 1;
     if (G > kMaxSplit) G = kMaxSplit;
     int grid = n_frames;
-    if (G > 1) {
+    // the frame queue (G == 1): at most `queue` work-groups, each taking frame tickets in order
+    const bool tickets = G > 1 || (queue > 0 && sync && queue < n_frames);
+    if (tickets) {
         // zero the ticket and arrival counters (16-byte multiple, from the allocation start)
         const size_t zb = (mask_sync_bytes(n_frames) + 15) & ~(size_t)15;
         hipError_t e = hipMemsetAsync(sync, 0, zb, s);
         if (e != hipSuccess) return e;
         const int64_t want = (int64_t)n_frames * G;
-        grid = (int)(slots > 0 && want > slots ? slots : want);
+        const int cap = G > 1 ? slots : queue;
+        grid = (int)(cap > 0 && want > cap ? cap : want);
     }
     kmark(s, sizeof(T) == 8 ? "k_mask_pose_f64" : "k_mask_pose");
     hipLaunchKernelGGL(k_mask_pose<T>, dim3(grid), dim3(kMaskThreads), 0, s, pts, flow, frame_off,
                        mode, mask_in, draws, lloyd_rec, reflection, bg_mask, out, n_frames, G, sync,
-                       parts);
+                       parts, order, tickets ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -1563,18 +1574,20 @@ size_t mask_parts_bytes(int n_frames, int G) {
 hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,
                             const int64_t* frame_off, int mode, const uint8_t* mask_in,
                             const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
-                            double* out, int G, int slots, uint32_t* sync, double* parts) {
+                            double* out, int G, int slots, uint32_t* sync, double* parts,
+                            const int32_t* order, int queue) {
     return launch_mask_pose_t(s, n_frames, pts, flow, frame_off, mode, mask_in, draws, lloyd_rec,
-                              reflection, bg_mask, out, G, slots, sync, parts);
+                              reflection, bg_mask, out, G, slots, sync, parts, order, queue);
 }
 
 #else
 hipError_t launch_mask_pose(hipStream_t s, int n_frames, const double* pts, const double* flow,
                             const int64_t* frame_off, int mode, const uint8_t* mask_in,
                             const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
-                            double* out, int G, int slots, uint32_t* sync, double* parts) {
+                            double* out, int G, int slots, uint32_t* sync, double* parts,
+                            const int32_t* order, int queue) {
     return launch_mask_pose_t(s, n_frames, pts, flow, frame_off, mode, mask_in, draws, lloyd_rec,
-                              reflection, bg_mask, out, G, slots, sync, parts);
+                              reflection, bg_mask, out, G, slots, sync, parts, order, queue);
 }
 
 #endif

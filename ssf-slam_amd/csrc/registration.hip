@@ -2372,6 +2372,9 @@ __global__ __launch_bounds__(kEdgeAssocThreads) void k_edge_associate(
 #define SSF_SOLVE_THREADS 256
 #endif
 constexpr int kSolveThreads = SSF_SOLVE_THREADS;
+#ifndef SSF_SOLVE_SPECIALISE
+#define SSF_SOLVE_SPECIALISE 1                   // one k_solve instantiation per solver mode (A/B: 0)
+#endif
 constexpr int kNE = 28;  // 21 (packed upper JtWJ) + 6 (JtWr) + cost
 
 SSF_DEV int pk(int u, int v) {
@@ -2807,7 +2810,10 @@ SSF_DEV void write_log(double* log, int max_iter, int p, int idx, const double q
 #endif
 // kEdges: point-to-line blocks (ecorr at ecurr_off / ecurr_count) join every evaluation; they
 // are compacted into the same LDS arrays after the planes.
-template <bool kEdges, int NT>
+// kMode: the solver this instantiation runs (SSF_SOLVER_GN / SSF_SOLVER_CERES_LM), so each mode's
+// register allocation covers its own loop only (the LM state does not weigh on the GN kernel);
+// -1 dispatches on the runtime `mode` (A/B: SSF_SOLVE_SPECIALISE=0).
+template <bool kEdges, int NT, int kMode>
 __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
                                                          const int64_t* __restrict__ curr_off,
                                                          const int32_t* __restrict__ curr_count,
@@ -2958,7 +2964,7 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
         }
         __syncthreads();
 #endif
-        if (mode == SSF_SOLVER_GN) {
+        if ((kMode >= 0 ? kMode : mode) == SSF_SOLVER_GN) {
             // every thread holds the same sums after the block reduction, so every thread runs
             // the same 6x6 solve on the same bits and carries the same pose: no lane-0 step, no
             // LDS broadcast, no extra barrier per iteration (thread 0 alone writes the log)
@@ -3346,10 +3352,18 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
                            edge->corr, cap);
     }
     kmark(s, "k_solve");
+#if SSF_SOLVE_SPECIALISE
 #define SSF_SOLVE_LAUNCH(E, NT, ...)                                                               \
-    hipLaunchKernelGGL((k_solve<E, NT>), dim3(n_pairs), dim3(NT), 0, s, corr, curr_off, curr_count, \
+    hipLaunchKernelGGL((cfg.solver == SSF_SOLVER_GN ? k_solve<E, NT, SSF_SOLVER_GN> : k_solve<E, NT, SSF_SOLVER_CERES_LM>), \
+                       dim3(n_pairs), dim3(NT), 0, s, corr, curr_off, curr_count, \
                        last_count, cfg.solver, cfg.max_iter, pin, ain, pose_rel, pose_abs, log, nlog, ncorr, \
                        __VA_ARGS__)
+#else
+#define SSF_SOLVE_LAUNCH(E, NT, ...)                                                               \
+    hipLaunchKernelGGL((k_solve<E, NT, -1>), dim3(n_pairs), dim3(NT), 0, s, corr, curr_off, curr_count, \
+                       last_count, cfg.solver, cfg.max_iter, pin, ain, pose_rel, pose_abs, log, nlog, ncorr, \
+                       __VA_ARGS__)
+#endif
     if (edge)
         SSF_SOLVE_LAUNCH(true, kSolveThreads, edge->corr, edge->curr_off, edge->curr_count, edge->ncorr);
     else

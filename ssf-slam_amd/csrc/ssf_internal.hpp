@@ -141,15 +141,19 @@ hipError_t launch_accumulate(hipStream_t s, int n, const double* rel, const doub
 // ---- launchers (mask_pose.hip) ----
 // G > 1 cuts every frame into G parts on G work-groups (sync: ticket + per-frame arrival
 // counters, mask_sync_bytes; parts: exchange slots, mask_parts_bytes); slots = resident
-// work-groups of k_mask_pose on the device (mask_pose_slots).
+// work-groups of k_mask_pose on the device (mask_pose_slots).  order (nullable): the dispatch
+// order of the frames (a device permutation); queue > 0 (G == 1): at most `queue` work-groups
+// taking frame tickets in order (the frame queue; sync holds the ticket).
 hipError_t launch_mask_pose(hipStream_t s, int n_frames, const float* pts, const float* flow,
                             const int64_t* frame_off, int mode, const uint8_t* mask_in,
                             const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
-                            double* out, int G, int slots, uint32_t* sync, double* parts);
+                            double* out, int G, int slots, uint32_t* sync, double* parts,
+                            const int32_t* order = nullptr, int queue = 0);
 hipError_t launch_mask_pose(hipStream_t s, int n_frames, const double* pts, const double* flow,
                             const int64_t* frame_off, int mode, const uint8_t* mask_in,
                             const double* draws, uint2* lloyd_rec, int reflection, uint8_t* bg_mask,
-                            double* out, int G, int slots, uint32_t* sync, double* parts);
+                            double* out, int G, int slots, uint32_t* sync, double* parts,
+                            const int32_t* order = nullptr, int queue = 0);
 int mask_pose_slots(int device);
 // ---- launcher (kabsch_f32.hip): the float32 slove_RT_by_SVD + Quaternion tail per frame; source
 // rows = dst + flow (f32) when flow is given, else src; keep_failures: leave frames whose status

@@ -39,6 +39,7 @@ EXPORTS = [
     "ssf_profile_read", "ssf_set_mask_split", "ssf_mask_pose_batch_f64",
     "ssf_edge_config_default", "ssf_set_edge_config", "ssf_extract_features_batch",
     "ssf_edge_table_batch", "ssf_register_batch_edges", "ssf_kabsch_f32_batch",
+    "ssf_set_mask_schedule",
 ]
 # Every symbol include/ssf_pointnet2.h declares (TFlow point-set operators).
 PN2_EXPORTS = [
@@ -136,6 +137,8 @@ def lib():
     L.ssf_register_pair.restype = i32
     L.ssf_set_mask_split.argtypes = [vp, i32]
     L.ssf_set_mask_split.restype = i32
+    L.ssf_set_mask_schedule.argtypes = [vp, vp, i32, i32]
+    L.ssf_set_mask_schedule.restype = i32
     L.ssf_profile_enable.argtypes = [vp, i32]
     L.ssf_profile_enable.restype = i32
     L.ssf_profile_read.argtypes = [vp, C.POINTER(KernelTime), i32, C.POINTER(i32)]

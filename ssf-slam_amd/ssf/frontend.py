@@ -133,6 +133,20 @@ class Frontend:
         """Work-groups per frame of the GMM fit (0 = automatic, 1..32 fixed)."""
         self._check(_abi.lib().ssf_set_mask_split(self._h, int(parts_per_frame)), "ssf_set_mask_split")
 
+    def mask_schedule(self, order=None, queue: int = 0):
+        """Frame scheduling of the next mask_pose launches (ssf_set_mask_schedule; outputs do not
+        depend on it): order = a device int32 permutation of the batch's frames (dispatch order,
+        e.g. longest-first by the previous step's passes; the tensor must outlive the launches
+        that read it -- keep a reference), queue = at most this many work-groups taking frame
+        tickets (0: one per frame).  mask_schedule() resets both."""
+        if order is not None:
+            order = self._dev(order, torch.int32)
+            if order.dim() != 1 or order.numel() == 0:
+                raise ValueError("order must be a non-empty 1-D int32 device tensor")
+        self._mask_order = order                   # the context keeps only the pointer
+        self._check(_abi.lib().ssf_set_mask_schedule(self._h, _ptr(order), 0 if order is None else order.numel(),
+                                                     int(queue)), "ssf_set_mask_schedule")
+
     def edge_config(self, **kw):
         """Edge-feature parameters (beyond the reference; ssf_set_edge_config): edge_min,
         edge_span, line_ratio, max_nn_d2.  No arguments: the current defaults."""

@@ -116,6 +116,47 @@ def test_frame_split_full_size_vs_oracle(oracle, dev, G):
         assert np.abs(o[0:3] - ref["t"]).max() < 1e-5
 
 
+@pytest.mark.parametrize("G", [1, 2])
+def test_mask_schedule_order_and_queue_same_outputs(dev, G):
+    """ssf_set_mask_schedule: a dispatch order (reversed, and longest-first by a first launch's
+    passes) and the frame queue (3 work-groups taking frame tickets for 7 frames) give the same
+    bits as the default one-work-group-per-frame launch -- every frame is fitted on its own;
+    with G = 2 the order maps (frame, part) tickets too.  A permutation of another length is
+    SSF_E_ARG, and an out-of-range entry skips that frame (its output row is left as it was)."""
+    import ssf
+    fr = [frame(s, k, n_az=500) for s, k in ((1, 0), (2, 3), (3, 1), (4, 5), (5, 2), (6, 4), (7, 7))]
+    F = len(fr)
+    draws = np.random.default_rng(3).random((F, 3))
+    fe = ssf.Frontend(64, device=dev.index)
+    fe.mask_split(G)
+    ref, bg_ref, _ = _run(fe, dev, [f[0] for f in fr], [f[1] for f in fr], draws=draws)
+    assert np.all(ref[:, 16] == 0)
+    longest = torch.from_numpy(np.argsort(-ref[:, 25], kind="stable").astype(np.int32)).to(dev)
+    rev = torch.arange(F - 1, -1, -1, dtype=torch.int32, device=dev)
+    for order, queue in ((rev, 0), (longest, 0), (None, 3), (longest, 3)):
+        if G > 1 and queue:
+            continue                         # the queue is the one-work-group-per-frame mode
+        fe.mask_schedule(order, queue)
+        out, bg, _ = _run(fe, dev, [f[0] for f in fr], [f[1] for f in fr], draws=draws)
+        assert np.array_equal(out.view(np.uint64), ref.view(np.uint64)), (order, queue)
+        assert np.array_equal(bg, bg_ref)
+    fe.mask_schedule(rev[:F - 1])
+    with pytest.raises(ssf.SSFError):
+        _run(fe, dev, [f[0] for f in fr], [f[1] for f in fr], draws=draws)
+    skip = torch.tensor([0, 1, 2, 3, 4, 5, 99], dtype=torch.int32, device=dev)   # frame 6 never runs
+    fe.mask_schedule(skip)
+    pts = torch.from_numpy(np.concatenate([f[0] for f in fr])).to(dev)
+    fl = torch.from_numpy(np.concatenate([f[1] for f in fr])).to(dev)
+    off, h_off = ssf.frame_offsets([f[0].shape[0] for f in fr], dev)
+    out_buf = torch.full((F, 32), -7.0, dtype=torch.float64, device=dev)
+    bg_buf = torch.empty(int(h_off[-1]), dtype=torch.uint8, device=dev)
+    out, _ = fe.mask_pose(pts, fl, off, h_off, draws=draws, out=(out_buf, bg_buf))
+    got = out.cpu().numpy()
+    assert np.array_equal(got[:F - 1].view(np.uint64), ref[:F - 1].view(np.uint64))
+    assert np.all(got[F - 1] == -7.0)
+    fe.mask_schedule()
+
+
 def test_frame_split_work_groups_take_several_tickets(oracle, dev):
     """Split G = 8 with n_frames * 8 > the resident work-groups (mask_pose_slots): the grid is
     capped at the slots, so work-groups take several (frame, part) tickets in order and reuse

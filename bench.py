@@ -46,10 +46,10 @@ F64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector, spec (AMD datasheet); f64 MFMA
 # HBM bytes per launch of every kernel / f64 FLOPs per k_mask_pose launch, measured with rocprofv3
 # PMC passes on a serial run of this bench (tools/pmc_traffic.py, tools/pmc_f64.py); used when
 # their workload config matches the run's.
-TRAFFIC_JSON = os.path.join(REPO, "profiles", "r05fin_traffic.json")
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "r06fin_traffic.json")
 # PMC traffic of the same build on the reference's own layout (--layout carla)
-TRAFFIC_JSONS = {"azimuth": TRAFFIC_JSON, "carla": os.path.join(REPO, "profiles", "r05fin_carla_traffic.json")}
-F64_JSON = os.path.join(REPO, "profiles", "r05fin_f64.json")
+TRAFFIC_JSONS = {"azimuth": TRAFFIC_JSON, "carla": os.path.join(REPO, "profiles", "r06fin_carla_traffic.json")}
+F64_JSON = os.path.join(REPO, "profiles", "r06fin_f64.json")
 METRIC = "LiDAR front-end frames/sec (mask+feature+GN), 64-beam 120k pts, 1/2/4/8 GPUs"
 
 
@@ -182,9 +182,11 @@ def parse(argv=None):
                     help="dispatch order of a mask launch's frames (ssf_set_mask_schedule): 'prev' = "
                          "longest-first by the passes of the previous launch on the same mask stream "
                          "(the same sequences' frames one stream cycle earlier); outputs are unchanged")
-    ap.add_argument("--mask-queue", type=int, default=0,
+    ap.add_argument("--mask-queue", type=int, default=-1,
                     help="mask launches as frame queues of at most this many work-groups (0: one "
-                         "work-group per frame)")
+                         "work-group per frame; -1: 3/4 of the device's CUs, 192 on MI355X -- "
+                         "r6h: 96 / 128 / 160 / 192 / 224 / one per frame gave 59.7 / 60.8 / 61.9 / "
+                         "62.3 / 60.4 / 55.6 k frames/s)")
     ap.add_argument("--mask-streams", type=int, default=3,
                     help="mask launches of consecutive steps alternate over this many streams: the "
                          "GMM of a frame depends on no other frame, so a step's slow frames overlap "
@@ -400,6 +402,8 @@ class Pipeline:
         self.ev = {k: [] for k in ("mask", "feat", "table", "reg")}
         # --mask-order prev: per mask stream, the previous launch's pose out and the order buffers
         # (int32 permutation the kernel reads; sort scratch), all on that stream
+        if args.mask_queue < 0:              # 3/4 of the CUs (one mask work-group fills a CU)
+            args.mask_queue = 3 * torch.cuda.get_device_properties(dev).multi_processor_count // 4
         self.mask_prev = [None] * len(self.s_masks)
         self.mask_ord = [(torch.empty(B, dtype=torch.float64, device=dev), torch.empty(B, dtype=torch.int64, device=dev),
                           torch.empty(B, dtype=torch.int32, device=dev)) for _ in self.s_masks]
@@ -452,10 +456,10 @@ class Pipeline:
             m0, m1 = mk(), mk()
             m0.record(s_mask)
             si = k % len(self.s_masks)
-            if streams is None and (a.mask_order == "prev" or a.mask_queue > 0):
+            if a.mask_order == "prev" or a.mask_queue > 0:
                 order = None
                 prev = self.mask_prev[si]
-                if a.mask_order == "prev" and prev is not None:
+                if a.mask_order == "prev" and prev is not None and streams is None:
                     vals, idx, order = self.mask_ord[si]
                     torch.sort(prev[:, 25], descending=True, stable=True, out=(vals, idx))
                     order.copy_(idx)
@@ -467,8 +471,8 @@ class Pipeline:
             m1.record(s_mask)
             if streams is None:
                 self.mask_prev[si] = out
-                if a.mask_order == "prev" or a.mask_queue > 0:
-                    self.fe_mask.mask_schedule()
+            if a.mask_order == "prev" or a.mask_queue > 0:
+                self.fe_mask.mask_schedule()
         keep = None
         if a.mask_before_features:          # configs[2]: the features wait for the mask
             if s_feat is not s_mask:

@@ -55,6 +55,7 @@ struct ssf_ctx {
     bool rtab_ready = false;
     // registration scratch
     DevBuf corr;
+    DevBuf cidx;                       // compacted-record scratch: per query (index, valid), per pair count
     // ssf_register_pair: offsets, counts, the last frame's plane table + search index, pose, log
     DevBuf pair;
     // mask: k-means++ draws staged per launch through a ring of slots, so launches on different
@@ -230,7 +231,7 @@ void ssf_destroy(ssf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     DevBuf* bufs[] = {&c->rid, &c->hist, &c->ring_off, &c->ring_xyzi, &c->sel, &c->sel_cnt, &c->fix,
-                      &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->pair, &c->start1, &c->vg,
+                      &c->plane1, &c->off1, &c->cnt1, &c->corr, &c->cidx, &c->pair, &c->start1, &c->vg,
                       &c->icp_cur, &c->icp_key, &c->icp_st, &c->icp_guess, &c->esel,
                       &c->ecorr, &c->fcnt, &c->fidx, &c->fbits, &c->fcurv, &c->rtab, &c->firr, &c->flmap};
     for (auto& ds : c->dslot) {
@@ -359,6 +360,8 @@ int32_t ssf_reserve(ssf_ctx* c, int32_t max_frames, int64_t max_points_per_frame
     int32_t rc = ensure_features(c, max_frames, total, max_points_per_frame);
     if (rc) return rc;
     SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(total, 1)), "alloc corr");
+    SSF_TRY_HIP(c, c->cidx.ensure(sizeof(int32_t) * ((size_t)std::max<int64_t>(total, 1) + (size_t)max_frames)),
+                "alloc corr index");
     for (auto& ds : c->dslot) {
         SSF_TRY_HIP(c, ds.d.ensure(sizeof(double) * 3 * (size_t)std::max(max_frames, 1)), "alloc draws");
         SSF_TRY_HIP(c, ds.rec.ensure(sizeof(uint2) * (size_t)(total + 2 * (int64_t)max_frames + 2) + sizeof(uint32_t) * (size_t)(total + 64 * (int64_t)max_frames)), "alloc lloyd records");
@@ -537,6 +540,8 @@ int32_t ssf_register_batch(ssf_ctx* c, void* stream, int32_t n_pairs, const floa
     if (n_pairs == 0) return SSF_OK;
     SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
     SSF_TRY_HIP(c, c->corr.ensure(sizeof(ssf::CorrRec) * (size_t)std::max<int64_t>(curr_total_points, 1)), "alloc corr");
+    const size_t nq = (size_t)std::max<int64_t>(curr_total_points, 1);
+    SSF_TRY_HIP(c, c->cidx.ensure(sizeof(int32_t) * (nq + (size_t)n_pairs)), "alloc corr index");
     ProfScope prof(c, stream);
     hipError_t e = ssf::launch_register(
         (hipStream_t)stream, c->cfg, n_pairs, reinterpret_cast<const float4*>(d_last_xyzi), d_last_off,
@@ -544,7 +549,7 @@ int32_t ssf_register_batch(ssf_ctx* c, void* stream, int32_t n_pairs, const floa
         d_last_sorted_idx, reinterpret_cast<const float4*>(d_curr_xyzi), d_curr_off,
         d_curr_count, max_plane_points, c->corr.as<ssf::CorrRec>(), d_pose_rel, d_pose_abs, d_log,
         d_nlog, d_ncorr, d_nn, nullptr, reinterpret_cast<const float4*>(d_last_strip_xyzi),
-        d_last_strip_head);
+        d_last_strip_head, nullptr, nullptr, c->cidx.as<int32_t>(), c->cidx.as<int32_t>() + nq);
     if (e != hipSuccess) return hip_fail(c, e, "register launch");
     return SSF_OK;
 }

@@ -194,6 +194,18 @@ SSF_DEV void key_insert(double (&kk)[K], double key) {
         key = hi;
     }
 }
+// key_insert that returns the key leaving the list (the new key itself when it does not enter)
+template <int K>
+SSF_DEV double key_insert_out(double (&kk)[K], double key) {
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        double hi;
+        asm("v_max_f64 %0, %1, %2" : "=v"(hi) : "v"(kk[s]), "v"(key));
+        asm("v_min_f64 %0, %0, %1" : "+v"(kk[s]) : "v"(key));
+        key = hi;
+    }
+    return key;
+}
 
 // Ring-diverse 5-point pick (:180-205), gate d2[n] < 1 (:207), 5x3 least-squares plane
 // (:208-220) and coplanarity gate (:222-232) from the sorted 30-NN key list kk of a point.
@@ -841,6 +853,16 @@ SSF_DEV uint32_t row_code(float fi) {
 }
 SSF_DEV int pt_row(const float4& p) { return (__float_as_int(p.w) >> 16) & 0xFF; }
 SSF_DEV int pt_id(const float4& p) { return __float_as_int(p.w) & 0xFFFF; }
+// The pick walks' keys carry the point's ring code too (round 6): low word = index << 8 | ring
+// code.  Indices are unique, so the key order is still exactly (distance, index); a key that
+// leaves the top-five list tells its ring by itself (pick_1m keeps two other-ring keys instead of
+// six).  The sentinel knn_key(d, 0x7fffffff) decodes as ring 255 (never another ring in 0..63).
+SSF_DEV double pick_key(float d, const float4& p) {
+    const int w = __float_as_int(p.w);
+    return __hiloint2double(__float_as_int(d), ((w & 0xFFFF) << 8) | ((w >> 16) & 0xFF));
+}
+SSF_DEV int pick_index(double k) { return (int)((uint32_t)__double2loint(k) >> 8); }
+SSF_DEV int pick_row(double k) { return __double2loint(k) & 0xFF; }
 
 // Visit the points of one strip with dx^2 + dy_lb^2 <= bound() (bound re-read at every step)
 // and < lim, from q's x position (start: the query's own strip position, or -1 = binary search).
@@ -976,9 +998,11 @@ SSF_DEV void pick_1m(const float4* __restrict__ P, const StripView<false>& v, co
     const double sent = knn_key(1.0f, 0x7fffffff);
 #pragma unroll
     for (int k = 0; k < 5; ++k) s.t5[k] = sent;
-    double o6[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) o6[k] = sent;
+    // o2: the two smallest other-ring keys that LEFT the top five.  Every key within 1 m either
+    // ends in the final top five or leaves it exactly once (the list only improves), so the keys
+    // that left are exactly those above the final rank-4 key: o2 = D1, D2 (when rank 0's ring is
+    // the query's own; otherwise the second walk below)
+    double o2[2] = {sent, sent};
     const int qrow = pt_row(q);
     int K1 = 0;
     s.pos[0] = j;
@@ -987,30 +1011,20 @@ SSF_DEV void pick_1m(const float4* __restrict__ P, const StripView<false>& v, co
     visit_1m(v, T, g, s.pos, q, [] { return 1.0f; }, [&](const float4& p) {
         const float d = l2_simple(q, p);
         if (d < 1.0f) {
-            const double key = knn_key(d, pt_id(p));
             ++K1;
-            key_insert<5>(s.t5, key);
-            const int row = pt_row(p);
-            if (row != qrow && row <= 63) key_insert<6>(o6, key);
+            const double out = key_insert_out<5>(s.t5, pick_key(d, p));
+            const int row = pick_row(out);
+            if (row != qrow && row <= 63) key_insert<2>(o2, out);
         }
     });
     s.K1 = K1;
     s.d1 = sent; s.d2 = sent;
     s.prow = -1;
     if (K1 <= 5) return;
-    s.prow = row_of(P[key_index(s.t5[0])].w);
+    s.prow = pick_row(s.t5[0]);                                        // row_of(P[rank 0].w)
     const double k5 = s.t5[4];
-    if (key_index(s.t5[0]) == pt_id(q) || s.prow == qrow) {
-        // D1, D2: the first two of o6 above rank 4
-        int c = 0;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) c += o6[k] <= k5;
-        double a = sent, b = sent;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            if (k == c) { a = o6[k]; b = o6[k + 1]; }
-        }
-        s.d1 = a; s.d2 = b;
+    if (pick_index(s.t5[0]) == pt_id(q) || s.prow == qrow) {
+        s.d1 = o2[0]; s.d2 = o2[1];
         return;
     }
     const int prow = s.prow;
@@ -1018,7 +1032,7 @@ SSF_DEV void pick_1m(const float4* __restrict__ P, const StripView<false>& v, co
     visit_1m(v, T, g, s.pos, q, [&] { return key_dist(dd[1]); }, [&](const float4& p) {
         const float d = l2_simple(q, p);
         const int row = pt_row(p);
-        const double key = knn_key(d, pt_id(p));
+        const double key = pick_key(d, p);
         if (d < 1.0f && key > k5 && row != prow && row <= 63) key_insert<2>(dd, key);
     });
     s.d1 = dd[0]; s.d2 = dd[1];
@@ -1028,9 +1042,9 @@ SSF_DEV void pick_finish(const float4* __restrict__ P, const PickState& s, int n
                          float* __restrict__ normal, uint8_t* __restrict__ valid) {
     int v5[5];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) v5[k] = key_index(s.t5[k]);
-    if (nvr == 1) v5[4] = key_index(s.d1);                             // :199-205
-    if (nvr == 2) { v5[3] = key_index(s.d1); v5[4] = key_index(s.d2); }
+    for (int k = 0; k < 5; ++k) v5[k] = pick_index(s.t5[k]);
+    if (nvr == 1) v5[4] = pick_index(s.d1);                            // :199-205
+    if (nvr == 2) { v5[3] = pick_index(s.d1); v5[4] = pick_index(s.d2); }
     float nrm[3];
     uint8_t ok;
     plane_from_pick(P, v5, plane_max, nrm, ok);
@@ -1052,7 +1066,7 @@ SSF_DEV bool pick_beyond_invalid(const StripView<false>& v, const StripLds& T, c
     visit_all(v, T, g, j, q, [&] { return key_dist(E); }, [&](const float4& p) {
         const float d = l2_simple(q, p);
         const int row = pt_row(p);
-        const double key = knn_key(d, pt_id(p));
+        const double key = pick_key(d, p);
         if (d >= 1.0f && row != prow && row <= 63 && key < E) E = key;
     });
     if (!(key_dist(E) < __builtin_inff())) return false;          // no other-ring point at all
@@ -1061,7 +1075,7 @@ SSF_DEV bool pick_beyond_invalid(const StripView<false>& v, const StripLds& T, c
     const float lim = key_dist(E);
     visit_all(v, T, g, j, q, [&] { return C >= need ? -1.0f : lim; }, [&](const float4& p) {
         const float d = l2_simple(q, p);
-        C += (d >= 1.0f && knn_key(d, pt_id(p)) < E);
+        C += (d >= 1.0f && pick_key(d, p) < E);
     });
     return C < need;
 }
@@ -1093,7 +1107,7 @@ SSF_DEV void table_pick_walks(const float4* __restrict__ P, const StripView<fals
                 const double b1 = s.d1, b2 = s.d2;
                 const float lim = f2 ? key_dist(b2) : key_dist(b1);
                 visit_1m(v, T, g, s.pos, q, [&] { return lim; }, [&](const float4& p) {
-                    const double key = knn_key(l2_simple(q, p), pt_id(p));
+                    const double key = pick_key(l2_simple(q, p), p);
                     r1 += key < b1;
                     r2 += key < b2;
                 });
@@ -1146,7 +1160,7 @@ SSF_DEV void table_pick_walks(const float4* __restrict__ P, const StripView<fals
                                 [&](const float4& p) {
                                     const float d = l2_simple(q, p);
                                     const int row = pt_row(p);
-                                    const double key = knn_key(d, pt_id(p));
+                                    const double key = pick_key(d, p);
                                     if (d >= 1.0f && row != prow && row <= 63 && key < E) E = key;
                                 });
                 }
@@ -1172,7 +1186,7 @@ SSF_DEV void table_pick_walks(const float4* __restrict__ P, const StripView<fals
                         strip_visit(v, T, sidx, st, q, __builtin_inff(), [&] { return lim; },
                                     [&](const float4& p) {
                                         const float d = l2_simple(q, p);
-                                        c += (d >= 1.0f && knn_key(d, pt_id(p)) < E);
+                                        c += (d >= 1.0f && pick_key(d, p) < E);
                                     });
                     }
 #pragma unroll
@@ -1861,6 +1875,9 @@ __global__ __launch_bounds__(kAssocThreads) void k_associate_lds(
 // kSoa: the strip-major points as x | y | z float arrays and a u16 original index (configs[4]
 // frames); otherwise float4 with the index in .w.  A last frame above the launch's staging
 // capacity walks the x-sorted copy in global memory, unbounded (exact, slow, not expected).
+#ifndef SSF_ASSOC_COMPACT
+#define SSF_ASSOC_COMPACT 1                      // lane-mode association writes compacted records (A/B: 0)
+#endif
 #ifndef SSF_ASSOC_DEFER
 #define SSF_ASSOC_DEFER 0                        // 1: far queries of the lane mode to a wave each (r5u: 256-pair launch 0.135 -> 0.200 ms)
 #endif
@@ -1900,9 +1917,17 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     const int32_t* __restrict__ last_sidx, const float4* __restrict__ curr,
     const int64_t* __restrict__ curr_off, const int32_t* __restrict__ curr_count,
     const double* __restrict__ pose_rel, CorrRec* __restrict__ corr, int32_t* __restrict__ nn_out,
-    int lds_cap, const float4* __restrict__ strip_xyzi, const int32_t* __restrict__ strip_head) {
+    int lds_cap, const float4* __restrict__ strip_xyzi, const int32_t* __restrict__ strip_head,
+    int32_t* __restrict__ nnv, int32_t* __restrict__ ncompact) {
     extern __shared__ float4 SL[];                  // [ml] strip-major, x-sorted in each strip
     __shared__ StripLds T;
+    // Compacted records (round 6): with one work-group per pair in the lane mode, the valid
+    // correspondences are written in query order at their ranks, [0, ncompact[p]) of the pair's
+    // records (a pair whose records are not compacted gets -1): k_solve then streams them into its
+    // LDS with no ballot pass and evaluates them on the way in.  Each query's (1-NN index, valid)
+    // goes to nnv first; the ranks need every query's validity.
+    const bool compact = kCoopG == 0 && !SSF_ASSOC_DEFER && ncompact && gridDim.y == 1;   // uniform
+    __shared__ int cwave[kStripWaves];
 #if SSF_ASSOC_DEFER == 2
     // far queries kept by their own wave (no barrier): each wave answers its list in groups of
     // kAssocDeferG lanes after its lane walks (not in the SoA launch: no LDS left there)
@@ -1922,7 +1947,10 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     const int p = blockIdx.x, tid = threadIdx.x;
     const int q0 = tid + (int)blockIdx.y * kStripThreads, qstep = kStripThreads * (int)gridDim.y;
     const int mc = curr_count[p], ml = last_count[p];
-    if (mc <= 0 || ml <= 10) return;                                    // uniform (:158)
+    if (mc <= 0 || ml <= 10) {                                          // uniform (:158)
+        if (compact && tid == 0) ncompact[p] = 0;
+        return;
+    }
     constexpr int kQpw = kCoopG > 0 ? kStripThreads / kCoopG : kStripThreads;   // queries per work-group
     if (kCoopG > 0 && (int)blockIdx.y * kQpw >= mc) return;             // uniform: no query here
     const int64_t lo = last_off[p], co = curr_off[p];
@@ -1938,6 +1966,7 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
     unsigned long long rt1 = rt0, mt1 = mt0;
 #endif
     if (ml > lds_cap) {                                                 // uniform
+        if (compact && tid == 0) ncompact[p] = -1;                      // records in query order
         const PtsF4 g{SP, SI};
         for (int i = q0; i < mc; i += qstep) {
             const float4 pc = curr[co + i];
@@ -1964,7 +1993,7 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
 #ifdef SSF_STRIPS_STAMPS
     rt1 = __builtin_amdgcn_s_memrealtime(); mt1 = __builtin_amdgcn_s_memtime();
 #elif !SSF_ASSOC_DEFER
-    if (kCoopG == 0 && q0 >= mc) return;                                // (after the barriers of the build)
+    if (kCoopG == 0 && q0 >= mc && !compact) return;                    // (after the barriers of the build)
 #endif
 #ifdef SSF_ASSOC_COUNT
     int vis = 0;
@@ -2110,10 +2139,46 @@ __global__ __launch_bounds__(kStripThreads) void k_associate_strips(
             }
 #endif
         }
-        if (!deferred) assoc_finish(L, lo, last_normal, last_valid, pc, v.id(max(bc, 0)), corr, nn_out, co + i);
+        if (compact) {
+            // the 1-NN's LDS position (its point and index are read back from the strips)
+            const int bp = max(bc, 0), bi = v.id(bp);
+            nnv[co + i] = last_valid[lo + bi] != 0 ? bp : -1 - bp;      // read back by this thread
+            if (nn_out) nn_out[co + i] = bi;
+        } else if (!deferred) {
+            assoc_finish(L, lo, last_normal, last_valid, pc, v.id(max(bc, 0)), corr, nn_out, co + i);
+        }
 #ifdef SSF_ASSOC_COUNT
         if (nn_out && !deferred) nn_out[co + i] = vis;
 #endif
+    }
+    if (compact) {
+        // query trip k (queries k T + tid, T = kStripThreads: the lane loop's own, so every thread
+        // reads back its own nnv entries): ballot + wave counts give the ranks in query order
+        const int lane = tid & 63, w = tid >> 6;
+        int base = 0;                                                   // uniform
+        for (int i0 = 0; i0 < mc; i0 += kStripThreads) {
+            const int i = i0 + tid;
+            const int e = i < mc ? nnv[co + i] : -1;
+            const bool val = e >= 0;
+            const uint64_t m = __ballot(val);
+            if (lane == 0) cwave[w] = __popcll(m);
+            __syncthreads();
+            int before = base, tot = 0;
+#pragma unroll
+            for (int j = 0; j < kStripWaves; ++j) { const int x = cwave[j]; if (j < w) before += x; tot += x; }
+            if (val) {
+                CorrRec rec;
+                const float4 pc = curr[co + i], pa = v.pt(e);                 // pa: L[bi]'s floats
+                const float* nr = last_normal + 3 * (lo + v.id(e));
+                rec.po[0] = pc.x; rec.po[1] = pc.y; rec.po[2] = pc.z; rec.valid = 1.0f;
+                rec.pa[0] = pa.x; rec.pa[1] = pa.y; rec.pa[2] = pa.z; rec.pad0 = 0.f;
+                rec.n[0] = nr[0]; rec.n[1] = nr[1]; rec.n[2] = nr[2]; rec.pad1 = 0.f;
+                corr[co + before + __popcll(m & lanemask_lt())] = rec;
+            }
+            base += tot;
+            __syncthreads();                                            // cwave is rewritten next trip
+        }
+        if (tid == 0) ncompact[p] = base;
     }
 #if SSF_ASSOC_DEFER
     // Deferred queries, one per wave: each level R searches every strip that can hold a point
@@ -2635,6 +2700,15 @@ SSF_DEV void evaluate(const CorrRec* __restrict__ rec, int n, const double q[4],
 #define SSF_SOLVE_STEP 2
 #endif
 constexpr int kSolveStep = SSF_SOLVE_STEP;
+#ifndef SSF_SOLVE_QDIRECT
+#define SSF_SOLVE_QDIRECT 0                      // A/B: every thread reads the warm start from global memory
+#endif
+#ifndef SSF_SOLVE_DIRECT
+#define SSF_SOLVE_DIRECT 1                       // compacted records: 1 loaded by the first evaluation, 2 copied first (A/B)
+#endif
+#ifndef SSF_SOLVE_LDS_PF
+#define SSF_SOLVE_LDS_PF 0                       // 1: LDS records of the next step in flight (r6m: 0.0706 vs 0.0674 ms, slower)
+#endif
 #ifndef SSF_SOLVE_RED
 #define SSF_SOLVE_RED 2                          // 0 block_sum_rs; block_sum_db: 1 DPP one barrier, 2 DPP two, 3 shuffles two
 #endif
@@ -2649,14 +2723,38 @@ SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double 
     hf2 H[kHF];
 #pragma unroll
     for (int k = 0; k < kHF; ++k) H[k] = hf2{0.0f, 0.0f};
+#if SSF_SOLVE_LDS_PF
+    // the next step's LDS records are read while this step's are evaluated (one wave per SIMD:
+    // nothing else hides the LDS latency); clamped reads, a step past nv is never used
+    float g[kSolveStep][9];
+    if (threadIdx.x < nv) {
+#pragma unroll
+        for (int h = 0; h < kSolveStep; ++h) {
+            const int ih = min((int)threadIdx.x + h * T, nv - 1);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) { g[h][d] = C.po[d][ih]; g[h][3 + d] = C.pa[d][ih]; g[h][6 + d] = C.n[d][ih]; }
+        }
+    }
+#endif
     for (int i = threadIdx.x; i < nv; i += kSolveStep * T) {
         float f[kSolveStep][9];
+#if SSF_SOLVE_LDS_PF
+#pragma unroll
+        for (int h = 0; h < kSolveStep; ++h) {
+            const int ih = min(i + kSolveStep * T + h * T, nv - 1);
+#pragma unroll
+            for (int d = 0; d < 9; ++d) f[h][d] = g[h][d];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) { g[h][d] = C.po[d][ih]; g[h][3 + d] = C.pa[d][ih]; g[h][6 + d] = C.n[d][ih]; }
+        }
+#else
 #pragma unroll
         for (int h = 0; h < kSolveStep; ++h) {
             const int ih = min(i + h * T, nv - 1);
 #pragma unroll
             for (int d = 0; d < 3; ++d) { f[h][d] = C.po[d][ih]; f[h][3 + d] = C.pa[d][ih]; f[h][6 + d] = C.n[d][ih]; }
         }
+#endif
 #pragma unroll
         for (int h = 0; h < kSolveStep; ++h) {
             const double po[3] = {f[h][0], f[h][1], f[h][2]}, pa[3] = {f[h][3], f[h][4], f[h][5]},
@@ -2673,6 +2771,66 @@ SSF_DEV void evaluate(const CorrLds& C, int nv, const double q[4], const double 
                      uu[3] = {C.n[0][i], C.n[1][i], C.n[2][i]};
         accum_edge(R, t, po, pa, uu, 1.0, ne);
     }
+#if SSF_SOLVE_RED == 0
+    (void)parity;
+    block_sum_rs<kNE>(ne, lds);
+#else
+    block_sum_db<kNE, NW, SSF_SOLVE_RED != 3, SSF_SOLVE_RED == 1>(ne, lds, parity);
+#endif
+#pragma unroll
+    for (int k = 0; k < kNE; ++k) ne[k] *= kNeScale[k];
+}
+
+// The first evaluation over records the association compacted ([0, nv) of rec, rank order, all
+// valid, nv <= kSolveLdsCap): evaluate<NW>()'s loop -- the same records per thread in the same
+// order and the same sums -- with each record read from global memory and stored to the LDS
+// arrays the later evaluations read (positions i + h T of thread t are read back by thread t
+// only: no barrier).  The loads of a step are in flight together; the first evaluation's
+// arithmetic overlaps the stream that the ballot compaction used to wait for alone.
+template <int NW>
+SSF_DEV void evaluate_load(const CorrRec* __restrict__ rec, CorrLds& C, int nv, const double q[4],
+                           const double t[3], double (&ne)[kNE], double* lds, int parity) {
+#pragma unroll
+    for (int k = 0; k < kNE; ++k) ne[k] = 0.0;
+    double R[9];
+    quat_to_R(q, R);
+    const int T = blockDim.x;
+    hf2 H[kHF];
+#pragma unroll
+    for (int k = 0; k < kHF; ++k) H[k] = hf2{0.0f, 0.0f};
+    // one step's records in flight ahead of the step being evaluated (clamped, unconditional
+    // loads: a step past nv re-reads record nv - 1 and is never used)
+    float4 n0[kSolveStep], n1[kSolveStep], n2[kSolveStep];
+#pragma unroll
+    for (int h = 0; h < kSolveStep; ++h) {
+        const float4* rp = reinterpret_cast<const float4*>(rec + min((int)threadIdx.x + h * T, nv - 1));
+        n0[h] = rp[0]; n1[h] = rp[1]; n2[h] = rp[2];
+    }
+    for (int i = threadIdx.x; i < nv; i += kSolveStep * T) {
+        float4 r0[kSolveStep], r1[kSolveStep], r2[kSolveStep];
+#pragma unroll
+        for (int h = 0; h < kSolveStep; ++h) {
+            r0[h] = n0[h]; r1[h] = n1[h]; r2[h] = n2[h];
+            const float4* rp = reinterpret_cast<const float4*>(rec + min(i + kSolveStep * T + h * T, nv - 1));
+            n0[h] = rp[0]; n1[h] = rp[1]; n2[h] = rp[2];
+        }
+#pragma unroll
+        for (int h = 0; h < kSolveStep; ++h) {
+            const int ih = i + h * T;
+            if (ih < nv) {
+                C.po[0][ih] = r0[h].x; C.po[1][ih] = r0[h].y; C.po[2][ih] = r0[h].z;
+                C.pa[0][ih] = r1[h].x; C.pa[1][ih] = r1[h].y; C.pa[2][ih] = r1[h].z;
+                C.n[0][ih] = r2[h].x; C.n[1][ih] = r2[h].y; C.n[2][ih] = r2[h].z;
+            }
+            const double po[3] = {r0[h].x, r0[h].y, r0[h].z}, pa[3] = {r1[h].x, r1[h].y, r1[h].z},
+                         nn[3] = {r2[h].x, r2[h].y, r2[h].z};
+            accum_corr(R, t, po, pa, nn, (h == 0 || ih < nv) ? 1.0 : 0.0, ne, H);
+        }
+    }
+#if SSF_SOLVE_HF32
+#pragma unroll
+    for (int e = 0; e < 21; ++e) ne[e] += (double)H[e >> 1][e & 1];
+#endif
 #if SSF_SOLVE_RED == 0
     (void)parity;
     block_sum_rs<kNE>(ne, lds);
@@ -2744,6 +2902,17 @@ SSF_DEV int chol_solve6(double M[6][6], const double b[6], double y[6]) {
 // Cholesky solve of the packed symmetric normal equations A y = -g (A = ne[0..20] upper packed,
 // g = ne[21..26]): 21 + 21 doubles of state, one reciprocal per diagonal instead of a division
 // per element (the GN path runs it redundantly on every thread).
+#ifndef SSF_SOLVE_CHOL_FMA
+#define SSF_SOLVE_CHOL_FMA 1                     // the 6x6 solve's multiply-subtracts as FMAs (A/B: 0)
+#endif
+// a - b c, as one fused operation (a shorter dependent chain; the step moves by rounding only)
+SSF_DEV double msub(double a, double b, double c) {
+#if SSF_SOLVE_CHOL_FMA
+    return __builtin_fma(-b, c, a);
+#else
+    return a - b * c;
+#endif
+}
 SSF_DEV int chol_solve_packed(const double (&ne)[kNE], double y[6]) {
     double L[21];                         // L(i, j), j <= i, at pk(j, i)
     double inv[6];
@@ -2751,7 +2920,7 @@ SSF_DEV int chol_solve_packed(const double (&ne)[kNE], double y[6]) {
     for (int j = 0; j < 6; ++j) {
         double s = ne[pk(j, j)];
 #pragma unroll
-        for (int k = 0; k < j; ++k) s -= L[pk(k, j)] * L[pk(k, j)];
+        for (int k = 0; k < j; ++k) s = msub(s, L[pk(k, j)], L[pk(k, j)]);
         if (!(s > 0.0)) return -1;
 #if SSF_SOLVE_RSQ
         const double r = (s > 1e-290 && s < 1e290) ? rsq_refined(s) : 1.0 / sqrt(s);
@@ -2766,7 +2935,7 @@ SSF_DEV int chol_solve_packed(const double (&ne)[kNE], double y[6]) {
         for (int i = j + 1; i < 6; ++i) {
             double v = ne[pk(i, j)];
 #pragma unroll
-            for (int k = 0; k < j; ++k) v -= L[pk(k, i)] * L[pk(k, j)];
+            for (int k = 0; k < j; ++k) v = msub(v, L[pk(k, i)], L[pk(k, j)]);
             L[pk(j, i)] = v * inv[j];
         }
     }
@@ -2775,14 +2944,14 @@ SSF_DEV int chol_solve_packed(const double (&ne)[kNE], double y[6]) {
     for (int i = 0; i < 6; ++i) {
         double v = -ne[21 + i];
 #pragma unroll
-        for (int k = 0; k < i; ++k) v -= L[pk(k, i)] * z[k];
+        for (int k = 0; k < i; ++k) v = msub(v, L[pk(k, i)], z[k]);
         z[i] = v * inv[i];
     }
 #pragma unroll
     for (int i = 5; i >= 0; --i) {
         double v = z[i];
 #pragma unroll
-        for (int k = i + 1; k < 6; ++k) v -= L[pk(i, k)] * y[k];
+        for (int k = i + 1; k < 6; ++k) v = msub(v, L[pk(i, k)], y[k]);
         y[i] = v * inv[i];
     }
     return 0;
@@ -2829,7 +2998,8 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
                                                          const CorrRec* __restrict__ ecorr,
                                                          const int64_t* __restrict__ ecurr_off,
                                                          const int32_t* __restrict__ ecurr_count,
-                                                         int32_t* __restrict__ ncorr_edge_out) {
+                                                         int32_t* __restrict__ ncorr_edge_out,
+                                                         const int32_t* __restrict__ ncompact) {
     __shared__ SolveShared S;
     __shared__ double red[2 * (NT / 64 + 1) * kNE];                   // block_sum_db: two halves
     __shared__ CorrLds C;
@@ -2841,6 +3011,9 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
     const int p = blockIdx.x, tid = threadIdx.x;
     const int n = curr_count[p];
     const CorrRec* rec = corr + curr_off[p];
+    // records the association already compacted (ncompact[p] >= 0): read with the other per-pair
+    // scalars, before the first barrier
+    const int ncp = (!kEdges && ncompact) ? ncompact[p] : -1;          // uniform
     const int en = kEdges ? ecurr_count[p] : 0;
     const CorrRec* erec = kEdges ? ecorr + ecurr_off[p] : nullptr;
 #ifdef SSF_SOLVE_STAMPS
@@ -2934,7 +3107,10 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
             return nv;
         };
 #endif
-        const int nv = compact(rec, n, 0);
+        // compacted records: [0, ncp) in rank order, streamed into LDS by the first evaluation
+        // itself (evaluate_load: the same per-thread order and sums as evaluate() from LDS), no
+        // ballot pass
+        const int nv = ncp >= 0 ? ncp : compact(rec, n, 0);
         const int nve = kEdges ? compact(erec, en, nv) : 0;
         const bool in_lds = nv + nve <= kSolveLdsCap;                  // uniform
 #ifdef SSF_SOLVE_STAMPS
@@ -2943,16 +3119,50 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
         if (tid == 0 && ncorr_out) ncorr_out[p] = nv;
         if (kEdges && tid == 0 && ncorr_edge_out) ncorr_edge_out[p] = nve;
         int par = 0;                                                    // block_sum_dpp's LDS half
+        // (compacted records beyond the LDS: every record of [0, nv) is valid)
+        const int nglob = ncp >= 0 ? nv : n;
         auto eval_at = [&](const double* qq, const double* tt, double (&ne_)[kNE]) {
             if (in_lds) evaluate<NT / 64>(C, nv, qq, tt, ne_, red, nve, par);
-            else evaluate(rec, n, qq, tt, ne_, red, erec, en);
+            else evaluate(rec, nglob, qq, tt, ne_, red, erec, en);
             par ^= 1;
         };
         double ne[kNE];
         double q[4], t[3];
+#if SSF_SOLVE_QDIRECT
+        for (int k = 0; k < 4; ++k) q[k] = pose_in[7 * p + k];                 // (A/B) uniform loads
+        for (int k = 0; k < 3; ++k) t[k] = pose_in[7 * p + 4 + k];
+#else
         for (int k = 0; k < 4; ++k) q[k] = S.q[k];
         for (int k = 0; k < 3; ++k) t[k] = S.t[k];
-        eval_at(q, t, ne);
+#endif
+        if (ncp >= 0 && in_lds && SSF_SOLVE_DIRECT == 1) {
+            evaluate_load<NT / 64>(rec, C, nv, q, t, ne, red, par);
+            par ^= 1;
+        } else {
+            if (ncp >= 0 && in_lds) {
+                // (A/B, SSF_SOLVE_DIRECT=2) a plain copy of the compacted records into LDS, four
+                // per thread in flight: thread t writes the positions t + k T it reads itself
+                const int T = blockDim.x;
+                for (int i0 = tid; i0 < nv; i0 += 4 * T) {
+                    float4 a[4][3];
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) {
+                        const float4* rp = reinterpret_cast<const float4*>(rec + min(i0 + h * T, nv - 1));
+                        a[h][0] = rp[0]; a[h][1] = rp[1]; a[h][2] = rp[2];
+                    }
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) {
+                        const int ih = i0 + h * T;
+                        if (ih < nv) {
+                            C.po[0][ih] = a[h][0].x; C.po[1][ih] = a[h][0].y; C.po[2][ih] = a[h][0].z;
+                            C.pa[0][ih] = a[h][1].x; C.pa[1][ih] = a[h][1].y; C.pa[2][ih] = a[h][1].z;
+                            C.n[0][ih] = a[h][2].x; C.n[1][ih] = a[h][2].y; C.n[2][ih] = a[h][2].z;
+                        }
+                    }
+                }
+            }
+            eval_at(q, t, ne);
+        }
 #ifdef SSF_SOLVE_STAMPS
         st2 = __builtin_amdgcn_s_memtime();
 #endif
@@ -3286,12 +3496,16 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
                            CorrRec* corr, double* pose_rel, double* pose_abs, double* log,
                            int32_t* nlog, int32_t* ncorr, int32_t* nn, const EdgeReg* edge,
                            const float4* last_strip_xyzi, const int32_t* last_strip_head,
-                           const double* pose_in, const double* pose_abs_in) {
+                           const double* pose_in, const double* pose_abs_in, int32_t* nnv,
+                           int32_t* ncompact) {
     if (n_pairs <= 0) return hipSuccess;
     // warm starts / start poses read from pose_in / pose_abs_in (default: in place), results
     // written to pose_rel / pose_abs: a chain reads pair k - 1's output slot directly
     const double* pin = pose_in ? pose_in : pose_rel;
     const double* ain = pose_abs_in ? pose_abs_in : pose_abs;
+    // compacted records (k_associate_strips' lane mode with one work-group per pair, planes only):
+    // the association writes the counts, the solve reads them; otherwise neither sees them
+    int32_t* ncp = nullptr;
     if (max_m > 0) {
         const int bx = (int)((max_m + 255) / 256);
 #ifndef SSF_ASSOC_XBAND
@@ -3312,6 +3526,8 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
                                                              std::max(8, 1024 / n_pairs))
                                     : (int)std::max<int64_t>(1, std::min<int64_t>({8, 256 / n_pairs,
                                                              (max_m + kStripThreads - 1) / kStripThreads}));
+            if (!coop && !bigc && qsplit == 1 && nnv && ncompact && !edge && !SSF_ASSOC_DEFER && SSF_ASSOC_COMPACT)
+                ncp = ncompact;
             kmark(s, coop ? "k_associate_strips_coop" : soa ? "k_associate_strips_soa" : "k_associate_strips");
             hipLaunchKernelGGL(coop ? (soa ? k_associate_strips<true, kAssocCoopG> : k_associate_strips<false, kAssocCoopG>)
                                     : bigc ? (soa ? k_associate_strips<true, kAssocBigG> : k_associate_strips<false, kAssocBigG>)
@@ -3319,7 +3535,8 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
                                dim3(n_pairs, qsplit), dim3(kStripThreads), lds, s, last, last_off, last_count,
                                last_normal, last_valid, last_sorted, last_sidx, curr, curr_off,
                                curr_count, pin, corr, nn, cap,
-                               last_strip_head ? last_strip_xyzi : nullptr, last_strip_head);
+                               last_strip_head ? last_strip_xyzi : nullptr, last_strip_head,
+                               ncp ? nnv : nullptr, ncp);
         } else
 #endif
         if (max_m <= kAssocSoaMax && last_sorted && last_sidx) {
@@ -3357,12 +3574,12 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
     hipLaunchKernelGGL((cfg.solver == SSF_SOLVER_GN ? k_solve<E, NT, SSF_SOLVER_GN> : k_solve<E, NT, SSF_SOLVER_CERES_LM>), \
                        dim3(n_pairs), dim3(NT), 0, s, corr, curr_off, curr_count, \
                        last_count, cfg.solver, cfg.max_iter, pin, ain, pose_rel, pose_abs, log, nlog, ncorr, \
-                       __VA_ARGS__)
+                       __VA_ARGS__, ncp)
 #else
 #define SSF_SOLVE_LAUNCH(E, NT, ...)                                                               \
     hipLaunchKernelGGL((k_solve<E, NT, -1>), dim3(n_pairs), dim3(NT), 0, s, corr, curr_off, curr_count, \
                        last_count, cfg.solver, cfg.max_iter, pin, ain, pose_rel, pose_abs, log, nlog, ncorr, \
-                       __VA_ARGS__)
+                       __VA_ARGS__, ncp)
 #endif
     if (edge)
         SSF_SOLVE_LAUNCH(true, kSolveThreads, edge->corr, edge->curr_off, edge->curr_count, edge->ncorr);

@@ -131,7 +131,10 @@ hipError_t launch_register(hipStream_t s, const ssf_config& cfg, int n_pairs, co
                            int32_t* nlog, int32_t* ncorr, int32_t* nn,
                            const EdgeReg* edge = nullptr, const float4* last_strip_xyzi = nullptr,
                            const int32_t* last_strip_head = nullptr, const double* pose_in = nullptr,
-                           const double* pose_abs_in = nullptr);
+                           const double* pose_abs_in = nullptr, int32_t* nnv = nullptr,
+                           int32_t* ncompact = nullptr);
+// (nnv [>= the current frames' total points] and ncompact [>= n_pairs]: scratch that lets the
+// lane-mode association hand the solve compacted records; nullptr = records in query order)
 hipError_t launch_edge_table(hipStream_t s, const ssf_edge_config& ec, int n_frames,
                              const float4* edges, const int64_t* frame_off, const int32_t* count,
                              int64_t max_m, float* line, uint8_t* valid);

@@ -116,6 +116,54 @@ def test_nan_warm_start_association_stays_in_frame(dev):
     assert np.array_equal(got[0], got[1])
 
 
+@pytest.mark.parametrize("solver,iters", [("gn", 10), ("ceres_lm", 8)])
+def test_compacted_records_same_bits(dev, solver, iters):
+    """Big launches (> 16 pairs, one association work-group per pair) hand the solve compacted
+    records in rank order and the solve streams them into LDS inside its first evaluation; a
+    single-pair launch (group-mode association) writes records in query order and the solve
+    compacts them itself.  Both feed the evaluations the same records in the same order: poses,
+    per-step logs and correspondence counts must be bit-identical."""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index, solver=solver, max_iter=iters)
+    # 17 pairs of one sequence (distinct current frames: the records live at their offsets)
+    P = 17
+    clouds = [frame(3, k, n_az=900)[0] for k in range(P + 1)]
+    pb = _planes(fe, dev, clouds)
+    table = fe.plane_table(pb)
+    rng = np.random.default_rng(11)
+    sel = [(k, k + 1) for k in range(P)]
+    q0 = np.zeros((P, 4)); q0[:, 2] = rng.uniform(-0.003, 0.003, P); q0[:, 3] = 1.0
+    q0 /= np.linalg.norm(q0, axis=1, keepdims=True)
+    t0 = np.c_[rng.uniform(0.6, 1.1, P), rng.uniform(-0.05, 0.05, P), np.zeros(P)]
+    init = torch.tensor(np.c_[q0, t0], dtype=torch.float64, device=dev)
+
+    def sub_pairs(idx):
+        import ssf as S
+        lo = torch.stack([pb.off[a] for a, _ in idx] + [pb.off[idx[-1][0] + 1]])
+        co = torch.stack([pb.off[b] for _, b in idx] + [pb.off[idx[-1][1] + 1]])
+        hl = torch.tensor([int(pb.h_off[a]) for a, _ in idx] + [int(pb.h_off[idx[-1][0] + 1])])
+        hc = torch.tensor([int(pb.h_off[b]) for _, b in idx] + [int(pb.h_off[idx[-1][1] + 1])])
+        cl = torch.stack([pb.count[a] for a, _ in idx]).contiguous()
+        cc = torch.stack([pb.count[b] for _, b in idx]).contiguous()
+        return (S.PlaneBatch(pb.xyzi, cl, lo.contiguous(), hl, pb.max_points),
+                S.PlaneBatch(pb.xyzi, cc, co.contiguous(), hc, pb.max_points))
+
+    last, curr = sub_pairs(sel)
+    big = fe.register(last, table, curr, init.clone(), want_log=True)
+    torch.cuda.synchronize()
+    for k in range(P):
+        l1, c1 = sub_pairs([sel[k]])
+        one = fe.register(l1, table, c1, init[k:k + 1].clone(), want_log=True)
+        torch.cuda.synchronize()
+        assert int(one["ncorr"][0]) == int(big["ncorr"][k]) > 0
+        assert np.array_equal(one["pose_rel"][0].cpu().numpy().view(np.uint64),
+                              big["pose_rel"][k].cpu().numpy().view(np.uint64)), k
+        n = int(one["nlog"][0])
+        assert n == int(big["nlog"][k])
+        assert np.array_equal(one["log"][0, :n].cpu().numpy().view(np.uint64),
+                              big["log"][k, :n].cpu().numpy().view(np.uint64)), k
+
+
 @pytest.mark.parametrize("solver,iters,mode,brute", [("ceres_lm", 8, 0, False), ("gn", 10, 1, False),
                                                      ("ceres_lm", 8, 0, True)])
 def test_register_pair_per_step(oracle, dev, solver, iters, mode, brute):

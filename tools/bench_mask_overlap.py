@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--streams", default="1,2,3,4")
     ap.add_argument("--launches", type=int, default=30)
     ap.add_argument("--distinct", type=int, default=32)
+    ap.add_argument("--queue", type=int, default=0, help="frame queue of at most this many work-groups "
+                    "per launch (ssf_set_mask_schedule; 0: one work-group per frame)")
     a = ap.parse_args()
     import ssf
     from ssf import synth
@@ -45,6 +47,8 @@ def main():
         fes = [ssf.Frontend(64, device=0) for _ in range(S)]
         for fe in fes:
             fe.reserve(B, N)
+            if a.queue:
+                fe.mask_schedule(None, a.queue)
         streams = [torch.cuda.Stream(dev) for _ in range(S)]
 
         def run(n):
@@ -58,7 +62,7 @@ def main():
         run(a.launches)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        print(json.dumps({"batch": B, "streams": S, "launches": a.launches,
+        print(json.dumps({"batch": B, "streams": S, "queue": a.queue, "launches": a.launches,
                           "ms_per_launch": round(dt / a.launches * 1e3, 3),
                           "frames_per_s": round(a.launches * B / dt, 1)}), flush=True)
         del fes

@@ -1,0 +1,14 @@
+# round 6r: k_solve correspondences per thread step 2 (default) / 4 / 3 and the one-barrier reduction (red1), GN-specialised kernel: parity, kernel times
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+T=r6r
+L=$PWD/ssf-slam_amd/ssf/_lib
+timeout -k 10 600 python -u -m pytest tests/test_gpu_registration.py tests/test_gpu_configs.py tests/test_gpu_nodes.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1 && echo PYTEST_OK || { tail -30 gpurun_out/${T}_pytest.log; exit 1; }
+for rep in 1 2 3; do
+for v in def st4 st3 red1; do
+  if [ $v = def ]; then lib=$L/libssf_frontend.so; else lib=$L/libssf_frontend_$v.so; fi
+  SSF_LIB=$lib timeout -k 10 200 python3 -u tools/bench_features.py --chain --reps 10 --distinct 32 --tag $v >> gpurun_out/${T}_feat.log 2>&1 || exit 1
+done
+done
+echo AB_OK

@@ -366,10 +366,18 @@ SSF_DEV void for_points_deep(const Ts* __restrict__ P, const Ts* __restrict__ Fl
     }
 }
 
-// EM: two points per step (i, i + T) so every Aq / bq read from LDS serves both (the per-point
-// LDS re-read of the parameter doubles is what bounds the EM pass).  The second point of the
-// last step may not exist (w1 = 0: computed on a duplicate, weighted out).  Loads clamped and
-// unconditional, as in for_points.
+// EM: two points per step (i, i + T) so every parameter read serves both.  The second point of
+// the last step may not exist (w1 = 0: computed on a duplicate, weighted out).  Loads clamped
+// and unconditional, as in for_points.  SSF_EM_DEEP = 4 (default): the next step's pair staged
+// by LDS-DMA, below; 1: in registers (the round-2..6 form; two pairs in flight, or the loop
+// unrolled with swapping register sets, were 6 % / 4 % slower: the compiler waits for the loads
+// right after issuing them, r6t / r6u).
+#ifndef SSF_EM_DEEP
+#define SSF_EM_DEEP 4
+#endif
+#ifndef SSF_EM_SGPR
+#define SSF_EM_SGPR (SSF_EM_DEEP == 4)           // E-step parameters as wave-uniform SGPR operands
+#endif
 template <class Ts, class Fn>
 SSF_DEV void for_point_pairs(const Ts* __restrict__ P, const Ts* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
     const int64_t T = blockDim.x;
@@ -388,6 +396,54 @@ SSF_DEV void for_point_pairs(const Ts* __restrict__ P, const Ts* __restrict__ Fl
         fn(xa, xb, wb);
     }
 }
+
+#if SSF_EM_DEEP == 4
+// The pair of the next step staged by LDS-DMA (global_load_lds_dwordx3: lane l's 12 bytes at
+// base + 16 l, tools/probes/glds_x3_layout.hip) into a per-wave 4 KiB slot (k-means++'s bsum
+// block, idle during EM), so the loads in flight hold no VGPRs and cannot be sunk to their use.
+// Same per-thread point order, so the same sums.  The slot is read (lgkmcnt(0)) before the next
+// DMA overwrites it; vmcnt(0) before the read.  hipcc drains every pending LDS-DMA before any
+// LDS read it cannot prove disjoint, so the loop reads no other LDS: the E-step parameters come
+// in SGPRs (SSF_EM_SGPR).
+SSF_DEV void glds_x3(const float* g, float* lds_base) {
+    __builtin_amdgcn_global_load_lds((const void*)g,
+                                     (__attribute__((address_space(3))) void*)lds_base, 12, 0, 0);
+}
+template <class Fn>
+SSF_DEV void for_point_pairs_glds(const float* __restrict__ P, const float* __restrict__ Fl,
+                                  int64_t r0, int64_t r1, float* slot, Fn&& fn) {
+    const int64_t T = blockDim.x;
+    const int lane = threadIdx.x & 63;
+    int64_t i = r0 + threadIdx.x;
+    if (i >= r1) return;
+    // a lane that has left the loop takes no part in a DMA and its 16 bytes of the slot are not
+    // written (EXEC-masked); the others' land at base + 16 lane as before
+    const int64_t last = r1 - 1;
+    auto issue = [&](int64_t ia, int64_t ib) {
+        ia = min(ia, last); ib = min(ib, last);
+        glds_x3(Fl + 3 * ia, slot);
+        glds_x3(P + 3 * ia, slot + 256);
+        glds_x3(Fl + 3 * ib, slot + 512);
+        glds_x3(P + 3 * ib, slot + 768);
+    };
+    issue(i, i + T);
+    for (; i < r1; i += 2 * T) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0): this step's DMA has landed
+        double xa[6], xb[6];
+        const float* s = slot + 4 * lane;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            xa[d] = (double)s[d];       xa[3 + d] = (double)s[256 + d];
+            xb[d] = (double)s[512 + d]; xb[3 + d] = (double)s[768 + d];
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0): the slot is read
+        const double wb = (i + T < r1) ? 1.0 : 0.0;
+        issue(i + 2 * T, i + 3 * T);
+        fn(xa, xb, wb);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);              // the last (clamped) DMA drained
+}
+#endif
 
 // 1/d for d in [1, 2] (d = 1 + e, e in (0, 1]): v_rcp_f64 and two Newton steps, ~1 ulp,
 // instead of the IEEE division sequence.
@@ -680,7 +736,11 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
     __shared__ double red[kNW * 32];
     __shared__ int ired[kNW];
     __shared__ unsigned long long cand_lds[2];
+#if SSF_EM_DEEP == 4
+    __shared__ __attribute__((aligned(16))) double bsum[kKppBlocks > kNW * 512 ? kKppBlocks : kNW * 512];  // + the EM's DMA slots
+#else
     __shared__ double bsum[kKppBlocks];   // k-means++ per-64-point-block distance totals
+#endif
     __shared__ uint32_t lq[kNW * kLQ];     // Lloyd skip passes: per-wave relabel entries of a trip
     __shared__ double xtmp[kSlot + kMaxSplit * kSlot];   // exchange totals + the gathered parts
     __shared__ int tk, okflag;
@@ -1336,8 +1396,8 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         if (it == 1 && tid == 0) S.dg_e[0] = S.dg_e[1] = S.dg_e[2] = 0.0;
         const unsigned long long e_t0 = __builtin_amdgcn_s_memtime();
 #endif
-#ifdef SSF_EM_SGPR
-        // A/B: the 27 E-step parameters as wave-uniform SGPR operands, read
+#if SSF_EM_SGPR
+        // the 27 E-step parameters as wave-uniform SGPR operands, read
         // from LDS once per pass instead of once per point pair
         double Aqs[21], bqs[6];
 #pragma unroll
@@ -1345,8 +1405,12 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
 #pragma unroll
         for (int k = 0; k < 6; ++k) bqs[k] = uni(S.bq[k]);
 #endif
+#if SSF_EM_DEEP == 4
+        auto em_pair = [&](const double* xa, const double* xb, double wb) {
+#else
         for_point_pairs(P, Fl, r0, r1, [&](const double* xa, const double* xb, double wb) {
-#ifdef SSF_EM_SGPR
+#endif
+#if SSF_EM_SGPR
             const double* Aq = Aqs;
             const double* bq = bqs;
 #else
@@ -1380,7 +1444,15 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
                     for (int b = a; b < 6; ++b) acc[7 + up(a, b)] += rv * v[b];
                 }
             }
+#if SSF_EM_DEEP == 4
+        };
+        if constexpr (sizeof(T) == 4)
+            for_point_pairs_glds(P, Fl, r0, r1, reinterpret_cast<float*>(bsum) + (tid >> 6) * 1024, em_pair);
+        else
+            for_point_pairs(P, Fl, r0, r1, em_pair);
+#else
         });
+#endif
         acc[28] += log(prod) + (double)pexp * 0.69314718055994530942;
         block_sum_rs<29>(acc, red);
 #ifdef SSF_MASK_STAMPS

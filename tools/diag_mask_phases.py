@@ -13,8 +13,9 @@ def main():
     import ssf
     from ssf import synth
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    k0 = int(sys.argv[2]) if len(sys.argv) > 2 else 0        # first frame index of the sequences
     dev = torch.device("cuda", 0)
-    fr = [synth.scan(s, 0, device=dev) for s in range(8)]
+    fr = [synth.scan(s, k0 + 7 * s, device=dev) for s in range(8)]
     pts = torch.cat([fr[b % 8]["pos1"] for b in range(B)]).contiguous()
     flow = torch.cat([fr[b % 8]["flow"] for b in range(B)]).contiguous()
     N = fr[0]["pos1"].shape[0]

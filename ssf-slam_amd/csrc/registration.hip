@@ -987,6 +987,8 @@ struct PickState {
     double t5[5];       // ranks 0..4
     double d1, d2;      // the first two other-ring keys of rank >= 5 within 1 m (sentinel: 1 m)
     int K1, prow;
+    int sl;             // keys that left the top five and are not other-ring (an upper bound
+                        // when d1 / d2 come from the second walk: then 1 << 30)
 };
 
 // Inside 1 m for query j, one walk: K1, the top five, and the six smallest keys of points on
@@ -1004,7 +1006,7 @@ SSF_DEV void pick_1m(const float4* __restrict__ P, const StripView<false>& v, co
     // the query's own; otherwise the second walk below)
     double o2[2] = {sent, sent};
     const int qrow = pt_row(q);
-    int K1 = 0;
+    int K1 = 0, sl = 0;
     s.pos[0] = j;
 #pragma unroll
     for (int k = 1; k < kPos1m; ++k) s.pos[k] = -1;
@@ -1015,9 +1017,11 @@ SSF_DEV void pick_1m(const float4* __restrict__ P, const StripView<false>& v, co
             const double out = key_insert_out<5>(s.t5, pick_key(d, p));
             const int row = pick_row(out);
             if (row != qrow && row <= 63) key_insert<2>(o2, out);
+            else ++sl;
         }
     });
     s.K1 = K1;
+    s.sl = 1 << 30;
     s.d1 = sent; s.d2 = sent;
     s.prow = -1;
     if (K1 <= 5) return;
@@ -1025,6 +1029,7 @@ SSF_DEV void pick_1m(const float4* __restrict__ P, const StripView<false>& v, co
     const double k5 = s.t5[4];
     if (pick_index(s.t5[0]) == pt_id(q) || s.prow == qrow) {
         s.d1 = o2[0]; s.d2 = o2[1];
+        s.sl = sl;
         return;
     }
     const int prow = s.prow;
@@ -1103,7 +1108,11 @@ SSF_DEV void table_pick_walks(const float4* __restrict__ P, const StripView<fals
         const bool f1 = key_dist(s.d1) < 1.0f, f2 = key_dist(s.d2) < 1.0f;
         if (s.K1 >= 30) {
             int r1 = 0, r2 = 0;                                            // ranks of D1, D2
-            if (f1) {
+            // the keys below D2 are the top five, D1 and left keys that are not other-ring (D1 /
+            // D2 are the two smallest other-ring keys that left): with L such keys r1 <= 5 + L,
+            // r2 <= 6 + L, so L <= 23 puts both inside the 30 without the rank walk.  sl = L + 5
+            // (the five sentinels left the list too: K1 >= 30)
+            if (f1 && s.sl > 28) {
                 const double b1 = s.d1, b2 = s.d2;
                 const float lim = f2 ? key_dist(b2) : key_dist(b1);
                 visit_1m(v, T, g, s.pos, q, [&] { return lim; }, [&](const float4& p) {

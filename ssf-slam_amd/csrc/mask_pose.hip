@@ -368,12 +368,14 @@ SSF_DEV void for_points_deep(const Ts* __restrict__ P, const Ts* __restrict__ Fl
 
 // EM: two points per step (i, i + T) so every parameter read serves both.  The second point of
 // the last step may not exist (w1 = 0: computed on a duplicate, weighted out).  Loads clamped
-// and unconditional, as in for_points.  SSF_EM_DEEP = 4 (default): the next step's pair staged
-// by LDS-DMA, below; 1: in registers (the round-2..6 form; two pairs in flight, or the loop
-// unrolled with swapping register sets, were 6 % / 4 % slower: the compiler waits for the loads
-// right after issuing them, r6t / r6u).
+// and unconditional, as in for_points.  SSF_EM_DEEP = 1 (default): the next step's pair in
+// registers; 4: staged by LDS-DMA with the parameters in SGPRs, below -- +1.5 % on the mask
+// alone (r6u) but not in the pipeline (r6za / r6zb: its 16 KiB more LDS keeps the other
+// kernels off the mask's CUs; a one-point 2 KiB-slot form without the extra LDS was no faster).
+// Two register pairs in flight, or the loop unrolled with swapping register sets, were 6 % / 4 %
+// slower (the compiler waits for the loads right after issuing them, r6t / r6u).
 #ifndef SSF_EM_DEEP
-#define SSF_EM_DEEP 4
+#define SSF_EM_DEEP 1
 #endif
 #ifndef SSF_EM_SGPR
 #define SSF_EM_SGPR (SSF_EM_DEEP == 4)           // E-step parameters as wave-uniform SGPR operands
@@ -398,7 +400,7 @@ SSF_DEV void for_point_pairs(const Ts* __restrict__ P, const Ts* __restrict__ Fl
 }
 
 #if SSF_EM_DEEP == 4
-// The pair of the next step staged by LDS-DMA (global_load_lds_dwordx3: lane l's 12 bytes at
+// A/B (SSF_EM_DEEP = 4): the pair of the next step staged by LDS-DMA (global_load_lds_dwordx3: lane l's 12 bytes at
 // base + 16 l, tools/probes/glds_x3_layout.hip) into a per-wave 4 KiB slot (k-means++'s bsum
 // block, idle during EM), so the loads in flight hold no VGPRs and cannot be sunk to their use.
 // Same per-thread point order, so the same sums.  The slot is read (lgkmcnt(0)) before the next

@@ -748,8 +748,12 @@ static int32_t mask_pose_batch(ssf_ctx* c, void* stream, int32_t n_frames, const
     if (c->mask_order && c->mask_order_n != n_frames)
         return fail(c, SSF_E_ARG, "mask_pose_batch: the frame order (ssf_set_mask_schedule) has another length");
     const int64_t total = h_frame_off[n_frames];
-    for (int f = 0; f < n_frames; ++f)
+    for (int f = 0; f < n_frames; ++f) {
         if (h_frame_off[f + 1] < h_frame_off[f]) return fail(c, SSF_E_ARG, "mask_pose_batch: offsets not monotone");
+        // the streaming loops address a frame with 32-bit byte offsets (mask_pose.hip load3_off)
+        if (h_frame_off[f + 1] - h_frame_off[f] > (int64_t)(0xFFFFFFFFu / (3 * sizeof(T))))
+            return fail(c, SSF_E_ARG, "mask_pose_batch: a frame above 2^32 / (3 sizeof(T)) points");
+    }
     hipStream_t s = (hipStream_t)stream;
     SSF_TRY_HIP(c, hipSetDevice(c->device), "hipSetDevice");
     ssf_ctx::DrawSlot& ds = c->dslot[c->dnext];

@@ -314,6 +314,17 @@ SSF_DEV void load_raw(const T* __restrict__ P, const T* __restrict__ Fl, int64_t
     r[3] = P[3 * i];  r[4] = P[3 * i + 1];  r[5] = P[3 * i + 2];
 }
 
+#ifndef SSF_EM_OFF32
+#define SSF_EM_OFF32 1                           // EM / Lloyd loads: 32-bit byte offsets from the part's base (A/B: 0)
+#endif
+// three consecutive Ts at byte offset o (< 2^32) of a wave-uniform base: the global_load's SGPR
+// base + 32-bit VGPR offset form, so the clamped index costs a min and a multiply per point
+// instead of 64-bit compares, selects and address arithmetic
+template <class Ts>
+SSF_DEV void load3_off(const Ts* __restrict__ base, uint32_t o, Ts r[3]) {
+    const Ts* p = reinterpret_cast<const Ts*>(reinterpret_cast<const char*>(base) + o);
+    r[0] = p[0]; r[1] = p[1]; r[2] = p[2];
+}
 // Points [r0, r1) of the frame (the work-group's part, see Split).
 template <class Ts, class Fn>
 SSF_DEV void for_points(const Ts* __restrict__ P, const Ts* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
@@ -345,6 +356,31 @@ SSF_DEV double uni(double v) {
 // at the join (the record-writing full pass took 411 k cycles against 264 k without records).
 template <int D, class Ts, class Fn>
 SSF_DEV void for_points_deep(const Ts* __restrict__ P, const Ts* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
+#if SSF_EM_OFF32
+    {   // frames of at most 2^32 / (3 sizeof(Ts)) points (mask_pose_batch rejects larger ones)
+        if (r1 <= r0) return;                              // uniform (an empty part)
+        const Ts* Pb = P + 3 * r0;
+        const Ts* Fb = Fl + 3 * r0;
+        const uint32_t n = (uint32_t)(r1 - r0), T = blockDim.x, last = n - 1;
+        constexpr uint32_t S = 3 * sizeof(Ts);
+        const uint32_t j0 = threadIdx.x;
+        auto load = [&](uint32_t k, Ts r[6]) { load3_off(Fb, k * S, r); load3_off(Pb, k * S, r + 3); };
+        Ts buf[D][6];
+#pragma unroll
+        for (int d = 0; d < D; ++d) load(min(j0 + d * T, last), buf[d]);
+        for (uint32_t base = j0; base < n; base += D * T) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const uint32_t j = base + d * T;
+                double x[6];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) x[k] = (double)buf[d][k];
+                load(min(j + D * T, last), buf[d]);
+                fn(r0 + (int64_t)j, x, j < n);
+            }
+        }
+    }
+#else
     const int64_t T = blockDim.x;
     const int64_t i0 = r0 + threadIdx.x;
     if (r1 <= r0) return;                                  // uniform (an empty part)
@@ -364,6 +400,7 @@ SSF_DEV void for_points_deep(const Ts* __restrict__ P, const Ts* __restrict__ Fl
             fn(i, x, i < r1);   // every slot (no branch around the body's stores); val = 0 is weighted out
         }
     }
+#endif
 }
 
 // EM: two points per step (i, i + T) so every parameter read serves both.  The second point of
@@ -377,11 +414,40 @@ SSF_DEV void for_points_deep(const Ts* __restrict__ P, const Ts* __restrict__ Fl
 #ifndef SSF_EM_DEEP
 #define SSF_EM_DEEP 1
 #endif
+#ifndef SSF_LLOYD_LDS_HOIST
+#define SSF_LLOYD_LDS_HOIST 0                    // Lloyd: the centres' bases laundered once per pass (A/B: 2.3x
+#endif                                           // slower, the centres hoisted into VGPRs spill in the loops, r6zd)
+#ifndef SSF_EM_LDS_HOIST
+#define SSF_EM_LDS_HOIST 1                       // EM: the LDS parameter bases laundered once per pass (r6zc/r6zd)
+#endif
 #ifndef SSF_EM_SGPR
 #define SSF_EM_SGPR (SSF_EM_DEEP == 4)           // E-step parameters as wave-uniform SGPR operands
 #endif
 template <class Ts, class Fn>
 SSF_DEV void for_point_pairs(const Ts* __restrict__ P, const Ts* __restrict__ Fl, int64_t r0, int64_t r1, Fn&& fn) {
+#if SSF_EM_OFF32
+    {   // frames of at most 2^32 / (3 sizeof(Ts)) points (mask_pose_batch rejects larger ones)
+        const Ts* Pb = P + 3 * r0;
+        const Ts* Fb = Fl + 3 * r0;
+        const uint32_t n = (uint32_t)(r1 - r0), T = blockDim.x, last = n - 1;
+        constexpr uint32_t S = 3 * sizeof(Ts);
+        uint32_t i = threadIdx.x;
+        if (i >= n) return;
+        Ts ra[6], rb[6];
+        auto load = [&](uint32_t k, Ts r[6]) { load3_off(Fb, k * S, r); load3_off(Pb, k * S, r + 3); };
+        load(i, ra);
+        load(min(i + T, last), rb);
+        for (; i < n; i += 2 * T) {
+            double xa[6], xb[6];
+#pragma unroll
+            for (int d = 0; d < 6; ++d) { xa[d] = (double)ra[d]; xb[d] = (double)rb[d]; }
+            const double wb = (i + T < n) ? 1.0 : 0.0;
+            load(min(i + 2 * T, last), ra);
+            load(min(i + 3 * T, last), rb);
+            fn(xa, xb, wb);
+        }
+    }
+#else
     const int64_t T = blockDim.x;
     int64_t i = r0 + threadIdx.x;
     if (i >= r1) return;
@@ -397,6 +463,7 @@ SSF_DEV void for_point_pairs(const Ts* __restrict__ P, const Ts* __restrict__ Fl
         load_raw(P, Fl, min(i + 3 * T, r1 - 1), rb);
         fn(xa, xb, wb);
     }
+#endif
 }
 
 #if SSF_EM_DEEP == 4
@@ -1157,8 +1224,15 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         // sums (full pass) or sum deltas (skip pass), changed count, new record
         // (val = 0: a pipeline slot with no point -- computed, weighted out, record written to
         // the frame's spare slot n)
+#if SSF_LLOYD_LDS_HOIST
+        const LdsDouble* cenL = lds_laundered(S.cen);   // once per pass (see SSF_EM_LDS_HOIST)
+#endif
         auto label = [&](auto wrec_c, int64_t i, const double* x, int lp, bool val) {
+#if SSF_LLOYD_LDS_HOIST
+            const LdsDouble* cen = cenL;
+#else
             const LdsDouble* cen = lds_laundered(S.cen);
+#endif
             double v[6], dt0 = 0.0, dt1 = 0.0, vn = 0.0;
 #pragma unroll
             for (int d = 0; d < 6; ++d) {
@@ -1183,9 +1257,16 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
             // every point: a prefetched stream of [flow, xyz]; the previous label is recomputed
             // from the previous centres (the pass that wrote it used the same expression)
             const double cpn0 = uni(S.csnp[0]), cpn1 = uni(S.csnp[1]);
+#if SSF_LLOYD_LDS_HOIST
+            const LdsDouble* cenpL = lds_laundered(S.cenp);
+#endif
             auto full_pass = [&](auto wrec_c) {
                 for_points_deep<kLloydDeep>(P, Fl, r0, r1, [&](int64_t i, const double* x, bool val) {
+#if SSF_LLOYD_LDS_HOIST
+                    const LdsDouble* cenp = cenpL;
+#else
                     const LdsDouble* cenp = lds_laundered(S.cenp);
+#endif
                     double dp0 = 0.0, dp1 = 0.0;
 #pragma unroll
                     for (int d = 0; d < 6; ++d) {
@@ -1406,6 +1487,13 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
         for (int k = 0; k < 21; ++k) Aqs[k] = uni(S.Aq[k]);
 #pragma unroll
         for (int k = 0; k < 6; ++k) bqs[k] = uni(S.bq[k]);
+#elif SSF_EM_LDS_HOIST
+        // the laundered LDS bases outside the loop: two loop-invariant VGPRs.  Laundered per
+        // pair, their constants were rematerialised every iteration into registers the
+        // prefetched point loads had landed in, so the loads were copied away (and waited for)
+        // right after they were issued
+        const LdsDouble* AqL = lds_laundered(S.Aq);
+        const LdsDouble* bqL = lds_laundered(S.bq);
 #endif
 #if SSF_EM_DEEP == 4
         auto em_pair = [&](const double* xa, const double* xb, double wb) {
@@ -1415,6 +1503,9 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_pose(
 #if SSF_EM_SGPR
             const double* Aq = Aqs;
             const double* bq = bqs;
+#elif SSF_EM_LDS_HOIST
+            const LdsDouble* Aq = AqL;
+            const LdsDouble* bq = bqL;
 #else
             // Aq / bq are re-read from LDS once per PAIR of points (lds_laundered)
             const LdsDouble* Aq = lds_laundered(S.Aq);

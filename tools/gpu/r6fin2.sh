@@ -1,6 +1,7 @@
 # round 6, final build part 2: the bench line of every config (profiles/r06fin_traffic.json,
 # r06fin_carla_traffic.json and r06fin_f64.json from part 1, same library); the default line also
-# at --warmup 60 and unstaggered (--stagger 0), and the one-GPU N = 2 gloo rehearsal
+# at --warmup 60 and unstaggered (--stagger 0), and the one-GPU N = 2 gloo rehearsal (copy part 1's
+# PMC JSONs from gpurun_out/ into profiles/ locally first: this call ships the local tree)
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"

@@ -2715,6 +2715,10 @@ constexpr int kSolveStep = SSF_SOLVE_STEP;
 #ifndef SSF_SOLVE_DIRECT
 #define SSF_SOLVE_DIRECT 1                       // compacted records: 1 loaded by the first evaluation, 2 copied first (A/B)
 #endif
+#ifndef SSF_SOLVE_LOADALL
+#define SSF_SOLVE_LOADALL 0                      // A/B: first evaluation requests every record of a thread at
+                                                 // once (r6zh: 23.2 k vs 15.5 k cycles, 0.070 vs 0.066 ms, slower)
+#endif
 #ifndef SSF_SOLVE_LDS_PF
 #define SSF_SOLVE_LDS_PF 0                       // 1: LDS records of the next step in flight (r6m: 0.0706 vs 0.0674 ms, slower)
 #endif
@@ -2807,6 +2811,38 @@ SSF_DEV void evaluate_load(const CorrRec* __restrict__ rec, CorrLds& C, int nv, 
     hf2 H[kHF];
 #pragma unroll
     for (int k = 0; k < kHF; ++k) H[k] = hf2{0.0f, 0.0f};
+#if SSF_SOLVE_LOADALL
+    // every record of this thread (<= kSolveLdsCap / T of them) requested at once into registers
+    // (one wave per SIMD: 512 VGPRs per lane to spend, and nothing else hides a load's latency),
+    // then the same steps in the same order as below; clamped, unconditional loads
+    constexpr int kR = kSolveLdsCap / (NW * 64);
+    static_assert(kR % kSolveStep == 0, "whole steps");
+    float4 a0[kR], a1[kR], a2[kR];
+#pragma unroll
+    for (int k = 0; k < kR; ++k) {
+        const float4* rp = reinterpret_cast<const float4*>(rec + min((int)threadIdx.x + k * T, nv - 1));
+        a0[k] = rp[0]; a1[k] = rp[1]; a2[k] = rp[2];
+    }
+#pragma unroll
+    for (int s0 = 0; s0 < kR; s0 += kSolveStep) {
+        const int i = (int)threadIdx.x + s0 * T;
+        if (i < nv) {
+#pragma unroll
+            for (int h = 0; h < kSolveStep; ++h) {
+                const int ih = i + h * T;
+                const int k = s0 + h;
+                if (ih < nv) {
+                    C.po[0][ih] = a0[k].x; C.po[1][ih] = a0[k].y; C.po[2][ih] = a0[k].z;
+                    C.pa[0][ih] = a1[k].x; C.pa[1][ih] = a1[k].y; C.pa[2][ih] = a1[k].z;
+                    C.n[0][ih] = a2[k].x; C.n[1][ih] = a2[k].y; C.n[2][ih] = a2[k].z;
+                }
+                const double po[3] = {a0[k].x, a0[k].y, a0[k].z}, pa[3] = {a1[k].x, a1[k].y, a1[k].z},
+                             nn[3] = {a2[k].x, a2[k].y, a2[k].z};
+                accum_corr(R, t, po, pa, nn, (h == 0 || ih < nv) ? 1.0 : 0.0, ne, H);
+            }
+        }
+    }
+#else
     // one step's records in flight ahead of the step being evaluated (clamped, unconditional
     // loads: a step past nv re-reads record nv - 1 and is never used)
     float4 n0[kSolveStep], n1[kSolveStep], n2[kSolveStep];
@@ -2836,6 +2872,7 @@ SSF_DEV void evaluate_load(const CorrRec* __restrict__ rec, CorrLds& C, int nv, 
             accum_corr(R, t, po, pa, nn, (h == 0 || ih < nv) ? 1.0 : 0.0, ne, H);
         }
     }
+#endif
 #if SSF_SOLVE_HF32
 #pragma unroll
     for (int e = 0; e < 21; ++e) ne[e] += (double)H[e >> 1][e & 1];
@@ -3030,6 +3067,11 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
     const unsigned long long st0 = __builtin_amdgcn_s_memtime();
     unsigned long long st1 = st0, st2 = st0;
 #endif
+#ifdef SSF_SOLVE_STAMPS2
+    // diagnostic build only: the GN iterations split into the 6x6 solve + pose update and the
+    // evaluation (replacing the compaction / first-evaluation stamps of the log row)
+    unsigned long long t_sol = 0, t_ev = 0;
+#endif
     if (tid == 0) {
         for (int k = 0; k < 4; ++k) S.q[k] = pose_in[7 * p + k];
         for (int k = 0; k < 3; ++k) S.t[k] = pose_in[7 * p + 4 + k];
@@ -3190,6 +3232,9 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
             int nl = 0;
             for (int it = 0; it < max_iter; ++it) {
                 double y[6];
+#ifdef SSF_SOLVE_STAMPS2
+                const unsigned long long sa = __builtin_amdgcn_s_memtime();
+#endif
                 if (chol_solve_packed(ne, y) != 0) {                         // uniform
                     if (tid == 0) write_log(log, max_iter, p, nl, q, t, ne[27], 2, 0);
                     ++nl;
@@ -3199,10 +3244,18 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
                 quat_plus_step(q, y, qn);
                 for (int k = 0; k < 4; ++k) q[k] = qn[k];
                 t[0] += y[3]; t[1] += y[4]; t[2] += y[5];
+#ifdef SSF_SOLVE_STAMPS2
+                const unsigned long long sb = __builtin_amdgcn_s_memtime();
+#endif
                 eval_at(q, t, ne);
+#ifdef SSF_SOLVE_STAMPS2
+                const unsigned long long sc = __builtin_amdgcn_s_memtime();
+                t_sol += sb - sa; t_ev += sc - sb;
+#endif
                 if (tid == 0) write_log(log, max_iter, p, nl, q, t, ne[27], 6, 0);
                 ++nl;
             }
+
             if (tid == 0) {
                 for (int k = 0; k < 4; ++k) S.q[k] = q[k];
                 for (int k = 0; k < 3; ++k) S.t[k] = t[k];
@@ -3424,7 +3477,11 @@ __global__ __launch_bounds__(NT) void k_solve(const CorrRec* __restrict__ corr,
 #ifdef SSF_SOLVE_STAMPS
         if (log) {
             double* r = log + ((int64_t)p * max_iter + max_iter - 1) * 10;
+#ifdef SSF_SOLVE_STAMPS2
+            r[7] = (double)t_sol; r[8] = (double)t_ev;
+#else
             r[7] = (double)(st1 - st0); r[8] = (double)(st2 - st1);
+#endif
             r[9] = (double)(__builtin_amdgcn_s_memtime() - st2);
         }
 #endif

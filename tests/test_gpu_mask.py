@@ -460,3 +460,23 @@ def test_slove_RT_by_SVD_float32(oracle, dev):
     with pytest.raises(ValueError):
         ssf.mask_and_pose(c["pos1"], c["flow"], mode="given", gt_mask=np.zeros(len(c["pos1"]), np.uint8),
                           kabsch_dtype="float32")
+
+
+def test_frame_above_32bit_offsets_rejected(dev):
+    """The streaming loops address a frame with 32-bit byte offsets (mask_pose.hip load3_off):
+    ssf_mask_pose_batch rejects a frame above 2^32 / 12 points (f32) or 2^32 / 24 (f64) with
+    SSF_E_ARG before anything is launched (the device pointers are never dereferenced here)."""
+    import ctypes as C
+    import ssf
+    from ssf import _abi
+    from ssf.frontend import MASK_MODES, _stream
+    MASK_GMM = MASK_MODES["gmm"]
+    fe = ssf.Frontend(64, device=dev.index)
+    lib = _abi.lib()
+    fake = C.c_void_p(16)                               # never touched: the check comes first
+    for name, bytes_per_point in (("ssf_mask_pose_batch", 12), ("ssf_mask_pose_batch_f64", 24)):
+        n = (2 ** 32 - 1) // bytes_per_point + 1
+        h_off = np.array([0, n], dtype=np.int64)
+        rc = getattr(lib, name)(fe._h, _stream(fe.device), 1, fake, fake, fake,
+                                C.c_void_p(h_off.ctypes.data), MASK_GMM, None, None, 0, None, fake)
+        assert rc == _abi.SSF_E_ARG, (name, n, rc)

@@ -92,6 +92,43 @@ def test_plane_table_duplicates_and_sizes(oracle, dev):
         assert np.array_equal(g.view(np.uint32), nr.view(np.uint32)), f
 
 
+def _rank_walk_cloud(oracle):
+    """A realistic plane cloud plus an isolated dense segment of ring 20 (48 points 1 cm apart)
+    with three points of rings 21 / 22 0.6-0.8 m beside it."""
+    base = oracle.extract_planes(frame(0, 0)[0], 64)
+    k = np.arange(48, dtype=np.float64)
+    seg = np.stack([200.0 + 0.01 * k, 200.0 + 0.002 * k, 0.3 + 1e-4 * k * k, k + 0.20], 1)
+    oth = np.array([[200.20, 200.60, 0.30, 3 + 0.21], [200.30, 200.70, 0.35, 4 + 0.21],
+                    [200.10, 200.80, 0.32, 5 + 0.22]])
+    return np.concatenate([base, seg, oth]).astype(np.float32), len(base)
+
+
+def test_plane_table_rank_walk_cases(oracle, dev):
+    """Queries whose first other-ring point D1 ranks beyond 30 behind many same-ring neighbours:
+    the count of non-other-ring keys that left the top five exceeds the skip bound (round 6), so
+    the D1 / D2 rank walk runs and decides them -- bit-exact against the oracle, as the rest of
+    the frame that takes the skip."""
+    import ssf
+    P, nb = _rank_walk_cloud(oracle)
+    # the scenario: for the segment's queries, the nearest other-ring point within 1 m ranks >= 30
+    Q = P[nb:nb + 48, :3].astype(np.float64)
+    rows = np.floor(100.0 * ((P[:, 3] - np.floor(P[:, 3])) + 0.002)).astype(int)
+    d = np.linalg.norm(P[None, :, :3].astype(np.float64) - Q[:, None, :], axis=2)
+    for j in range(48):
+        order = np.argsort(d[j], kind="stable")
+        ranks = [r for r, i in enumerate(order) if rows[i] != 20 and d[j, i] < 1.0]
+        assert ranks and ranks[0] >= 30, (j, ranks[:3])
+    fe = ssf.Frontend(64, device=dev.index)
+    off, h_off = ssf.frame_offsets([len(P)], dev)
+    xyzi = torch.from_numpy(P).to(dev)
+    pb = ssf.PlaneBatch(xyzi, torch.tensor([len(P)], dtype=torch.int32, device=dev), off, h_off, len(P))
+    normal, valid, _, _ = fe.plane_table(pb)
+    nr, vr, _, _ = oracle.plane_table(P, 0.05)
+    assert np.array_equal(valid.cpu().numpy(), vr.astype(np.uint8))
+    g = normal.cpu().numpy()
+    assert np.array_equal(g.view(np.uint32), nr.view(np.uint32)), "normal bits differ"
+
+
 def test_nan_warm_start_association_stays_in_frame(dev):
     """A NaN warm start (an ill-conditioned link of a chain) makes every query point NaN: no
     candidate wins.  Both association modes -- the group mode of launches of <= 16 pairs and the

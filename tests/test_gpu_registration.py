@@ -201,6 +201,50 @@ def test_compacted_records_same_bits(dev, solver, iters):
                               big["log"][k, :n].cpu().numpy().view(np.uint64)), k
 
 
+def test_compacted_records_edge_pairs(dev):
+    """The compacted-record path's edge cases inside one big launch (> 16 pairs): a pair whose
+    last frame has <= 10 plane points (:158, skipped, count 0), a pair with an empty current
+    frame, and a pair whose current frame is cut to 3 points -- every pair's pose, log and count
+    bit-identical to its own single-pair launch (group-mode association, solve-side compaction)."""
+    import ssf
+    fe = ssf.Frontend(64, device=dev.index, solver="gn", max_iter=10)
+    P = 18
+    clouds = [frame(4, k, n_az=900)[0] for k in range(P + 1)]
+    pb = _planes(fe, dev, clouds)
+    table = fe.plane_table(pb)
+    init = torch.tensor([[0.0, 0.0, 0.001, 1.0, 0.8, 0.0, 0.0]] * P, dtype=torch.float64, device=dev)
+    init[:, :4] /= torch.linalg.norm(init[:, :4], dim=1, keepdim=True)
+    cut_last = {2: 8, 9: 10}                   # last-frame plane counts <= 10
+    cut_curr = {5: 0, 13: 3}                   # an empty and a 3-point current frame
+
+    def pairs(idx):
+        lo = torch.stack([pb.off[k] for k in idx] + [pb.off[idx[-1] + 1]])
+        co = torch.stack([pb.off[k + 1] for k in idx] + [pb.off[idx[-1] + 2]])
+        hl = torch.tensor([int(pb.h_off[k]) for k in idx] + [int(pb.h_off[idx[-1] + 1])])
+        hc = torch.tensor([int(pb.h_off[k + 1]) for k in idx] + [int(pb.h_off[idx[-1] + 2])])
+        cl = torch.stack([torch.clamp(pb.count[k], max=cut_last.get(k, 1 << 30)) for k in idx]).contiguous()
+        cc = torch.stack([torch.clamp(pb.count[k + 1], max=cut_curr.get(k, 1 << 30)) for k in idx]).contiguous()
+        return (ssf.PlaneBatch(pb.xyzi, cl, lo.contiguous(), hl, pb.max_points),
+                ssf.PlaneBatch(pb.xyzi, cc, co.contiguous(), hc, pb.max_points))
+
+    last, curr = pairs(list(range(P)))
+    big = fe.register(last, table, curr, init.clone(), want_log=True)
+    torch.cuda.synchronize()
+    for k in range(P):
+        l1, c1 = pairs([k])
+        one = fe.register(l1, table, c1, init[k:k + 1].clone(), want_log=True)
+        torch.cuda.synchronize()
+        assert int(one["ncorr"][0]) == int(big["ncorr"][k]), k
+        assert np.array_equal(one["pose_rel"][0].cpu().numpy().view(np.uint64),
+                              big["pose_rel"][k].cpu().numpy().view(np.uint64)), k
+        n = int(one["nlog"][0])
+        assert n == int(big["nlog"][k]), k
+        assert np.array_equal(one["log"][0, :n].cpu().numpy().view(np.uint64),
+                              big["log"][k, :n].cpu().numpy().view(np.uint64)), k
+    for k in list(cut_last) + [5]:
+        assert int(big["ncorr"][k]) <= 0, (k, int(big["ncorr"][k]))
+
+
 @pytest.mark.parametrize("solver,iters,mode,brute", [("ceres_lm", 8, 0, False), ("gn", 10, 1, False),
                                                      ("ceres_lm", 8, 0, True)])
 def test_register_pair_per_step(oracle, dev, solver, iters, mode, brute):

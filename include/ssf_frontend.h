@@ -320,6 +320,8 @@ int32_t ssf_register_batch_edges(ssf_ctx* ctx, void* stream, int32_t n_pairs,
  *              1: flip Vt[2] (the evident intent of :32-33).
  *   d_bg_mask  out, nullable: uint8 per point, 1 = background.
  *   d_out      out [F*SSF_POSE_OUT_STRIDE] doubles, see SSF_POSE_OUT_* below.
+ *   A frame of more than 2^32 / 12 points (2^32 / 24 for the f64 form) fails with SSF_E_ARG
+ *   before any launch: the kernel addresses a frame with 32-bit byte offsets.
  */
 #define SSF_POSE_OUT_STRIDE 32
 enum {
